@@ -1,0 +1,519 @@
+// BLS12-381 groups G1 (over Fq) and G2 (over Fq2): Jacobian arithmetic, the zcash point
+// codec with pairing 0.14's decode checks, and fast subgroup membership tests.
+//
+// Replaces pairing 0.14.2 src/bls12_381/ec.rs (external crate, /root/reference/Cargo.toml:27)
+// as used through threshold_crypto's serde and combine paths (A3/A6).
+//
+// Decode semantics (bit-exact with G{1,2}Compressed::into_affine):
+//   bit7 must be set (compressed); bit6 = infinity -> all remaining bits must be zero;
+//   bit5 = "y is lexicographically largest"; coordinates must be < p; x^3 + b must be a
+//   square; the point must lie in the r-order subgroup.  Any failure = HBTC_DECODE_ERR.
+// The subgroup test uses the curve endomorphisms instead of pairing 0.14's [r]P == O:
+//   G1: phi(P) == [-x^2] P   (phi(x, y) = (beta x, y));   G2: psi(P) == [x] P.
+// Both are exact membership tests for BLS12-381 (Scott, "A note on group membership tests
+// for G1, G2 and GT on BLS pairing-friendly curves", 2021); tests/ cross-check them against
+// [r]P on points with every small cofactor component.
+#pragma once
+#include "field.h"
+
+namespace hbtc {
+
+// ---------------------------------------------------------------- generic field wrappers
+HD void fadd(Fq& r, const Fq& a, const Fq& b) { fq_add(r, a, b); }
+HD void fadd(Fq2& r, const Fq2& a, const Fq2& b) { fq2_add(r, a, b); }
+HD void fsub(Fq& r, const Fq& a, const Fq& b) { fq_sub(r, a, b); }
+HD void fsub(Fq2& r, const Fq2& a, const Fq2& b) { fq2_sub(r, a, b); }
+HD void fmul(Fq& r, const Fq& a, const Fq& b) { fq_mul(r, a, b); }
+HD void fmul(Fq2& r, const Fq2& a, const Fq2& b) { fq2_mul(r, a, b); }
+HD void fsqr(Fq& r, const Fq& a) { fq_sqr(r, a); }
+HD void fsqr(Fq2& r, const Fq2& a) { fq2_sqr(r, a); }
+HD void fdbl(Fq& r, const Fq& a) { fq_dbl(r, a); }
+HD void fdbl(Fq2& r, const Fq2& a) { fq2_dbl(r, a); }
+HD void fneg(Fq& r, const Fq& a) { fq_neg(r, a); }
+HD void fneg(Fq2& r, const Fq2& a) { fq2_neg(r, a); }
+HD bool fis_zero(const Fq& a) { return fq_is_zero(a); }
+HD bool fis_zero(const Fq2& a) { return fq2_is_zero(a); }
+HD bool feq(const Fq& a, const Fq& b) { return fq_eq(a, b); }
+HD bool feq(const Fq2& a, const Fq2& b) { return fq2_eq(a, b); }
+HD void fone(Fq& r) { fq_one(r); }
+HD void fone(Fq2& r) { fq2_one(r); }
+HD void fzero(Fq& r) { fq_zero(r); }
+HD void fzero(Fq2& r) { fq2_zero(r); }
+HD void finv(Fq& r, const Fq& a) { fq_inv(r, a); }
+HD void finv(Fq2& r, const Fq2& a) { fq2_inv(r, a); }
+
+template <class F>
+struct Aff {
+  F x, y;
+  uint32_t inf;  // 1 = point at infinity
+};
+
+template <class F>
+struct Jac {
+  F x, y, z;  // (X/Z^2, Y/Z^3); Z == 0 is infinity
+};
+
+typedef Aff<Fq> G1A;
+typedef Aff<Fq2> G2A;
+typedef Jac<Fq> G1J;
+typedef Jac<Fq2> G2J;
+
+template <class F>
+HD void jac_set_inf(Jac<F>& r) {
+  fone(r.x);
+  fone(r.y);
+  fzero(r.z);
+}
+template <class F>
+HD bool jac_is_inf(const Jac<F>& p) {
+  return fis_zero(p.z);
+}
+template <class F>
+HD void jac_from_aff(Jac<F>& r, const Aff<F>& a) {
+  if (a.inf) {
+    jac_set_inf(r);
+  } else {
+    r.x = a.x;
+    r.y = a.y;
+    fone(r.z);
+  }
+}
+
+// dbl-2009-l (a = 0): 2M + 5S
+template <class F>
+HD void jac_dbl(Jac<F>& r, const Jac<F>& p) {
+  F A, B, C, D, E, Fv, t;
+  fsqr(A, p.x);
+  fsqr(B, p.y);
+  fsqr(C, B);
+  fadd(t, p.x, B);
+  fsqr(t, t);
+  fsub(t, t, A);
+  fsub(t, t, C);
+  fdbl(D, t);
+  fdbl(E, A);
+  fadd(E, E, A);
+  fsqr(Fv, E);
+  F z3;
+  fmul(z3, p.y, p.z);
+  fdbl(z3, z3);
+  F x3;
+  fdbl(t, D);
+  fsub(x3, Fv, t);
+  F y3;
+  fsub(t, D, x3);
+  fmul(y3, E, t);
+  fdbl(C, C);
+  fdbl(C, C);
+  fdbl(C, C);
+  fsub(y3, y3, C);
+  r.x = x3;
+  r.y = y3;
+  r.z = z3;  // Y == 0 never happens for points of odd order; Z stays 0 for infinity
+}
+
+// madd-2007-bl: r = p + q (q affine), handles all special cases
+template <class F>
+HD void jac_add_aff(Jac<F>& r, const Jac<F>& p, const Aff<F>& q) {
+  if (q.inf) {
+    r = p;
+    return;
+  }
+  if (jac_is_inf(p)) {
+    jac_from_aff(r, q);
+    return;
+  }
+  F z1z1, u2, s2, H, HH, I, J, rr, V, t;
+  fsqr(z1z1, p.z);
+  fmul(u2, q.x, z1z1);
+  fmul(s2, q.y, p.z);
+  fmul(s2, s2, z1z1);
+  fsub(H, u2, p.x);
+  fsub(rr, s2, p.y);
+  if (fis_zero(H)) {
+    if (fis_zero(rr)) {
+      jac_dbl(r, p);
+    } else {
+      jac_set_inf(r);
+    }
+    return;
+  }
+  fsqr(HH, H);
+  fdbl(I, HH);
+  fdbl(I, I);
+  fmul(J, H, I);
+  fdbl(rr, rr);
+  fmul(V, p.x, I);
+  F x3, y3, z3;
+  fsqr(x3, rr);
+  fsub(x3, x3, J);
+  fdbl(t, V);
+  fsub(x3, x3, t);
+  fsub(t, V, x3);
+  fmul(y3, rr, t);
+  fmul(t, p.y, J);
+  fdbl(t, t);
+  fsub(y3, y3, t);
+  fadd(z3, p.z, H);
+  fsqr(z3, z3);
+  fsub(z3, z3, z1z1);
+  fsub(z3, z3, HH);
+  r.x = x3;
+  r.y = y3;
+  r.z = z3;
+}
+
+// add-2007-bl: r = p + q (both Jacobian)
+template <class F>
+HD void jac_add(Jac<F>& r, const Jac<F>& p, const Jac<F>& q) {
+  if (jac_is_inf(p)) {
+    r = q;
+    return;
+  }
+  if (jac_is_inf(q)) {
+    r = p;
+    return;
+  }
+  F z1z1, z2z2, u1, u2, s1, s2, H, I, J, rr, V, t;
+  fsqr(z1z1, p.z);
+  fsqr(z2z2, q.z);
+  fmul(u1, p.x, z2z2);
+  fmul(u2, q.x, z1z1);
+  fmul(s1, p.y, q.z);
+  fmul(s1, s1, z2z2);
+  fmul(s2, q.y, p.z);
+  fmul(s2, s2, z1z1);
+  fsub(H, u2, u1);
+  fsub(rr, s2, s1);
+  if (fis_zero(H)) {
+    if (fis_zero(rr)) {
+      jac_dbl(r, p);
+    } else {
+      jac_set_inf(r);
+    }
+    return;
+  }
+  fdbl(I, H);
+  fsqr(I, I);
+  fmul(J, H, I);
+  fdbl(rr, rr);
+  fmul(V, u1, I);
+  F x3, y3, z3;
+  fsqr(x3, rr);
+  fsub(x3, x3, J);
+  fdbl(t, V);
+  fsub(x3, x3, t);
+  fsub(t, V, x3);
+  fmul(y3, rr, t);
+  fmul(t, s1, J);
+  fdbl(t, t);
+  fsub(y3, y3, t);
+  fadd(z3, p.z, q.z);
+  fsqr(z3, z3);
+  fsub(z3, z3, z1z1);
+  fsub(z3, z3, z2z2);
+  fmul(z3, z3, H);
+  r.x = x3;
+  r.y = y3;
+  r.z = z3;
+}
+
+template <class F>
+HD void jac_neg(Jac<F>& r, const Jac<F>& p) {
+  r.x = p.x;
+  fneg(r.y, p.y);
+  r.z = p.z;
+}
+
+template <class F>
+HD void aff_neg(Aff<F>& r, const Aff<F>& p) {
+  r.x = p.x;
+  fneg(r.y, p.y);
+  r.inf = p.inf;
+}
+
+template <class F>
+HD void jac_to_aff(Aff<F>& r, const Jac<F>& p) {
+  if (jac_is_inf(p)) {
+    fzero(r.x);
+    fzero(r.y);
+    r.inf = 1;
+    return;
+  }
+  F zi, zi2;
+  finv(zi, p.z);
+  fsqr(zi2, zi);
+  fmul(r.x, p.x, zi2);
+  fmul(zi2, zi2, zi);
+  fmul(r.y, p.y, zi2);
+  r.inf = 0;
+}
+
+// [k] q for a 64-bit k (MSB-first double-and-add, q affine)
+template <class F>
+HD void jac_mul_u64(Jac<F>& r, const Aff<F>& q, uint64_t k) {
+  Jac<F> acc;
+  jac_set_inf(acc);
+  for (int b = 63; b >= 0; --b) {
+    jac_dbl(acc, acc);
+    if ((k >> b) & 1ull) jac_add_aff(acc, acc, q);
+  }
+  r = acc;
+}
+
+// [k] q for a Jacobian base and 64-bit k
+template <class F>
+HD void jac_mul_u64_jac(Jac<F>& r, const Jac<F>& q, uint64_t k) {
+  Jac<F> acc;
+  jac_set_inf(acc);
+  for (int b = 63; b >= 0; --b) {
+    jac_dbl(acc, acc);
+    if ((k >> b) & 1ull) jac_add(acc, acc, q);
+  }
+  r = acc;
+}
+
+// [k] q for a canonical (non-Montgomery) 8-limb scalar (MSB-first double-and-add)
+template <class F>
+HD void jac_mul_fr(Jac<F>& r, const Aff<F>& q, const Fr& k) {
+  Jac<F> acc;
+  jac_set_inf(acc);
+  if (q.inf) {
+    r = acc;
+    return;
+  }
+  for (int b = 255; b >= 0; --b) {
+    jac_dbl(acc, acc);
+    if ((k.v[b >> 5] >> (b & 31)) & 1u) jac_add_aff(acc, acc, q);
+  }
+  r = acc;
+}
+
+// Is the Jacobian point p equal to the affine point (ax, ay)?  (p not infinity)
+template <class F>
+HD bool jac_eq_aff(const Jac<F>& p, const F& ax, const F& ay) {
+  F z2, z3, t;
+  fsqr(z2, p.z);
+  fmul(z3, z2, p.z);
+  fmul(t, ax, z2);
+  if (!feq(t, p.x)) return false;
+  fmul(t, ay, z3);
+  return feq(t, p.y);
+}
+
+template <class F>
+HD bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
+  bool pi = jac_is_inf(p), qi = jac_is_inf(q);
+  if (pi || qi) return pi && qi;
+  F z1z1, z2z2, a, b;
+  fsqr(z1z1, p.z);
+  fsqr(z2z2, q.z);
+  fmul(a, p.x, z2z2);
+  fmul(b, q.x, z1z1);
+  if (!feq(a, b)) return false;
+  fmul(a, p.y, z2z2);
+  fmul(a, a, q.z);
+  fmul(b, q.y, z1z1);
+  fmul(b, b, p.z);
+  return feq(a, b);
+}
+
+// ---------------------------------------------------------------- subgroup tests
+HD bool g1_in_subgroup(const G1A& p) {
+  if (p.inf) return true;
+  G1J t, t2;
+  jac_mul_u64(t, p, BLS_X_ABS);
+  jac_mul_u64_jac(t2, t, BLS_X_ABS);  // [x^2] P
+  if (jac_is_inf(t2)) return false;   // phi(P) != O for P != O
+  Fq bx, ny;
+  Fq beta;
+  fq_set(beta, G1_BETA);
+  fq_mul(bx, p.x, beta);
+  fq_neg(ny, p.y);  // phi(P) == -[x^2]P  <=>  (beta x, -y) == [x^2] P
+  return jac_eq_aff(t2, bx, ny);
+}
+
+HD void g2_psi(Fq2& rx, Fq2& ry, const G2A& p) {
+  Fq2 c, k;
+  fq2_conj(c, p.x);
+  fq2_set(k, G2_PSI_CX);
+  fq2_mul(rx, c, k);
+  fq2_conj(c, p.y);
+  fq2_set(k, G2_PSI_CY);
+  fq2_mul(ry, c, k);
+}
+
+HD bool g2_in_subgroup(const G2A& p) {
+  if (p.inf) return true;
+  G2J t;
+  jac_mul_u64(t, p, BLS_X_ABS);  // [|x|] P ; [x]P = -[|x|]P
+  if (jac_is_inf(t)) return false;
+  Fq2 px, py, npy;
+  g2_psi(px, py, p);
+  fq2_neg(npy, py);  // psi(P) == -[|x|]P  <=>  (psi_x, -psi_y) == [|x|]P
+  return jac_eq_aff(t, px, npy);
+}
+
+// ---------------------------------------------------------------- codec
+// big-endian 48 bytes (as 12 big-endian 32-bit words, first word most significant) <-> limbs
+HD void fq_from_be_words(Fq& r, const uint32_t* w) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint32_t x = w[11 - i];
+    r.v[i] = (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+  }
+}
+HD void fq_to_be_words(uint32_t* w, const Fq& a) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint32_t x = a.v[11 - i];
+    w[i] = (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+  }
+}
+
+// Flags live in the first byte = the low byte of word 0 (little-endian load of BE bytes).
+enum : uint32_t { FLAG_COMPRESSED = 0x80u, FLAG_INFINITY = 0x40u, FLAG_LARGEST = 0x20u };
+
+// G1Compressed::into_affine.  w = the 48 input bytes as 12 little-endian-loaded words.
+HD bool g1_decompress(G1A& out, const uint32_t* w_in) {
+  uint32_t w[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) w[i] = w_in[i];
+  const uint32_t flags = w[0] & 0xffu;
+  fq_zero(out.x);
+  fq_zero(out.y);
+  out.inf = 0;
+  if (!(flags & FLAG_COMPRESSED)) return false;
+  if (flags & FLAG_INFINITY) {
+    uint32_t acc = (w[0] & ~0xc0u);
+#pragma unroll
+    for (int i = 1; i < 12; ++i) acc |= w[i];
+    out.inf = 1;
+    return acc == 0;
+  }
+  const bool greatest = (flags & FLAG_LARGEST) != 0;
+  w[0] &= ~0xe0u;
+  Fq xc;
+  fq_from_be_words(xc, w);
+  if (!limbs_lt_const<12>(xc, FQ_P)) return false;
+  Fq x, rhs, b, y;
+  fq_to_mont(x, xc);
+  fq_sqr(rhs, x);
+  fq_mul(rhs, rhs, x);
+  fq_set(b, G1_B);
+  fq_add(rhs, rhs, b);
+  if (!fq_sqrt(y, rhs)) return false;
+  // choose y if (y < -y) ^ greatest, else -y   (pairing 0.14 get_point_from_x)
+  const bool y_largest = fq_is_lex_largest(y);  // y > -y
+  if (y_largest != greatest) fq_neg(y, y);
+  out.x = x;
+  fq_canon(out.y, y);
+  fq_canon(out.x, out.x);
+  return g1_in_subgroup(out);
+}
+
+HD bool g2_decompress(G2A& out, const uint32_t* w_in) {
+  uint32_t w[24];
+#pragma unroll
+  for (int i = 0; i < 24; ++i) w[i] = w_in[i];
+  const uint32_t flags = w[0] & 0xffu;
+  fq2_zero(out.x);
+  fq2_zero(out.y);
+  out.inf = 0;
+  if (!(flags & FLAG_COMPRESSED)) return false;
+  if (flags & FLAG_INFINITY) {
+    uint32_t acc = (w[0] & ~0xc0u);
+#pragma unroll
+    for (int i = 1; i < 24; ++i) acc |= w[i];
+    out.inf = 1;
+    return acc == 0;
+  }
+  const bool greatest = (flags & FLAG_LARGEST) != 0;
+  w[0] &= ~0xe0u;
+  Fq x1c, x0c;
+  fq_from_be_words(x1c, w);       // x.c1 first
+  fq_from_be_words(x0c, w + 12);  // then x.c0
+  if (!limbs_lt_const<12>(x0c, FQ_P) || !limbs_lt_const<12>(x1c, FQ_P)) return false;
+  Fq2 x, rhs, b, y;
+  fq_to_mont(x.c0, x0c);
+  fq_to_mont(x.c1, x1c);
+  fq2_sqr(rhs, x);
+  fq2_mul(rhs, rhs, x);
+  fq2_set(b, G2_B);
+  fq2_add(rhs, rhs, b);
+  if (!fq2_sqrt(y, rhs)) return false;
+  const bool y_largest = fq2_is_lex_largest(y);
+  if (y_largest != greatest) fq2_neg(y, y);
+  fq_canon(out.x.c0, x.c0);
+  fq_canon(out.x.c1, x.c1);
+  fq_canon(out.y.c0, y.c0);
+  fq_canon(out.y.c1, y.c1);
+  return g2_in_subgroup(out);
+}
+
+// G1Compressed::from_affine -> 12 words (to be stored little-endian => BE bytes)
+HD void g1_compress(uint32_t* w, const G1A& p) {
+  if (p.inf) {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) w[i] = 0;
+    w[0] = 0xc0u;
+    return;
+  }
+  Fq xc;
+  fq_from_mont(xc, p.x);
+  fq_to_be_words(w, xc);
+  uint32_t f = FLAG_COMPRESSED;
+  if (fq_is_lex_largest(p.y)) f |= FLAG_LARGEST;
+  w[0] |= f;
+}
+
+HD void g2_compress(uint32_t* w, const G2A& p) {
+  if (p.inf) {
+#pragma unroll
+    for (int i = 0; i < 24; ++i) w[i] = 0;
+    w[0] = 0xc0u;
+    return;
+  }
+  Fq c;
+  fq_from_mont(c, p.x.c1);
+  fq_to_be_words(w, c);
+  fq_from_mont(c, p.x.c0);
+  fq_to_be_words(w + 12, c);
+  uint32_t f = FLAG_COMPRESSED;
+  if (fq2_is_lex_largest(p.y)) f |= FLAG_LARGEST;
+  w[0] |= f;
+}
+
+// G2Uncompressed::from_affine (192 bytes = 48 words: x.c1, x.c0, y.c1, y.c0)
+HD void g2_uncompress_words(uint32_t* w, const G2A& p) {
+  if (p.inf) {
+#pragma unroll
+    for (int i = 0; i < 48; ++i) w[i] = 0;
+    w[0] = 0x40u;
+    return;
+  }
+  Fq c;
+  fq_from_mont(c, p.x.c1);
+  fq_to_be_words(w, c);
+  fq_from_mont(c, p.x.c0);
+  fq_to_be_words(w + 12, c);
+  fq_from_mont(c, p.y.c1);
+  fq_to_be_words(w + 24, c);
+  fq_from_mont(c, p.y.c0);
+  fq_to_be_words(w + 36, c);
+}
+
+// Signature::parity: popcount parity of the XOR of all 192 uncompressed bytes
+HD uint32_t g2_parity(const G2A& p) {
+  uint32_t w[48];
+  g2_uncompress_words(w, p);
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 48; ++i) x ^= w[i];
+  x ^= x >> 16;
+  x ^= x >> 8;
+  x &= 0xffu;
+  return __builtin_popcount(x) & 1u;
+}
+
+}  // namespace hbtc

@@ -1,0 +1,779 @@
+// BLS12-381 field arithmetic for gfx950 (and, for tests/host hashing, the host).
+//
+// Replaces the field layer of pairing 0.14.2 (src/bls12_381/{fq,fq2,fq6,fq12,fr}.rs,
+// an external crate used by hbbft at /root/reference/Cargo.toml:27) — see SURVEY.md §8a A15.
+//
+// Representation (MI355X-first):
+//   * Fq: 12 x 32-bit limbs, Montgomery form with R = 2^384.  Because 4p < R the product
+//     of two values in [0, 2p) is again in [0, 2p) without a final subtraction, so every
+//     Fq value lives in the "lazy" range [0, 2p) and is canonicalised only for
+//     comparisons and encoding.
+//   * The Montgomery product is CIOS written so that hipcc emits one v_mad_u64_u32 per
+//     32x32->64 partial product followed by one v_addc_co_u32 carry step (the measured
+//     fastest multiply on gfx950: tools/microbench/intmul.hip, profiles/r01_intmul_microbench.txt).
+//   * The outer CIOS loop is a real (non-unrolled by default) loop over the multiplier
+//     limbs with the multiplier rotated through registers, which keeps each Fq
+//     multiplication ~70 instructions of code: the pairing is ~10^4 multiplications
+//     per share and a fully unrolled body would not fit the instruction cache.
+//   * Fr: 8 x 32-bit limbs, Montgomery with R = 2^256 (Lagrange coefficients, scalars).
+#pragma once
+#include <cstdint>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define HD __host__ __device__ __forceinline__
+#define HBTC_CONST static constexpr
+#else
+#define HD static inline
+#define HBTC_CONST static constexpr
+#endif
+
+#include "bls_constants.h"
+
+#ifndef HBTC_FQ_UNROLL
+#define HBTC_FQ_UNROLL 1
+#endif
+
+#define HBTC_PRAGMA(x) _Pragma(#x)
+#define HBTC_UNROLL_N(n) HBTC_PRAGMA(unroll n)
+
+namespace hbtc {
+
+// ============================================================================ limbs
+template <int N>
+struct Limbs {
+  uint32_t v[N];
+};
+
+typedef Limbs<12> Fq;
+typedef Limbs<8> Fr;
+
+HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+  return __builtin_addc(a, b, cin, cout);
+}
+HD uint32_t subb32(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
+  return __builtin_subc(a, b, bin, bout);
+}
+
+// r = a + b (N limbs), returns carry
+template <int N>
+HD uint32_t limbs_add(Limbs<N>& r, const Limbs<N>& a, const Limbs<N>& b) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.v[i] = addc32(a.v[i], b.v[i], c, &c);
+  return c;
+}
+
+// r = a - b, returns borrow
+template <int N>
+HD uint32_t limbs_sub(Limbs<N>& r, const Limbs<N>& a, const Limbs<N>& b) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.v[i] = subb32(a.v[i], b.v[i], c, &c);
+  return c;
+}
+
+template <int N>
+HD uint32_t limbs_sub_const(Limbs<N>& r, const Limbs<N>& a, const uint32_t* m) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.v[i] = subb32(a.v[i], m[i], c, &c);
+  return c;
+}
+
+template <int N>
+HD uint32_t limbs_add_const(Limbs<N>& r, const Limbs<N>& a, const uint32_t* m) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.v[i] = addc32(a.v[i], m[i], c, &c);
+  return c;
+}
+
+template <int N>
+HD void limbs_select(Limbs<N>& r, bool take_b, const Limbs<N>& a, const Limbs<N>& b) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.v[i] = take_b ? b.v[i] : a.v[i];
+}
+
+template <int N>
+HD bool limbs_is_zero(const Limbs<N>& a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) acc |= a.v[i];
+  return acc == 0;
+}
+
+template <int N>
+HD bool limbs_eq(const Limbs<N>& a, const Limbs<N>& b) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) acc |= a.v[i] ^ b.v[i];
+  return acc == 0;
+}
+
+// a < m (constant), unsigned
+template <int N>
+HD bool limbs_lt_const(const Limbs<N>& a, const uint32_t* m) {
+  Limbs<N> t;
+  return limbs_sub_const<N>(t, a, m) != 0;
+}
+
+template <int N>
+HD void limbs_set_const(Limbs<N>& r, const uint32_t* m) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.v[i] = m[i];
+}
+
+template <int N>
+HD void limbs_zero(Limbs<N>& r) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) r.v[i] = 0;
+}
+
+// ============================================================================ Montgomery core
+// CIOS: r = a * b * 2^(-32N) mod m.  Inputs < 2m (lazy) give output < 2m provided 4m < 2^(32N).
+// Two-pass inner steps: N independent v_mad_u64_u32 (a_j * b_i + t_j), then one carry chain.
+template <int N, int UNROLL>
+HD void mont_mul(Limbs<N>& r, const Limbs<N>& a, const Limbs<N>& bin, const uint32_t* m,
+                 uint32_t np) {
+  uint32_t t[N + 2];
+#pragma unroll
+  for (int j = 0; j < N + 2; ++j) t[j] = 0;
+  Limbs<N> b = bin;
+  HBTC_UNROLL_N(UNROLL)
+  for (int i = 0; i < N; ++i) {
+    const uint32_t bi = b.v[0];
+#pragma unroll
+    for (int j = 0; j < N - 1; ++j) b.v[j] = b.v[j + 1];  // rotate multiplier (static indexing)
+    uint64_t s[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) s[j] = (uint64_t)a.v[j] * bi + t[j];
+    uint32_t c = 0;
+    t[0] = (uint32_t)s[0];
+#pragma unroll
+    for (int j = 1; j < N; ++j) t[j] = addc32((uint32_t)s[j], (uint32_t)(s[j - 1] >> 32), c, &c);
+    t[N] = addc32(t[N], (uint32_t)(s[N - 1] >> 32), c, &c);
+    t[N + 1] = c;
+    const uint32_t q = t[0] * np;
+#pragma unroll
+    for (int j = 0; j < N; ++j) s[j] = (uint64_t)q * m[j] + t[j];
+    c = 0;
+#pragma unroll
+    for (int j = 1; j < N; ++j)
+      t[j - 1] = addc32((uint32_t)s[j], (uint32_t)(s[j - 1] >> 32), c, &c);
+    t[N - 1] = addc32(t[N], (uint32_t)(s[N - 1] >> 32), c, &c);
+    t[N] = t[N + 1] + c;
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) r.v[j] = t[j];
+}
+
+// ============================================================================ Fq
+HD void fq_zero(Fq& r) { limbs_zero<12>(r); }
+HD void fq_one(Fq& r) { limbs_set_const<12>(r, FQ_ONE); }
+HD void fq_set(Fq& r, const uint32_t* c) { limbs_set_const<12>(r, c); }
+
+// reduce [0, 4p) -> [0, 2p)
+HD void fq_reduce_2p(Fq& r) {
+  Fq t;
+  uint32_t borrow = limbs_sub_const<12>(t, r, FQ_2P);
+  limbs_select<12>(r, borrow == 0, r, t);
+}
+
+HD void fq_add(Fq& r, const Fq& a, const Fq& b) {
+  limbs_add<12>(r, a, b);  // < 4p < 2^384: no carry out
+  fq_reduce_2p(r);
+}
+
+HD void fq_dbl(Fq& r, const Fq& a) { fq_add(r, a, a); }
+
+HD void fq_sub(Fq& r, const Fq& a, const Fq& b) {
+  uint32_t borrow = limbs_sub<12>(r, a, b);
+  Fq t;
+  limbs_add_const<12>(t, r, FQ_2P);
+  limbs_select<12>(r, borrow != 0, r, t);
+}
+
+HD void fq_neg(Fq& r, const Fq& a) {
+  Fq z;
+  fq_zero(z);
+  fq_sub(r, z, a);
+}
+
+HD void fq_mul(Fq& r, const Fq& a, const Fq& b) {
+  mont_mul<12, HBTC_FQ_UNROLL>(r, a, b, FQ_P, FQ_NP);
+}
+HD void fq_sqr(Fq& r, const Fq& a) { fq_mul(r, a, a); }
+
+// canonical value in [0, p)
+HD void fq_canon(Fq& r, const Fq& a) {
+  Fq t;
+  uint32_t borrow = limbs_sub_const<12>(t, a, FQ_P);
+  limbs_select<12>(r, borrow == 0, a, t);
+}
+
+HD bool fq_is_zero(const Fq& a) {
+  Fq c;
+  fq_canon(c, a);
+  return limbs_is_zero<12>(c);
+}
+
+HD bool fq_eq(const Fq& a, const Fq& b) {
+  Fq d;
+  fq_sub(d, a, b);
+  return fq_is_zero(d);
+}
+
+HD void fq_to_mont(Fq& r, const Fq& a) {
+  Fq r2;
+  fq_set(r2, FQ_R2);
+  fq_mul(r, a, r2);
+}
+
+// Montgomery -> canonical integer
+HD void fq_from_mont(Fq& r, const Fq& a) {
+  Fq one;
+  limbs_zero<12>(one);
+  one.v[0] = 1;
+  Fq t;
+  fq_mul(t, a, one);
+  fq_canon(r, t);
+}
+
+// a^e for a constant 12-limb exponent e (square-and-multiply, MSB first)
+HD void fq_pow_const(Fq& r, const Fq& a, const uint32_t* e) {
+  Fq acc;
+  fq_one(acc);
+  for (int w = 11; w >= 0; --w) {
+    const uint32_t word = e[w];
+    for (int b = 31; b >= 0; --b) {
+      fq_sqr(acc, acc);
+      if ((word >> b) & 1u) fq_mul(acc, acc, a);
+    }
+  }
+  r = acc;
+}
+
+HD void fq_inv(Fq& r, const Fq& a) { fq_pow_const(r, a, EXP_P_MINUS_2); }
+
+// Returns true and r = sqrt(a) if a is a square (p = 3 mod 4: a^((p+1)/4)).
+HD bool fq_sqrt(Fq& r, const Fq& a) {
+  Fq t, y;
+  fq_pow_const(t, a, EXP_P_MINUS_3_DIV_4);  // a^((p-3)/4)
+  fq_mul(y, t, a);                          // a^((p+1)/4)
+  Fq y2;
+  fq_sqr(y2, y);
+  r = y;
+  return fq_eq(y2, a);
+}
+
+// canonical(a) > (p-1)/2   <=>  a > -a  (pairing 0.14 ordering on canonical values, a != 0)
+HD bool fq_is_lex_largest(const Fq& a) {
+  Fq c;
+  fq_from_mont(c, a);
+  Fq t;
+  uint32_t borrow = limbs_sub_const<12>(t, c, P_MINUS_1_DIV_2);  // c - (p-1)/2
+  return borrow == 0 && !limbs_is_zero<12>(t);
+}
+
+// ============================================================================ Fr (scalars)
+HD void fr_mul(Fr& r, const Fr& a, const Fr& b) { mont_mul<8, 8>(r, a, b, FR_R, FR_NP); }
+
+HD void fr_canon(Fr& r, const Fr& a) {
+  Fr t;
+  uint32_t borrow = limbs_sub_const<8>(t, a, FR_R);
+  limbs_select<8>(r, borrow == 0, a, t);
+}
+
+HD void fr_add(Fr& r, const Fr& a, const Fr& b) {
+  // inputs canonical (< r < 2^255): sum < 2^256
+  limbs_add<8>(r, a, b);
+  fr_canon(r, r);
+}
+
+HD void fr_sub(Fr& r, const Fr& a, const Fr& b) {
+  uint32_t borrow = limbs_sub<8>(r, a, b);
+  Fr t;
+  limbs_add_const<8>(t, r, FR_R);
+  limbs_select<8>(r, borrow != 0, r, t);
+}
+
+HD void fr_to_mont(Fr& r, const Fr& a) {
+  Fr r2;
+  limbs_set_const<8>(r2, FR_R2);
+  fr_mul(r, a, r2);
+  fr_canon(r, r);
+}
+
+HD void fr_from_mont(Fr& r, const Fr& a) {
+  Fr one;
+  limbs_zero<8>(one);
+  one.v[0] = 1;
+  fr_mul(r, a, one);
+  fr_canon(r, r);
+}
+
+HD void fr_pow_const(Fr& r, const Fr& a, const uint32_t* e) {
+  Fr acc;
+  limbs_set_const<8>(acc, FR_ONE);
+  for (int w = 7; w >= 0; --w) {
+    const uint32_t word = e[w];
+    for (int b = 31; b >= 0; --b) {
+      fr_mul(acc, acc, acc);
+      if ((word >> b) & 1u) fr_mul(acc, acc, a);
+    }
+  }
+  fr_canon(r, acc);
+}
+
+HD void fr_inv(Fr& r, const Fr& a) { fr_pow_const(r, a, EXP_R_MINUS_2); }
+
+// ============================================================================ Fq2 = Fq[u]/(u^2+1)
+struct Fq2 {
+  Fq c0, c1;
+};
+
+HD void fq2_zero(Fq2& r) {
+  fq_zero(r.c0);
+  fq_zero(r.c1);
+}
+HD void fq2_one(Fq2& r) {
+  fq_one(r.c0);
+  fq_zero(r.c1);
+}
+HD void fq2_set(Fq2& r, const uint32_t* c) {
+  fq_set(r.c0, c);
+  fq_set(r.c1, c + 12);
+}
+HD void fq2_add(Fq2& r, const Fq2& a, const Fq2& b) {
+  fq_add(r.c0, a.c0, b.c0);
+  fq_add(r.c1, a.c1, b.c1);
+}
+HD void fq2_sub(Fq2& r, const Fq2& a, const Fq2& b) {
+  fq_sub(r.c0, a.c0, b.c0);
+  fq_sub(r.c1, a.c1, b.c1);
+}
+HD void fq2_dbl(Fq2& r, const Fq2& a) { fq2_add(r, a, a); }
+HD void fq2_neg(Fq2& r, const Fq2& a) {
+  fq_neg(r.c0, a.c0);
+  fq_neg(r.c1, a.c1);
+}
+HD void fq2_conj(Fq2& r, const Fq2& a) {
+  r.c0 = a.c0;
+  fq_neg(r.c1, a.c1);
+}
+// Karatsuba: 3 Fq multiplications
+HD void fq2_mul(Fq2& r, const Fq2& a, const Fq2& b) {
+  Fq t0, t1, s0, s1;
+  fq_mul(t0, a.c0, b.c0);
+  fq_mul(t1, a.c1, b.c1);
+  fq_add(s0, a.c0, a.c1);
+  fq_add(s1, b.c0, b.c1);
+  fq_mul(s0, s0, s1);
+  fq_sub(r.c0, t0, t1);
+  fq_sub(s0, s0, t0);
+  fq_sub(r.c1, s0, t1);
+}
+// (a0 + a1 u)^2 = (a0 + a1)(a0 - a1) + 2 a0 a1 u
+HD void fq2_sqr(Fq2& r, const Fq2& a) {
+  Fq s, d, m;
+  fq_add(s, a.c0, a.c1);
+  fq_sub(d, a.c0, a.c1);
+  fq_mul(m, a.c0, a.c1);
+  fq_mul(r.c0, s, d);
+  fq_dbl(r.c1, m);
+}
+HD void fq2_mul_fq(Fq2& r, const Fq2& a, const Fq& b) {
+  fq_mul(r.c0, a.c0, b);
+  fq_mul(r.c1, a.c1, b);
+}
+// multiply by xi = 1 + u
+HD void fq2_mul_xi(Fq2& r, const Fq2& a) {
+  Fq t0, t1;
+  fq_sub(t0, a.c0, a.c1);
+  fq_add(t1, a.c0, a.c1);
+  r.c0 = t0;
+  r.c1 = t1;
+}
+HD bool fq2_is_zero(const Fq2& a) { return fq_is_zero(a.c0) && fq_is_zero(a.c1); }
+HD bool fq2_eq(const Fq2& a, const Fq2& b) { return fq_eq(a.c0, b.c0) && fq_eq(a.c1, b.c1); }
+HD void fq2_inv(Fq2& r, const Fq2& a) {
+  Fq t0, t1;
+  fq_sqr(t0, a.c0);
+  fq_sqr(t1, a.c1);
+  fq_add(t0, t0, t1);
+  fq_inv(t0, t0);
+  fq_mul(r.c0, a.c0, t0);
+  fq_mul(t1, a.c1, t0);
+  fq_neg(r.c1, t1);
+}
+
+// Square root in Fq2 via the norm: two Fq exponentiations.  Returns false if a is a
+// non-square.  Any root is fine: callers choose between y and -y by pairing 0.14's order.
+HD bool fq2_sqrt(Fq2& r, const Fq2& a) {
+  Fq n, t;
+  fq_sqr(n, a.c0);
+  fq_sqr(t, a.c1);
+  fq_add(n, n, t);  // norm a0^2 + a1^2
+  Fq s;
+  fq_sqrt(s, n);    // validity checked at the end (r^2 == a)
+  Fq half;
+  fq_set(half, FQ_INV2);
+  Fq d;
+  fq_add(d, a.c0, s);
+  fq_mul(d, d, half);  // delta = (a0 + s)/2
+  if (fq_is_zero(d)) {
+    fq_sub(d, a.c0, s);
+    fq_mul(d, d, half);
+  }
+  Fq tt, x0;
+  fq_pow_const(tt, d, EXP_P_MINUS_3_DIV_4);  // t = delta^((p-3)/4)
+  fq_mul(x0, tt, d);                         // x0 = delta^((p+1)/4)
+  Fq chk;
+  fq_mul(chk, tt, x0);  // delta^((p-1)/2) = +-1
+  Fq one;
+  fq_one(one);
+  Fq2 cand;
+  if (fq_eq(chk, one)) {
+    // x = (x0, a1 * t / 2)
+    cand.c0 = x0;
+    fq_mul(cand.c1, a.c1, tt);
+    fq_mul(cand.c1, cand.c1, half);
+  } else {
+    // delta non-square: x = (-a1 * t / 2, x0)
+    Fq u;
+    fq_mul(u, a.c1, tt);
+    fq_mul(u, u, half);
+    fq_neg(cand.c0, u);
+    cand.c1 = x0;
+  }
+  Fq2 sq;
+  fq2_sqr(sq, cand);
+  r = cand;
+  return fq2_eq(sq, a);
+}
+
+// pairing 0.14 Ord for Fq2 (c1, then c0): is a > -a ?
+HD bool fq2_is_lex_largest(const Fq2& a) {
+  if (!fq_is_zero(a.c1)) return fq_is_lex_largest(a.c1);
+  return fq_is_lex_largest(a.c0);
+}
+
+// a^(p^k): conjugation for odd k
+HD void fq2_frob(Fq2& r, const Fq2& a, int k) {
+  if (k & 1)
+    fq2_conj(r, a);
+  else
+    r = a;
+}
+
+// ============================================================================ Fq6 = Fq2[v]/(v^3 - xi)
+struct Fq6 {
+  Fq2 c0, c1, c2;
+};
+
+HD void fq6_zero(Fq6& r) {
+  fq2_zero(r.c0);
+  fq2_zero(r.c1);
+  fq2_zero(r.c2);
+}
+HD void fq6_one(Fq6& r) {
+  fq2_one(r.c0);
+  fq2_zero(r.c1);
+  fq2_zero(r.c2);
+}
+HD void fq6_add(Fq6& r, const Fq6& a, const Fq6& b) {
+  fq2_add(r.c0, a.c0, b.c0);
+  fq2_add(r.c1, a.c1, b.c1);
+  fq2_add(r.c2, a.c2, b.c2);
+}
+HD void fq6_sub(Fq6& r, const Fq6& a, const Fq6& b) {
+  fq2_sub(r.c0, a.c0, b.c0);
+  fq2_sub(r.c1, a.c1, b.c1);
+  fq2_sub(r.c2, a.c2, b.c2);
+}
+HD void fq6_neg(Fq6& r, const Fq6& a) {
+  fq2_neg(r.c0, a.c0);
+  fq2_neg(r.c1, a.c1);
+  fq2_neg(r.c2, a.c2);
+}
+// multiply by v: (c0, c1, c2) -> (xi c2, c0, c1)
+HD void fq6_mul_v(Fq6& r, const Fq6& a) {
+  Fq2 t;
+  fq2_mul_xi(t, a.c2);
+  r.c2 = a.c1;
+  r.c1 = a.c0;
+  r.c0 = t;
+}
+// Karatsuba: 6 Fq2 multiplications
+HD void fq6_mul(Fq6& r, const Fq6& a, const Fq6& b) {
+  Fq2 v0, v1, v2, s, t, c0, c1, c2;
+  fq2_mul(v0, a.c0, b.c0);
+  fq2_mul(v1, a.c1, b.c1);
+  fq2_mul(v2, a.c2, b.c2);
+  // c0 = v0 + xi((a1 + a2)(b1 + b2) - v1 - v2)
+  fq2_add(s, a.c1, a.c2);
+  fq2_add(t, b.c1, b.c2);
+  fq2_mul(s, s, t);
+  fq2_sub(s, s, v1);
+  fq2_sub(s, s, v2);
+  fq2_mul_xi(s, s);
+  fq2_add(c0, v0, s);
+  // c1 = (a0 + a1)(b0 + b1) - v0 - v1 + xi v2
+  fq2_add(s, a.c0, a.c1);
+  fq2_add(t, b.c0, b.c1);
+  fq2_mul(s, s, t);
+  fq2_sub(s, s, v0);
+  fq2_sub(s, s, v1);
+  fq2_mul_xi(t, v2);
+  fq2_add(c1, s, t);
+  // c2 = (a0 + a2)(b0 + b2) - v0 - v2 + v1
+  fq2_add(s, a.c0, a.c2);
+  fq2_add(t, b.c0, b.c2);
+  fq2_mul(s, s, t);
+  fq2_sub(s, s, v0);
+  fq2_sub(s, s, v2);
+  fq2_add(c2, s, v1);
+  r.c0 = c0;
+  r.c1 = c1;
+  r.c2 = c2;
+}
+// CH-SQR2
+HD void fq6_sqr(Fq6& r, const Fq6& a) {
+  Fq2 s0, s1, s2, s3, s4, t;
+  fq2_sqr(s0, a.c0);
+  fq2_mul(s1, a.c0, a.c1);
+  fq2_dbl(s1, s1);
+  fq2_sub(t, a.c0, a.c1);
+  fq2_add(t, t, a.c2);
+  fq2_sqr(s2, t);
+  fq2_mul(s3, a.c1, a.c2);
+  fq2_dbl(s3, s3);
+  fq2_sqr(s4, a.c2);
+  Fq6 o;
+  fq2_mul_xi(t, s3);
+  fq2_add(o.c0, s0, t);
+  fq2_mul_xi(t, s4);
+  fq2_add(o.c1, s1, t);
+  fq2_add(t, s1, s2);
+  fq2_add(t, t, s3);
+  fq2_sub(t, t, s0);
+  fq2_sub(o.c2, t, s4);
+  r = o;
+}
+// a * (b0 + b1 v)   (5 Fq2 multiplications)
+HD void fq6_mul_by_01(Fq6& r, const Fq6& a, const Fq2& b0, const Fq2& b1) {
+  Fq2 t0, t1, s, t, c0, c1, c2;
+  fq2_mul(t0, a.c0, b0);
+  fq2_mul(t1, a.c1, b1);
+  // c0 = t0 + xi * a2 * b1
+  fq2_mul(s, a.c2, b1);
+  fq2_mul_xi(s, s);
+  fq2_add(c0, t0, s);
+  // c1 = (a0 + a1)(b0 + b1) - t0 - t1
+  fq2_add(s, a.c0, a.c1);
+  fq2_add(t, b0, b1);
+  fq2_mul(s, s, t);
+  fq2_sub(s, s, t0);
+  fq2_sub(c1, s, t1);
+  // c2 = t1 + a2 * b0
+  fq2_mul(s, a.c2, b0);
+  fq2_add(c2, t1, s);
+  r.c0 = c0;
+  r.c1 = c1;
+  r.c2 = c2;
+}
+// a * (b1 v)   (3 Fq2 multiplications)
+HD void fq6_mul_by_1(Fq6& r, const Fq6& a, const Fq2& b1) {
+  Fq2 t0, t1, t2;
+  fq2_mul(t2, a.c2, b1);
+  fq2_mul_xi(t2, t2);
+  fq2_mul(t0, a.c0, b1);
+  fq2_mul(t1, a.c1, b1);
+  r.c0 = t2;
+  r.c1 = t0;
+  r.c2 = t1;
+}
+HD void fq6_inv(Fq6& r, const Fq6& a) {
+  Fq2 t0, t1, t2, s, d;
+  // t0 = c0^2 - xi c1 c2
+  fq2_sqr(t0, a.c0);
+  fq2_mul(s, a.c1, a.c2);
+  fq2_mul_xi(s, s);
+  fq2_sub(t0, t0, s);
+  // t1 = xi c2^2 - c0 c1
+  fq2_sqr(t1, a.c2);
+  fq2_mul_xi(t1, t1);
+  fq2_mul(s, a.c0, a.c1);
+  fq2_sub(t1, t1, s);
+  // t2 = c1^2 - c0 c2
+  fq2_sqr(t2, a.c1);
+  fq2_mul(s, a.c0, a.c2);
+  fq2_sub(t2, t2, s);
+  // d = c0 t0 + xi (c2 t1 + c1 t2)
+  fq2_mul(d, a.c2, t1);
+  fq2_mul(s, a.c1, t2);
+  fq2_add(d, d, s);
+  fq2_mul_xi(d, d);
+  fq2_mul(s, a.c0, t0);
+  fq2_add(d, d, s);
+  fq2_inv(d, d);
+  fq2_mul(r.c0, t0, d);
+  fq2_mul(r.c1, t1, d);
+  fq2_mul(r.c2, t2, d);
+}
+HD void fq6_frob(Fq6& r, const Fq6& a, int k) {
+  Fq2 c1, c2;
+  fq2_frob(r.c0, a.c0, k);
+  fq2_frob(c1, a.c1, k);
+  fq2_frob(c2, a.c2, k);
+  Fq2 g1, g2;
+  if (k == 1) {
+    fq2_set(g1, FROB6_C1_1);
+    fq2_set(g2, FROB6_C2_1);
+  } else if (k == 2) {
+    fq2_set(g1, FROB6_C1_2);
+    fq2_set(g2, FROB6_C2_2);
+  } else {
+    fq2_set(g1, FROB6_C1_3);
+    fq2_set(g2, FROB6_C2_3);
+  }
+  fq2_mul(r.c1, c1, g1);
+  fq2_mul(r.c2, c2, g2);
+}
+
+// ============================================================================ Fq12 = Fq6[w]/(w^2 - v)
+struct Fq12 {
+  Fq6 c0, c1;
+};
+
+HD void fq12_one(Fq12& r) {
+  fq6_one(r.c0);
+  fq6_zero(r.c1);
+}
+HD void fq12_conj(Fq12& r, const Fq12& a) {
+  r.c0 = a.c0;
+  fq6_neg(r.c1, a.c1);
+}
+HD void fq12_mul(Fq12& r, const Fq12& a, const Fq12& b) {
+  Fq6 aa, bb, s, t;
+  fq6_mul(aa, a.c0, b.c0);
+  fq6_mul(bb, a.c1, b.c1);
+  fq6_add(s, a.c0, a.c1);
+  fq6_add(t, b.c0, b.c1);
+  fq6_mul(s, s, t);
+  fq6_sub(s, s, aa);
+  fq6_sub(r.c1, s, bb);
+  fq6_mul_v(t, bb);
+  fq6_add(r.c0, aa, t);
+}
+// complex squaring: 2 Fq6 multiplications
+HD void fq12_sqr(Fq12& r, const Fq12& a) {
+  Fq6 ab, s, t;
+  fq6_mul(ab, a.c0, a.c1);
+  fq6_add(s, a.c0, a.c1);
+  fq6_mul_v(t, a.c1);
+  fq6_add(t, a.c0, t);
+  fq6_mul(s, s, t);
+  fq6_sub(s, s, ab);
+  fq6_mul_v(t, ab);
+  fq6_sub(r.c0, s, t);
+  fq6_add(r.c1, ab, ab);
+}
+// f * line where line = (l00 + l01 v) + (l11 v) w
+HD void fq12_mul_by_line(Fq12& f, const Fq2& l00, const Fq2& l01, const Fq2& l11) {
+  Fq6 t0, t1, s;
+  fq6_mul_by_01(t0, f.c0, l00, l01);
+  fq6_mul_by_1(t1, f.c1, l11);
+  fq6_add(s, f.c0, f.c1);
+  Fq2 m;
+  fq2_add(m, l01, l11);
+  fq6_mul_by_01(s, s, l00, m);
+  fq6_sub(s, s, t0);
+  fq6_sub(f.c1, s, t1);
+  fq6_mul_v(s, t1);
+  fq6_add(f.c0, t0, s);
+}
+HD void fq12_inv(Fq12& r, const Fq12& a) {
+  Fq6 t0, t1;
+  fq6_sqr(t0, a.c0);
+  fq6_sqr(t1, a.c1);
+  fq6_mul_v(t1, t1);
+  fq6_sub(t0, t0, t1);
+  fq6_inv(t0, t0);
+  fq6_mul(r.c0, a.c0, t0);
+  fq6_mul(t1, a.c1, t0);
+  fq6_neg(r.c1, t1);
+}
+HD void fq12_frob(Fq12& r, const Fq12& a, int k) {
+  Fq6 c1;
+  fq6_frob(r.c0, a.c0, k);
+  fq6_frob(c1, a.c1, k);
+  Fq2 g;
+  if (k == 1)
+    fq2_set(g, FROB12_C1_1);
+  else if (k == 2)
+    fq2_set(g, FROB12_C1_2);
+  else
+    fq2_set(g, FROB12_C1_3);
+  fq2_mul(r.c1.c0, c1.c0, g);
+  fq2_mul(r.c1.c1, c1.c1, g);
+  fq2_mul(r.c1.c2, c1.c2, g);
+}
+HD bool fq12_is_one(const Fq12& a) {
+  Fq2 one;
+  fq2_one(one);
+  return fq2_eq(a.c0.c0, one) && fq2_is_zero(a.c0.c1) && fq2_is_zero(a.c0.c2) &&
+         fq2_is_zero(a.c1.c0) && fq2_is_zero(a.c1.c1) && fq2_is_zero(a.c1.c2);
+}
+
+// Granger-Scott squaring in the cyclotomic subgroup (6 Fq2 multiplications).
+// Fq12 viewed as Fq4^3: (c0.c0, c1.c1), (c1.c0, c0.c2), (c0.c1, c1.c2).
+HD void fq4_sqr(Fq2& t0, Fq2& t1, const Fq2& a, const Fq2& b) {
+  Fq2 tmp, s, u;
+  fq2_mul(tmp, a, b);
+  fq2_add(s, a, b);
+  fq2_mul_xi(u, b);
+  fq2_add(u, u, a);
+  fq2_mul(s, s, u);
+  fq2_sub(s, s, tmp);
+  fq2_mul_xi(u, tmp);
+  fq2_sub(t0, s, u);  // a^2 + xi b^2
+  fq2_dbl(t1, tmp);   // 2ab
+}
+HD void fq12_cyclotomic_sqr(Fq12& r, const Fq12& a) {
+  Fq2 t0, t1, t2, t3, t4, t5, tmp;
+  fq4_sqr(t0, t1, a.c0.c0, a.c1.c1);
+  fq4_sqr(t2, t3, a.c1.c0, a.c0.c2);
+  fq4_sqr(t4, t5, a.c0.c1, a.c1.c2);
+  Fq12 o;
+  // z0 = 3 t0 - 2 z0
+  fq2_sub(tmp, t0, a.c0.c0);
+  fq2_dbl(tmp, tmp);
+  fq2_add(o.c0.c0, tmp, t0);
+  // z1 = 3 t1 + 2 z1
+  fq2_add(tmp, t1, a.c1.c1);
+  fq2_dbl(tmp, tmp);
+  fq2_add(o.c1.c1, tmp, t1);
+  // z2 = 3 xi t5 + 2 z2
+  Fq2 x5;
+  fq2_mul_xi(x5, t5);
+  fq2_add(tmp, x5, a.c1.c0);
+  fq2_dbl(tmp, tmp);
+  fq2_add(o.c1.c0, tmp, x5);
+  // z3 = 3 t4 - 2 z3
+  fq2_sub(tmp, t4, a.c0.c2);
+  fq2_dbl(tmp, tmp);
+  fq2_add(o.c0.c2, tmp, t4);
+  // z4 = 3 t2 - 2 z4
+  fq2_sub(tmp, t2, a.c0.c1);
+  fq2_dbl(tmp, tmp);
+  fq2_add(o.c0.c1, tmp, t2);
+  // z5 = 3 t3 + 2 z5
+  fq2_add(tmp, t3, a.c1.c2);
+  fq2_dbl(tmp, tmp);
+  fq2_add(o.c1.c2, tmp, t3);
+  r = o;
+}
+
+}  // namespace hbtc

@@ -1,0 +1,247 @@
+// Optimal-ate pairing on BLS12-381 for *pairing-equality checks* with fixed G2 arguments.
+//
+// Replaces Bls12::pairing / miller_loop / final_exponentiation of pairing 0.14.2
+// (src/bls12_381/mod.rs, external crate) as used by threshold_crypto's verifiers
+// (SURVEY.md §8a A1/A2/A5/A7 and A15).  hbbft only ever compares two pairings for equality
+// (e(a, b) == e(c, d)), so the kernels evaluate  e(a, b) * e(-c, d) == 1  as ONE product of
+// Miller loops and ONE final exponentiation — the decision is identical.
+//
+// Fixed-argument structure (the MI355X-first lever): in every hot-path check the G2
+// arguments are per-instance constants (H = hash_g2(nonce) for a coin; H and w for a
+// ciphertext), shared by up to N shares.  Their Miller-loop line functions are computed
+// ONCE per instance (g2_precompute_lines, affine-normalised by one batched inversion) and
+// every share only evaluates 68 precomputed lines at its G1 point:
+//     line_j(P) = (A_j) + (B_j * xP) v + (yP) v w        (Fq12 = Fq6[w]/(w^2 - v))
+// which equals the affine line (lambda x_T - y_T) - lambda xP w^2 + yP w^3 scaled by
+// w^3 (a subfield element removed by the final exponentiation).
+#pragma once
+#include "curve.h"
+
+namespace hbtc {
+
+// |x| = 0xd201000000010000: 63 doubling steps (bits 62..0) and 5 addition steps.
+constexpr int MILLER_STEPS = 68;
+
+struct Line {
+  Fq2 a, b;  // affine-normalised: l00 = a, l01 = b * xP, l11 = yP
+};
+
+// Evaluate the line at P = (xP, yP) and multiply into f.
+HD void fq12_mul_line_at(Fq12& f, const Line& l, const Fq& xP, const Fq& yP) {
+  Fq2 l01, l11;
+  fq2_mul_fq(l01, l.b, xP);
+  l11.c0 = yP;
+  fq_zero(l11.c1);
+  fq12_mul_by_line(f, l.a, l01, l11);
+}
+
+// Unnormalised projective line for the doubling step at T (Jacobian) and T <- 2T.
+//   A = 3X^3 - 2Y^2,  B = -3X^2 Z^2,  C = 2 Y Z^3   (line ~ (A, B, C) ~ (A/C, B/C, 1))
+HD void g2_dbl_step(G2J& T, Fq2& A, Fq2& B, Fq2& C) {
+  Fq2 x2, z2, t, y2;
+  fq2_sqr(x2, T.x);
+  fq2_sqr(z2, T.z);
+  fq2_sqr(y2, T.y);
+  // A = 3 X^3 - 2 Y^2
+  fq2_mul(t, x2, T.x);
+  fq2_dbl(A, t);
+  fq2_add(A, A, t);
+  fq2_dbl(t, y2);
+  fq2_sub(A, A, t);
+  // B = -3 X^2 Z^2
+  fq2_mul(t, x2, z2);
+  fq2_dbl(B, t);
+  fq2_add(B, B, t);
+  fq2_neg(B, B);
+  // C = 2 Y Z^3
+  fq2_mul(t, T.y, T.z);
+  fq2_mul(t, t, z2);
+  fq2_dbl(C, t);
+  jac_dbl(T, T);
+}
+
+// Addition step T <- T + Q (Q affine):  r = yQ Z^3 - Y, H = xQ Z^2 - X,
+//   A = r xQ - yQ Z H,  B = -r,  C = Z H
+HD void g2_add_step(G2J& T, const G2A& Q, Fq2& A, Fq2& B, Fq2& C) {
+  Fq2 z2, z3, r, H, t;
+  fq2_sqr(z2, T.z);
+  fq2_mul(z3, z2, T.z);
+  fq2_mul(r, Q.y, z3);
+  fq2_sub(r, r, T.y);
+  fq2_mul(H, Q.x, z2);
+  fq2_sub(H, H, T.x);
+  fq2_mul(C, T.z, H);
+  fq2_mul(A, r, Q.x);
+  fq2_mul(t, Q.y, C);
+  fq2_sub(A, A, t);
+  fq2_neg(B, r);
+  jac_add_aff(T, T, Q);
+}
+
+// Precompute the 68 affine-normalised lines of a G2 point Q (not infinity): one pass of
+// projective steps, then Montgomery's batched inversion of the 68 C values.  Local arrays
+// live in private memory; this runs once per instance, not per share.
+HD void g2_precompute_lines(Line* lines, const G2A& Q) {
+  G2J T;
+  jac_from_aff(T, Q);
+  Fq2 Cs[MILLER_STEPS];
+  int j = 0;
+  for (int bit = 62; bit >= 0; --bit) {
+    g2_dbl_step(T, lines[j].a, lines[j].b, Cs[j]);
+    ++j;
+    if ((BLS_X_ABS >> bit) & 1ull) {
+      g2_add_step(T, Q, lines[j].a, lines[j].b, Cs[j]);
+      ++j;
+    }
+  }
+  Fq2 pre[MILLER_STEPS];
+  pre[0] = Cs[0];
+  for (int k = 1; k < MILLER_STEPS; ++k) fq2_mul(pre[k], pre[k - 1], Cs[k]);
+  Fq2 inv;
+  fq2_inv(inv, pre[MILLER_STEPS - 1]);
+  for (int k = MILLER_STEPS - 1; k >= 0; --k) {
+    Fq2 cinv;
+    if (k > 0) {
+      fq2_mul(cinv, inv, pre[k - 1]);
+      fq2_mul(inv, inv, Cs[k]);
+    } else {
+      cinv = inv;
+    }
+    fq2_mul(lines[k].a, lines[k].a, cinv);
+    fq2_mul(lines[k].b, lines[k].b, cinv);
+  }
+}
+
+// Miller loop product over two pairs with precomputed lines:
+//   f = f_{|x|,Q1}(P1) * f_{|x|,Q2}(P2), conjugated (x < 0).
+// P1/P2 at infinity (or a line table flagged infinite) contribute 1.
+template <class LineLoader>
+HD void miller_loop_2(Fq12& f, const LineLoader& L1, const G1A& P1, bool use1,
+                      const LineLoader& L2, const G1A& P2, bool use2) {
+  fq12_one(f);
+  int j = 0;
+  bool first = true;
+  for (int bit = 62; bit >= 0; --bit) {
+    if (!first) fq12_sqr(f, f);
+    first = false;
+    if (use1) {
+      Line l;
+      L1.load(l, j);
+      fq12_mul_line_at(f, l, P1.x, P1.y);
+    }
+    if (use2) {
+      Line l;
+      L2.load(l, j);
+      fq12_mul_line_at(f, l, P2.x, P2.y);
+    }
+    ++j;
+    if ((BLS_X_ABS >> bit) & 1ull) {
+      if (use1) {
+        Line l;
+        L1.load(l, j);
+        fq12_mul_line_at(f, l, P1.x, P1.y);
+      }
+      if (use2) {
+        Line l;
+        L2.load(l, j);
+        fq12_mul_line_at(f, l, P2.x, P2.y);
+      }
+      ++j;
+    }
+  }
+  fq12_conj(f, f);
+}
+
+// Miller loop for (P1, fixed Q1 via lines) and (P2 fixed-in-G1, Q2 variable in G2):
+//   f_{|x|,Q1}(P1) * f_{|x|,Q2}(P2) with Q2's lines computed on the fly (used for
+//   SignatureShare checks, where sigma_i varies per share and P2 = -G1).
+template <class LineLoader>
+HD void miller_loop_fixed_var(Fq12& f, const LineLoader& L1, const G1A& P1, bool use1,
+                              const G1A& P2, const G2A& Q2, bool use2) {
+  fq12_one(f);
+  G2J T;
+  jac_from_aff(T, Q2);
+  int j = 0;
+  bool first = true;
+  for (int bit = 62; bit >= 0; --bit) {
+    if (!first) fq12_sqr(f, f);
+    first = false;
+    if (use1) {
+      Line l;
+      L1.load(l, j);
+      fq12_mul_line_at(f, l, P1.x, P1.y);
+    }
+    if (use2) {
+      Fq2 A, B, C;
+      g2_dbl_step(T, A, B, C);
+      // unnormalised line: (A) + (B xP) v + (C yP) v w
+      Fq2 l01, l11;
+      fq2_mul_fq(l01, B, P2.x);
+      fq2_mul_fq(l11, C, P2.y);
+      fq12_mul_by_line(f, A, l01, l11);
+    }
+    ++j;
+    if ((BLS_X_ABS >> bit) & 1ull) {
+      if (use1) {
+        Line l;
+        L1.load(l, j);
+        fq12_mul_line_at(f, l, P1.x, P1.y);
+      }
+      if (use2) {
+        Fq2 A, B, C;
+        g2_add_step(T, Q2, A, B, C);
+        Fq2 l01, l11;
+        fq2_mul_fq(l01, B, P2.x);
+        fq2_mul_fq(l11, C, P2.y);
+        fq12_mul_by_line(f, A, l01, l11);
+      }
+      ++j;
+    }
+  }
+  fq12_conj(f, f);
+}
+
+// y^x for y in the cyclotomic subgroup (x negative: y^|x| then conjugate)
+HD void fq12_exp_by_x(Fq12& r, const Fq12& y) {
+  Fq12 acc = y;
+  for (int bit = 62; bit >= 0; --bit) {
+    fq12_cyclotomic_sqr(acc, acc);
+    if ((BLS_X_ABS >> bit) & 1ull) fq12_mul(acc, acc, y);
+  }
+  fq12_conj(r, acc);
+}
+
+// Final exponentiation.  Easy part f^((p^6-1)(p^2+1)); hard part by the x-adic chain of
+// Hayashida-Hayasaka-Teruya (eprint 2020/875), which yields the hard exponent times 3.
+// Only equality with 1 is ever tested and gcd(3, r) = 1, so the decision is exact.
+HD void final_exponentiation(Fq12& out, const Fq12& f) {
+  Fq12 t0, t1, r;
+  // easy part
+  fq12_inv(t0, f);
+  fq12_conj(t1, f);
+  fq12_mul(r, t1, t0);  // f^(p^6 - 1)
+  fq12_frob(t0, r, 2);
+  fq12_mul(r, t0, r);  // ^(p^2 + 1)
+  // hard part
+  Fq12 y0, y1, y2;
+  fq12_cyclotomic_sqr(y0, r);
+  fq12_exp_by_x(y1, r);
+  fq12_conj(y2, r);
+  fq12_mul(y1, y1, y2);
+  fq12_exp_by_x(y2, y1);
+  fq12_conj(y1, y1);
+  fq12_mul(y1, y1, y2);
+  fq12_exp_by_x(y2, y1);
+  fq12_frob(y1, y1, 1);
+  fq12_mul(y1, y1, y2);
+  fq12_mul(r, r, y0);
+  fq12_exp_by_x(y0, y1);
+  fq12_exp_by_x(y2, y0);
+  fq12_frob(y0, y1, 2);
+  fq12_conj(y1, y1);
+  fq12_mul(y1, y1, y2);
+  fq12_mul(y1, y1, y0);
+  fq12_mul(out, r, y1);
+}
+
+}  // namespace hbtc
