@@ -1,17 +1,50 @@
-# Build recipes.  The product is hbbft_amd/libhbtc.so (gfx950 HIP + host C++, C ABI in
-# include/hbtc.h).  hosttest = the kernel arithmetic headers compiled for the host (tests).
+# Build recipes.  The product is hbbft_amd/libhbtc.so (gfx950 HIP kernels + host C++ behind the
+# C ABI of include/hbtc.h).  The kernel file is compiled once per kernel group (HBTC_PART=1..5)
+# so the groups build in parallel (`make -j8 lib`).
+#   hosttest : the kernel arithmetic headers compiled for the HOST (tests/native, test-only)
+#   oracle   : the C restatement of threshold_crypto (oracle/c, test + CPU-baseline only)
 HIPCC ?= /opt/rocm/bin/hipcc
 CLANGXX ?= /opt/rocm/lib/llvm/bin/clang++
+CC ?= gcc
 ARCH ?= gfx950
 CSRC := hbbft_amd/csrc
 HDRS := $(wildcard $(CSRC)/*.h) include/hbtc.h
+BUILD := build
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC)
+PARTS := 1 2 3 4 5
+KOBJS := $(foreach p,$(PARTS),$(BUILD)/hbtc_kernels.p$(p).o)
+LIB := hbbft_amd/libhbtc.so
 
-.PHONY: all hosttest lib oracle clean
+.PHONY: all lib hosttest oracle clean resources
 all: lib hosttest oracle
+
+lib: $(LIB)
+
+$(BUILD):
+	mkdir -p $(BUILD)
+
+$(BUILD)/hbtc_kernels.p%.o: $(CSRC)/hbtc_kernels.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
+
+$(BUILD)/hbtc_api.o: $(CSRC)/hbtc_api.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(KOBJS) $(BUILD)/hbtc_api.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
+
+# per-kernel VGPR / scratch / occupancy report (one part at a time: make resources PART=2)
+PART ?= 2
+resources:
+	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$(PART) -c $(CSRC)/hbtc_kernels.hip -o /dev/null \
+	  -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs|AGPRs|Scratch|Occupancy|Spill"
 
 hosttest: tests/native/libhbtc_hosttest.so
 tests/native/libhbtc_hosttest.so: tests/native/hbtc_hosttest.cpp $(HDRS)
 	$(CLANGXX) -O2 -std=c++17 -shared -fPIC -I$(CSRC) $< -o $@
 
+oracle: oracle/c/libtcoracle.so
+oracle/c/libtcoracle.so: oracle/c/tc_oracle.c
+	$(CC) -O3 -march=native -std=c11 -shared -fPIC -pthread $< -o $@
+
 clean:
-	rm -f tests/native/*.so hbbft_amd/*.so oracle/c/*.so
+	rm -rf $(BUILD) tests/native/*.so hbbft_amd/*.so oracle/c/*.so

@@ -1,0 +1,286 @@
+"""ctypes binding of the hbtc C ABI (include/hbtc.h) — the product's only compute path.
+
+The library is ``hbbft_amd/libhbtc.so``, built in-tree by ``make lib`` (hipcc, gfx950).  If it is
+missing or fails to load, every entry point raises ``NativeUnavailable``: there is no CPU
+fallback, by design (the oracle under ``oracle/`` is test infrastructure only).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhbtc.so")
+
+# ---- status codes (include/hbtc.h) ------------------------------------------------------------
+ACCEPT = 0
+REJECT = 1
+DECODE_ERR = 2
+UNKNOWN_SENDER = 3
+INSTANCE_ERR = 4
+NOT_ENOUGH_SHARES = 5
+DUPLICATE_ENTRY = 6
+STATUS_NAMES = {ACCEPT: "ACCEPT", REJECT: "REJECT", DECODE_ERR: "DECODE_ERR",
+                UNKNOWN_SENDER: "UNKNOWN_SENDER", INSTANCE_ERR: "INSTANCE_ERR",
+                NOT_ENOUGH_SHARES: "NOT_ENOUGH_SHARES", DUPLICATE_ENTRY: "DUPLICATE_ENTRY"}
+
+
+class NativeUnavailable(RuntimeError):
+    """libhbtc.so is not built or cannot be loaded (no fallback exists)."""
+
+
+class HbtcError(RuntimeError):
+    pass
+
+
+_P = ctypes.c_void_p
+_U32 = ctypes.c_uint32
+_I32 = ctypes.c_int
+_SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); every symbol declared in include/hbtc.h
+SIGNATURES = {
+    "hbtc_device_count": (_I32, []),
+    "hbtc_version": (ctypes.c_char_p, []),
+    "hbtc_ctx_create": (_I32, [_I32, ctypes.POINTER(_P)]),
+    "hbtc_ctx_destroy": (None, [_P]),
+    "hbtc_last_error": (ctypes.c_char_p, [_P]),
+    "hbtc_keyset_load": (_I32, [_P, _P, _U32, ctypes.POINTER(_U32), ctypes.POINTER(_U32)]),
+    "hbtc_keyset_free": (_I32, [_P, _U32]),
+    "hbtc_verify_sig_shares": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P]),
+    "hbtc_verify_sigs": (_I32, [_P, _U32, _P, _P, _P, _P]),
+    "hbtc_combine_sigs": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P, _P]),
+    "hbtc_verify_dec_shares": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P, _P]),
+    "hbtc_combine_dec": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P]),
+    "hbtc_verify_ciphertexts": (_I32, [_P, _U32, _P, _P, _P, _P]),
+    "hbtc_g1_mul": (_I32, [_P, _U32, _P, _U32, _P, _P, _P]),
+    "hbtc_g2_mul": (_I32, [_P, _U32, _P, _U32, _P, _P, _P]),
+    "hbtc_dev_alloc": (_I32, [_P, _SZ, ctypes.POINTER(_P)]),
+    "hbtc_dev_free": (_I32, [_P, _P]),
+    "hbtc_dev_upload": (_I32, [_P, _P, _P, _SZ]),
+    "hbtc_dev_download": (_I32, [_P, _P, _P, _SZ]),
+    "hbtc_sync": (_I32, [_P]),
+    "hbtc_verify_dec_shares_dev": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P, _P]),
+    "hbtc_verify_sig_shares_dev": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P]),
+    "hbtc_combine_dec_dev": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P]),
+    "hbtc_combine_sigs_dev": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P, _P]),
+    "hbtc_timing_enable": (_I32, [_P, _I32]),
+    "hbtc_timing_read": (_I32, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(ctypes.c_uint64)]),
+    "hbtc_timing_reset": (_I32, [_P]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libhbtc.so once; raise NativeUnavailable when it is absent or broken."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeUnavailable("%s is not built: run `make -j8 lib` (hipcc --offload-arch=gfx950)"
+                                % LIB_PATH)
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:
+        raise NativeUnavailable("cannot load %s: %s" % (LIB_PATH, e))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def device_count():
+    return load().hbtc_device_count()
+
+
+def _u8(buf, item_bytes=None):
+    a = np.frombuffer(bytes(buf), dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else \
+        np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+    if item_bytes is not None and a.size % item_bytes:
+        raise ValueError("buffer length %d is not a multiple of %d" % (a.size, item_bytes))
+    return np.ascontiguousarray(a)
+
+
+def _join(items, size):
+    """list of byte strings (or one packed buffer) -> contiguous uint8 array."""
+    if isinstance(items, (list, tuple)):
+        for it in items:
+            if len(it) != size:
+                raise ValueError("expected %d-byte items" % size)
+        return np.frombuffer(b"".join(bytes(i) for i in items), dtype=np.uint8).copy() \
+            if items else np.zeros(0, np.uint8)
+    return _u8(items, size)
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None and a.size else ctypes.c_void_p(0)
+
+
+def _offsets(counts_or_offsets, is_offsets):
+    if is_offsets:
+        off = np.ascontiguousarray(counts_or_offsets, dtype=np.uint32)
+    else:
+        c = np.asarray(counts_or_offsets, dtype=np.uint64).reshape(-1)
+        off = np.zeros(c.size + 1, dtype=np.uint32)
+        off[1:] = np.cumsum(c)
+    return off
+
+
+class Context:
+    """One hbtc context (one GPU).  Methods take host data (bytes / numpy) and return numpy."""
+
+    def __init__(self, device=0):
+        self.lib = load()
+        h = ctypes.c_void_p()
+        rc = self.lib.hbtc_ctx_create(int(device), ctypes.byref(h))
+        if rc != 0:
+            raise HbtcError("hbtc_ctx_create(device=%d) failed: %d" % (device, rc))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.hbtc_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.lib.hbtc_last_error(self.h)
+            raise HbtcError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+    # ---- key sets
+    def keyset_load(self, pk_shares):
+        pk = _join(pk_shares, 48)
+        n = pk.size // 48
+        kid, bad = _U32(), _U32()
+        self._check(self.lib.hbtc_keyset_load(self.h, _ptr(pk), n, ctypes.byref(kid),
+                                              ctypes.byref(bad)), "hbtc_keyset_load")
+        return kid.value, bad.value
+
+    def keyset_free(self, kid):
+        self._check(self.lib.hbtc_keyset_free(self.h, kid), "hbtc_keyset_free")
+
+    # ---- verification
+    def verify_sig_shares(self, keyset, H, counts, idx, sigs, offsets=None):
+        off = _offsets(offsets if offsets is not None else counts, offsets is not None)
+        n_inst = off.size - 1
+        Hb, sb = _join(H, 96), _join(sigs, 96)
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        st = np.empty(int(off[-1]), dtype=np.int32)
+        self._check(self.lib.hbtc_verify_sig_shares(self.h, keyset, n_inst, _ptr(Hb), _ptr(off),
+                                                    _ptr(ix), _ptr(sb), _ptr(st)),
+                    "hbtc_verify_sig_shares")
+        return st
+
+    def verify_dec_shares(self, keyset, H, w, counts, idx, shares, offsets=None):
+        off = _offsets(offsets if offsets is not None else counts, offsets is not None)
+        n_ct = off.size - 1
+        Hb, wb, sb = _join(H, 96), _join(w, 96), _join(shares, 48)
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        st = np.empty(int(off[-1]), dtype=np.int32)
+        self._check(self.lib.hbtc_verify_dec_shares(self.h, keyset, n_ct, _ptr(Hb), _ptr(wb),
+                                                    _ptr(off), _ptr(ix), _ptr(sb), _ptr(st)),
+                    "hbtc_verify_dec_shares")
+        return st
+
+    def verify_sigs(self, pks, H, sigs):
+        pk, Hb, sb = _join(pks, 48), _join(H, 96), _join(sigs, 96)
+        n = pk.size // 48
+        st = np.empty(n, dtype=np.int32)
+        self._check(self.lib.hbtc_verify_sigs(self.h, n, _ptr(pk), _ptr(Hb), _ptr(sb), _ptr(st)),
+                    "hbtc_verify_sigs")
+        return st
+
+    def verify_ciphertexts(self, us, H, ws):
+        u, Hb, wb = _join(us, 48), _join(H, 96), _join(ws, 96)
+        n = u.size // 48
+        st = np.empty(n, dtype=np.int32)
+        self._check(self.lib.hbtc_verify_ciphertexts(self.h, n, _ptr(u), _ptr(Hb), _ptr(wb),
+                                                     _ptr(st)), "hbtc_verify_ciphertexts")
+        return st
+
+    # ---- combines
+    def combine_sigs(self, counts, idx, sigs, t, offsets=None):
+        off = _offsets(offsets if offsets is not None else counts, offsets is not None)
+        n = off.size - 1
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        sb = _join(sigs, 96)
+        out = np.zeros(96 * n, np.uint8)
+        par = np.zeros(n, np.uint8)
+        st = np.empty(n, np.int32)
+        self._check(self.lib.hbtc_combine_sigs(self.h, n, _ptr(off), _ptr(ix), _ptr(sb), t,
+                                               _ptr(out), _ptr(par), _ptr(st)), "hbtc_combine_sigs")
+        return [bytes(out[96 * k:96 * k + 96]) for k in range(n)], par, st
+
+    def combine_dec(self, counts, idx, shares, t, offsets=None):
+        off = _offsets(offsets if offsets is not None else counts, offsets is not None)
+        n = off.size - 1
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        sb = _join(shares, 48)
+        out = np.zeros(48 * n, np.uint8)
+        st = np.empty(n, np.int32)
+        self._check(self.lib.hbtc_combine_dec(self.h, n, _ptr(off), _ptr(ix), _ptr(sb), t,
+                                              _ptr(out), _ptr(st)), "hbtc_combine_dec")
+        return [bytes(out[48 * k:48 * k + 48]) for k in range(n)], st
+
+    # ---- scalar multiplication
+    def _mul(self, fn, size, bases, scalars):
+        sc = np.frombuffer(b"".join(int(k).to_bytes(32, "little") for k in scalars),
+                           dtype=np.uint8).copy() if not isinstance(scalars, np.ndarray) else \
+            np.ascontiguousarray(scalars, dtype=np.uint8).reshape(-1)
+        n = sc.size // 32
+        if isinstance(bases, (bytes, bytearray)) and len(bases) == size:
+            b, stride = np.frombuffer(bytes(bases), dtype=np.uint8).copy(), 0
+        else:
+            b, stride = _join(bases, size), 1
+        out = np.zeros(size * n, np.uint8)
+        st = np.empty(n, np.int32)
+        self._check(fn(self.h, n, _ptr(b), stride, _ptr(sc), _ptr(out), _ptr(st)), "point mul")
+        return out, st
+
+    def g1_mul(self, bases, scalars):
+        """k_i * P_i (bases: one 48-byte point shared by all, or a list); returns (uint8[n*48], status)."""
+        return self._mul(self.lib.hbtc_g1_mul, 48, bases, scalars)
+
+    def g2_mul(self, bases, scalars):
+        return self._mul(self.lib.hbtc_g2_mul, 96, bases, scalars)
+
+    # ---- device memory (benchmarks)
+    def dev_alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        self._check(self.lib.hbtc_dev_alloc(self.h, nbytes, ctypes.byref(p)), "hbtc_dev_alloc")
+        return p
+
+    def dev_free(self, p):
+        self._check(self.lib.hbtc_dev_free(self.h, p), "hbtc_dev_free")
+
+    def dev_upload(self, p, arr):
+        a = np.ascontiguousarray(arr)
+        self._check(self.lib.hbtc_dev_upload(self.h, p, _ptr(a), a.nbytes), "hbtc_dev_upload")
+
+    def dev_download(self, arr, p):
+        self._check(self.lib.hbtc_dev_download(self.h, _ptr(arr), p, arr.nbytes), "hbtc_dev_download")
+
+    def sync(self):
+        self._check(self.lib.hbtc_sync(self.h), "hbtc_sync")
+
+    def timing_enable(self, on=True):
+        self._check(self.lib.hbtc_timing_enable(self.h, 1 if on else 0), "hbtc_timing_enable")
+
+    def timing_reset(self):
+        self._check(self.lib.hbtc_timing_reset(self.h), "hbtc_timing_reset")
+
+    def timing_read(self, family):
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        self._check(self.lib.hbtc_timing_read(self.h, family.encode(), ctypes.byref(ms),
+                                              ctypes.byref(n)), "hbtc_timing_read")
+        return ms.value, n.value

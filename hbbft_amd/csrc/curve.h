@@ -233,7 +233,7 @@ HD void aff_neg(Aff<F>& r, const Aff<F>& p) {
 }
 
 template <class F>
-HD void jac_to_aff(Aff<F>& r, const Jac<F>& p) {
+HDN void jac_to_aff(Aff<F>& r, const Jac<F>& p) {
   if (jac_is_inf(p)) {
     fzero(r.x);
     fzero(r.y);
@@ -251,7 +251,7 @@ HD void jac_to_aff(Aff<F>& r, const Jac<F>& p) {
 
 // [k] q for a 64-bit k (MSB-first double-and-add, q affine)
 template <class F>
-HD void jac_mul_u64(Jac<F>& r, const Aff<F>& q, uint64_t k) {
+HDN void jac_mul_u64(Jac<F>& r, const Aff<F>& q, uint64_t k) {
   Jac<F> acc;
   jac_set_inf(acc);
   for (int b = 63; b >= 0; --b) {
@@ -263,7 +263,7 @@ HD void jac_mul_u64(Jac<F>& r, const Aff<F>& q, uint64_t k) {
 
 // [k] q for a Jacobian base and 64-bit k
 template <class F>
-HD void jac_mul_u64_jac(Jac<F>& r, const Jac<F>& q, uint64_t k) {
+HDN void jac_mul_u64_jac(Jac<F>& r, const Jac<F>& q, uint64_t k) {
   Jac<F> acc;
   jac_set_inf(acc);
   for (int b = 63; b >= 0; --b) {
@@ -273,20 +273,34 @@ HD void jac_mul_u64_jac(Jac<F>& r, const Jac<F>& q, uint64_t k) {
   r = acc;
 }
 
-// [k] q for a canonical (non-Montgomery) 8-limb scalar (MSB-first double-and-add)
-template <class F>
-HD void jac_mul_fr(Jac<F>& r, const Aff<F>& q, const Fr& k) {
+// [k] q for an NW-limb little-endian integer scalar (MSB-first double-and-add).  The limbs
+// are rotated through registers (static indexing only) so the device build never puts the
+// scalar in scratch memory.
+template <class F, int NW>
+HDN void jac_mul_limbs(Jac<F>& r, const Aff<F>& q, const Limbs<NW>& k) {
   Jac<F> acc;
   jac_set_inf(acc);
   if (q.inf) {
     r = acc;
     return;
   }
-  for (int b = 255; b >= 0; --b) {
-    jac_dbl(acc, acc);
-    if ((k.v[b >> 5] >> (b & 31)) & 1u) jac_add_aff(acc, acc, q);
+  Limbs<NW> kk = k;
+  for (int w = 0; w < NW; ++w) {
+    const uint32_t word = kk.v[NW - 1];
+#pragma unroll
+    for (int j = NW - 1; j > 0; --j) kk.v[j] = kk.v[j - 1];
+    for (int b = 31; b >= 0; --b) {
+      jac_dbl(acc, acc);
+      if ((word >> b) & 1u) jac_add_aff(acc, acc, q);
+    }
   }
   r = acc;
+}
+
+// [k] q for a canonical (non-Montgomery) 8-limb scalar
+template <class F>
+HD void jac_mul_fr(Jac<F>& r, const Aff<F>& q, const Fr& k) {
+  jac_mul_limbs<F, 8>(r, q, k);
 }
 
 // Is the Jacobian point p equal to the affine point (ax, ay)?  (p not infinity)
@@ -319,7 +333,7 @@ HD bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
 }
 
 // ---------------------------------------------------------------- subgroup tests
-HD bool g1_in_subgroup(const G1A& p) {
+HDN bool g1_in_subgroup(const G1A& p) {
   if (p.inf) return true;
   G1J t, t2;
   jac_mul_u64(t, p, BLS_X_ABS);
@@ -343,7 +357,7 @@ HD void g2_psi(Fq2& rx, Fq2& ry, const G2A& p) {
   fq2_mul(ry, c, k);
 }
 
-HD bool g2_in_subgroup(const G2A& p) {
+HDN bool g2_in_subgroup(const G2A& p) {
   if (p.inf) return true;
   G2J t;
   jac_mul_u64(t, p, BLS_X_ABS);  // [|x|] P ; [x]P = -[|x|]P
@@ -375,7 +389,7 @@ HD void fq_to_be_words(uint32_t* w, const Fq& a) {
 enum : uint32_t { FLAG_COMPRESSED = 0x80u, FLAG_INFINITY = 0x40u, FLAG_LARGEST = 0x20u };
 
 // G1Compressed::into_affine.  w = the 48 input bytes as 12 little-endian-loaded words.
-HD bool g1_decompress(G1A& out, const uint32_t* w_in) {
+HDN bool g1_decompress(G1A& out, const uint32_t* w_in) {
   uint32_t w[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) w[i] = w_in[i];
@@ -412,7 +426,7 @@ HD bool g1_decompress(G1A& out, const uint32_t* w_in) {
   return g1_in_subgroup(out);
 }
 
-HD bool g2_decompress(G2A& out, const uint32_t* w_in) {
+HDN bool g2_decompress(G2A& out, const uint32_t* w_in) {
   uint32_t w[24];
 #pragma unroll
   for (int i = 0; i < 24; ++i) w[i] = w_in[i];
@@ -452,7 +466,7 @@ HD bool g2_decompress(G2A& out, const uint32_t* w_in) {
 }
 
 // G1Compressed::from_affine -> 12 words (to be stored little-endian => BE bytes)
-HD void g1_compress(uint32_t* w, const G1A& p) {
+HDN void g1_compress(uint32_t* w, const G1A& p) {
   if (p.inf) {
 #pragma unroll
     for (int i = 0; i < 12; ++i) w[i] = 0;
@@ -467,7 +481,7 @@ HD void g1_compress(uint32_t* w, const G1A& p) {
   w[0] |= f;
 }
 
-HD void g2_compress(uint32_t* w, const G2A& p) {
+HDN void g2_compress(uint32_t* w, const G2A& p) {
   if (p.inf) {
 #pragma unroll
     for (int i = 0; i < 24; ++i) w[i] = 0;
@@ -515,5 +529,8 @@ HD uint32_t g2_parity(const G2A& p) {
   x &= 0xffu;
   return __builtin_popcount(x) & 1u;
 }
+
+HD uint32_t point_parity(const G1A&) { return 0; }
+HD uint32_t point_parity(const G2A& p) { return g2_parity(p); }
 
 }  // namespace hbtc

@@ -19,12 +19,21 @@
 #pragma once
 #include <cstdint>
 
+// HD  = always inlined (the small field/curve steps that make up the hot loop bodies).
+// HDN = kept out of line: operations executed a handful of times per item that wrap a long
+//       loop or a large body (exponentiations, decode, final-exponentiation pieces, the Miller
+//       loops themselves).  Inlining those into one kernel body produces ~10^5-instruction
+//       functions whose register allocation takes the compiler tens of minutes and whose code
+//       does not fit the instruction cache; a call boundary costs a few hundred bytes of
+//       scratch traffic per call, negligible next to the work inside.
 #if defined(__HIPCC__) || defined(__HIP__)
 #include <hip/hip_runtime.h>
 #define HD __host__ __device__ __forceinline__
+#define HDN __host__ __device__ inline __attribute__((noinline))
 #define HBTC_CONST static constexpr
 #else
 #define HD static inline
+#define HDN static inline __attribute__((noinline))
 #define HBTC_CONST static constexpr
 #endif
 
@@ -241,7 +250,7 @@ HD void fq_from_mont(Fq& r, const Fq& a) {
 }
 
 // a^e for a constant 12-limb exponent e (square-and-multiply, MSB first)
-HD void fq_pow_const(Fq& r, const Fq& a, const uint32_t* e) {
+HDN void fq_pow_const(Fq& r, const Fq& a, const uint32_t* e) {
   Fq acc;
   fq_one(acc);
   for (int w = 11; w >= 0; --w) {
@@ -277,12 +286,18 @@ HD bool fq_is_lex_largest(const Fq& a) {
 }
 
 // ============================================================================ Fr (scalars)
-HD void fr_mul(Fr& r, const Fr& a, const Fr& b) { mont_mul<8, 8>(r, a, b, FR_R, FR_NP); }
-
 HD void fr_canon(Fr& r, const Fr& a) {
   Fr t;
   uint32_t borrow = limbs_sub_const<8>(t, a, FR_R);
   limbs_select<8>(r, borrow == 0, a, t);
+}
+
+// 4r > 2^256, so Fr cannot use Fq's lazy [0, 2m) range: inputs must be canonical (< r), the
+// CIOS output is < 2r and one conditional subtraction makes it canonical again.
+HD void fr_mul(Fr& r, const Fr& a, const Fr& b) {
+  Fr t;
+  mont_mul<8, 8>(t, a, b, FR_R, FR_NP);
+  fr_canon(r, t);
 }
 
 HD void fr_add(Fr& r, const Fr& a, const Fr& b) {
@@ -313,7 +328,7 @@ HD void fr_from_mont(Fr& r, const Fr& a) {
   fr_canon(r, r);
 }
 
-HD void fr_pow_const(Fr& r, const Fr& a, const uint32_t* e) {
+HDN void fr_pow_const(Fr& r, const Fr& a, const uint32_t* e) {
   Fr acc;
   limbs_set_const<8>(acc, FR_ONE);
   for (int w = 7; w >= 0; --w) {
@@ -327,6 +342,15 @@ HD void fr_pow_const(Fr& r, const Fr& a, const uint32_t* e) {
 }
 
 HD void fr_inv(Fr& r, const Fr& a) { fr_pow_const(r, a, EXP_R_MINUS_2); }
+
+// small canonical integer -> Montgomery Fr
+HD void fr_from_u64(Fr& r, uint64_t x) {
+  Fr a;
+  limbs_zero<8>(a);
+  a.v[0] = (uint32_t)x;
+  a.v[1] = (uint32_t)(x >> 32);
+  fr_to_mont(r, a);
+}
 
 // ============================================================================ Fq2 = Fq[u]/(u^2+1)
 struct Fq2 {
@@ -410,7 +434,7 @@ HD void fq2_inv(Fq2& r, const Fq2& a) {
 
 // Square root in Fq2 via the norm: two Fq exponentiations.  Returns false if a is a
 // non-square.  Any root is fine: callers choose between y and -y by pairing 0.14's order.
-HD bool fq2_sqrt(Fq2& r, const Fq2& a) {
+HDN bool fq2_sqrt(Fq2& r, const Fq2& a) {
   Fq n, t;
   fq_sqr(n, a.c0);
   fq_sqr(t, a.c1);
@@ -594,7 +618,7 @@ HD void fq6_mul_by_1(Fq6& r, const Fq6& a, const Fq2& b1) {
   r.c1 = t0;
   r.c2 = t1;
 }
-HD void fq6_inv(Fq6& r, const Fq6& a) {
+HDN void fq6_inv(Fq6& r, const Fq6& a) {
   Fq2 t0, t1, t2, s, d;
   // t0 = c0^2 - xi c1 c2
   fq2_sqr(t0, a.c0);
@@ -655,7 +679,7 @@ HD void fq12_conj(Fq12& r, const Fq12& a) {
   r.c0 = a.c0;
   fq6_neg(r.c1, a.c1);
 }
-HD void fq12_mul(Fq12& r, const Fq12& a, const Fq12& b) {
+HDN void fq12_mul(Fq12& r, const Fq12& a, const Fq12& b) {
   Fq6 aa, bb, s, t;
   fq6_mul(aa, a.c0, b.c0);
   fq6_mul(bb, a.c1, b.c1);
@@ -694,7 +718,7 @@ HD void fq12_mul_by_line(Fq12& f, const Fq2& l00, const Fq2& l01, const Fq2& l11
   fq6_mul_v(s, t1);
   fq6_add(f.c0, t0, s);
 }
-HD void fq12_inv(Fq12& r, const Fq12& a) {
+HDN void fq12_inv(Fq12& r, const Fq12& a) {
   Fq6 t0, t1;
   fq6_sqr(t0, a.c0);
   fq6_sqr(t1, a.c1);
@@ -705,7 +729,7 @@ HD void fq12_inv(Fq12& r, const Fq12& a) {
   fq6_mul(t1, a.c1, t0);
   fq6_neg(r.c1, t1);
 }
-HD void fq12_frob(Fq12& r, const Fq12& a, int k) {
+HDN void fq12_frob(Fq12& r, const Fq12& a, int k) {
   Fq6 c1;
   fq6_frob(r.c0, a.c0, k);
   fq6_frob(c1, a.c1, k);

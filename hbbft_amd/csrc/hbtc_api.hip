@@ -1,0 +1,677 @@
+// C ABI of the batched threshold-crypto verifier (include/hbtc.h): context, resident key
+// tables, workspaces, batch shaping (tiles) and kernel timing.  Device work lives in
+// hbtc_kernels.hip.  Every entry point validates its arguments and fails loudly (negative
+// return + hbtc_last_error) — there is no CPU fallback anywhere in the product path.
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "hbtc_kernels.h"
+
+using namespace hbtc;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+struct Keyset {
+  G1A* pk = nullptr;
+  int32_t* st = nullptr;
+  uint32_t n = 0;
+};
+
+struct Span {
+  std::string family;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct hbtc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  std::map<uint32_t, Keyset> keysets;
+  uint32_t next_keyset = 1;
+  std::map<std::string, DevBuf> bufs;
+  Tile* h_tiles = nullptr;  // pinned staging for the tile table
+  size_t h_tiles_cap = 0;
+  uint32_t* h_u32 = nullptr;  // pinned staging for small host-shaped arrays (offsets)
+  size_t h_u32_cap = 0;
+  bool timing = false;
+  std::vector<Span> spans;
+  std::map<std::string, std::pair<double, uint64_t>> totals;
+};
+
+namespace {
+
+#define HB_CHECK(c, expr)                                                                   \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) {                                                                 \
+      (c)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                         \
+      return HBTC_ERR_DEVICE;                                                               \
+    }                                                                                       \
+  } while (0)
+
+#define HB_TRY(expr)            \
+  do {                          \
+    int rc_ = (expr);           \
+    if (rc_ != HBTC_OK) return rc_; \
+  } while (0)
+
+int fail(hbtc_ctx* c, int code, const std::string& msg) {
+  c->err = msg;
+  return code;
+}
+
+// Grow-only named device workspace.
+int ws(hbtc_ctx* c, const char* name, size_t bytes, void** out) {
+  DevBuf& b = c->bufs[name];
+  if (bytes == 0) bytes = 16;
+  if (b.cap < bytes) {
+    if (b.p) HB_CHECK(c, hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+    size_t want = bytes + bytes / 4;
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) return fail(c, HBTC_ERR_OOM, std::string("hipMalloc ") + name);
+    b.cap = want;
+  }
+  *out = b.p;
+  return HBTC_OK;
+}
+
+template <class T>
+int wst(hbtc_ctx* c, const char* name, size_t count, T** out) {
+  void* p;
+  HB_TRY(ws(c, name, count * sizeof(T), &p));
+  *out = static_cast<T*>(p);
+  return HBTC_OK;
+}
+
+int upload(hbtc_ctx* c, const char* name, const void* src, size_t bytes, void** out) {
+  HB_TRY(ws(c, name, bytes, out));
+  if (bytes) HB_CHECK(c, hipMemcpyAsync(*out, src, bytes, hipMemcpyHostToDevice, c->stream));
+  return HBTC_OK;
+}
+
+int download(hbtc_ctx* c, void* dst, const void* src, size_t bytes) {
+  if (bytes) HB_CHECK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+  return HBTC_OK;
+}
+
+int sync(hbtc_ctx* c) {
+  HB_CHECK(c, hipStreamSynchronize(c->stream));
+  return HBTC_OK;
+}
+
+// Record a kernel family's launch between two events on the context stream.
+template <class F>
+int timed(hbtc_ctx* c, const char* family, F&& launch) {
+  Span sp;
+  if (c->timing) {
+    HB_CHECK(c, hipEventCreate(&sp.a));
+    HB_CHECK(c, hipEventCreate(&sp.b));
+    HB_CHECK(c, hipEventRecord(sp.a, c->stream));
+  }
+  hipError_t e = launch();
+  if (e != hipSuccess) return fail(c, HBTC_ERR_DEVICE, std::string(family) + " launch: " + hipGetErrorString(e));
+  if (c->timing) {
+    HB_CHECK(c, hipEventRecord(sp.b, c->stream));
+    sp.family = family;
+    c->spans.push_back(sp);
+  }
+  return HBTC_OK;
+}
+
+int collect_spans(hbtc_ctx* c) {
+  for (Span& sp : c->spans) {
+    HB_CHECK(c, hipEventSynchronize(sp.b));
+    float ms = 0.f;
+    HB_CHECK(c, hipEventElapsedTime(&ms, sp.a, sp.b));
+    auto& t = c->totals[sp.family];
+    t.first += ms;
+    t.second += 1;
+    (void)hipEventDestroy(sp.a);
+    (void)hipEventDestroy(sp.b);
+  }
+  c->spans.clear();
+  return HBTC_OK;
+}
+
+int check_offsets(hbtc_ctx* c, uint32_t n_inst, const uint32_t* offsets, uint32_t* n_items) {
+  if (!offsets) return fail(c, HBTC_ERR_ARG, "offsets is NULL");
+  if (offsets[0] != 0) return fail(c, HBTC_ERR_ARG, "offsets[0] must be 0");
+  for (uint32_t k = 0; k < n_inst; ++k)
+    if (offsets[k + 1] < offsets[k]) return fail(c, HBTC_ERR_ARG, "offsets must be non-decreasing");
+  *n_items = offsets[n_inst];
+  return HBTC_OK;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Split every instance into tiles of <= 64 items; upload the table.  The pinned staging
+// buffer is reused, so wait for the stream first (the previous upload may still read it).
+int make_tiles(hbtc_ctx* c, uint32_t n_inst, const uint32_t* offsets, Tile** d_tiles,
+               uint32_t* n_tiles) {
+  size_t nt = 0;
+  for (uint32_t k = 0; k < n_inst; ++k)
+    nt += (offsets[k + 1] - offsets[k] + TILE_ITEMS - 1) / TILE_ITEMS;
+  HB_TRY(sync(c));
+  if (c->h_tiles_cap < nt) {
+    if (c->h_tiles) HB_CHECK(c, hipHostFree(c->h_tiles));
+    c->h_tiles = nullptr;
+    size_t want = nt + nt / 4 + 64;
+    HB_CHECK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_tiles), want * sizeof(Tile)));
+    c->h_tiles_cap = want;
+  }
+  size_t j = 0;
+  for (uint32_t k = 0; k < n_inst; ++k)
+    for (uint32_t s = offsets[k]; s < offsets[k + 1]; s += TILE_ITEMS) {
+      const uint32_t cnt = offsets[k + 1] - s < TILE_ITEMS ? offsets[k + 1] - s : TILE_ITEMS;
+      c->h_tiles[j++] = Tile{k, s, cnt, 0};
+    }
+  if (nt > 0xffffffffull) return fail(c, HBTC_ERR_ARG, "too many tiles");
+  void* p;
+  HB_TRY(upload(c, "tiles", c->h_tiles, nt * sizeof(Tile), &p));
+  *d_tiles = static_cast<Tile*>(p);
+  *n_tiles = (uint32_t)nt;
+  return HBTC_OK;
+}
+
+// Host array of n+1 offsets -> device (pinned staging, same reuse rule as the tiles).
+int upload_offsets(hbtc_ctx* c, const char* name, uint32_t n_inst, const uint32_t* offsets,
+                   uint32_t** d) {
+  HB_TRY(sync(c));
+  const size_t n = (size_t)n_inst + 1;
+  if (c->h_u32_cap < n) {
+    if (c->h_u32) HB_CHECK(c, hipHostFree(c->h_u32));
+    c->h_u32 = nullptr;
+    HB_CHECK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_u32), (n + 64) * sizeof(uint32_t)));
+    c->h_u32_cap = n + 64;
+  }
+  memcpy(c->h_u32, offsets, n * sizeof(uint32_t));
+  void* p;
+  HB_TRY(upload(c, name, c->h_u32, n * sizeof(uint32_t), &p));
+  *d = static_cast<uint32_t*>(p);
+  return HBTC_OK;
+}
+
+int get_keyset(hbtc_ctx* c, uint32_t id, Keyset** ks) {
+  auto it = c->keysets.find(id);
+  if (it == c->keysets.end()) return fail(c, HBTC_ERR_NO_KEYSET, "unknown keyset id");
+  *ks = &it->second;
+  return HBTC_OK;
+}
+
+// Decode + line tables for n per-instance G2 arguments (named workspace prefix `tag`).
+int prepare_g2(hbtc_ctx* c, const char* tag, const uint8_t* d_c96, uint32_t n, G2A** aff,
+               int32_t** st, Line** lines) {
+  std::string t(tag);
+  Fq2* wsp;
+  HB_TRY(wst(c, (t + ".aff").c_str(), n, aff));
+  HB_TRY(wst(c, (t + ".st").c_str(), n, st));
+  HB_TRY(wst(c, (t + ".lines").c_str(), (size_t)n * MILLER_STEPS, lines));
+  HB_TRY(wst(c, (t + ".ws").c_str(), (size_t)n * 2 * MILLER_STEPS, &wsp));
+  G2A* a = *aff;
+  int32_t* s = *st;
+  Line* l = *lines;
+  return timed(c, "prepare", [&] { return launch_g2_prepare(c->stream, d_c96, n, a, l, wsp, s); });
+}
+
+// ---------------------------------------------------------------- device-pointer cores
+int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t* d_H,
+                   const uint8_t* d_w, const uint32_t* offsets, const uint32_t* d_idx,
+                   const uint8_t* d_share, int32_t* d_status) {
+  Keyset* ks;
+  HB_TRY(get_keyset(c, keyset_id, &ks));
+  uint32_t n_items;
+  HB_TRY(check_offsets(c, n_ct, offsets, &n_items));
+  if (n_items == 0) return HBTC_OK;
+  if (!aligned16(d_H) || !aligned16(d_w) || !aligned16(d_share))
+    return fail(c, HBTC_ERR_ARG, "item arrays must be 16-byte aligned");
+  G2A *h_aff, *w_aff;
+  int32_t *h_st, *w_st;
+  Line *h_lines, *w_lines;
+  HB_TRY(prepare_g2(c, "H", d_H, n_ct, &h_aff, &h_st, &h_lines));
+  HB_TRY(prepare_g2(c, "W", d_w, n_ct, &w_aff, &w_st, &w_lines));
+  Tile* tiles;
+  uint32_t n_tiles;
+  HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles));
+  return timed(c, "dec_verify", [&] {
+    return launch_dec_verify(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n,
+                             h_aff, h_st, h_lines, w_aff, w_st, w_lines, d_status);
+  });
+}
+
+int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8_t* d_H,
+                   const uint32_t* offsets, const uint32_t* d_idx, const uint8_t* d_sig,
+                   int32_t* d_status) {
+  Keyset* ks;
+  HB_TRY(get_keyset(c, keyset_id, &ks));
+  uint32_t n_items;
+  HB_TRY(check_offsets(c, n_inst, offsets, &n_items));
+  if (n_items == 0) return HBTC_OK;
+  if (!aligned16(d_H) || !aligned16(d_sig))
+    return fail(c, HBTC_ERR_ARG, "item arrays must be 16-byte aligned");
+  G2A* h_aff;
+  int32_t* h_st;
+  Line* h_lines;
+  HB_TRY(prepare_g2(c, "H", d_H, n_inst, &h_aff, &h_st, &h_lines));
+  Tile* tiles;
+  uint32_t n_tiles;
+  HB_TRY(make_tiles(c, n_inst, offsets, &tiles, &n_tiles));
+  return timed(c, "sig_verify", [&] {
+    return launch_sig_verify(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->n,
+                             h_aff, h_st, h_lines, d_status);
+  });
+}
+
+int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets,
+                const uint32_t* d_idx, const uint8_t* d_pts, uint32_t t, uint8_t* d_out,
+                uint8_t* d_parity, int32_t* d_inst_status) {
+  uint32_t n_items;
+  HB_TRY(check_offsets(c, n_inst, offsets, &n_items));
+  if (n_inst == 0) return HBTC_OK;
+  if (t == 0) return fail(c, HBTC_ERR_ARG, "t must be >= 1");
+  if (!aligned16(d_pts) || !aligned16(d_out))
+    return fail(c, HBTC_ERR_ARG, "point arrays must be 16-byte aligned");
+  uint32_t* d_off;
+  HB_TRY(upload_offsets(c, "comb.offsets", n_inst, offsets, &d_off));
+  // Lagrange coefficients only for instances that have at least t items: compact them into
+  // a dense (instance, t) grid so the kernel never reads past an instance's items.
+  std::vector<uint32_t> firsts(n_inst);
+  for (uint32_t k = 0; k < n_inst; ++k)
+    firsts[k] = (offsets[k + 1] - offsets[k] >= t) ? offsets[k] : 0xffffffffu;
+  // instances lacking items get a harmless idx window: point them at a zero-filled dummy
+  std::vector<uint32_t> h_first(n_inst);
+  bool any_short = false;
+  for (uint32_t k = 0; k < n_inst; ++k) {
+    if (firsts[k] == 0xffffffffu) {
+      any_short = true;
+      h_first[k] = n_items;  // start of the dummy tail appended below
+    } else {
+      h_first[k] = firsts[k];
+    }
+  }
+  const uint32_t* idx_for_lagrange = d_idx;
+  if (any_short) {
+    // copy idx into a workspace with t zero entries appended (distinct-free dummy; the
+    // instance status is NOT_ENOUGH_SHARES regardless of what lambda becomes)
+    uint32_t* d_idx2;
+    HB_TRY(wst(c, "comb.idx2", (size_t)n_items + t, &d_idx2));
+    if (n_items)
+      HB_CHECK(c, hipMemcpyAsync(d_idx2, d_idx, (size_t)n_items * 4, hipMemcpyDeviceToDevice, c->stream));
+    HB_CHECK(c, hipMemsetAsync(d_idx2 + n_items, 0, (size_t)t * 4, c->stream));
+    idx_for_lagrange = d_idx2;
+  }
+  uint32_t* d_first;
+  {
+    HB_TRY(sync(c));
+    void* p;
+    HB_TRY(ws(c, "comb.first", (size_t)n_inst * 4, &p));
+    d_first = static_cast<uint32_t*>(p);
+    HB_CHECK(c, hipMemcpy(d_first, h_first.data(), (size_t)n_inst * 4, hipMemcpyHostToDevice));
+  }
+  Fr* d_lambda;
+  uint32_t* d_dup;
+  HB_TRY(wst(c, "comb.lambda", (size_t)n_inst * t, &d_lambda));
+  HB_TRY(wst(c, "comb.dup", n_inst, &d_dup));
+  HB_CHECK(c, hipMemsetAsync(d_dup, 0, (size_t)n_inst * 4, c->stream));
+  HB_TRY(timed(c, "lagrange", [&] {
+    return launch_lagrange(c->stream, d_first, n_inst, t, idx_for_lagrange, d_lambda, d_dup);
+  }));
+  return timed(c, "combine", [&] {
+    return launch_combine(c->stream, group, n_inst, d_off, t, d_pts, d_lambda, d_dup,
+                          d_inst_status, d_out, d_parity);
+  });
+}
+
+int point_mul_host(hbtc_ctx* c, int group, uint32_t n, const uint8_t* base,
+                   uint32_t base_stride, const uint8_t* scalars, uint8_t* out, int32_t* status) {
+  const size_t pb = group == 1 ? 48 : 96;
+  if (base_stride > 1) return fail(c, HBTC_ERR_ARG, "base_stride must be 0 or 1");
+  if (n == 0) return HBTC_OK;
+  void *d_base, *d_k, *d_out, *d_st;
+  HB_TRY(upload(c, "in0", base, pb * (base_stride ? n : 1), &d_base));
+  HB_TRY(upload(c, "in1", scalars, (size_t)32 * n, &d_k));
+  HB_TRY(ws(c, "out0", pb * n, &d_out));
+  HB_TRY(ws(c, "out1", (size_t)4 * n, &d_st));
+  HB_TRY(timed(c, "mul", [&] {
+    return launch_point_mul(c->stream, group, n, (const uint8_t*)d_base, base_stride,
+                            (const uint8_t*)d_k, (uint8_t*)d_out, (int32_t*)d_st);
+  }));
+  HB_TRY(download(c, out, d_out, pb * n));
+  HB_TRY(download(c, status, d_st, (size_t)4 * n));
+  return sync(c);
+}
+
+struct Guard {
+  hbtc_ctx* c;
+  std::lock_guard<std::mutex> lk;
+  explicit Guard(hbtc_ctx* ctx) : c(ctx), lk(ctx->mu) { (void)hipSetDevice(ctx->device); }
+};
+
+}  // namespace
+
+// ============================================================================ C ABI
+extern "C" {
+
+int hbtc_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+const char* hbtc_version(void) { return "hbtc 0.1 gfx950 (HIP, VALU 32-bit-limb Montgomery)"; }
+
+int hbtc_ctx_create(int device, hbtc_ctx** out) {
+  if (!out) return HBTC_ERR_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return HBTC_ERR_DEVICE;
+  if (hipSetDevice(device) != hipSuccess) return HBTC_ERR_DEVICE;
+  hbtc_ctx* c = new hbtc_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return HBTC_ERR_DEVICE;
+  }
+  *out = c;
+  return HBTC_OK;
+}
+
+void hbtc_ctx_destroy(hbtc_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& kv : c->bufs)
+    if (kv.second.p) (void)hipFree(kv.second.p);
+  for (auto& kv : c->keysets) {
+    (void)hipFree(kv.second.pk);
+    (void)hipFree(kv.second.st);
+  }
+  for (Span& sp : c->spans) {
+    (void)hipEventDestroy(sp.a);
+    (void)hipEventDestroy(sp.b);
+  }
+  if (c->h_tiles) (void)hipHostFree(c->h_tiles);
+  if (c->h_u32) (void)hipHostFree(c->h_u32);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* hbtc_last_error(hbtc_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int hbtc_keyset_load(hbtc_ctx* c, const uint8_t* pk_c48, uint32_t n, uint32_t* keyset_id,
+                     uint32_t* n_bad) {
+  if (!c || !pk_c48 || !keyset_id || n == 0) return HBTC_ERR_ARG;
+  Guard g(c);
+  Keyset ks;
+  ks.n = n;
+  HB_CHECK(c, hipMalloc(&ks.pk, sizeof(G1A) * n));
+  HB_CHECK(c, hipMalloc(&ks.st, sizeof(int32_t) * n));
+  void* d_in;
+  HB_TRY(upload(c, "in0", pk_c48, (size_t)48 * n, &d_in));
+  HB_TRY(timed(c, "prepare", [&] {
+    return launch_g1_decode(c->stream, (const uint8_t*)d_in, n, ks.pk, ks.st);
+  }));
+  std::vector<int32_t> st(n);
+  HB_TRY(download(c, st.data(), ks.st, sizeof(int32_t) * n));
+  HB_TRY(sync(c));
+  uint32_t bad = 0;
+  for (uint32_t i = 0; i < n; ++i) bad += st[i] != HBTC_ACCEPT;
+  if (n_bad) *n_bad = bad;
+  const uint32_t id = c->next_keyset++;
+  c->keysets[id] = ks;
+  *keyset_id = id;
+  return HBTC_OK;
+}
+
+int hbtc_keyset_free(hbtc_ctx* c, uint32_t keyset_id) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  auto it = c->keysets.find(keyset_id);
+  if (it == c->keysets.end()) return fail(c, HBTC_ERR_NO_KEYSET, "unknown keyset id");
+  HB_TRY(sync(c));
+  (void)hipFree(it->second.pk);
+  (void)hipFree(it->second.st);
+  c->keysets.erase(it);
+  return HBTC_OK;
+}
+
+int hbtc_verify_sig_shares(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8_t* H,
+                           const uint32_t* offsets, const uint32_t* idx, const uint8_t* sig,
+                           int32_t* status) {
+  if (!c || (n_inst && (!H || !offsets))) return HBTC_ERR_ARG;
+  Guard g(c);
+  uint32_t n;
+  HB_TRY(check_offsets(c, n_inst, offsets, &n));
+  if (n && (!idx || !sig || !status)) return fail(c, HBTC_ERR_ARG, "NULL item array");
+  void *d_H, *d_idx, *d_sig, *d_st;
+  HB_TRY(upload(c, "in0", H, (size_t)96 * n_inst, &d_H));
+  HB_TRY(upload(c, "in1", idx, (size_t)4 * n, &d_idx));
+  HB_TRY(upload(c, "in2", sig, (size_t)96 * n, &d_sig));
+  HB_TRY(ws(c, "out0", (size_t)4 * n, &d_st));
+  HB_TRY(sig_shares_dev(c, keyset_id, n_inst, (const uint8_t*)d_H, offsets,
+                        (const uint32_t*)d_idx, (const uint8_t*)d_sig, (int32_t*)d_st));
+  HB_TRY(download(c, status, d_st, (size_t)4 * n));
+  return sync(c);
+}
+
+int hbtc_verify_sigs(hbtc_ctx* c, uint32_t n, const uint8_t* pk, const uint8_t* H,
+                     const uint8_t* sig, int32_t* status) {
+  if (!c || (n && (!pk || !H || !sig || !status))) return HBTC_ERR_ARG;
+  Guard g(c);
+  if (n == 0) return HBTC_OK;
+  void *d_pk, *d_H, *d_sig, *d_st;
+  HB_TRY(upload(c, "in0", pk, (size_t)48 * n, &d_pk));
+  HB_TRY(upload(c, "in1", H, (size_t)96 * n, &d_H));
+  HB_TRY(upload(c, "in2", sig, (size_t)96 * n, &d_sig));
+  HB_TRY(ws(c, "out0", (size_t)4 * n, &d_st));
+  // e(pk, H) == e(G1, sig)
+  HB_TRY(timed(c, "pair_verify", [&] {
+    return launch_pair_verify(c->stream, n, (const uint8_t*)d_pk, (const uint8_t*)d_H, nullptr,
+                              (const uint8_t*)d_sig, (int32_t*)d_st);
+  }));
+  HB_TRY(download(c, status, d_st, (size_t)4 * n));
+  return sync(c);
+}
+
+int hbtc_verify_ciphertexts(hbtc_ctx* c, uint32_t n, const uint8_t* u, const uint8_t* H,
+                            const uint8_t* w, int32_t* status) {
+  if (!c || (n && (!u || !H || !w || !status))) return HBTC_ERR_ARG;
+  Guard g(c);
+  if (n == 0) return HBTC_OK;
+  void *d_u, *d_H, *d_w, *d_st;
+  HB_TRY(upload(c, "in0", u, (size_t)48 * n, &d_u));
+  HB_TRY(upload(c, "in1", H, (size_t)96 * n, &d_H));
+  HB_TRY(upload(c, "in2", w, (size_t)96 * n, &d_w));
+  HB_TRY(ws(c, "out0", (size_t)4 * n, &d_st));
+  // e(G1, w) == e(u, H)
+  HB_TRY(timed(c, "pair_verify", [&] {
+    return launch_pair_verify(c->stream, n, nullptr, (const uint8_t*)d_w, (const uint8_t*)d_u,
+                              (const uint8_t*)d_H, (int32_t*)d_st);
+  }));
+  HB_TRY(download(c, status, d_st, (size_t)4 * n));
+  return sync(c);
+}
+
+int hbtc_combine_sigs(hbtc_ctx* c, uint32_t n_inst, const uint32_t* offsets, const uint32_t* idx,
+                      const uint8_t* sig, uint32_t t, uint8_t* out_sig, uint8_t* out_parity,
+                      int32_t* inst_status) {
+  if (!c || (n_inst && (!offsets || !out_sig || !out_parity || !inst_status))) return HBTC_ERR_ARG;
+  Guard g(c);
+  if (n_inst == 0) return HBTC_OK;
+  uint32_t n;
+  HB_TRY(check_offsets(c, n_inst, offsets, &n));
+  void *d_idx, *d_sig, *d_out, *d_par, *d_st;
+  HB_TRY(upload(c, "in0", idx, (size_t)4 * n, &d_idx));
+  HB_TRY(upload(c, "in1", sig, (size_t)96 * n, &d_sig));
+  HB_TRY(ws(c, "out0", (size_t)96 * n_inst, &d_out));
+  HB_TRY(ws(c, "out1", (size_t)n_inst, &d_par));
+  HB_TRY(ws(c, "out2", (size_t)4 * n_inst, &d_st));
+  HB_TRY(combine_dev(c, 2, n_inst, offsets, (const uint32_t*)d_idx, (const uint8_t*)d_sig, t,
+                     (uint8_t*)d_out, (uint8_t*)d_par, (int32_t*)d_st));
+  HB_TRY(download(c, out_sig, d_out, (size_t)96 * n_inst));
+  HB_TRY(download(c, out_parity, d_par, (size_t)n_inst));
+  HB_TRY(download(c, inst_status, d_st, (size_t)4 * n_inst));
+  return sync(c);
+}
+
+int hbtc_verify_dec_shares(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t* H,
+                           const uint8_t* w, const uint32_t* offsets, const uint32_t* idx,
+                           const uint8_t* share, int32_t* status) {
+  if (!c || (n_ct && (!H || !w || !offsets))) return HBTC_ERR_ARG;
+  Guard g(c);
+  uint32_t n;
+  HB_TRY(check_offsets(c, n_ct, offsets, &n));
+  if (n && (!idx || !share || !status)) return fail(c, HBTC_ERR_ARG, "NULL item array");
+  void *d_H, *d_w, *d_idx, *d_sh, *d_st;
+  HB_TRY(upload(c, "in0", H, (size_t)96 * n_ct, &d_H));
+  HB_TRY(upload(c, "in1", w, (size_t)96 * n_ct, &d_w));
+  HB_TRY(upload(c, "in2", idx, (size_t)4 * n, &d_idx));
+  HB_TRY(upload(c, "in3", share, (size_t)48 * n, &d_sh));
+  HB_TRY(ws(c, "out0", (size_t)4 * n, &d_st));
+  HB_TRY(dec_shares_dev(c, keyset_id, n_ct, (const uint8_t*)d_H, (const uint8_t*)d_w, offsets,
+                        (const uint32_t*)d_idx, (const uint8_t*)d_sh, (int32_t*)d_st));
+  HB_TRY(download(c, status, d_st, (size_t)4 * n));
+  return sync(c);
+}
+
+int hbtc_combine_dec(hbtc_ctx* c, uint32_t n_ct, const uint32_t* offsets, const uint32_t* idx,
+                     const uint8_t* share, uint32_t t, uint8_t* out_g, int32_t* inst_status) {
+  if (!c || (n_ct && (!offsets || !out_g || !inst_status))) return HBTC_ERR_ARG;
+  Guard g(c);
+  if (n_ct == 0) return HBTC_OK;
+  uint32_t n;
+  HB_TRY(check_offsets(c, n_ct, offsets, &n));
+  void *d_idx, *d_sh, *d_out, *d_st;
+  HB_TRY(upload(c, "in0", idx, (size_t)4 * n, &d_idx));
+  HB_TRY(upload(c, "in1", share, (size_t)48 * n, &d_sh));
+  HB_TRY(ws(c, "out0", (size_t)48 * n_ct, &d_out));
+  HB_TRY(ws(c, "out2", (size_t)4 * n_ct, &d_st));
+  HB_TRY(combine_dev(c, 1, n_ct, offsets, (const uint32_t*)d_idx, (const uint8_t*)d_sh, t,
+                     (uint8_t*)d_out, nullptr, (int32_t*)d_st));
+  HB_TRY(download(c, out_g, d_out, (size_t)48 * n_ct));
+  HB_TRY(download(c, inst_status, d_st, (size_t)4 * n_ct));
+  return sync(c);
+}
+
+int hbtc_g1_mul(hbtc_ctx* c, uint32_t n, const uint8_t* base, uint32_t base_stride,
+                const uint8_t* scalars, uint8_t* out, int32_t* status) {
+  if (!c || (n && (!base || !scalars || !out || !status))) return HBTC_ERR_ARG;
+  Guard g(c);
+  return point_mul_host(c, 1, n, base, base_stride, scalars, out, status);
+}
+
+int hbtc_g2_mul(hbtc_ctx* c, uint32_t n, const uint8_t* base, uint32_t base_stride,
+                const uint8_t* scalars, uint8_t* out, int32_t* status) {
+  if (!c || (n && (!base || !scalars || !out || !status))) return HBTC_ERR_ARG;
+  Guard g(c);
+  return point_mul_host(c, 2, n, base, base_stride, scalars, out, status);
+}
+
+// ---- device-resident variants
+int hbtc_dev_alloc(hbtc_ctx* c, size_t bytes, void** d_ptr) {
+  if (!c || !d_ptr) return HBTC_ERR_ARG;
+  Guard g(c);
+  HB_CHECK(c, hipMalloc(d_ptr, bytes ? bytes : 16));
+  return HBTC_OK;
+}
+
+int hbtc_dev_free(hbtc_ctx* c, void* d_ptr) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  HB_TRY(sync(c));
+  HB_CHECK(c, hipFree(d_ptr));
+  return HBTC_OK;
+}
+
+int hbtc_dev_upload(hbtc_ctx* c, void* d_dst, const void* h_src, size_t bytes) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  HB_CHECK(c, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, c->stream));
+  return sync(c);
+}
+
+int hbtc_dev_download(hbtc_ctx* c, void* h_dst, const void* d_src, size_t bytes) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  HB_CHECK(c, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, c->stream));
+  return sync(c);
+}
+
+int hbtc_sync(hbtc_ctx* c) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  return sync(c);
+}
+
+int hbtc_verify_dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct,
+                               const uint8_t* d_H, const uint8_t* d_w, const uint32_t* offsets,
+                               const uint32_t* d_idx, const uint8_t* d_share, int32_t* d_status) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  return dec_shares_dev(c, keyset_id, n_ct, d_H, d_w, offsets, d_idx, d_share, d_status);
+}
+
+int hbtc_verify_sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst,
+                               const uint8_t* d_H, const uint32_t* offsets,
+                               const uint32_t* d_idx, const uint8_t* d_sig, int32_t* d_status) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  return sig_shares_dev(c, keyset_id, n_inst, d_H, offsets, d_idx, d_sig, d_status);
+}
+
+int hbtc_combine_dec_dev(hbtc_ctx* c, uint32_t n_ct, const uint32_t* offsets,
+                         const uint32_t* d_idx, const uint8_t* d_share, uint32_t t,
+                         uint8_t* d_out_g, int32_t* d_inst_status) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  return combine_dev(c, 1, n_ct, offsets, d_idx, d_share, t, d_out_g, nullptr, d_inst_status);
+}
+
+int hbtc_combine_sigs_dev(hbtc_ctx* c, uint32_t n_inst, const uint32_t* offsets,
+                          const uint32_t* d_idx, const uint8_t* d_sig, uint32_t t,
+                          uint8_t* d_out_sig, uint8_t* d_out_parity, int32_t* d_inst_status) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  return combine_dev(c, 2, n_inst, offsets, d_idx, d_sig, t, d_out_sig, d_out_parity,
+                     d_inst_status);
+}
+
+int hbtc_timing_enable(hbtc_ctx* c, int enable) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  c->timing = enable != 0;
+  return HBTC_OK;
+}
+
+int hbtc_timing_read(hbtc_ctx* c, const char* family, double* total_ms, uint64_t* launches) {
+  if (!c || !family) return HBTC_ERR_ARG;
+  Guard g(c);
+  HB_TRY(collect_spans(c));
+  auto it = c->totals.find(family);
+  if (total_ms) *total_ms = it == c->totals.end() ? 0.0 : it->second.first;
+  if (launches) *launches = it == c->totals.end() ? 0 : it->second.second;
+  return HBTC_OK;
+}
+
+int hbtc_timing_reset(hbtc_ctx* c) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  HB_TRY(collect_spans(c));
+  c->totals.clear();
+  return HBTC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,42 @@
+// Launch interface between the C-ABI host code (hbtc_api.hip) and the gfx950 kernels
+// (hbtc_kernels.hip).  Every launcher enqueues on `s` and returns hipGetLastError().
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "hbtc.h"
+#include "pairing.h"
+
+namespace hbtc {
+
+// Up to 64 consecutive items of ONE instance: one wave (workgroup) per tile, so the
+// instance's line tables are read with wave-uniform loads.
+struct Tile {
+  uint32_t inst, first, count, pad;
+};
+constexpr uint32_t TILE_ITEMS = 64;
+
+hipError_t launch_g1_decode(hipStream_t s, const uint8_t* in, uint32_t n, G1A* out,
+                            int32_t* status);
+hipError_t launch_g2_prepare(hipStream_t s, const uint8_t* in, uint32_t n, G2A* aff, Line* lines,
+                             Fq2* ws, int32_t* status);
+hipError_t launch_dec_verify(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                             const uint32_t* idx, const uint8_t* shares, const G1A* pk,
+                             const int32_t* pk_status, uint32_t n_pk, const G2A* h_aff,
+                             const int32_t* h_status, const Line* h_lines, const G2A* w_aff,
+                             const int32_t* w_status, const Line* w_lines, int32_t* status);
+hipError_t launch_sig_verify(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                             const uint32_t* idx, const uint8_t* sigs, const G1A* pk,
+                             const int32_t* pk_status, uint32_t n_pk, const G2A* h_aff,
+                             const int32_t* h_status, const Line* h_lines, int32_t* status);
+hipError_t launch_pair_verify(hipStream_t s, uint32_t n, const uint8_t* a1, const uint8_t* a2,
+                              const uint8_t* b1, const uint8_t* b2, int32_t* status);
+hipError_t launch_point_mul(hipStream_t s, int group, uint32_t n, const uint8_t* base,
+                            uint32_t base_stride, const uint8_t* scalars, uint8_t* out,
+                            int32_t* status);
+hipError_t launch_lagrange(hipStream_t s, const uint32_t* first, uint32_t n_inst, uint32_t t,
+                           const uint32_t* idx, Fr* lambda, uint32_t* dup);
+hipError_t launch_combine(hipStream_t s, int group, uint32_t n_inst, const uint32_t* offsets,
+                          uint32_t t, const uint8_t* pts, const Fr* lambda, const uint32_t* dup,
+                          int32_t* inst_status, uint8_t* out, uint8_t* parity);
+
+}  // namespace hbtc

@@ -1,0 +1,495 @@
+// gfx950 kernels of the batched threshold-crypto verifier (C ABI in include/hbtc.h, host side
+// in hbtc_api.hip).
+//
+// Replaces, per item, threshold_crypto's pairing checks and combines as called by hbbft
+// (SURVEY.md §8a): PublicKeyShare::verify (src/coin.rs:151), verify_decryption_share
+// (src/threshold_decryption.rs:159), PublicKey::verify (src/coin.rs:196), Ciphertext::verify
+// (src/threshold_decryption.rs:98), combine_signatures / decrypt (src/coin.rs:190,
+// src/threshold_decryption.rs:184) and the zcash point codec of their serde impls.
+//
+// Data layout in HBM:
+//   * compressed items exactly as on hbbft's wire, item-major (G1 48 B, G2 96 B), read with
+//     16-byte loads as little-endian words of the big-endian byte string (curve.h's codec
+//     works on those words directly);
+//   * decoded points G1A / G2A (canonical Montgomery limbs + infinity flag);
+//   * per-instance line tables: 68 Lines (2 Fq2 = 192 B) per fixed G2 argument.  A wave only
+//     ever verifies items of ONE instance (a Tile = up to 64 consecutive items), so every lane
+//     reads the same line: the loads are wave-uniform and go through the scalar cache into
+//     SGPRs, which the multiplies consume directly as operands.
+#include "hbtc_kernels.h"
+
+// The file is compiled once per kernel group (Makefile: -DHBTC_PART=1..5) so the groups,
+// each minutes of register allocation, build in parallel; HBTC_PART=0 builds all of them.
+#ifndef HBTC_PART
+#define HBTC_PART 0
+#endif
+#define HBTC_IN_PART(n) (HBTC_PART == 0 || HBTC_PART == (n))
+
+namespace hbtc {
+
+// ------------------------------------------------------------------------------ helpers
+__device__ __forceinline__ void load_words(uint32_t* w, const uint8_t* base, size_t item,
+                                           int nwords) {
+  const uint4* q = reinterpret_cast<const uint4*>(base + item * (size_t)(nwords * 4));
+  for (int i = 0; i < nwords / 4; ++i) {
+    const uint4 v = q[i];
+    w[4 * i] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+}
+
+__device__ __forceinline__ void store_words(uint8_t* base, size_t item, const uint32_t* w,
+                                            int nwords) {
+  uint4* q = reinterpret_cast<uint4*>(base + item * (size_t)(nwords * 4));
+  for (int i = 0; i < nwords / 4; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+struct TableLines {
+  const Line* __restrict__ l;
+  __device__ __forceinline__ void load(Line& out, int j) const { out = l[j]; }
+};
+
+__device__ __forceinline__ void neg_g1_generator(G1A& g) {
+  fq_set(g.x, G1_GEN_X);
+  Fq y;
+  fq_set(y, G1_GEN_Y);
+  fq_neg(g.y, y);
+  g.inf = 0;
+}
+
+__device__ __forceinline__ void g1_generator(G1A& g) {
+  fq_set(g.x, G1_GEN_X);
+  fq_set(g.y, G1_GEN_Y);
+  g.inf = 0;
+}
+
+HD bool pt_decompress(G1A& p, const uint32_t* w) { return g1_decompress(p, w); }
+HD bool pt_decompress(G2A& p, const uint32_t* w) { return g2_decompress(p, w); }
+HD void pt_compress(uint32_t* w, const G1A& p) { g1_compress(w, p); }
+HD void pt_compress(uint32_t* w, const G2A& p) { g2_compress(w, p); }
+
+#if HBTC_IN_PART(1)
+// ------------------------------------------------------------------------------ decode / prepare
+__global__ void __launch_bounds__(64) k_g1_decode(const uint8_t* __restrict__ in, uint32_t n,
+                                                  G1A* __restrict__ out,
+                                                  int32_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[12];
+  load_words(w, in, i, 12);
+  G1A p;
+  const bool ok = g1_decompress(p, w);
+  out[i] = p;
+  status[i] = ok ? HBTC_ACCEPT : HBTC_DECODE_ERR;
+}
+
+// Decode a fixed per-instance G2 argument (H = hash_g2(nonce), or w) and precompute its 68
+// affine-normalised Miller-loop lines (pairing.h).  One lane per instance.
+__global__ void __launch_bounds__(64) k_g2_prepare(const uint8_t* __restrict__ in, uint32_t n,
+                                                   G2A* __restrict__ aff,
+                                                   Line* __restrict__ lines,
+                                                   Fq2* __restrict__ ws,
+                                                   int32_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[24];
+  load_words(w, in, i, 24);
+  G2A q;
+  const bool ok = g2_decompress(q, w);
+  aff[i] = q;
+  status[i] = ok ? HBTC_ACCEPT : HBTC_DECODE_ERR;
+  if (ok && !q.inf) {
+    Fq2* cs = ws + (size_t)i * 2 * MILLER_STEPS;
+    g2_precompute_lines_ws(lines + (size_t)i * MILLER_STEPS, cs, cs + MILLER_STEPS, q);
+  }
+}
+
+#endif  // part 1
+
+// ------------------------------------------------------------------------------ share checks
+#if HBTC_IN_PART(2)
+// DecryptionShare: e(share_i, H_k) == e(pk_idx, w_k)  <=>  e(share_i, H_k) e(-pk_idx, w_k) == 1.
+// Both G2 arguments are per-ciphertext constants: two precomputed line tables, one Fq12
+// squaring chain, one final exponentiation per item.
+__global__ void __launch_bounds__(64) k_dec_verify(
+    const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
+    const uint8_t* __restrict__ shares, const G1A* __restrict__ pk,
+    const int32_t* __restrict__ pk_status, uint32_t n_pk, const G2A* __restrict__ h_aff,
+    const int32_t* __restrict__ h_status, const Line* __restrict__ h_lines,
+    const G2A* __restrict__ w_aff, const int32_t* __restrict__ w_status,
+    const Line* __restrict__ w_lines, int32_t* __restrict__ status) {
+  const Tile tile = tiles[blockIdx.x];
+  const uint32_t lane = threadIdx.x;
+  if (lane >= tile.count) return;
+  const size_t item = (size_t)tile.first + lane;
+  const uint32_t k = tile.inst;
+  if (h_status[k] != HBTC_ACCEPT || w_status[k] != HBTC_ACCEPT) {
+    status[item] = HBTC_INSTANCE_ERR;
+    return;
+  }
+  const uint32_t id = idx[item];
+  if (id >= n_pk) {
+    status[item] = HBTC_UNKNOWN_SENDER;
+    return;
+  }
+  if (pk_status[id] != HBTC_ACCEPT) {
+    status[item] = HBTC_DECODE_ERR;
+    return;
+  }
+  uint32_t w[12];
+  load_words(w, shares, item, 12);
+  G1A s;
+  if (!g1_decompress(s, w)) {
+    status[item] = HBTC_DECODE_ERR;
+    return;
+  }
+  G1A npk;
+  aff_neg(npk, pk[id]);
+  const bool h_inf = h_aff[k].inf != 0, w_inf = w_aff[k].inf != 0;
+  Fq12 f, e;
+  miller_loop_2(f, TableLines{h_lines + (size_t)k * MILLER_STEPS}, s, !s.inf && !h_inf,
+                TableLines{w_lines + (size_t)k * MILLER_STEPS}, npk, !npk.inf && !w_inf);
+  final_exponentiation(e, f);
+  status[item] = fq12_is_one(e) ? HBTC_ACCEPT : HBTC_REJECT;
+}
+
+#endif  // part 2
+
+#if HBTC_IN_PART(3)
+// SignatureShare: e(pk_idx, H_k) == e(G1, sig_i)  <=>  e(pk_idx, H_k) e(-G1, sig_i) == 1.
+// H_k's lines are precomputed per instance; sig_i's lines are computed on the fly.
+__global__ void __launch_bounds__(64) k_sig_verify(
+    const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
+    const uint8_t* __restrict__ sigs, const G1A* __restrict__ pk,
+    const int32_t* __restrict__ pk_status, uint32_t n_pk, const G2A* __restrict__ h_aff,
+    const int32_t* __restrict__ h_status, const Line* __restrict__ h_lines,
+    int32_t* __restrict__ status) {
+  const Tile tile = tiles[blockIdx.x];
+  const uint32_t lane = threadIdx.x;
+  if (lane >= tile.count) return;
+  const size_t item = (size_t)tile.first + lane;
+  const uint32_t k = tile.inst;
+  if (h_status[k] != HBTC_ACCEPT) {
+    status[item] = HBTC_INSTANCE_ERR;
+    return;
+  }
+  const uint32_t id = idx[item];
+  if (id >= n_pk) {
+    status[item] = HBTC_UNKNOWN_SENDER;
+    return;
+  }
+  if (pk_status[id] != HBTC_ACCEPT) {
+    status[item] = HBTC_DECODE_ERR;
+    return;
+  }
+  uint32_t w[24];
+  load_words(w, sigs, item, 24);
+  G2A sg;
+  if (!g2_decompress(sg, w)) {
+    status[item] = HBTC_DECODE_ERR;
+    return;
+  }
+  const G1A P = pk[id];
+  G1A ng;
+  neg_g1_generator(ng);
+  const bool h_inf = h_aff[k].inf != 0;
+  Fq12 f, e;
+  miller_loop_fixed_var(f, TableLines{h_lines + (size_t)k * MILLER_STEPS}, P,
+                        !P.inf && !h_inf, ng, sg, !sg.inf);
+  final_exponentiation(e, f);
+  status[item] = fq12_is_one(e) ? HBTC_ACCEPT : HBTC_REJECT;
+}
+
+#endif  // part 3
+
+#if HBTC_IN_PART(4)
+// Generic e(a1, a2) == e(b1, b2) with every argument per item; a null G1 pointer means the
+// G1 generator.  verify_sigs: (pk, H) vs (G1, sig).  verify_ciphertexts: (G1, w) vs (u, H).
+__global__ void __launch_bounds__(64) k_pair_verify(uint32_t n, const uint8_t* __restrict__ a1,
+                                                    const uint8_t* __restrict__ a2,
+                                                    const uint8_t* __restrict__ b1,
+                                                    const uint8_t* __restrict__ b2,
+                                                    int32_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[24];
+  G1A A1, B1;
+  G2A A2, B2;
+  bool ok = true;
+  if (a1) {
+    load_words(w, a1, i, 12);
+    ok &= g1_decompress(A1, w);
+  } else {
+    g1_generator(A1);
+  }
+  if (b1) {
+    load_words(w, b1, i, 12);
+    ok &= g1_decompress(B1, w);
+  } else {
+    g1_generator(B1);
+  }
+  load_words(w, a2, i, 24);
+  ok &= g2_decompress(A2, w);
+  load_words(w, b2, i, 24);
+  ok &= g2_decompress(B2, w);
+  if (!ok) {
+    status[i] = HBTC_DECODE_ERR;
+    return;
+  }
+  G1A nB1;
+  aff_neg(nB1, B1);
+  Fq12 f, e;
+  miller_loop_var_var(f, A1, A2, !A1.inf && !A2.inf, nB1, B2, !nB1.inf && !B2.inf);
+  final_exponentiation(e, f);
+  status[i] = fq12_is_one(e) ? HBTC_ACCEPT : HBTC_REJECT;
+}
+
+#endif  // part 4
+
+#if HBTC_IN_PART(1)
+// ------------------------------------------------------------------------------ scalar mult
+template <class F, int NW>
+__global__ void __launch_bounds__(64) k_point_mul(uint32_t n, const uint8_t* __restrict__ base,
+                                                  uint32_t base_stride,
+                                                  const uint8_t* __restrict__ scalars,
+                                                  uint8_t* __restrict__ out,
+                                                  int32_t* __restrict__ status) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[NW];
+  load_words(w, base, (size_t)i * base_stride, NW);
+  Aff<F> p;
+  if (!pt_decompress(p, w)) {
+    status[i] = HBTC_DECODE_ERR;
+    for (int j = 0; j < NW; ++j) w[j] = 0;
+    store_words(out, i, w, NW);
+    return;
+  }
+  Fr k;
+  load_words(k.v, scalars, i, 8);
+  Jac<F> r;
+  jac_mul_fr(r, p, k);
+  Aff<F> a;
+  jac_to_aff(a, r);
+  pt_compress(w, a);
+  store_words(out, i, w, NW);
+  status[i] = HBTC_ACCEPT;
+}
+
+template __global__ void k_point_mul<Fq, 12>(uint32_t, const uint8_t*, uint32_t, const uint8_t*,
+                                             uint8_t*, int32_t*);
+template __global__ void k_point_mul<Fq2, 24>(uint32_t, const uint8_t*, uint32_t,
+                                              const uint8_t*, uint8_t*, int32_t*);
+
+#endif  // part 1
+
+#if HBTC_IN_PART(5)
+// ------------------------------------------------------------------------------ combine
+// Lagrange coefficients at 0 of the first t abscissae x = idx + 1 of every instance:
+// lambda_i = prod_{j != i} x_j / (x_j - x_i).  One lane per (instance, i); a repeated x sets
+// the instance's duplicate flag (threshold_crypto's DuplicateEntry).
+__global__ void __launch_bounds__(256) k_lagrange(const uint32_t* __restrict__ first,
+                                                  uint32_t n_inst, uint32_t t,
+                                                  const uint32_t* __restrict__ idx,
+                                                  Fr* __restrict__ lambda,
+                                                  uint32_t* __restrict__ dup) {
+  const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (uint64_t)n_inst * t) return;
+  const uint32_t k = (uint32_t)(g / t), i = (uint32_t)(g % t);
+  const uint32_t* ix = idx + first[k];
+  const uint32_t xi_raw = ix[i];
+  Fr xi, num, den;
+  fr_from_u64(xi, (uint64_t)xi_raw + 1);
+  limbs_set_const<8>(num, FR_ONE);
+  limbs_set_const<8>(den, FR_ONE);
+  bool is_dup = false;
+  for (uint32_t j = 0; j < t; ++j) {
+    if (j == i) continue;
+    const uint32_t xj_raw = ix[j];
+    is_dup |= (xj_raw == xi_raw);
+    Fr xj, d;
+    fr_from_u64(xj, (uint64_t)xj_raw + 1);
+    fr_mul(num, num, xj);
+    fr_sub(d, xj, xi);
+    fr_mul(den, den, d);
+  }
+  if (is_dup) atomicOr(&dup[k], 1u);
+  Fr inv, l, lc;
+  fr_inv(inv, den);
+  fr_mul(l, num, inv);
+  fr_from_mont(lc, l);
+  lambda[g] = lc;
+}
+
+// sum_i lambda_i * P_i over the first t items of each instance; one workgroup per instance,
+// LDS tree reduction of Jacobian partial sums, lane 0 normalises and encodes.
+template <class F, int NW, int BS>
+__global__ void __launch_bounds__(BS) k_combine(const uint32_t* __restrict__ offsets, uint32_t t,
+                                                const uint8_t* __restrict__ pts,
+                                                const Fr* __restrict__ lambda,
+                                                const uint32_t* __restrict__ dup,
+                                                int32_t* __restrict__ inst_status,
+                                                uint8_t* __restrict__ out,
+                                                uint8_t* __restrict__ parity) {
+  __shared__ Jac<F> red[BS];
+  __shared__ uint32_t bad;
+  const uint32_t k = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) bad = 0;
+  __syncthreads();
+  const uint32_t first = offsets[k];
+  const bool enough = offsets[k + 1] - first >= t;
+  Jac<F> acc;
+  jac_set_inf(acc);
+  if (enough) {
+    for (uint32_t i = tid; i < t; i += BS) {
+      uint32_t w[NW];
+      load_words(w, pts, (size_t)first + i, NW);
+      Aff<F> p;
+      if (!pt_decompress(p, w)) {
+        atomicOr(&bad, 1u);
+        continue;
+      }
+      Jac<F> m;
+      jac_mul_fr(m, p, lambda[(size_t)k * t + i]);
+      jac_add(acc, acc, m);
+    }
+  }
+  red[tid] = acc;
+  __syncthreads();
+  for (uint32_t s = BS / 2; s > 0; s >>= 1) {
+    if (tid < s) {
+      Jac<F> a = red[tid], b = red[tid + s];
+      jac_add(a, a, b);
+      red[tid] = a;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const int32_t st = !enough ? HBTC_NOT_ENOUGH_SHARES
+                       : bad   ? HBTC_DECODE_ERR
+                       : dup[k] ? HBTC_DUPLICATE_ENTRY
+                                : HBTC_ACCEPT;
+    inst_status[k] = st;
+    Aff<F> a;
+    jac_to_aff(a, red[0]);
+    uint32_t w[NW];
+    pt_compress(w, a);
+    if (st != HBTC_ACCEPT)
+      for (int j = 0; j < NW; ++j) w[j] = 0;
+    store_words(out, k, w, NW);
+    if (parity) parity[k] = (st == HBTC_ACCEPT) ? (uint8_t)point_parity(a) : 0;
+  }
+}
+
+template __global__ void k_combine<Fq, 12, 256>(const uint32_t*, uint32_t, const uint8_t*,
+                                                const Fr*, const uint32_t*, int32_t*, uint8_t*,
+                                                uint8_t*);
+template __global__ void k_combine<Fq2, 24, 128>(const uint32_t*, uint32_t, const uint8_t*,
+                                                 const Fr*, const uint32_t*, int32_t*, uint8_t*,
+                                                 uint8_t*);
+
+#endif  // part 5
+
+// ------------------------------------------------------------------------------ launchers
+static inline uint32_t blocks_for(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
+
+#if HBTC_IN_PART(1)
+hipError_t launch_g1_decode(hipStream_t s, const uint8_t* in, uint32_t n, G1A* out,
+                            int32_t* status) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_g1_decode, dim3(blocks_for(n, 64)), dim3(64), 0, s, in, n, out, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_g2_prepare(hipStream_t s, const uint8_t* in, uint32_t n, G2A* aff, Line* lines,
+                             Fq2* ws, int32_t* status) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_g2_prepare, dim3(blocks_for(n, 64)), dim3(64), 0, s, in, n, aff, lines, ws,
+                     status);
+  return hipGetLastError();
+}
+
+#endif  // part 1
+
+#if HBTC_IN_PART(2)
+hipError_t launch_dec_verify(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                             const uint32_t* idx, const uint8_t* shares, const G1A* pk,
+                             const int32_t* pk_status, uint32_t n_pk, const G2A* h_aff,
+                             const int32_t* h_status, const Line* h_lines, const G2A* w_aff,
+                             const int32_t* w_status, const Line* w_lines, int32_t* status) {
+  if (n_tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_dec_verify, dim3(n_tiles), dim3(64), 0, s, tiles, idx, shares, pk,
+                     pk_status, n_pk, h_aff, h_status, h_lines, w_aff, w_status, w_lines, status);
+  return hipGetLastError();
+}
+
+#endif  // part 2
+
+#if HBTC_IN_PART(3)
+hipError_t launch_sig_verify(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                             const uint32_t* idx, const uint8_t* sigs, const G1A* pk,
+                             const int32_t* pk_status, uint32_t n_pk, const G2A* h_aff,
+                             const int32_t* h_status, const Line* h_lines, int32_t* status) {
+  if (n_tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sig_verify, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk,
+                     pk_status, n_pk, h_aff, h_status, h_lines, status);
+  return hipGetLastError();
+}
+
+#endif  // part 3
+
+#if HBTC_IN_PART(4)
+hipError_t launch_pair_verify(hipStream_t s, uint32_t n, const uint8_t* a1, const uint8_t* a2,
+                              const uint8_t* b1, const uint8_t* b2, int32_t* status) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pair_verify, dim3(blocks_for(n, 64)), dim3(64), 0, s, n, a1, a2, b1, b2,
+                     status);
+  return hipGetLastError();
+}
+
+#endif  // part 4
+
+#if HBTC_IN_PART(1)
+hipError_t launch_point_mul(hipStream_t s, int group, uint32_t n, const uint8_t* base,
+                            uint32_t base_stride, const uint8_t* scalars, uint8_t* out,
+                            int32_t* status) {
+  if (n == 0) return hipSuccess;
+  if (group == 1)
+    hipLaunchKernelGGL((k_point_mul<Fq, 12>), dim3(blocks_for(n, 64)), dim3(64), 0, s, n, base,
+                       base_stride, scalars, out, status);
+  else
+    hipLaunchKernelGGL((k_point_mul<Fq2, 24>), dim3(blocks_for(n, 64)), dim3(64), 0, s, n, base,
+                       base_stride, scalars, out, status);
+  return hipGetLastError();
+}
+
+#endif  // part 1
+
+#if HBTC_IN_PART(5)
+hipError_t launch_lagrange(hipStream_t s, const uint32_t* first, uint32_t n_inst, uint32_t t,
+                           const uint32_t* idx, Fr* lambda, uint32_t* dup) {
+  const uint64_t n = (uint64_t)n_inst * t;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_lagrange, dim3(blocks_for(n, 256)), dim3(256), 0, s, first, n_inst, t, idx,
+                     lambda, dup);
+  return hipGetLastError();
+}
+
+hipError_t launch_combine(hipStream_t s, int group, uint32_t n_inst, const uint32_t* offsets,
+                          uint32_t t, const uint8_t* pts, const Fr* lambda, const uint32_t* dup,
+                          int32_t* inst_status, uint8_t* out, uint8_t* parity) {
+  if (n_inst == 0) return hipSuccess;
+  if (group == 1)
+    hipLaunchKernelGGL((k_combine<Fq, 12, 256>), dim3(n_inst), dim3(256), 0, s, offsets, t, pts,
+                       lambda, dup, inst_status, out, parity);
+  else
+    hipLaunchKernelGGL((k_combine<Fq2, 24, 128>), dim3(n_inst), dim3(128), 0, s, offsets, t, pts,
+                       lambda, dup, inst_status, out, parity);
+  return hipGetLastError();
+}
+
+#endif  // part 5
+
+}  // namespace hbtc

@@ -79,12 +79,12 @@ HD void g2_add_step(G2J& T, const G2A& Q, Fq2& A, Fq2& B, Fq2& C) {
 }
 
 // Precompute the 68 affine-normalised lines of a G2 point Q (not infinity): one pass of
-// projective steps, then Montgomery's batched inversion of the 68 C values.  Local arrays
-// live in private memory; this runs once per instance, not per share.
-HD void g2_precompute_lines(Line* lines, const G2A& Q) {
+// projective steps, then Montgomery's batched inversion of the 68 C values.  `Cs` and `pre`
+// are MILLER_STEPS-entry workspaces (global memory on the device, so no per-lane private
+// arrays inflate the scratch reservation); this runs once per instance, not per share.
+HDN void g2_precompute_lines_ws(Line* lines, Fq2* Cs, Fq2* pre, const G2A& Q) {
   G2J T;
   jac_from_aff(T, Q);
-  Fq2 Cs[MILLER_STEPS];
   int j = 0;
   for (int bit = 62; bit >= 0; --bit) {
     g2_dbl_step(T, lines[j].a, lines[j].b, Cs[j]);
@@ -94,9 +94,12 @@ HD void g2_precompute_lines(Line* lines, const G2A& Q) {
       ++j;
     }
   }
-  Fq2 pre[MILLER_STEPS];
   pre[0] = Cs[0];
-  for (int k = 1; k < MILLER_STEPS; ++k) fq2_mul(pre[k], pre[k - 1], Cs[k]);
+  for (int k = 1; k < MILLER_STEPS; ++k) {
+    Fq2 t;
+    fq2_mul(t, pre[k - 1], Cs[k]);
+    pre[k] = t;
+  }
   Fq2 inv;
   fq2_inv(inv, pre[MILLER_STEPS - 1]);
   for (int k = MILLER_STEPS - 1; k >= 0; --k) {
@@ -107,16 +110,26 @@ HD void g2_precompute_lines(Line* lines, const G2A& Q) {
     } else {
       cinv = inv;
     }
-    fq2_mul(lines[k].a, lines[k].a, cinv);
-    fq2_mul(lines[k].b, lines[k].b, cinv);
+    Line l = lines[k];
+    fq2_mul(l.a, l.a, cinv);
+    fq2_mul(l.b, l.b, cinv);
+    lines[k] = l;
   }
 }
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Host convenience wrapper (tests, host hashing): workspaces on the stack.
+static inline void g2_precompute_lines(Line* lines, const G2A& Q) {
+  Fq2 Cs[MILLER_STEPS], pre[MILLER_STEPS];
+  g2_precompute_lines_ws(lines, Cs, pre, Q);
+}
+#endif
 
 // Miller loop product over two pairs with precomputed lines:
 //   f = f_{|x|,Q1}(P1) * f_{|x|,Q2}(P2), conjugated (x < 0).
 // P1/P2 at infinity (or a line table flagged infinite) contribute 1.
 template <class LineLoader>
-HD void miller_loop_2(Fq12& f, const LineLoader& L1, const G1A& P1, bool use1,
+HDN void miller_loop_2(Fq12& f, const LineLoader& L1, const G1A& P1, bool use1,
                       const LineLoader& L2, const G1A& P2, bool use2) {
   fq12_one(f);
   int j = 0;
@@ -156,7 +169,7 @@ HD void miller_loop_2(Fq12& f, const LineLoader& L1, const G1A& P1, bool use1,
 //   f_{|x|,Q1}(P1) * f_{|x|,Q2}(P2) with Q2's lines computed on the fly (used for
 //   SignatureShare checks, where sigma_i varies per share and P2 = -G1).
 template <class LineLoader>
-HD void miller_loop_fixed_var(Fq12& f, const LineLoader& L1, const G1A& P1, bool use1,
+HDN void miller_loop_fixed_var(Fq12& f, const LineLoader& L1, const G1A& P1, bool use1,
                               const G1A& P2, const G2A& Q2, bool use2) {
   fq12_one(f);
   G2J T;
@@ -201,8 +214,51 @@ HD void miller_loop_fixed_var(Fq12& f, const LineLoader& L1, const G1A& P1, bool
   fq12_conj(f, f);
 }
 
+// On-the-fly line at P from the projective step output (A, B, C): (A) + (B xP) v + (C yP) v w
+HD void fq12_mul_proj_line(Fq12& f, const Fq2& A, const Fq2& B, const Fq2& C, const G1A& P) {
+  Fq2 l01, l11;
+  fq2_mul_fq(l01, B, P.x);
+  fq2_mul_fq(l11, C, P.y);
+  fq12_mul_by_line(f, A, l01, l11);
+}
+
+// Miller loop product for two pairs whose G2 arguments both vary per item (non-threshold
+// PublicKey::verify, Ciphertext::verify): lines computed on the fly for both.
+HDN void miller_loop_var_var(Fq12& f, const G1A& P1, const G2A& Q1, bool use1, const G1A& P2,
+                            const G2A& Q2, bool use2) {
+  fq12_one(f);
+  G2J T1, T2;
+  jac_from_aff(T1, Q1);
+  jac_from_aff(T2, Q2);
+  bool first = true;
+  for (int bit = 62; bit >= 0; --bit) {
+    if (!first) fq12_sqr(f, f);
+    first = false;
+    Fq2 A, B, C;
+    if (use1) {
+      g2_dbl_step(T1, A, B, C);
+      fq12_mul_proj_line(f, A, B, C, P1);
+    }
+    if (use2) {
+      g2_dbl_step(T2, A, B, C);
+      fq12_mul_proj_line(f, A, B, C, P2);
+    }
+    if ((BLS_X_ABS >> bit) & 1ull) {
+      if (use1) {
+        g2_add_step(T1, Q1, A, B, C);
+        fq12_mul_proj_line(f, A, B, C, P1);
+      }
+      if (use2) {
+        g2_add_step(T2, Q2, A, B, C);
+        fq12_mul_proj_line(f, A, B, C, P2);
+      }
+    }
+  }
+  fq12_conj(f, f);
+}
+
 // y^x for y in the cyclotomic subgroup (x negative: y^|x| then conjugate)
-HD void fq12_exp_by_x(Fq12& r, const Fq12& y) {
+HDN void fq12_exp_by_x(Fq12& r, const Fq12& y) {
   Fq12 acc = y;
   for (int bit = 62; bit >= 0; --bit) {
     fq12_cyclotomic_sqr(acc, acc);
@@ -214,7 +270,7 @@ HD void fq12_exp_by_x(Fq12& r, const Fq12& y) {
 // Final exponentiation.  Easy part f^((p^6-1)(p^2+1)); hard part by the x-adic chain of
 // Hayashida-Hayasaka-Teruya (eprint 2020/875), which yields the hard exponent times 3.
 // Only equality with 1 is ever tested and gcd(3, r) = 1, so the decision is exact.
-HD void final_exponentiation(Fq12& out, const Fq12& f) {
+HDN void final_exponentiation(Fq12& out, const Fq12& f) {
   Fq12 t0, t1, r;
   // easy part
   fq12_inv(t0, f);

@@ -1,0 +1,164 @@
+/* hbtc — MI355X-native batched threshold-crypto verifier for hbbft's per-epoch hot path.
+ *
+ * C ABI (plain pointers and sizes; no torch / HIP types in the signatures).  Each entry point
+ * replaces calls the reference makes into the `threshold_crypto` crate (re-exported as
+ * `crypto` at /root/reference/src/lib.rs:136), batched over a whole epoch:
+ *
+ *   hbtc_verify_sig_shares   PublicKeyShare::verify(&SignatureShare, nonce)   src/coin.rs:151
+ *   hbtc_verify_sigs         PublicKey::verify(&Signature, msg)               src/coin.rs:192-197,
+ *                              src/dynamic_honey_badger/votes.rs:154, dynamic_honey_badger.rs:439
+ *   hbtc_combine_sigs        PublicKeySet::combine_signatures + Signature::parity
+ *                                                                             src/coin.rs:185-191,173
+ *   hbtc_verify_dec_shares   PublicKeyShare::verify_decryption_share          src/threshold_decryption.rs:159
+ *   hbtc_combine_dec         PublicKeySet::decrypt, the G1 interpolation      src/threshold_decryption.rs:181-185
+ *                            (plaintext = v XOR hash_bytes(g, |v|) stays with the caller)
+ *   hbtc_verify_ciphertexts  Ciphertext::verify inside SecretKeyShare::decrypt_share
+ *                                                                             src/threshold_decryption.rs:98
+ *   hbtc_keyset_load         the public_key_share(idx) table of NetworkInfo::new
+ *                                                                             src/messaging.rs:253-256
+ *   hbtc_g1_mul/hbtc_g2_mul  batched scalar multiplication (Poly::commitment src/sync_key_gen.rs:366,
+ *                            SecretKeyShare::sign src/coin.rs:142, decrypt_share src/threshold_decryption.rs:98)
+ *   hbtc_hash_g2             threshold_crypto's hash_g2 (SHA3-256 -> ChaCha -> G2::rand), the
+ *                            coin nonce hash behind src/coin.rs:142,151 (host + GPU cofactor clearing)
+ *
+ * Encodings are hbbft's wire encodings of the points (zcash compressed: G1 = 48 bytes, G2 =
+ * 96 bytes with x.c1 first; flag bits 0x80 compressed, 0x40 infinity, 0x20 lexicographically
+ * largest y).  Decoding and the r-order subgroup check run on the GPU; an encoding that
+ * pairing 0.14's `into_affine` would reject yields HBTC_DECODE_ERR for that item (the
+ * reference would have rejected the message in serde before calling the verifier).
+ *
+ * Batches are CSR-shaped: instance k (a coin instance or a ciphertext) owns items
+ * [offsets[k], offsets[k+1]) with offsets[0] == 0.  `idx` is the sender's node index
+ * (NetworkInfo::node_index, src/messaging.rs:334): it selects pk_idx from the loaded key set
+ * and gives x = idx + 1 in the Lagrange interpolation.  Item arrays are item-major
+ * (48 or 96 bytes per item, 16-byte aligned base).
+ *
+ * Threading: one context per GPU; calls on one context are serialised by an internal mutex.
+ * Host entry points block until the results are on the host; *_dev entry points take
+ * device pointers (from hbtc_dev_alloc) and are ordered on the context's HIP stream.
+ * The caller owns every buffer; nothing is retained after a call returns.
+ */
+#ifndef HBTC_H
+#define HBTC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes (< 0: API / device error) ---------------------------------------------- */
+#define HBTC_OK 0
+#define HBTC_ERR_ARG (-1)
+#define HBTC_ERR_DEVICE (-2)
+#define HBTC_ERR_NO_KEYSET (-3)
+#define HBTC_ERR_OOM (-4)
+
+/* ---- per-item / per-instance status ------------------------------------------------------- */
+#define HBTC_ACCEPT 0            /* verifies (combine: combined)                               */
+#define HBTC_REJECT 1            /* well-formed, but the pairing equation fails                */
+#define HBTC_DECODE_ERR 2        /* encoding rejected (serde would have refused the message)   */
+#define HBTC_UNKNOWN_SENDER 3    /* idx >= key-set size (public_key_share(id) == None)          */
+#define HBTC_INSTANCE_ERR 4      /* the instance's own H / w failed to decode                  */
+#define HBTC_NOT_ENOUGH_SHARES 5 /* combine: fewer than t items (crypto Error::NotEnoughShares) */
+#define HBTC_DUPLICATE_ENTRY 6   /* combine: repeated index among the first t (DuplicateEntry) */
+
+typedef struct hbtc_ctx hbtc_ctx;
+
+/* Number of visible HIP devices (0 without a GPU); does not create a context. */
+int hbtc_device_count(void);
+/* Build identification string (static storage). */
+const char* hbtc_version(void);
+
+/* Create a context on HIP device `device`. */
+int hbtc_ctx_create(int device, hbtc_ctx** out);
+void hbtc_ctx_destroy(hbtc_ctx* ctx);
+/* Description of the last error on this context (valid until the next call). */
+const char* hbtc_last_error(hbtc_ctx* ctx);
+
+/* ---- key sets ------------------------------------------------------------------------------ */
+/* Upload and decode n compressed G1 public-key shares (pk_0 .. pk_{n-1}, node-index order).
+ * *n_bad counts shares that failed to decode (their senders can never be ACCEPTed). */
+int hbtc_keyset_load(hbtc_ctx* ctx, const uint8_t* pk_shares_c48, uint32_t n,
+                     uint32_t* keyset_id, uint32_t* n_bad);
+int hbtc_keyset_free(hbtc_ctx* ctx, uint32_t keyset_id);
+
+/* ---- signature shares (Coin) ---------------------------------------------------------------- */
+/* H_k = hash_g2(nonce_k) (compressed G2, one per instance).  Item i of instance k is checked as
+ * e(pk_{idx_i}, H_k) == e(G1, sig_i).  status[i] receives an HBTC_* item status. */
+int hbtc_verify_sig_shares(hbtc_ctx* ctx, uint32_t keyset_id, uint32_t n_inst,
+                           const uint8_t* H_c96, const uint32_t* offsets, const uint32_t* idx,
+                           const uint8_t* sig_c96, int32_t* status);
+
+/* Non-threshold verify: e(pk_i, H_i) == e(G1, sig_i) for n independent items. */
+int hbtc_verify_sigs(hbtc_ctx* ctx, uint32_t n, const uint8_t* pk_c48, const uint8_t* H_c96,
+                     const uint8_t* sig_c96, int32_t* status);
+
+/* Lagrange combine of the first t items of each instance (x = idx + 1) in G2: the compressed
+ * signature, Signature::parity() (0/1) and an instance status (ACCEPT, NOT_ENOUGH_SHARES,
+ * DUPLICATE_ENTRY, DECODE_ERR). */
+int hbtc_combine_sigs(hbtc_ctx* ctx, uint32_t n_inst, const uint32_t* offsets,
+                      const uint32_t* idx, const uint8_t* sig_c96, uint32_t t,
+                      uint8_t* out_sig_c96, uint8_t* out_parity, int32_t* inst_status);
+
+/* ---- decryption shares (ThresholdDecryption / HoneyBadger) -------------------------------- */
+/* Ciphertext k = (u_k, v_k, w_k); the caller passes H_k = hash_g1_g2(u_k, v_k) and w_k.  Item i
+ * of ciphertext k is checked as e(share_i, H_k) == e(pk_{idx_i}, w_k). */
+int hbtc_verify_dec_shares(hbtc_ctx* ctx, uint32_t keyset_id, uint32_t n_ct,
+                           const uint8_t* H_c96, const uint8_t* w_c96, const uint32_t* offsets,
+                           const uint32_t* idx, const uint8_t* share_c48, int32_t* status);
+
+/* G1 Lagrange combine of the first t decryption shares of each ciphertext (compressed g). */
+int hbtc_combine_dec(hbtc_ctx* ctx, uint32_t n_ct, const uint32_t* offsets, const uint32_t* idx,
+                     const uint8_t* share_c48, uint32_t t, uint8_t* out_g_c48,
+                     int32_t* inst_status);
+
+/* Ciphertext::verify: e(G1, w_i) == e(u_i, H_i) with H_i = hash_g1_g2(u_i, v_i). */
+int hbtc_verify_ciphertexts(hbtc_ctx* ctx, uint32_t n, const uint8_t* u_c48,
+                            const uint8_t* H_c96, const uint8_t* w_c96, int32_t* status);
+
+/* ---- batched scalar multiplication -------------------------------------------------------- */
+/* out_i = k_i * P_i with 32-byte little-endian scalars (any value < 2^256).  base_stride is 1
+ * for one base per item or 0 for a single shared base.  status[i] = ACCEPT or DECODE_ERR. */
+int hbtc_g1_mul(hbtc_ctx* ctx, uint32_t n, const uint8_t* base_c48, uint32_t base_stride,
+                const uint8_t* scalars_le32, uint8_t* out_c48, int32_t* status);
+int hbtc_g2_mul(hbtc_ctx* ctx, uint32_t n, const uint8_t* base_c96, uint32_t base_stride,
+                const uint8_t* scalars_le32, uint8_t* out_c96, int32_t* status);
+
+/* ---- device-resident variants (benchmarks, pipelined callers) ----------------------------- */
+int hbtc_dev_alloc(hbtc_ctx* ctx, size_t bytes, void** d_ptr);
+int hbtc_dev_free(hbtc_ctx* ctx, void* d_ptr);
+int hbtc_dev_upload(hbtc_ctx* ctx, void* d_dst, const void* h_src, size_t bytes);
+int hbtc_dev_download(hbtc_ctx* ctx, void* h_dst, const void* d_src, size_t bytes);
+int hbtc_sync(hbtc_ctx* ctx);
+/* Same semantics as the host entry points; every d_* argument is a device pointer from
+ * hbtc_dev_alloc and `offsets` stays a HOST array (it shapes the launch).  Work is enqueued on
+ * the context's stream; call hbtc_sync before reading results. */
+int hbtc_verify_dec_shares_dev(hbtc_ctx* ctx, uint32_t keyset_id, uint32_t n_ct,
+                               const uint8_t* d_H_c96, const uint8_t* d_w_c96,
+                               const uint32_t* offsets, const uint32_t* d_idx,
+                               const uint8_t* d_share_c48, int32_t* d_status);
+int hbtc_verify_sig_shares_dev(hbtc_ctx* ctx, uint32_t keyset_id, uint32_t n_inst,
+                               const uint8_t* d_H_c96, const uint32_t* offsets,
+                               const uint32_t* d_idx, const uint8_t* d_sig_c96,
+                               int32_t* d_status);
+int hbtc_combine_dec_dev(hbtc_ctx* ctx, uint32_t n_ct, const uint32_t* offsets,
+                         const uint32_t* d_idx, const uint8_t* d_share_c48, uint32_t t,
+                         uint8_t* d_out_g_c48, int32_t* d_inst_status);
+int hbtc_combine_sigs_dev(hbtc_ctx* ctx, uint32_t n_inst, const uint32_t* offsets,
+                          const uint32_t* d_idx, const uint8_t* d_sig_c96, uint32_t t,
+                          uint8_t* d_out_sig_c96, uint8_t* d_out_parity, int32_t* d_inst_status);
+
+/* ---- kernel timing (HIP events on the context's stream) ---------------------------------- */
+/* Families: "prepare", "dec_verify", "sig_verify", "pair_verify", "lagrange", "combine",
+ * "mul".  Reading synchronises the stream. */
+int hbtc_timing_enable(hbtc_ctx* ctx, int enable);
+int hbtc_timing_read(hbtc_ctx* ctx, const char* family, double* total_ms, uint64_t* launches);
+int hbtc_timing_reset(hbtc_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HBTC_H */
