@@ -15,7 +15,7 @@ PARTS := 1 2 3 4 5
 KOBJS := $(foreach p,$(PARTS),$(BUILD)/hbtc_kernels.p$(p).o)
 LIB := hbbft_amd/libhbtc.so
 
-.PHONY: all lib hosttest oracle clean resources
+.PHONY: all lib hosttest oracle clean resources roofline-constants
 all: lib hosttest oracle
 
 lib: $(LIB)
@@ -48,3 +48,10 @@ oracle/c/libtcoracle.so: oracle/c/tc_oracle.c
 
 clean:
 	rm -rf $(BUILD) tests/native/*.so hbbft_amd/*.so oracle/c/*.so
+
+# Fqm per unit of work, measured on the kernels' own headers (host build, counting on)
+roofline-constants: bench/roofline_constants.json
+bench/roofline_constants.json: tools/fqm_count.cpp $(HDRS)
+	mkdir -p bench build
+	$(CLANGXX) -O1 -std=c++17 -DHBTC_COUNT_FQM -I$(CSRC) $< -o build/fqm_count
+	build/fqm_count > $@

@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""Benchmark: verified BLS12-381 shares/sec (whole node) at N=1000 + combines/sec.
+
+Workload (BASELINE.json configs[2], the configuration the metric is quoted on, "at N=1000"):
+one HoneyBadger epoch = 1000 ciphertexts x 1000 DecryptionShares (every share of every
+ciphertext verified: e(share_i, H_ct) == e(pk_i, w_ct), src/threshold_decryption.rs:159) plus
+the 1000 G1 Lagrange combines of t = 334 shares (PublicKeySet::decrypt, td.rs:184).
+A step = one such epoch through the HIP path; inputs (compressed shares as on the wire, per-
+ciphertext H = hash_g1_g2(u, v) and w, the node index of every share) are already resident in
+HBM when the timed region starts; decode + subgroup checks are inside it.  ~1% of shares are
+corrupted (valid points, wrong share) and a few carry invalid encodings; decisions are checked
+against the construction after timing.
+
+Multi-GPU (weak scaling): one process per GPU (torch.distributed.run), each rank verifies its
+own epoch shard of 1000 ciphertexts (shards are independent, SURVEY.md §8e: no data-path
+collective); gloo carries the barrier and the max-over-ranks time only.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with "roofline" (dominant
+kernel k_dec_verify, Fqm counted by tools/fqm_count.cpp -> bench/roofline_constants.json) and
+"cpu_baseline" (the oracle's threshold_crypto restatement timed on this host).
+"""
+import argparse
+import json
+import os
+import random
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from hbbft_amd import _native as N  # noqa: E402
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+G1_GEN = bytes.fromhex("97f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb")
+G2_GEN = bytes.fromhex("93e02b6052719f607dacd3a088274f65596bd0d09920b61ab5da61bbdc7f5049334cf11213945d57e5ac7d055d042b7e"
+                       "024aa2b2f08f0a91260805272dc51051c6e47ad4fa403b02b4510b647ae3d1770bac0326a805bbefd48056c8c121bdb8")
+SEED = 0x6862626674
+# measured v_mad_u64_u32 lane-op throughput on MI355X (tools/microbench/intmul.hip,
+# profiles/r01_intmul_microbench.txt): the VALU integer-multiply roofline of the Fqm kernels
+MAD_U64_PEAK = 29.51e12
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def scalars_bytes(vals):
+    return np.frombuffer(b"".join(int(v).to_bytes(32, "little") for v in vals), dtype=np.uint8).copy()
+
+
+class Epoch:
+    """Synthetic C3 epoch for one rank, generated on the GPU with the library's batched scalar
+    multiplication (setup, outside the timed region)."""
+
+    def __init__(self, ctx, n, n_ct, seed, corrupt_frac=0.01):
+        rng = random.Random(seed)
+        self.n, self.n_ct = n, n_ct
+        self.f = (n - 1) // 3
+        self.t = self.f + 1
+        coeffs = [rng.randrange(1, R) for _ in range(self.f + 1)]
+        self.master_sk = coeffs[0]
+        sks = []
+        for i in range(n):
+            acc = 0
+            for c in reversed(coeffs):
+                acc = (acc * (i + 1) + c) % R
+            sks.append(acc)
+        pk, st = ctx.g1_mul(G1_GEN, scalars_bytes(sks))
+        assert not st.any()
+        self.keyset, bad = ctx.keyset_load(pk)
+        assert bad == 0
+        rs = [rng.randrange(1, R) for _ in range(n_ct)]
+        hs = [rng.randrange(1, R) for _ in range(n_ct)]
+        self.rs = rs
+        H, _ = ctx.g2_mul(G2_GEN, scalars_bytes(hs))
+        w, _ = ctx.g2_mul(G2_GEN, scalars_bytes([r * h % R for r, h in zip(rs, hs)]))
+        total = n * n_ct
+        scal = [sks[i] * rs[k] % R for k in range(n_ct) for i in range(n)]
+        # corruption: wrong shares (valid points) and bad encodings, never among the first t
+        # shares of a ciphertext (those feed the combine, as verified shares would)
+        self.expected = np.zeros(total, np.int32)
+        n_bad = int(total * corrupt_frac)
+        cand = [j for j in rng.sample(range(total), min(total, 2 * n_bad + 16)) if j % n >= self.t]
+        wrong, enc = cand[:n_bad], cand[n_bad:n_bad + 8]
+        for j in wrong:
+            scal[j] = (scal[j] + 1) % R
+            self.expected[j] = N.REJECT
+        shares, st = ctx.g1_mul(G1_GEN, scalars_bytes(scal))
+        assert not st.any()
+        shares = shares.reshape(total, 48)
+        for j in enc:
+            shares[j, 0] &= 0x7F  # clear the compression flag: pairing 0.14 rejects it
+            self.expected[j] = N.DECODE_ERR
+        self.offsets = np.arange(0, total + 1, n, dtype=np.uint32)
+        idx = np.tile(np.arange(n, dtype=np.uint32), n_ct)
+        # resident device copies
+        self.d = {}
+        for name, arr in (("H", H), ("w", w), ("idx", idx), ("shares", shares.reshape(-1))):
+            p = ctx.dev_alloc(arr.nbytes)
+            ctx.dev_upload(p, arr)
+            self.d[name] = p
+        self.d["status"] = ctx.dev_alloc(4 * total)
+        self.d["g"] = ctx.dev_alloc(48 * n_ct)
+        self.d["cst"] = ctx.dev_alloc(4 * n_ct)
+        self.total = total
+        self.host_shares = shares
+
+    def step(self, ctx):
+        lib, h, d = ctx.lib, ctx.h, self.d
+        off = N._ptr(self.offsets)
+        ctx._check(lib.hbtc_verify_dec_shares_dev(h, self.keyset, self.n_ct, d["H"], d["w"], off,
+                                                  d["idx"], d["shares"], d["status"]),
+                   "verify_dec_shares_dev")
+        ctx._check(lib.hbtc_combine_dec_dev(h, self.n_ct, off, d["idx"], d["shares"], self.t,
+                                            d["g"], d["cst"]), "combine_dec_dev")
+
+    def check(self, ctx):
+        st = np.empty(self.total, np.int32)
+        ctx.dev_download(st, self.d["status"])
+        mism = int((st != self.expected).sum())
+        g = np.empty(48 * self.n_ct, np.uint8)
+        ctx.dev_download(g, self.d["g"])
+        cst = np.empty(self.n_ct, np.int32)
+        ctx.dev_download(cst, self.d["cst"])
+        want, _ = ctx.g1_mul(G1_GEN, scalars_bytes([self.master_sk * r % R for r in self.rs]))
+        comb_ok = bool((cst == 0).all() and bytes(g) == bytes(want))
+        return mism, comb_ok, int((st == N.ACCEPT).sum())
+
+
+def cpu_baseline(ep, budget_s):
+    """The oracle (threshold_crypto restatement) on a bounded sample of the same workload: per
+    share the reference's verify_decryption_share = hash_g1_g2(u, v) + two full pairings, plus
+    the serde decode (subgroup check) of the share.  C restatement when built (oracle/c), else
+    the Python restatement across a process pool."""
+    try:
+        from oracle.cbaseline import run_dec_share_baseline
+        return run_dec_share_baseline(ep, budget_s)
+    except ImportError:
+        pass
+    from oracle.pybaseline import run_dec_share_baseline
+    return run_dec_share_baseline(ep, budget_s)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=1000, help="validators N (f = (N-1)/3)")
+    ap.add_argument("--cts", type=int, default=1000, help="ciphertexts per epoch per GPU")
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    ctx = N.Context(local)
+    t0 = time.time()
+    ep = Epoch(ctx, args.n, args.cts, SEED + 7919 * rank)
+    log("rank %d: setup %.1fs (%d shares)" % (rank, time.time() - t0, ep.total))
+
+    ctx.timing_enable(True)
+    for _ in range(args.warmup):
+        ep.step(ctx)
+    ctx.sync()
+    ctx.timing_reset()
+    if dist:
+        dist.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ep.step(ctx)
+    ctx.sync()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kv_ms, kv_n = ctx.timing_read("dec_verify")
+    kc_ms, kc_n = ctx.timing_read("combine")
+    kl_ms, _ = ctx.timing_read("lagrange")
+    kp_ms, _ = ctx.timing_read("prepare")
+    mism, comb_ok, n_acc = ep.check(ctx)
+    log("rank %d: %.3fs for %d steps; dec_verify %.1f ms/launch, combine %.1f ms, lagrange %.1f ms, "
+        "prepare %.1f ms per step; mismatches %d, combine ok %s"
+        % (rank, elapsed, args.steps, kv_ms / max(kv_n, 1), kc_ms / max(kc_n, 1),
+           kl_ms / args.steps, kp_ms / args.steps, mism, comb_ok))
+    if mism or not comb_ok:
+        raise SystemExit("rank %d: results differ from the construction (%d mismatches, combine %s)"
+                         % (rank, mism, comb_ok))
+
+    shares_total = ep.total * world * args.steps
+    value = shares_total / elapsed
+    combines = args.cts * world * args.steps / elapsed
+    consts = json.load(open(os.path.join(ROOT, "bench", "roofline_constants.json")))
+    fqm_share = consts["dec_share"]["total"]
+    kv_avg_s = kv_ms / max(kv_n, 1) / 1e3
+    achieved = fqm_share * ep.total / kv_avg_s * consts["mad_u64_u32_per_fqm"] / 1e12
+    out = {
+        "metric": "verified BLS12-381 shares/sec (whole node) at N=1000; combines/sec",
+        "value": round(value, 1),
+        "unit": "shares/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 (381-bit Montgomery limbs)",
+        "data": "synthetic (seeded key set, shares generated on device; ~1% corrupted)",
+        "config": {"workload": "C3 HoneyBadger epoch: %d ciphertexts x %d DecryptionShares verified + %d G1 combines (t=%d) per GPU"
+                   % (args.cts, args.n, args.cts, ep.t),
+                   "N": args.n, "f": ep.f, "t": ep.t, "ciphertexts_per_gpu": args.cts,
+                   "shares_per_step": ep.total * world, "parallelism": "shard ciphertexts over %d GPU(s)" % world},
+        "combines_per_s": round(combines, 1),
+        "accepted_per_step_rank0": n_acc,
+        "roofline": {
+            "bound": "valu-int (v_mad_u64_u32)",
+            "kernel": "k_dec_verify",
+            "achieved": round(achieved, 3),
+            "peak": MAD_U64_PEAK / 1e12,
+            "unit": "T mad_u64_u32/s",
+            "frac": round(achieved / (MAD_U64_PEAK / 1e12), 4),
+            "traffic": None,
+            "fqm_per_share": fqm_share,
+            "kernel_ms_per_launch": round(kv_avg_s * 1e3, 3),
+            "shares_per_launch": ep.total,
+        },
+    }
+    if rank == 0 and not args.no_cpu:
+        try:
+            out["cpu_baseline"] = cpu_baseline(ep, args.cpu_budget)
+        except Exception as e:  # the baseline is reported, never the product path
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -209,7 +209,17 @@ HD void fq_neg(Fq& r, const Fq& a) {
   fq_sub(r, z, a);
 }
 
+// Host-only instrumentation (tools/fqm_count.cpp): counts Fq Montgomery multiplications so the
+// roofline's algorithmic work per item is measured on the very code the kernels run.
+#if defined(HBTC_COUNT_FQM) && !defined(__HIP_DEVICE_COMPILE__)
+extern unsigned long long hbtc_fqm_count;
+#define HBTC_COUNT_FQ_MUL() (++hbtc_fqm_count)
+#else
+#define HBTC_COUNT_FQ_MUL() ((void)0)
+#endif
+
 HD void fq_mul(Fq& r, const Fq& a, const Fq& b) {
+  HBTC_COUNT_FQ_MUL();
   mont_mul<12, HBTC_FQ_UNROLL>(r, a, b, FQ_P, FQ_NP);
 }
 HD void fq_sqr(Fq& r, const Fq& a) { fq_mul(r, a, a); }

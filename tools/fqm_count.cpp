@@ -1,0 +1,121 @@
+// Counts Fq Montgomery multiplications (Fqm) per unit of work for the exact algorithms the
+// gfx950 kernels run (same headers, host build with HBTC_COUNT_FQM).  Output: JSON on stdout,
+// frozen into bench/roofline_constants.json by `make roofline-constants`.
+//
+// Units:
+//   dec_share   one DecryptionShare check: G1 decode + subgroup test, 2-pair Miller loop with
+//               two precomputed line tables, final exponentiation        (k_dec_verify, per item)
+//   sig_share   one SignatureShare check: G2 decode + subgroup test, Miller loop with one
+//               precomputed table and one on-the-fly G2 argument, final exp (k_sig_verify)
+//   g2_prepare  per-instance G2 decode + 68-line precomputation           (k_g2_prepare)
+//   g1_combine_item  one G1 combine term: decode + 255-bit double-and-add  (k_combine<Fq>)
+#include <cstdio>
+#include <cstring>
+#include <random>
+
+#include "pairing.h"
+
+namespace hbtc {
+unsigned long long hbtc_fqm_count = 0;
+}
+
+using namespace hbtc;
+
+namespace {
+struct HL {
+  const Line* l;
+  void load(Line& o, int j) const { o = l[j]; }
+};
+
+// [k] G for a random k, compressed (host build of the same code; counting disabled around it)
+void rand_scalar(Fr& k, std::mt19937_64& g) {
+  for (int i = 0; i < 8; ++i) k.v[i] = (uint32_t)g();
+  k.v[7] &= 0x3fffffffu;
+}
+}  // namespace
+
+int main() {
+  std::mt19937_64 g(42);
+  G1A gen1;
+  fq_set(gen1.x, G1_GEN_X);
+  fq_set(gen1.y, G1_GEN_Y);
+  gen1.inf = 0;
+  G2A gen2;
+  fq2_set(gen2.x, G2_GEN_X);
+  fq2_set(gen2.y, G2_GEN_Y);
+  gen2.inf = 0;
+  Fr k;
+  rand_scalar(k, g);
+  G1J pj;
+  jac_mul_fr(pj, gen1, k);
+  G1A share;
+  jac_to_aff(share, pj);
+  uint32_t w1[12];
+  g1_compress(w1, share);
+  G2J qj;
+  jac_mul_fr(qj, gen2, k);
+  G2A sig;
+  jac_to_aff(sig, qj);
+  uint32_t w2[24];
+  g2_compress(w2, sig);
+  static Line l1[MILLER_STEPS], l2[MILLER_STEPS];
+
+  // per-instance preparation
+  hbtc_fqm_count = 0;
+  G2A H;
+  g2_decompress(H, w2);
+  g2_precompute_lines(l1, H);
+  const unsigned long long prepare = hbtc_fqm_count;
+  g2_precompute_lines(l2, gen2);
+
+  // decryption share
+  hbtc_fqm_count = 0;
+  G1A s;
+  g1_decompress(s, w1);
+  const unsigned long long dec_decode = hbtc_fqm_count;
+  G1A npk;
+  aff_neg(npk, gen1);
+  Fq12 f, e;
+  hbtc_fqm_count = 0;
+  miller_loop_2(f, HL{l1}, s, true, HL{l2}, npk, true);
+  const unsigned long long ml2 = hbtc_fqm_count;
+  hbtc_fqm_count = 0;
+  final_exponentiation(e, f);
+  const unsigned long long fe = hbtc_fqm_count;
+
+  // signature share
+  hbtc_fqm_count = 0;
+  G2A sg;
+  g2_decompress(sg, w2);
+  const unsigned long long sig_decode = hbtc_fqm_count;
+  hbtc_fqm_count = 0;
+  miller_loop_fixed_var(f, HL{l1}, gen1, true, npk, sg, true);
+  const unsigned long long mlfv = hbtc_fqm_count;
+
+  // combine term (G1): decode + 255-bit scalar mult + accumulate
+  hbtc_fqm_count = 0;
+  G1A cp;
+  g1_decompress(cp, w1);
+  G1J m, acc;
+  jac_mul_fr(m, cp, k);
+  jac_add(acc, pj, m);
+  const unsigned long long comb1 = hbtc_fqm_count;
+  hbtc_fqm_count = 0;
+  G2A cq;
+  g2_decompress(cq, w2);
+  G2J m2, acc2;
+  jac_mul_fr(m2, cq, k);
+  jac_add(acc2, qj, m2);
+  const unsigned long long comb2 = hbtc_fqm_count;
+
+  printf("{\n");
+  printf("  \"unit\": \"Fqm (12x32-bit-limb CIOS Montgomery multiplications; 288 v_mad_u64_u32 + 12 v_mul_lo_u32 each)\",\n");
+  printf("  \"mul32_per_fqm\": 300,\n  \"mad_u64_u32_per_fqm\": 288,\n");
+  printf("  \"g2_prepare\": %llu,\n", prepare);
+  printf("  \"dec_share\": {\"decode\": %llu, \"miller_loop_2\": %llu, \"final_exp\": %llu, \"total\": %llu},\n",
+         dec_decode, ml2, fe, dec_decode + ml2 + fe);
+  printf("  \"sig_share\": {\"decode\": %llu, \"miller_loop_fixed_var\": %llu, \"final_exp\": %llu, \"total\": %llu},\n",
+         sig_decode, mlfv, fe, sig_decode + mlfv + fe);
+  printf("  \"g1_combine_item\": %llu,\n  \"g2_combine_item\": %llu\n}\n", comb1, comb2);
+  return 0;
+}
