@@ -44,7 +44,7 @@ tests/native/libhbtc_hosttest.so: tests/native/hbtc_hosttest.cpp $(HDRS)
 
 oracle: oracle/c/libtcoracle.so
 oracle/c/libtcoracle.so: oracle/c/tc_oracle.c
-	$(CC) -O3 -march=native -std=c11 -shared -fPIC -pthread $< -o $@
+	$(CC) -O3 -std=gnu11 -shared -fPIC -pthread $< -o $@
 
 clean:
 	rm -rf $(BUILD) tests/native/*.so hbbft_amd/*.so oracle/c/*.so

@@ -77,6 +77,10 @@ class Epoch:
         self.rs = rs
         H, _ = ctx.g2_mul(G2_GEN, scalars_bytes(hs))
         w, _ = ctx.g2_mul(G2_GEN, scalars_bytes([r * h % R for r, h in zip(rs, hs)]))
+        u, _ = ctx.g1_mul(G1_GEN, scalars_bytes(rs))
+        self.pk_bytes = [bytes(pk[48 * i:48 * i + 48]) for i in range(n)]
+        self.u_bytes = [bytes(u[48 * k:48 * k + 48]) for k in range(n_ct)]
+        self.w_bytes = [bytes(w[96 * k:96 * k + 96]) for k in range(n_ct)]
         total = n * n_ct
         scal = [sks[i] * rs[k] % R for k in range(n_ct) for i in range(n)]
         # corruption: wrong shares (valid points) and bad encodings, never among the first t

@@ -1,0 +1,127 @@
+"""ctypes binding of the C restatement oracle/c/libtcoracle.so — TEST / BASELINE ONLY.
+
+Used by tests/ (cross-checks against the Python oracle and the golden fixtures) and by
+bench.py's cpu_baseline leg (the reference's per-call algorithm over a pthread pool on the
+host's cores).  Raises ImportError when the library is not built, so bench.py can fall back to
+the Python restatement for the baseline.
+"""
+import ctypes
+import os
+import random
+
+_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "libtcoracle.so")
+if not os.path.exists(_PATH):
+    raise ImportError("oracle/c/libtcoracle.so not built (make oracle)")
+_lib = ctypes.CDLL(_PATH)
+_B = ctypes.c_char_p
+_lib.tco_init.restype = None
+_lib.tco_pairing_eq.argtypes = [_B, _B, _B, _B]
+_lib.tco_g1_mul.argtypes = [_B, _B, ctypes.c_void_p]
+_lib.tco_g2_mul.argtypes = [_B, _B, ctypes.c_void_p]
+_lib.tco_hash_g2.argtypes = [_B, ctypes.c_size_t, ctypes.c_void_p]
+_lib.tco_hash_g2.restype = None
+_lib.tco_hash_g1_g2.argtypes = [_B, _B, ctypes.c_size_t, ctypes.c_void_p]
+_lib.tco_hash_g1_g2.restype = None
+_lib.tco_sha3_256.argtypes = [_B, ctypes.c_size_t, ctypes.c_void_p]
+_lib.tco_sha3_256.restype = None
+_lib.tco_sig_parity.argtypes = [_B]
+_lib.tco_combine_g1.argtypes = [ctypes.c_uint32, ctypes.c_void_p, _B, ctypes.c_uint32, ctypes.c_void_p]
+_lib.tco_combine_g2.argtypes = [ctypes.c_uint32, ctypes.c_void_p, _B, ctypes.c_uint32, ctypes.c_void_p]
+_lib.tco_bench_dec_shares.restype = ctypes.c_uint64
+_lib.tco_bench_dec_shares.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, _B, ctypes.c_uint32,
+                                      _B, _B, _B, ctypes.c_size_t, _B,
+                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
+_lib.tco_init()
+
+
+def pairing_eq(p1, q1, p2, q2):
+    """e(p1, q1) == e(p2, q2) by two full pairings: True/False, None on a decode error."""
+    r = _lib.tco_pairing_eq(bytes(p1), bytes(q1), bytes(p2), bytes(q2))
+    return None if r < 0 else bool(r)
+
+
+def g1_mul(p48, k):
+    out = ctypes.create_string_buffer(48)
+    if _lib.tco_g1_mul(bytes(p48), int(k).to_bytes(32, "little"), out) != 0:
+        return None
+    return out.raw
+
+
+def g2_mul(p96, k):
+    out = ctypes.create_string_buffer(96)
+    if _lib.tco_g2_mul(bytes(p96), int(k).to_bytes(32, "little"), out) != 0:
+        return None
+    return out.raw
+
+
+def sha3_256(msg):
+    out = ctypes.create_string_buffer(32)
+    _lib.tco_sha3_256(bytes(msg), len(msg), out)
+    return out.raw
+
+
+def hash_g2(msg):
+    out = ctypes.create_string_buffer(96)
+    _lib.tco_hash_g2(bytes(msg), len(msg), out)
+    return out.raw
+
+
+def hash_g1_g2(g1_48, msg):
+    out = ctypes.create_string_buffer(96)
+    _lib.tco_hash_g1_g2(bytes(g1_48), bytes(msg), len(msg), out)
+    return out.raw
+
+
+def sig_parity(sig96):
+    return _lib.tco_sig_parity(bytes(sig96))
+
+
+def combine(group, idx, pts, t):
+    """(status, bytes): status 0 ok, 5 NotEnoughShares, 6 DuplicateEntry, 2 decode error."""
+    size = 48 if group == 1 else 96
+    n = len(idx)
+    ix = (ctypes.c_uint32 * max(n, 1))(*idx)
+    out = ctypes.create_string_buffer(size)
+    fn = _lib.tco_combine_g1 if group == 1 else _lib.tco_combine_g2
+    st = fn(n, ix, b"".join(bytes(p) for p in pts), t, out)
+    return st, (out.raw if st == 0 else None)
+
+
+def bench_dec_shares(mode, threads, budget_s, shares, pk48, u48, v, w96):
+    """Run the C baseline: mode 0 = threshold_crypto's per-call path, 1 = optimized CPU."""
+    wall, acc = ctypes.c_double(), ctypes.c_uint64()
+    blob = b"".join(bytes(s) for s in shares)
+    done = _lib.tco_bench_dec_shares(mode, threads, budget_s, blob, len(shares), bytes(pk48),
+                                     bytes(u48), bytes(v), len(v), bytes(w96), ctypes.byref(wall),
+                                     ctypes.byref(acc))
+    return int(done), wall.value, int(acc.value)
+
+
+def run_dec_share_baseline(ep, budget_s, cores=None):
+    """bench.py cpu_baseline leg: the reference-faithful per-call path on all host cores (up to
+    the box's CPU share), on real decryption shares of the benchmark's ciphertext 0."""
+    cores = cores or min(16, os.cpu_count() or 1)
+    rng = random.Random(3)
+    k = 0
+    shares = [bytes(ep.host_shares[k * ep.n + i]) for i in range(ep.n)]
+    # ciphertext 0's own u / w / pk_0 in compressed form
+    pk0 = ep.pk_bytes[0]
+    u = ep.u_bytes[k]
+    w = ep.w_bytes[k]
+    v = bytes(rng.randrange(256) for _ in range(64))
+    done, wall, acc = bench_dec_shares(0, cores, budget_s, shares, pk0, u, v, w)
+    done_o, wall_o, _ = bench_dec_shares(1, cores, min(10.0, budget_s / 2), shares, pk0, u, v, w)
+    return {
+        "value": round(done / wall, 2),
+        "unit": "shares/s",
+        "cores": cores,
+        "kind": "port",
+        "impl": "C restatement of threshold_crypto 0.1 / pairing 0.14 (oracle/c/tc_oracle.c), pthreads",
+        "sample": "%d DecryptionShare checks of ciphertext 0 in %.1fs: per share serde decode ([r]P "
+                  "subgroup check) + hash_g1_g2(u, v) + two full pairings, as hbbft calls "
+                  "verify_decryption_share (src/threshold_decryption.rs:159)" % (done, wall),
+        "optimized_cpu": {"value": round(done_o / wall_o, 2), "unit": "shares/s",
+                          "sample": "%d shares in %.1fs: hash + G2 preparation once per ciphertext, one "
+                                    "2-pair multi-Miller loop + one final exponentiation per share"
+                                    % (done_o, wall_o)},
+    }

@@ -168,7 +168,7 @@ int main(int argc, char** argv) {
   void *d_in, *d_out, *d_lines, *d_pts, *d_f;
   const int nthreads = 256 * 1024;  // 4 waves per SIMD worth of lanes
   CHK(hipMalloc(&d_in, sizeof(Fq) * 1024));
-  CHK(hipMalloc(&d_out, sizeof(Fq12) * nthreads));
+  CHK(hipMalloc(&d_out, sizeof(Fq12) * 16384 * 64));  // largest grid below: 1M lanes
   CHK(hipMalloc(&d_lines, sizeof(Line) * 2 * MILLER_STEPS));
   CHK(hipMalloc(&d_pts, sizeof(G1A) * 1024));
   CHK(hipMalloc(&d_f, sizeof(Fq12) * 1024));
