@@ -12,7 +12,8 @@ HDRS := $(wildcard $(CSRC)/*.h) include/hbtc.h
 BUILD := build
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC)
 PARTS := 1 2 3 4 5
-KOBJS := $(foreach p,$(PARTS),$(BUILD)/hbtc_kernels.p$(p).o)
+RLC_PARTS := 6 7
+KOBJS := $(foreach p,$(PARTS),$(BUILD)/hbtc_kernels.p$(p).o) $(foreach p,$(RLC_PARTS),$(BUILD)/hbtc_rlc.p$(p).o)
 LIB := hbbft_amd/libhbtc.so
 
 .PHONY: all lib hosttest oracle clean resources roofline-constants
@@ -24,6 +25,9 @@ $(BUILD):
 	mkdir -p $(BUILD)
 
 $(BUILD)/hbtc_kernels.p%.o: $(CSRC)/hbtc_kernels.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
+
+$(BUILD)/hbtc_rlc.p%.o: $(CSRC)/hbtc_rlc.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
 
 $(BUILD)/hbtc_api.o: $(CSRC)/hbtc_api.hip $(HDRS) | $(BUILD)

@@ -19,6 +19,8 @@ UNKNOWN_SENDER = 3
 INSTANCE_ERR = 4
 NOT_ENOUGH_SHARES = 5
 DUPLICATE_ENTRY = 6
+MODE_PER_SHARE = 0
+MODE_RLC = 1
 STATUS_NAMES = {ACCEPT: "ACCEPT", REJECT: "REJECT", DECODE_ERR: "DECODE_ERR",
                 UNKNOWN_SENDER: "UNKNOWN_SENDER", INSTANCE_ERR: "INSTANCE_ERR",
                 NOT_ENOUGH_SHARES: "NOT_ENOUGH_SHARES", DUPLICATE_ENTRY: "DUPLICATE_ENTRY"}
@@ -63,6 +65,8 @@ SIGNATURES = {
     "hbtc_verify_sig_shares_dev": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P]),
     "hbtc_combine_dec_dev": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P]),
     "hbtc_combine_sigs_dev": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P, _P]),
+    "hbtc_set_verify_mode": (_I32, [_P, _I32]),
+    "hbtc_rlc_last_leaves": (_I32, [_P, ctypes.POINTER(_U32)]),
     "hbtc_timing_enable": (_I32, [_P, _I32]),
     "hbtc_timing_read": (_I32, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(ctypes.c_uint64)]),
@@ -272,6 +276,16 @@ class Context:
 
     def sync(self):
         self._check(self.lib.hbtc_sync(self.h), "hbtc_sync")
+
+    def set_verify_mode(self, mode):
+        """MODE_RLC (default): batched random-linear-combination checks with exact fallback;
+        MODE_PER_SHARE: one pairing check per share."""
+        self._check(self.lib.hbtc_set_verify_mode(self.h, int(mode)), "hbtc_set_verify_mode")
+
+    def rlc_last_leaves(self):
+        n = _U32()
+        self._check(self.lib.hbtc_rlc_last_leaves(self.h, ctypes.byref(n)), "hbtc_rlc_last_leaves")
+        return n.value
 
     def timing_enable(self, on=True):
         self._check(self.lib.hbtc_timing_enable(self.h, 1 if on else 0), "hbtc_timing_enable")

@@ -6,6 +6,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -45,6 +46,11 @@ struct hbtc_ctx {
   size_t h_tiles_cap = 0;
   uint32_t* h_u32 = nullptr;  // pinned staging for small host-shaped arrays (offsets)
   size_t h_u32_cap = 0;
+  uint32_t* h_inst_tiles = nullptr;  // pinned staging: first tile of every instance
+  size_t h_inst_tiles_cap = 0;
+  int verify_mode = HBTC_MODE_RLC;
+  const uint32_t* last_leaf_count = nullptr;  // device counter of the last RLC call
+  std::random_device rd;
   bool timing = false;
   std::vector<Span> spans;
   std::map<std::string, std::pair<double, uint64_t>> totals;
@@ -161,7 +167,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 // Split every instance into tiles of <= 64 items; upload the table.  The pinned staging
 // buffer is reused, so wait for the stream first (the previous upload may still read it).
 int make_tiles(hbtc_ctx* c, uint32_t n_inst, const uint32_t* offsets, Tile** d_tiles,
-               uint32_t* n_tiles) {
+               uint32_t* n_tiles, uint32_t** d_inst_tiles = nullptr) {
   size_t nt = 0;
   for (uint32_t k = 0; k < n_inst; ++k)
     nt += (offsets[k + 1] - offsets[k] + TILE_ITEMS - 1) / TILE_ITEMS;
@@ -173,12 +179,27 @@ int make_tiles(hbtc_ctx* c, uint32_t n_inst, const uint32_t* offsets, Tile** d_t
     HB_CHECK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_tiles), want * sizeof(Tile)));
     c->h_tiles_cap = want;
   }
+  if (d_inst_tiles && c->h_inst_tiles_cap < (size_t)n_inst + 1) {
+    if (c->h_inst_tiles) HB_CHECK(c, hipHostFree(c->h_inst_tiles));
+    c->h_inst_tiles = nullptr;
+    HB_CHECK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_inst_tiles),
+                              ((size_t)n_inst + 65) * sizeof(uint32_t)));
+    c->h_inst_tiles_cap = (size_t)n_inst + 65;
+  }
   size_t j = 0;
-  for (uint32_t k = 0; k < n_inst; ++k)
+  for (uint32_t k = 0; k < n_inst; ++k) {
+    if (d_inst_tiles) c->h_inst_tiles[k] = (uint32_t)j;
     for (uint32_t s = offsets[k]; s < offsets[k + 1]; s += TILE_ITEMS) {
       const uint32_t cnt = offsets[k + 1] - s < TILE_ITEMS ? offsets[k + 1] - s : TILE_ITEMS;
       c->h_tiles[j++] = Tile{k, s, cnt, 0};
     }
+  }
+  if (d_inst_tiles) {
+    c->h_inst_tiles[n_inst] = (uint32_t)j;
+    void* p;
+    HB_TRY(upload(c, "inst_tiles", c->h_inst_tiles, ((size_t)n_inst + 1) * sizeof(uint32_t), &p));
+    *d_inst_tiles = static_cast<uint32_t*>(p);
+  }
   if (nt > 0xffffffffull) return fail(c, HBTC_ERR_ARG, "too many tiles");
   void* p;
   HB_TRY(upload(c, "tiles", c->h_tiles, nt * sizeof(Tile), &p));
@@ -245,11 +266,45 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   HB_TRY(prepare_g2(c, "W", d_w, n_ct, &w_aff, &w_st, &w_lines));
   Tile* tiles;
   uint32_t n_tiles;
-  HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles));
-  return timed(c, "dec_verify", [&] {
-    return launch_dec_verify(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n,
-                             h_aff, h_st, h_lines, w_aff, w_st, w_lines, d_status);
-  });
+  if (c->verify_mode == HBTC_MODE_PER_SHARE) {
+    HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles));
+    return timed(c, "dec_verify", [&] {
+      return launch_dec_verify(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n,
+                               h_aff, h_st, h_lines, w_aff, w_st, w_lines, d_status);
+    });
+  }
+  // RLC batch verification with hierarchical fallback (hbtc_rlc.hip)
+  uint32_t* inst_tiles;
+  HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles, &inst_tiles));
+  RlcKey key;
+  for (int i = 0; i < 8; ++i) key.k[i] = c->rd();
+  TileSums* sums;
+  uint8_t *inst_pass, *tile_pass;
+  uint32_t *leaf_count, *leaves;
+  HB_TRY(wst(c, "rlc.sums", n_tiles, &sums));
+  HB_TRY(wst(c, "rlc.inst_pass", n_ct, &inst_pass));
+  HB_TRY(wst(c, "rlc.tile_pass", n_tiles, &tile_pass));
+  HB_TRY(wst(c, "rlc.leaf_count", 1, &leaf_count));
+  HB_TRY(wst(c, "rlc.leaves", (size_t)2 * n_items, &leaves));
+  HB_CHECK(c, hipMemsetAsync(leaf_count, 0, sizeof(uint32_t), c->stream));
+  HB_TRY(timed(c, "rlc_items", [&] {
+    return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n, h_st,
+                            w_st, key, sums, d_status);
+  }));
+  HB_TRY(timed(c, "rlc_groups", [&] {
+    return launch_rlc_check_groups(c->stream, n_ct, n_tiles, tiles, inst_tiles, sums, h_aff,
+                                   h_lines, w_aff, w_lines, inst_pass, tile_pass);
+  }));
+  HB_TRY(timed(c, "rlc_sub", [&] {
+    return launch_rlc_sub(c->stream, n_tiles, tiles, sums, inst_pass, tile_pass, h_aff, h_lines,
+                          w_aff, w_lines, d_status, leaf_count, leaves);
+  }));
+  HB_TRY(timed(c, "rlc_leaves", [&] {
+    return launch_rlc_leaves(c->stream, n_items, leaf_count, leaves, d_idx, d_share, ks->pk, h_aff,
+                             h_lines, w_aff, w_lines, d_status);
+  }));
+  c->last_leaf_count = leaf_count;
+  return timed(c, "rlc_finalize", [&] { return launch_rlc_finalize(c->stream, n_items, d_status); });
 }
 
 int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8_t* d_H,
@@ -405,6 +460,7 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
   }
   if (c->h_tiles) (void)hipHostFree(c->h_tiles);
   if (c->h_u32) (void)hipHostFree(c->h_u32);
+  if (c->h_inst_tiles) (void)hipHostFree(c->h_inst_tiles);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -647,6 +703,22 @@ int hbtc_combine_sigs_dev(hbtc_ctx* c, uint32_t n_inst, const uint32_t* offsets,
   Guard g(c);
   return combine_dev(c, 2, n_inst, offsets, d_idx, d_sig, t, d_out_sig, d_out_parity,
                      d_inst_status);
+}
+
+int hbtc_set_verify_mode(hbtc_ctx* c, int mode) {
+  if (!c || (mode != HBTC_MODE_PER_SHARE && mode != HBTC_MODE_RLC)) return HBTC_ERR_ARG;
+  Guard g(c);
+  c->verify_mode = mode;
+  return HBTC_OK;
+}
+
+int hbtc_rlc_last_leaves(hbtc_ctx* c, uint32_t* leaves) {
+  if (!c || !leaves) return HBTC_ERR_ARG;
+  Guard g(c);
+  *leaves = 0;
+  if (!c->last_leaf_count) return HBTC_OK;
+  HB_CHECK(c, hipMemcpyAsync(leaves, c->last_leaf_count, 4, hipMemcpyDeviceToHost, c->stream));
+  return sync(c);
 }
 
 int hbtc_timing_enable(hbtc_ctx* c, int enable) {

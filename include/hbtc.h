@@ -150,9 +150,23 @@ int hbtc_combine_sigs_dev(hbtc_ctx* ctx, uint32_t n_inst, const uint32_t* offset
                           const uint32_t* d_idx, const uint8_t* d_sig_c96, uint32_t t,
                           uint8_t* d_out_sig_c96, uint8_t* d_out_parity, int32_t* d_inst_status);
 
+/* ---- verification strategy ----------------------------------------------------------------- */
+/* HBTC_MODE_RLC (default): shares of one instance are checked together by a random linear
+ * combination (fresh 64-bit ChaCha20 scalars per call, prime-order points only), failing groups
+ * are split ciphertext -> 64 -> 8 -> 1 share, single shares get the exact pairing check.  The
+ * decisions equal the per-share decisions except with probability <= 2^-64 per group check.
+ * HBTC_MODE_PER_SHARE: every share gets its own 2-pair pairing check (the reference's count).
+ * Applies to hbtc_verify_dec_shares[_dev]. */
+#define HBTC_MODE_PER_SHARE 0
+#define HBTC_MODE_RLC 1
+int hbtc_set_verify_mode(hbtc_ctx* ctx, int mode);
+/* Number of shares that needed the exact single-share check in the last RLC call (syncs). */
+int hbtc_rlc_last_leaves(hbtc_ctx* ctx, uint32_t* leaves);
+
 /* ---- kernel timing (HIP events on the context's stream) ---------------------------------- */
 /* Families: "prepare", "dec_verify", "sig_verify", "pair_verify", "lagrange", "combine",
- * "mul".  Reading synchronises the stream. */
+ * "mul", "rlc_items", "rlc_groups", "rlc_sub", "rlc_leaves", "rlc_finalize".  Reading
+ * synchronises the stream. */
 int hbtc_timing_enable(hbtc_ctx* ctx, int enable);
 int hbtc_timing_read(hbtc_ctx* ctx, const char* family, double* total_ms, uint64_t* launches);
 int hbtc_timing_reset(hbtc_ctx* ctx);
