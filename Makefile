@@ -27,6 +27,10 @@ $(BUILD):
 $(BUILD)/hbtc_kernels.p%.o: $(CSRC)/hbtc_kernels.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
 
+# part 6 (per-item G1 work) is built with every helper inlined: no calls, no scratch
+$(BUILD)/hbtc_rlc.p6.o: $(CSRC)/hbtc_rlc.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=6 -DHBTC_INLINE_ALL -c $< -o $@
+
 $(BUILD)/hbtc_rlc.p%.o: $(CSRC)/hbtc_rlc.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
 

@@ -113,13 +113,15 @@ class Epoch:
         self.host_shares = shares
 
     def step(self, ctx):
+        """One epoch: the 1000 combines (enqueued first; they run on the library's combine
+        stream, overlapping the verification) and the 10^6 share checks."""
         lib, h, d = ctx.lib, ctx.h, self.d
         off = N._ptr(self.offsets)
+        ctx._check(lib.hbtc_combine_dec_dev(h, self.n_ct, off, d["idx"], d["shares"], self.t,
+                                            d["g"], d["cst"]), "combine_dec_dev")
         ctx._check(lib.hbtc_verify_dec_shares_dev(h, self.keyset, self.n_ct, d["H"], d["w"], off,
                                                   d["idx"], d["shares"], d["status"]),
                    "verify_dec_shares_dev")
-        ctx._check(lib.hbtc_combine_dec_dev(h, self.n_ct, off, d["idx"], d["shares"], self.t,
-                                            d["g"], d["cst"]), "combine_dec_dev")
 
     def check(self, ctx):
         st = np.empty(self.total, np.int32)

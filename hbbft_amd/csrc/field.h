@@ -26,10 +26,17 @@
 //       functions whose register allocation takes the compiler tens of minutes and whose code
 //       does not fit the instruction cache; a call boundary costs a few hundred bytes of
 //       scratch traffic per call, negligible next to the work inside.
+// A translation unit that only runs light group arithmetic (G1 decode / scalar mult) defines
+// HBTC_INLINE_ALL: with no calls the compiler can size registers for the real working set and
+// run several waves per SIMD.
 #if defined(__HIPCC__) || defined(__HIP__)
 #include <hip/hip_runtime.h>
 #define HD __host__ __device__ __forceinline__
+#if defined(HBTC_INLINE_ALL)
+#define HDN __host__ __device__ __forceinline__
+#else
 #define HDN __host__ __device__ inline __attribute__((noinline))
+#endif
 #define HBTC_CONST static constexpr
 #else
 #define HD static inline
@@ -218,10 +225,22 @@ extern unsigned long long hbtc_fqm_count;
 #define HBTC_COUNT_FQ_MUL() ((void)0)
 #endif
 
+#if defined(HBTC_FQMUL_CALL) && defined(__HIP_DEVICE_COMPILE__)
+// One out-of-line copy of the Montgomery product with its operands passed in VGPRs: callers
+// then keep only their own live values, which lets light group arithmetic run several waves
+// per SIMD (the call costs ~40 moves against ~600 instructions of multiply).
+__device__ __attribute__((noinline)) Fq fq_mul_call(Fq a, Fq b) {
+  Fq r;
+  mont_mul<12, HBTC_FQ_UNROLL>(r, a, b, FQ_P, FQ_NP);
+  return r;
+}
+HD void fq_mul(Fq& r, const Fq& a, const Fq& b) { r = fq_mul_call(a, b); }
+#else
 HD void fq_mul(Fq& r, const Fq& a, const Fq& b) {
   HBTC_COUNT_FQ_MUL();
   mont_mul<12, HBTC_FQ_UNROLL>(r, a, b, FQ_P, FQ_NP);
 }
+#endif
 HD void fq_sqr(Fq& r, const Fq& a) { fq_mul(r, a, a); }
 
 // canonical value in [0, p)

@@ -32,22 +32,29 @@ struct Span {
   hipEvent_t a, b;
 };
 
+// Pinned host staging buffer for small host-shaped tables (tiles, offsets); `ev` marks the
+// completion of the last copy out of it, so it is reused without synchronising a stream.
+struct Stage {
+  void* h = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  bool used = false;
+};
+
 }  // namespace
 
 struct hbtc_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // main: items, checks, leaves
+  hipStream_t s_prep = nullptr;  // per-instance G2 preparation, overlapped with the item pass
+  hipStream_t s_comb = nullptr;  // combines (Lagrange), overlapped with verification
+  hipEvent_t ev_main = nullptr, ev_prep = nullptr, ev_comb = nullptr;
+  std::map<std::string, Stage> stages;
   std::mutex mu;
   std::string err;
   std::map<uint32_t, Keyset> keysets;
   uint32_t next_keyset = 1;
   std::map<std::string, DevBuf> bufs;
-  Tile* h_tiles = nullptr;  // pinned staging for the tile table
-  size_t h_tiles_cap = 0;
-  uint32_t* h_u32 = nullptr;  // pinned staging for small host-shaped arrays (offsets)
-  size_t h_u32_cap = 0;
-  uint32_t* h_inst_tiles = nullptr;  // pinned staging: first tile of every instance
-  size_t h_inst_tiles_cap = 0;
   int verify_mode = HBTC_MODE_RLC;
   const uint32_t* last_leaf_count = nullptr;  // device counter of the last RLC call
   std::random_device rd;
@@ -116,25 +123,59 @@ int download(hbtc_ctx* c, void* dst, const void* src, size_t bytes) {
 
 int sync(hbtc_ctx* c) {
   HB_CHECK(c, hipStreamSynchronize(c->stream));
+  HB_CHECK(c, hipStreamSynchronize(c->s_prep));
+  HB_CHECK(c, hipStreamSynchronize(c->s_comb));
   return HBTC_OK;
 }
 
-// Record a kernel family's launch between two events on the context stream.
+// `waiter` runs everything enqueued after this behind all work already on `on`.
+int stream_after(hbtc_ctx* c, hipStream_t waiter, hipStream_t on, hipEvent_t ev) {
+  HB_CHECK(c, hipEventRecord(ev, on));
+  HB_CHECK(c, hipStreamWaitEvent(waiter, ev, 0));
+  return HBTC_OK;
+}
+
+// Record a kernel family's launch between two events on the stream it runs on.
 template <class F>
-int timed(hbtc_ctx* c, const char* family, F&& launch) {
+int timed_on(hbtc_ctx* c, hipStream_t st, const char* family, F&& launch) {
   Span sp;
   if (c->timing) {
     HB_CHECK(c, hipEventCreate(&sp.a));
     HB_CHECK(c, hipEventCreate(&sp.b));
-    HB_CHECK(c, hipEventRecord(sp.a, c->stream));
+    HB_CHECK(c, hipEventRecord(sp.a, st));
   }
   hipError_t e = launch();
   if (e != hipSuccess) return fail(c, HBTC_ERR_DEVICE, std::string(family) + " launch: " + hipGetErrorString(e));
   if (c->timing) {
-    HB_CHECK(c, hipEventRecord(sp.b, c->stream));
+    HB_CHECK(c, hipEventRecord(sp.b, st));
     sp.family = family;
     c->spans.push_back(sp);
   }
+  return HBTC_OK;
+}
+template <class F>
+int timed(hbtc_ctx* c, const char* family, F&& launch) {
+  return timed_on(c, c->stream, family, launch);
+}
+
+// Host table -> device workspace `name` through its pinned stage, ordered on `st`.
+int stage_upload(hbtc_ctx* c, const char* name, const void* src, size_t bytes, hipStream_t st,
+                 void** d_out) {
+  Stage& sg = c->stages[name];
+  if (sg.used) HB_CHECK(c, hipEventSynchronize(sg.ev));  // the previous copy out of it is done
+  if (sg.cap < bytes || !sg.h) {
+    if (sg.h) HB_CHECK(c, hipHostFree(sg.h));
+    sg.h = nullptr;
+    const size_t want = bytes + bytes / 4 + 256;
+    HB_CHECK(c, hipHostMalloc(&sg.h, want));
+    sg.cap = want;
+  }
+  if (!sg.ev) HB_CHECK(c, hipEventCreateWithFlags(&sg.ev, hipEventDisableTiming));
+  if (bytes) memcpy(sg.h, src, bytes);
+  HB_TRY(ws(c, name, bytes, d_out));
+  if (bytes) HB_CHECK(c, hipMemcpyAsync(*d_out, sg.h, bytes, hipMemcpyHostToDevice, st));
+  HB_CHECK(c, hipEventRecord(sg.ev, st));
+  sg.used = true;
   return HBTC_OK;
 }
 
@@ -164,65 +205,28 @@ int check_offsets(hbtc_ctx* c, uint32_t n_inst, const uint32_t* offsets, uint32_
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-// Split every instance into tiles of <= 64 items; upload the table.  The pinned staging
-// buffer is reused, so wait for the stream first (the previous upload may still read it).
+// Split every instance into tiles of <= 64 items and upload the table (and, when asked, the
+// first tile of every instance) through pinned stages on the main stream.
 int make_tiles(hbtc_ctx* c, uint32_t n_inst, const uint32_t* offsets, Tile** d_tiles,
                uint32_t* n_tiles, uint32_t** d_inst_tiles = nullptr) {
-  size_t nt = 0;
-  for (uint32_t k = 0; k < n_inst; ++k)
-    nt += (offsets[k + 1] - offsets[k] + TILE_ITEMS - 1) / TILE_ITEMS;
-  HB_TRY(sync(c));
-  if (c->h_tiles_cap < nt) {
-    if (c->h_tiles) HB_CHECK(c, hipHostFree(c->h_tiles));
-    c->h_tiles = nullptr;
-    size_t want = nt + nt / 4 + 64;
-    HB_CHECK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_tiles), want * sizeof(Tile)));
-    c->h_tiles_cap = want;
-  }
-  if (d_inst_tiles && c->h_inst_tiles_cap < (size_t)n_inst + 1) {
-    if (c->h_inst_tiles) HB_CHECK(c, hipHostFree(c->h_inst_tiles));
-    c->h_inst_tiles = nullptr;
-    HB_CHECK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_inst_tiles),
-                              ((size_t)n_inst + 65) * sizeof(uint32_t)));
-    c->h_inst_tiles_cap = (size_t)n_inst + 65;
-  }
-  size_t j = 0;
+  std::vector<Tile> tiles;
+  std::vector<uint32_t> inst_tiles(n_inst + 1);
   for (uint32_t k = 0; k < n_inst; ++k) {
-    if (d_inst_tiles) c->h_inst_tiles[k] = (uint32_t)j;
+    inst_tiles[k] = (uint32_t)tiles.size();
     for (uint32_t s = offsets[k]; s < offsets[k + 1]; s += TILE_ITEMS) {
       const uint32_t cnt = offsets[k + 1] - s < TILE_ITEMS ? offsets[k + 1] - s : TILE_ITEMS;
-      c->h_tiles[j++] = Tile{k, s, cnt, 0};
+      tiles.push_back(Tile{k, s, cnt, 0});
     }
   }
+  inst_tiles[n_inst] = (uint32_t)tiles.size();
+  void* p;
+  HB_TRY(stage_upload(c, "tiles", tiles.data(), tiles.size() * sizeof(Tile), c->stream, &p));
+  *d_tiles = static_cast<Tile*>(p);
+  *n_tiles = (uint32_t)tiles.size();
   if (d_inst_tiles) {
-    c->h_inst_tiles[n_inst] = (uint32_t)j;
-    void* p;
-    HB_TRY(upload(c, "inst_tiles", c->h_inst_tiles, ((size_t)n_inst + 1) * sizeof(uint32_t), &p));
+    HB_TRY(stage_upload(c, "inst_tiles", inst_tiles.data(), inst_tiles.size() * 4, c->stream, &p));
     *d_inst_tiles = static_cast<uint32_t*>(p);
   }
-  if (nt > 0xffffffffull) return fail(c, HBTC_ERR_ARG, "too many tiles");
-  void* p;
-  HB_TRY(upload(c, "tiles", c->h_tiles, nt * sizeof(Tile), &p));
-  *d_tiles = static_cast<Tile*>(p);
-  *n_tiles = (uint32_t)nt;
-  return HBTC_OK;
-}
-
-// Host array of n+1 offsets -> device (pinned staging, same reuse rule as the tiles).
-int upload_offsets(hbtc_ctx* c, const char* name, uint32_t n_inst, const uint32_t* offsets,
-                   uint32_t** d) {
-  HB_TRY(sync(c));
-  const size_t n = (size_t)n_inst + 1;
-  if (c->h_u32_cap < n) {
-    if (c->h_u32) HB_CHECK(c, hipHostFree(c->h_u32));
-    c->h_u32 = nullptr;
-    HB_CHECK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_u32), (n + 64) * sizeof(uint32_t)));
-    c->h_u32_cap = n + 64;
-  }
-  memcpy(c->h_u32, offsets, n * sizeof(uint32_t));
-  void* p;
-  HB_TRY(upload(c, name, c->h_u32, n * sizeof(uint32_t), &p));
-  *d = static_cast<uint32_t*>(p);
   return HBTC_OK;
 }
 
@@ -235,7 +239,8 @@ int get_keyset(hbtc_ctx* c, uint32_t id, Keyset** ks) {
 
 // Decode + line tables for n per-instance G2 arguments (named workspace prefix `tag`).
 int prepare_g2(hbtc_ctx* c, const char* tag, const uint8_t* d_c96, uint32_t n, G2A** aff,
-               int32_t** st, Line** lines) {
+               int32_t** st, Line** lines, hipStream_t on = nullptr) {
+  hipStream_t strm = on ? on : c->stream;
   std::string t(tag);
   Fq2* wsp;
   HB_TRY(wst(c, (t + ".aff").c_str(), n, aff));
@@ -245,7 +250,7 @@ int prepare_g2(hbtc_ctx* c, const char* tag, const uint8_t* d_c96, uint32_t n, G
   G2A* a = *aff;
   int32_t* s = *st;
   Line* l = *lines;
-  return timed(c, "prepare", [&] { return launch_g2_prepare(c->stream, d_c96, n, a, l, wsp, s); });
+  return timed_on(c, strm, "prepare", [&] { return launch_g2_prepare(strm, d_c96, n, a, l, wsp, s); });
 }
 
 // ---------------------------------------------------------------- device-pointer cores
@@ -262,18 +267,22 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   G2A *h_aff, *w_aff;
   int32_t *h_st, *w_st;
   Line *h_lines, *w_lines;
-  HB_TRY(prepare_g2(c, "H", d_H, n_ct, &h_aff, &h_st, &h_lines));
-  HB_TRY(prepare_g2(c, "W", d_w, n_ct, &w_aff, &w_st, &w_lines));
   Tile* tiles;
   uint32_t n_tiles;
   if (c->verify_mode == HBTC_MODE_PER_SHARE) {
+    HB_TRY(prepare_g2(c, "H", d_H, n_ct, &h_aff, &h_st, &h_lines));
+    HB_TRY(prepare_g2(c, "W", d_w, n_ct, &w_aff, &w_st, &w_lines));
     HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles));
     return timed(c, "dec_verify", [&] {
       return launch_dec_verify(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n,
                                h_aff, h_st, h_lines, w_aff, w_st, w_lines, d_status);
     });
   }
-  // RLC batch verification with hierarchical fallback (hbtc_rlc.hip)
+  // RLC batch verification with hierarchical fallback (hbtc_rlc.hip).  The per-ciphertext G2
+  // preparation runs on s_prep concurrently with the item pass; the checks wait for both.
+  HB_TRY(stream_after(c, c->s_prep, c->stream, c->ev_main));
+  HB_TRY(prepare_g2(c, "H", d_H, n_ct, &h_aff, &h_st, &h_lines, c->s_prep));
+  HB_TRY(prepare_g2(c, "W", d_w, n_ct, &w_aff, &w_st, &w_lines, c->s_prep));
   uint32_t* inst_tiles;
   HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles, &inst_tiles));
   RlcKey key;
@@ -288,12 +297,13 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   HB_TRY(wst(c, "rlc.leaves", (size_t)2 * n_items, &leaves));
   HB_CHECK(c, hipMemsetAsync(leaf_count, 0, sizeof(uint32_t), c->stream));
   HB_TRY(timed(c, "rlc_items", [&] {
-    return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n, h_st,
-                            w_st, key, sums, d_status);
+    return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n,
+                            key, sums, d_status);
   }));
+  HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
   HB_TRY(timed(c, "rlc_groups", [&] {
     return launch_rlc_check_groups(c->stream, n_ct, n_tiles, tiles, inst_tiles, sums, h_aff,
-                                   h_lines, w_aff, w_lines, inst_pass, tile_pass);
+                                   h_lines, w_aff, w_lines, h_st, w_st, inst_pass, tile_pass);
   }));
   HB_TRY(timed(c, "rlc_sub", [&] {
     return launch_rlc_sub(c->stream, n_tiles, tiles, sums, inst_pass, tile_pass, h_aff, h_lines,
@@ -304,7 +314,9 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
                              h_lines, w_aff, w_lines, d_status);
   }));
   c->last_leaf_count = leaf_count;
-  return timed(c, "rlc_finalize", [&] { return launch_rlc_finalize(c->stream, n_items, d_status); });
+  return timed(c, "rlc_finalize", [&] {
+    return launch_rlc_finalize(c->stream, n_tiles, tiles, h_st, w_st, d_status);
+  });
 }
 
 int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8_t* d_H,
@@ -330,6 +342,8 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   });
 }
 
+// Lagrange combine on s_comb: ordered after everything already on the main stream (its inputs),
+// overlapped with whatever the main stream does next.
 int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets,
                 const uint32_t* d_idx, const uint8_t* d_pts, uint32_t t, uint8_t* d_out,
                 uint8_t* d_parity, int32_t* d_inst_status) {
@@ -339,54 +353,42 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
   if (t == 0) return fail(c, HBTC_ERR_ARG, "t must be >= 1");
   if (!aligned16(d_pts) || !aligned16(d_out))
     return fail(c, HBTC_ERR_ARG, "point arrays must be 16-byte aligned");
-  uint32_t* d_off;
-  HB_TRY(upload_offsets(c, "comb.offsets", n_inst, offsets, &d_off));
-  // Lagrange coefficients only for instances that have at least t items: compact them into
-  // a dense (instance, t) grid so the kernel never reads past an instance's items.
-  std::vector<uint32_t> firsts(n_inst);
-  for (uint32_t k = 0; k < n_inst; ++k)
-    firsts[k] = (offsets[k + 1] - offsets[k] >= t) ? offsets[k] : 0xffffffffu;
-  // instances lacking items get a harmless idx window: point them at a zero-filled dummy
+  hipStream_t sc = c->s_comb;
+  HB_TRY(stream_after(c, sc, c->stream, c->ev_main));
+  void* p;
+  HB_TRY(stage_upload(c, "comb.offsets", offsets, ((size_t)n_inst + 1) * 4, sc, &p));
+  uint32_t* d_off = static_cast<uint32_t*>(p);
+  // Lagrange coefficients over a dense (instance, t) grid; an instance with fewer than t
+  // items reads a zero-filled dummy window (its status is NOT_ENOUGH_SHARES regardless).
   std::vector<uint32_t> h_first(n_inst);
   bool any_short = false;
   for (uint32_t k = 0; k < n_inst; ++k) {
-    if (firsts[k] == 0xffffffffu) {
-      any_short = true;
-      h_first[k] = n_items;  // start of the dummy tail appended below
-    } else {
-      h_first[k] = firsts[k];
-    }
+    const bool enough = offsets[k + 1] - offsets[k] >= t;
+    any_short |= !enough;
+    h_first[k] = enough ? offsets[k] : n_items;
   }
   const uint32_t* idx_for_lagrange = d_idx;
   if (any_short) {
-    // copy idx into a workspace with t zero entries appended (distinct-free dummy; the
-    // instance status is NOT_ENOUGH_SHARES regardless of what lambda becomes)
     uint32_t* d_idx2;
     HB_TRY(wst(c, "comb.idx2", (size_t)n_items + t, &d_idx2));
     if (n_items)
-      HB_CHECK(c, hipMemcpyAsync(d_idx2, d_idx, (size_t)n_items * 4, hipMemcpyDeviceToDevice, c->stream));
-    HB_CHECK(c, hipMemsetAsync(d_idx2 + n_items, 0, (size_t)t * 4, c->stream));
+      HB_CHECK(c, hipMemcpyAsync(d_idx2, d_idx, (size_t)n_items * 4, hipMemcpyDeviceToDevice, sc));
+    HB_CHECK(c, hipMemsetAsync(d_idx2 + n_items, 0, (size_t)t * 4, sc));
     idx_for_lagrange = d_idx2;
   }
-  uint32_t* d_first;
-  {
-    HB_TRY(sync(c));
-    void* p;
-    HB_TRY(ws(c, "comb.first", (size_t)n_inst * 4, &p));
-    d_first = static_cast<uint32_t*>(p);
-    HB_CHECK(c, hipMemcpy(d_first, h_first.data(), (size_t)n_inst * 4, hipMemcpyHostToDevice));
-  }
+  HB_TRY(stage_upload(c, "comb.first", h_first.data(), (size_t)n_inst * 4, sc, &p));
+  uint32_t* d_first = static_cast<uint32_t*>(p);
   Fr* d_lambda;
   uint32_t* d_dup;
   HB_TRY(wst(c, "comb.lambda", (size_t)n_inst * t, &d_lambda));
   HB_TRY(wst(c, "comb.dup", n_inst, &d_dup));
-  HB_CHECK(c, hipMemsetAsync(d_dup, 0, (size_t)n_inst * 4, c->stream));
-  HB_TRY(timed(c, "lagrange", [&] {
-    return launch_lagrange(c->stream, d_first, n_inst, t, idx_for_lagrange, d_lambda, d_dup);
+  HB_CHECK(c, hipMemsetAsync(d_dup, 0, (size_t)n_inst * 4, sc));
+  HB_TRY(timed_on(c, sc, "lagrange", [&] {
+    return launch_lagrange(sc, d_first, n_inst, t, idx_for_lagrange, d_lambda, d_dup);
   }));
-  return timed(c, "combine", [&] {
-    return launch_combine(c->stream, group, n_inst, d_off, t, d_pts, d_lambda, d_dup,
-                          d_inst_status, d_out, d_parity);
+  return timed_on(c, sc, "combine", [&] {
+    return launch_combine(sc, group, n_inst, d_off, t, d_pts, d_lambda, d_dup, d_inst_status,
+                          d_out, d_parity);
   });
 }
 
@@ -436,7 +438,12 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return HBTC_ERR_DEVICE;
   hbtc_ctx* c = new hbtc_ctx();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->s_prep, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->s_comb, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_prep, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return HBTC_ERR_DEVICE;
   }
@@ -447,7 +454,7 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
 void hbtc_ctx_destroy(hbtc_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
+  (void)hipDeviceSynchronize();
   for (auto& kv : c->bufs)
     if (kv.second.p) (void)hipFree(kv.second.p);
   for (auto& kv : c->keysets) {
@@ -458,9 +465,15 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
     (void)hipEventDestroy(sp.a);
     (void)hipEventDestroy(sp.b);
   }
-  if (c->h_tiles) (void)hipHostFree(c->h_tiles);
-  if (c->h_u32) (void)hipHostFree(c->h_u32);
-  if (c->h_inst_tiles) (void)hipHostFree(c->h_inst_tiles);
+  for (auto& kv : c->stages) {
+    if (kv.second.h) (void)hipHostFree(kv.second.h);
+    if (kv.second.ev) (void)hipEventDestroy(kv.second.ev);
+  }
+  (void)hipEventDestroy(c->ev_main);
+  (void)hipEventDestroy(c->ev_prep);
+  (void)hipEventDestroy(c->ev_comb);
+  (void)hipStreamDestroy(c->s_prep);
+  (void)hipStreamDestroy(c->s_comb);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -577,6 +590,7 @@ int hbtc_combine_sigs(hbtc_ctx* c, uint32_t n_inst, const uint32_t* offsets, con
   HB_TRY(ws(c, "out2", (size_t)4 * n_inst, &d_st));
   HB_TRY(combine_dev(c, 2, n_inst, offsets, (const uint32_t*)d_idx, (const uint8_t*)d_sig, t,
                      (uint8_t*)d_out, (uint8_t*)d_par, (int32_t*)d_st));
+  HB_TRY(stream_after(c, c->stream, c->s_comb, c->ev_comb));
   HB_TRY(download(c, out_sig, d_out, (size_t)96 * n_inst));
   HB_TRY(download(c, out_parity, d_par, (size_t)n_inst));
   HB_TRY(download(c, inst_status, d_st, (size_t)4 * n_inst));
@@ -617,6 +631,7 @@ int hbtc_combine_dec(hbtc_ctx* c, uint32_t n_ct, const uint32_t* offsets, const 
   HB_TRY(ws(c, "out2", (size_t)4 * n_ct, &d_st));
   HB_TRY(combine_dev(c, 1, n_ct, offsets, (const uint32_t*)d_idx, (const uint8_t*)d_sh, t,
                      (uint8_t*)d_out, nullptr, (int32_t*)d_st));
+  HB_TRY(stream_after(c, c->stream, c->s_comb, c->ev_comb));
   HB_TRY(download(c, out_g, d_out, (size_t)48 * n_ct));
   HB_TRY(download(c, inst_status, d_st, (size_t)4 * n_ct));
   return sync(c);
@@ -662,6 +677,7 @@ int hbtc_dev_upload(hbtc_ctx* c, void* d_dst, const void* h_src, size_t bytes) {
 int hbtc_dev_download(hbtc_ctx* c, void* h_dst, const void* d_src, size_t bytes) {
   if (!c) return HBTC_ERR_ARG;
   Guard g(c);
+  HB_TRY(sync(c));  // results of any stream (verification, combines) are complete
   HB_CHECK(c, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, c->stream));
   return sync(c);
 }

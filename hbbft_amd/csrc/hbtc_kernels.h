@@ -28,12 +28,12 @@ struct TileSums {
 
 hipError_t launch_rlc_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* shares, const G1A* pk, const int32_t* pk_status,
-                            uint32_t n_pk, const int32_t* h_status, const int32_t* w_status,
-                            RlcKey key, TileSums* sums, int32_t* status);
+                            uint32_t n_pk, RlcKey key, TileSums* sums, int32_t* status);
 hipError_t launch_rlc_check_groups(hipStream_t s, uint32_t n_inst, uint32_t n_tiles,
                                    const Tile* tiles, const uint32_t* inst_tiles,
                                    const TileSums* sums, const G2A* h_aff, const Line* h_lines,
-                                   const G2A* w_aff, const Line* w_lines, uint8_t* inst_pass,
+                                   const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
+                                   const int32_t* w_status, uint8_t* inst_pass,
                                    uint8_t* tile_pass);
 hipError_t launch_rlc_sub(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const TileSums* sums,
                           const uint8_t* inst_pass, const uint8_t* tile_pass, const G2A* h_aff,
@@ -43,7 +43,8 @@ hipError_t launch_rlc_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t*
                              const uint32_t* leaves, const uint32_t* idx, const uint8_t* shares,
                              const G1A* pk, const G2A* h_aff, const Line* h_lines,
                              const G2A* w_aff, const Line* w_lines, int32_t* status);
-hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n, int32_t* status);
+hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                               const int32_t* h_status, const int32_t* w_status, int32_t* status);
 
 hipError_t launch_g1_decode(hipStream_t s, const uint8_t* in, uint32_t n, G1A* out,
                             int32_t* status);

@@ -96,14 +96,15 @@ __device__ bool rlc_pair_check(const G1J& S, const G1J& P, const Line* hl, bool 
 // ------------------------------------------------------------------------------ per item
 // One wave per tile: decode every share, draw r_i, compute r_i d_i and r_i pk_i (64-bit
 // double-and-add on G1, Jacobian), then reduce across the wave in LDS: 8 sub-tile sums (groups
-// of 8 lanes) and the tile sum.  Items that cannot be checked (decode error, unknown sender,
-// instance error) get their final status here and contribute the identity.
+// of 8 lanes) and the tile sum.  Items that cannot be checked (decode error, unknown sender)
+// get their final status here and contribute the identity; a ciphertext whose own H / w failed
+// to decode is resolved by k_rlc_finalize.  Needs nothing from the per-ciphertext preparation,
+// so it runs concurrently with k_g2_prepare on another stream.
 __global__ void __launch_bounds__(64) k_rlc_items(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
     const uint8_t* __restrict__ shares, const G1A* __restrict__ pk,
-    const int32_t* __restrict__ pk_status, uint32_t n_pk, const int32_t* __restrict__ h_status,
-    const int32_t* __restrict__ w_status, RlcKey key, TileSums* __restrict__ sums,
-    int32_t* __restrict__ status) {
+    const int32_t* __restrict__ pk_status, uint32_t n_pk, RlcKey key,
+    TileSums* __restrict__ sums, int32_t* __restrict__ status) {
   __shared__ G1J redS[64];
   __shared__ G1J redP[64];
   const Tile tile = tiles[blockIdx.x];
@@ -114,11 +115,8 @@ __global__ void __launch_bounds__(64) k_rlc_items(
   jac_set_inf(P);
   if (lane < tile.count) {
     int32_t st = HBTC_RLC_PENDING;
-    const uint32_t k = tile.inst;
     const uint32_t id = idx[item];
-    if (h_status[k] != HBTC_ACCEPT || w_status[k] != HBTC_ACCEPT) {
-      st = HBTC_INSTANCE_ERR;
-    } else if (id >= n_pk) {
+    if (id >= n_pk) {
       st = HBTC_UNKNOWN_SENDER;
     } else if (pk_status[id] != HBTC_ACCEPT) {
       st = HBTC_DECODE_ERR;
@@ -185,13 +183,21 @@ __global__ void __launch_bounds__(64) k_rlc_check_groups(
     const uint32_t* __restrict__ inst_tiles, const TileSums* __restrict__ sums,
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
     const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
+    const int32_t* __restrict__ h_status, const int32_t* __restrict__ w_status,
     uint8_t* __restrict__ inst_pass, uint8_t* __restrict__ tile_pass) {
   const uint32_t g = blockIdx.x * 64 + threadIdx.x;
   if (g >= n_inst + n_tiles) return;
   G1J S, P;
-  uint32_t k;
+  uint32_t k = g < n_inst ? g : tiles[g - n_inst].inst;
+  if (h_status[k] != HBTC_ACCEPT || w_status[k] != HBTC_ACCEPT) {
+    // undecodable H / w: no group work; k_rlc_finalize marks the items INSTANCE_ERR
+    if (g < n_inst)
+      inst_pass[g] = 1;
+    else
+      tile_pass[g - n_inst] = 1;
+    return;
+  }
   if (g < n_inst) {
-    k = g;
     jac_set_inf(S);
     jac_set_inf(P);
     for (uint32_t t = inst_tiles[k]; t < inst_tiles[k + 1]; ++t) {
@@ -200,7 +206,6 @@ __global__ void __launch_bounds__(64) k_rlc_check_groups(
     }
   } else {
     const uint32_t t = g - n_inst;
-    k = tiles[t].inst;
     S = sums[t].S[8];
     P = sums[t].P[8];
   }
@@ -269,10 +274,19 @@ __global__ void __launch_bounds__(64) k_rlc_leaves(
 #endif  // part 7
 
 #if HBTC_IN_PART(6)
-// Every item still pending passed some group check: ACCEPT.
-__global__ void __launch_bounds__(256) k_rlc_finalize(uint32_t n, int32_t* __restrict__ status) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n && status[i] == HBTC_RLC_PENDING) status[i] = HBTC_ACCEPT;
+// Every item still pending passed some group check: ACCEPT.  Items of a ciphertext whose own
+// H / w failed to decode: INSTANCE_ERR.
+__global__ void __launch_bounds__(64) k_rlc_finalize(const Tile* __restrict__ tiles,
+                                                     const int32_t* __restrict__ h_status,
+                                                     const int32_t* __restrict__ w_status,
+                                                     int32_t* __restrict__ status) {
+  const Tile tile = tiles[blockIdx.x];
+  if (threadIdx.x >= tile.count) return;
+  const uint32_t i = tile.first + threadIdx.x;
+  if (h_status[tile.inst] != HBTC_ACCEPT || w_status[tile.inst] != HBTC_ACCEPT)
+    status[i] = HBTC_INSTANCE_ERR;
+  else if (status[i] == HBTC_RLC_PENDING)
+    status[i] = HBTC_ACCEPT;
 }
 #endif  // part 6
 
@@ -282,16 +296,17 @@ static inline uint32_t rlc_blocks(uint64_t n, uint32_t bs) { return (uint32_t)((
 #if HBTC_IN_PART(6)
 hipError_t launch_rlc_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* shares, const G1A* pk, const int32_t* pk_status,
-                            uint32_t n_pk, const int32_t* h_status, const int32_t* w_status,
-                            RlcKey key, TileSums* sums, int32_t* status) {
+                            uint32_t n_pk, RlcKey key, TileSums* sums, int32_t* status) {
   if (n_tiles == 0) return hipSuccess;
   hipLaunchKernelGGL(k_rlc_items, dim3(n_tiles), dim3(64), 0, s, tiles, idx, shares, pk, pk_status,
-                     n_pk, h_status, w_status, key, sums, status);
+                     n_pk, key, sums, status);
   return hipGetLastError();
 }
-hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n, int32_t* status) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rlc_finalize, dim3(rlc_blocks(n, 256)), dim3(256), 0, s, n, status);
+hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                               const int32_t* h_status, const int32_t* w_status, int32_t* status) {
+  if (n_tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rlc_finalize, dim3(n_tiles), dim3(64), 0, s, tiles, h_status, w_status,
+                     status);
   return hipGetLastError();
 }
 #endif  // part 6
@@ -300,12 +315,14 @@ hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n, int32_t* status) {
 hipError_t launch_rlc_check_groups(hipStream_t s, uint32_t n_inst, uint32_t n_tiles,
                                    const Tile* tiles, const uint32_t* inst_tiles,
                                    const TileSums* sums, const G2A* h_aff, const Line* h_lines,
-                                   const G2A* w_aff, const Line* w_lines, uint8_t* inst_pass,
+                                   const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
+                                   const int32_t* w_status, uint8_t* inst_pass,
                                    uint8_t* tile_pass) {
   const uint64_t n = (uint64_t)n_inst + n_tiles;
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_rlc_check_groups, dim3(rlc_blocks(n, 64)), dim3(64), 0, s, n_inst, n_tiles,
-                     tiles, inst_tiles, sums, h_aff, h_lines, w_aff, w_lines, inst_pass, tile_pass);
+                     tiles, inst_tiles, sums, h_aff, h_lines, w_aff, w_lines, h_status, w_status,
+                     inst_pass, tile_pass);
   return hipGetLastError();
 }
 hipError_t launch_rlc_sub(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const TileSums* sums,
