@@ -198,8 +198,8 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    fams = ["dec_verify", "rlc_items", "rlc_groups", "rlc_sub", "rlc_leaves", "rlc_finalize",
-            "combine", "lagrange", "prepare"]
+    fams = ["dec_verify", "rlc_items", "rlc_groups", "rlc_triage", "rlc_sub", "rlc_leaves",
+            "rlc_finalize", "combine", "lagrange", "prepare"]
     breakdown = {f: ctx.timing_read(f) for f in fams}
     leaves = ctx.rlc_last_leaves() if args.mode == "rlc" else ep.total
     mism, comb_ok, n_acc = ep.check(ctx)
@@ -220,7 +220,7 @@ def main():
     fqm_per_launch = {
         "dec_verify": consts["dec_share"]["total"] * ep.total,
         "rlc_items": consts["rlc_item"] * ep.total,
-        "rlc_groups": consts["rlc_group_check"] * (ep.n_ct + n_tiles),
+        "rlc_groups": consts["rlc_group_check"] * (ep.n_ct + 2 * n_tiles),
         "rlc_leaves": consts["dec_share"]["total"] * leaves,
         "combine": consts["g1_combine_item"] * ep.t * ep.n_ct,
     }

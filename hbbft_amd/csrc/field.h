@@ -779,6 +779,10 @@ HD bool fq12_is_one(const Fq12& a) {
   return fq2_eq(a.c0.c0, one) && fq2_is_zero(a.c0.c1) && fq2_is_zero(a.c0.c2) &&
          fq2_is_zero(a.c1.c0) && fq2_is_zero(a.c1.c1) && fq2_is_zero(a.c1.c2);
 }
+HD bool fq12_eq(const Fq12& a, const Fq12& b) {
+  return fq2_eq(a.c0.c0, b.c0.c0) && fq2_eq(a.c0.c1, b.c0.c1) && fq2_eq(a.c0.c2, b.c0.c2) &&
+         fq2_eq(a.c1.c0, b.c1.c0) && fq2_eq(a.c1.c1, b.c1.c1) && fq2_eq(a.c1.c2, b.c1.c2);
+}
 
 // Granger-Scott squaring in the cyclotomic subgroup (6 Fq2 multiplications).
 // Fq12 viewed as Fq4^3: (c0.c0, c1.c1), (c1.c0, c0.c2), (c0.c1, c1.c2).

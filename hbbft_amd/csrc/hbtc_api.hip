@@ -289,13 +289,18 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   for (int i = 0; i < 8; ++i) key.k[i] = c->rd();
   TileSums* sums;
   uint8_t *inst_pass, *tile_pass;
-  uint32_t *leaf_count, *leaves;
+  int32_t* tile_loc;
+  uint32_t *counters, *sub_list, *leaves;
   HB_TRY(wst(c, "rlc.sums", n_tiles, &sums));
   HB_TRY(wst(c, "rlc.inst_pass", n_ct, &inst_pass));
   HB_TRY(wst(c, "rlc.tile_pass", n_tiles, &tile_pass));
-  HB_TRY(wst(c, "rlc.leaf_count", 1, &leaf_count));
+  HB_TRY(wst(c, "rlc.tile_loc", n_tiles, &tile_loc));
+  HB_TRY(wst(c, "rlc.counters", 2, &counters));  // [0] leaves, [1] sub-tile list
+  HB_TRY(wst(c, "rlc.sub_list", n_tiles, &sub_list));
   HB_TRY(wst(c, "rlc.leaves", (size_t)2 * n_items, &leaves));
-  HB_CHECK(c, hipMemsetAsync(leaf_count, 0, sizeof(uint32_t), c->stream));
+  uint32_t* leaf_count = counters;
+  uint32_t* sub_count = counters + 1;
+  HB_CHECK(c, hipMemsetAsync(counters, 0, 2 * sizeof(uint32_t), c->stream));
   HB_TRY(timed(c, "rlc_items", [&] {
     return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n,
                             key, sums, d_status);
@@ -303,10 +308,15 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
   HB_TRY(timed(c, "rlc_groups", [&] {
     return launch_rlc_check_groups(c->stream, n_ct, n_tiles, tiles, inst_tiles, sums, h_aff,
-                                   h_lines, w_aff, w_lines, h_st, w_st, inst_pass, tile_pass);
+                                   h_lines, w_aff, w_lines, h_st, w_st, inst_pass, tile_pass,
+                                   tile_loc);
+  }));
+  HB_TRY(timed(c, "rlc_triage", [&] {
+    return launch_rlc_triage(c->stream, n_tiles, tiles, inst_pass, tile_pass, tile_loc, d_status,
+                             sub_count, sub_list);
   }));
   HB_TRY(timed(c, "rlc_sub", [&] {
-    return launch_rlc_sub(c->stream, n_tiles, tiles, sums, inst_pass, tile_pass, h_aff, h_lines,
+    return launch_rlc_sub(c->stream, n_tiles, sub_count, sub_list, tiles, sums, h_aff, h_lines,
                           w_aff, w_lines, d_status, leaf_count, leaves);
   }));
   HB_TRY(timed(c, "rlc_leaves", [&] {

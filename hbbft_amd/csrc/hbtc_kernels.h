@@ -20,10 +20,14 @@ constexpr int32_t HBTC_RLC_PENDING = -1;  // internal: decided by a group check 
 struct RlcKey {
   uint32_t k[8];  // ChaCha20 key, fresh from the host's random source for every call
 };
-// Partial sums of one tile: [0..7] the 8-share sub-tiles, [8] the whole tile.
+// Partial sums of one tile: [0..7] the 8-share sub-tiles, [8] the whole tile.  The weighted
+// sums carry the position of every share inside its group (0..7 in a sub-tile, 0..63 in the
+// tile): they locate a single wrong share without per-share pairings (hbtc_rlc.hip).
 struct TileSums {
-  G1J S[9];  // sum r_i d_i
-  G1J P[9];  // sum r_i pk_i
+  G1J S[9];   // sum r_i d_i
+  G1J P[9];   // sum r_i pk_i
+  G1J SW[9];  // sum pos_i r_i d_i
+  G1J PW[9];  // sum pos_i r_i pk_i
 };
 
 hipError_t launch_rlc_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
@@ -34,11 +38,16 @@ hipError_t launch_rlc_check_groups(hipStream_t s, uint32_t n_inst, uint32_t n_ti
                                    const TileSums* sums, const G2A* h_aff, const Line* h_lines,
                                    const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
                                    const int32_t* w_status, uint8_t* inst_pass,
-                                   uint8_t* tile_pass);
-hipError_t launch_rlc_sub(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const TileSums* sums,
-                          const uint8_t* inst_pass, const uint8_t* tile_pass, const G2A* h_aff,
-                          const Line* h_lines, const G2A* w_aff, const Line* w_lines,
-                          const int32_t* status, uint32_t* leaf_count, uint32_t* leaves);
+                                   uint8_t* tile_pass, int32_t* tile_loc);
+hipError_t launch_rlc_triage(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                             const uint8_t* inst_pass, const uint8_t* tile_pass,
+                             const int32_t* tile_loc, int32_t* status, uint32_t* sub_count,
+                             uint32_t* sub_list);
+hipError_t launch_rlc_sub(hipStream_t s, uint32_t max_tiles, const uint32_t* sub_count,
+                          const uint32_t* sub_list, const Tile* tiles, const TileSums* sums,
+                          const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
+                          const Line* w_lines, int32_t* status, uint32_t* leaf_count,
+                          uint32_t* leaves);
 hipError_t launch_rlc_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t* leaf_count,
                              const uint32_t* leaves, const uint32_t* idx, const uint8_t* shares,
                              const G1A* pk, const G2A* h_aff, const Line* h_lines,

@@ -1,17 +1,31 @@
 // Random-linear-combination (RLC) batch verification of DecryptionShares with hierarchical
-// fallback — the fast path behind hbtc_verify_dec_shares (PublicKeyShare::
-// verify_decryption_share, /root/reference/src/threshold_decryption.rs:159, called once per
-// share by the reference).
+// fallback and single-error location — the fast path behind hbtc_verify_dec_shares
+// (PublicKeyShare::verify_decryption_share, /root/reference/src/threshold_decryption.rs:159,
+// called once per share by the reference).
 //
-// For a group G of shares of ONE ciphertext (u, v, w), H = hash_g1_g2(u, v):
-//     every share valid  =>  e(sum_G r_i d_i, H) == e(sum_G r_i pk_i, w)
-// and, for r_i drawn uniformly from [0, 2^64) AFTER the shares are fixed (a ChaCha20 stream
-// under a fresh 256-bit host key per call), an invalid share makes the equation fail except
-// with probability <= 2^-64 per check (all points are in the prime-order subgroup: decode
-// checks it).  Decisions therefore equal the per-share decisions of the reference except with
-// probability <= 2^-64 per check; every group that fails is split, down to single shares, which
-// get the exact per-share check of k_dec_verify.  Levels:
-//     ciphertext (all its shares) -> tile (<= 64 shares, one wave) -> sub-tile (8) -> share
+// For a group G of shares of ONE ciphertext (u, v, w), H = hash_g1_g2(u, v), and
+// E_i = e(d_i, H) / e(pk_i, w) (E_i == 1 iff share i is valid):
+//     every share valid  =>  e(sum_G r_i d_i, H) * e(-sum_G r_i pk_i, w) == prod E_i^r_i == 1
+// and, for r_i drawn uniformly from a set of 2^64 scalars AFTER the shares are fixed (a ChaCha20
+// stream under a fresh 256-bit host key per call), an invalid share makes the equation fail
+// except with probability <= 2^-64 per check (every point is in the prime-order subgroup: decode
+// checks it, so E_i has order 1 or r).
+//
+// Single-error location.  Next to the plain sum the item pass also forms the position-weighted
+// sum (weights = the share's position p_i inside its group), so each group yields
+//     T = prod E_i^r_i      and      T_w = prod E_i^(p_i r_i).
+// If exactly one share b is wrong, T_w == T^(p_b): the search over p = 0..|G|-1 finds it with
+// |G|-1 GT multiplications instead of per-share pairings, and the rest of the group is valid.
+// With two or more wrong shares, T_w == T^p holds for some p only if prod_i E_i^(r_i (p_i - p))
+// == 1 with a nonzero exponent on a wrong share, i.e. with probability <= 2^-64 per p (the same
+// argument as the plain check), <= |G| 2^-64 <= 2^-58 per located group; such groups are split.
+//
+// Levels:
+//     k_rlc_check_groups  ciphertext checks + (plain, weighted) checks of every 64-share tile;
+//                         a failing tile with one wrong share is located right there
+//     k_rlc_triage        failing, unlocated tiles -> compact list
+//     k_rlc_sub           (plain, weighted) checks of their 8-share sub-tiles, located likewise
+//     k_rlc_leaves        the exact per-share check for sub-tiles with >= 2 wrong shares
 // Work per share in the honest case: decode + two 64-bit scalar multiplications in G1
 // (r_i d_i, r_i pk_i) + a share of the wave's reduction tree; the pairing work is per group.
 #include "hbtc_kernels.h"
@@ -76,37 +90,110 @@ struct RlcTableLines {
   __device__ __forceinline__ void load(Line& out, int j) const { out = l[j]; }
 };
 
-// e(S, H) * e(-P, w) == 1 for aggregated Jacobian S, P (per-lane instance: vector line loads)
-__device__ bool rlc_pair_check(const G1J& S, const G1J& P, const Line* hl, bool h_inf,
+#if HBTC_IN_PART(7)
+// T = e(S, H) * e(-P, w) for aggregated Jacobian S, P (per-lane instance: vector line loads);
+// returns T == 1.
+__device__ bool rlc_pair_value(Fq12& e, const G1J& S, const G1J& P, const Line* hl, bool h_inf,
                                const Line* wl, bool w_inf) {
   G1A s, p;
   jac_to_aff(s, S);
   jac_to_aff(p, P);
   const bool use1 = !s.inf && !h_inf, use2 = !p.inf && !w_inf;
-  if (!use1 && !use2) return true;
+  if (!use1 && !use2) {
+    fq12_one(e);
+    return true;
+  }
   G1A np;
   aff_neg(np, p);
-  Fq12 f, e;
+  Fq12 f;
   miller_loop_2(f, RlcTableLines{hl}, s, use1, RlcTableLines{wl}, np, use2);
   final_exponentiation(e, f);
   return fq12_is_one(e);
 }
 
+// Exchange a GT value with the partner lane (lane ^ 1) of the wave.
+__device__ __forceinline__ void fq_shfl_xor1(Fq& r, const Fq& a) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = (uint32_t)__shfl_xor((int)a.v[i], 1);
+}
+__device__ __forceinline__ void fq12_shfl_xor1(Fq12& r, const Fq12& a) {
+  fq_shfl_xor1(r.c0.c0.c0, a.c0.c0.c0);
+  fq_shfl_xor1(r.c0.c0.c1, a.c0.c0.c1);
+  fq_shfl_xor1(r.c0.c1.c0, a.c0.c1.c0);
+  fq_shfl_xor1(r.c0.c1.c1, a.c0.c1.c1);
+  fq_shfl_xor1(r.c0.c2.c0, a.c0.c2.c0);
+  fq_shfl_xor1(r.c0.c2.c1, a.c0.c2.c1);
+  fq_shfl_xor1(r.c1.c0.c0, a.c1.c0.c0);
+  fq_shfl_xor1(r.c1.c0.c1, a.c1.c0.c1);
+  fq_shfl_xor1(r.c1.c1.c0, a.c1.c1.c0);
+  fq_shfl_xor1(r.c1.c1.c1, a.c1.c1.c1);
+  fq_shfl_xor1(r.c1.c2.c0, a.c1.c2.c0);
+  fq_shfl_xor1(r.c1.c2.c1, a.c1.c2.c1);
+}
+
+// Smallest p < count with Tw == T^p, or -1 (T != 1: the group failed).
+__device__ __attribute__((noinline)) int32_t rlc_locate(const Fq12& T, const Fq12& Tw,
+                                                        uint32_t count) {
+  Fq12 acc;
+  fq12_one(acc);
+  for (uint32_t p = 0; p < count; ++p) {
+    if (fq12_eq(acc, Tw)) return (int32_t)p;
+    fq12_mul(acc, acc, T);
+  }
+  return -1;
+}
+#endif  // part 7
+
 #if HBTC_IN_PART(6)
 // ------------------------------------------------------------------------------ per item
+// Tree reduction of the per-lane points q over the wave (lane = position in the tile): the sum
+// A and the position-weighted sum B of every aligned group of 8 (-> outA/outB[0..7]) and of the
+// tile (-> [8]).  Merging halves of size s:  A = A_l + A_r,  B = B_l + B_r + s A_r.
+__device__ void rlc_reduce(G1J* redA, G1J* redB, const G1J& q, uint32_t lane, G1J* outA,
+                           G1J* outB) {
+  G1J z;
+  jac_set_inf(z);
+  redA[lane] = q;
+  redB[lane] = z;
+  __syncthreads();
+  for (uint32_t s = 1; s < 64; s <<= 1) {
+    if ((lane & (2 * s - 1)) == 0) {
+      G1J a = redA[lane], ar = redA[lane + s];
+      G1J b = redB[lane], br = redB[lane + s];
+      jac_add(b, b, br);
+      G1J sa = ar;
+      for (uint32_t d = 1; d < s; d <<= 1) jac_dbl(sa, sa);
+      jac_add(b, b, sa);
+      jac_add(a, a, ar);
+      redA[lane] = a;
+      redB[lane] = b;
+    }
+    __syncthreads();
+    if (s == 4 && (lane & 7) == 0) {
+      outA[lane >> 3] = redA[lane];
+      outB[lane >> 3] = redB[lane];
+    }
+  }
+  if (lane == 0) {
+    outA[8] = redA[0];
+    outB[8] = redB[0];
+  }
+  __syncthreads();  // the arrays are reused by the next reduction
+}
+
 // One wave per tile: decode every share, draw r_i, compute r_i d_i and r_i pk_i (64-bit
-// double-and-add on G1, Jacobian), then reduce across the wave in LDS: 8 sub-tile sums (groups
-// of 8 lanes) and the tile sum.  Items that cannot be checked (decode error, unknown sender)
-// get their final status here and contribute the identity; a ciphertext whose own H / w failed
-// to decode is resolved by k_rlc_finalize.  Needs nothing from the per-ciphertext preparation,
-// so it runs concurrently with k_g2_prepare on another stream.
+// double-and-add on G1, Jacobian), then the plain and weighted group sums.  Items that cannot
+// be checked (decode error, unknown sender) get their final status here and contribute the
+// identity; a ciphertext whose own H / w failed to decode is resolved by k_rlc_finalize.
+// Needs nothing from the per-ciphertext preparation, so it runs concurrently with
+// k_g2_prepare on another stream.
 __global__ void __launch_bounds__(64) k_rlc_items(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
     const uint8_t* __restrict__ shares, const G1A* __restrict__ pk,
     const int32_t* __restrict__ pk_status, uint32_t n_pk, RlcKey key,
     TileSums* __restrict__ sums, int32_t* __restrict__ status) {
-  __shared__ G1J redS[64];
-  __shared__ G1J redP[64];
+  __shared__ G1J redA[64];
+  __shared__ G1J redB[64];
   const Tile tile = tiles[blockIdx.x];
   const uint32_t lane = threadIdx.x;
   const size_t item = (size_t)tile.first + lane;
@@ -134,111 +221,141 @@ __global__ void __launch_bounds__(64) k_rlc_items(
     }
     status[item] = st;
   }
-  redS[lane] = S;
-  redP[lane] = P;
-  __syncthreads();
-  // groups of 8 -> sub-tile sums
-  for (uint32_t s = 1; s < 8; s <<= 1) {
-    if ((lane & (2 * s - 1)) == 0) {
-      G1J a = redS[lane], b = redS[lane + s];
-      jac_add(a, a, b);
-      redS[lane] = a;
-      G1J c = redP[lane], d = redP[lane + s];
-      jac_add(c, c, d);
-      redP[lane] = c;
-    }
-    __syncthreads();
-  }
   TileSums* ts = sums + blockIdx.x;
-  if ((lane & 7) == 0) {
-    ts->S[lane >> 3] = redS[lane];
-    ts->P[lane >> 3] = redP[lane];
-  }
-  for (uint32_t s = 8; s < 64; s <<= 1) {
-    if ((lane & (2 * s - 1)) == 0) {
-      G1J a = redS[lane], b = redS[lane + s];
-      jac_add(a, a, b);
-      redS[lane] = a;
-      G1J c = redP[lane], d = redP[lane + s];
-      jac_add(c, c, d);
-      redP[lane] = c;
-    }
-    __syncthreads();
-  }
-  if (lane == 0) {
-    ts->S[8] = redS[0];
-    ts->P[8] = redP[0];
-  }
+  rlc_reduce(redA, redB, S, lane, ts->S, ts->SW);
+  rlc_reduce(redA, redB, P, lane, ts->P, ts->PW);
 }
 #endif  // part 6
 
 #if HBTC_IN_PART(7)
 // ------------------------------------------------------------------------------ group checks
-// Lanes [0, n_inst): ciphertext-level checks (sum of the instance's tile sums).
-// Lanes [n_inst, n_inst + n_tiles): tile-level checks — run together with the ciphertext level
-// (one round of pairing latency instead of two); a tile whose ciphertext passes is resolved
-// by the ciphertext verdict in k_rlc_sub.
+// Lanes [0, 2 n_tiles): tile g/2, plain (g even) and weighted (g odd) sums — partners in one
+// wave.  Lanes [2 n_tiles, 2 n_tiles + n_inst): ciphertext-level checks (sum of the tile sums).
+// All run in one launch (one round of pairing latency); a tile whose ciphertext passes is
+// resolved by the ciphertext verdict in k_rlc_triage.
 __global__ void __launch_bounds__(64) k_rlc_check_groups(
     uint32_t n_inst, uint32_t n_tiles, const Tile* __restrict__ tiles,
     const uint32_t* __restrict__ inst_tiles, const TileSums* __restrict__ sums,
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
     const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
     const int32_t* __restrict__ h_status, const int32_t* __restrict__ w_status,
-    uint8_t* __restrict__ inst_pass, uint8_t* __restrict__ tile_pass) {
+    uint8_t* __restrict__ inst_pass, uint8_t* __restrict__ tile_pass,
+    int32_t* __restrict__ tile_loc) {
   const uint32_t g = blockIdx.x * 64 + threadIdx.x;
-  if (g >= n_inst + n_tiles) return;
+  const uint32_t n_tl = 2 * n_tiles;
+  const bool active = g < n_tl + n_inst;
+  const bool is_tile = g < n_tl;
+  const bool weighted = (g & 1u) != 0;
+  const uint32_t t = g >> 1;
+  uint32_t k = 0, count = 0;
+  bool inst_ok = false;
   G1J S, P;
-  uint32_t k = g < n_inst ? g : tiles[g - n_inst].inst;
-  if (h_status[k] != HBTC_ACCEPT || w_status[k] != HBTC_ACCEPT) {
-    // undecodable H / w: no group work; k_rlc_finalize marks the items INSTANCE_ERR
-    if (g < n_inst)
-      inst_pass[g] = 1;
-    else
-      tile_pass[g - n_inst] = 1;
+  jac_set_inf(S);
+  jac_set_inf(P);
+  if (active) {
+    if (is_tile) {
+      const Tile tile = tiles[t];
+      k = tile.inst;
+      count = tile.count;
+    } else {
+      k = g - n_tl;
+    }
+    inst_ok = h_status[k] == HBTC_ACCEPT && w_status[k] == HBTC_ACCEPT;
+    if (inst_ok) {
+      if (is_tile) {
+        S = weighted ? sums[t].SW[8] : sums[t].S[8];
+        P = weighted ? sums[t].PW[8] : sums[t].P[8];
+      } else {
+        for (uint32_t u = inst_tiles[k]; u < inst_tiles[k + 1]; ++u) {
+          jac_add(S, S, sums[u].S[8]);
+          jac_add(P, P, sums[u].P[8]);
+        }
+      }
+    }
+  }
+  Fq12 e;
+  bool ok = true;
+  if (active && inst_ok)
+    ok = rlc_pair_value(e, S, P, h_lines + (size_t)k * MILLER_STEPS, h_aff[k].inf != 0,
+                        w_lines + (size_t)k * MILLER_STEPS, w_aff[k].inf != 0);
+  else
+    fq12_one(e);
+  Fq12 ew;
+  fq12_shfl_xor1(ew, e);  // the plain lane receives its partner's weighted value
+  if (!active) return;
+  // undecodable H / w: no group work; k_rlc_finalize marks the items INSTANCE_ERR
+  if (!is_tile) {
+    inst_pass[k] = (ok || !inst_ok) ? 1 : 0;
     return;
   }
-  if (g < n_inst) {
-    jac_set_inf(S);
-    jac_set_inf(P);
-    for (uint32_t t = inst_tiles[k]; t < inst_tiles[k + 1]; ++t) {
-      jac_add(S, S, sums[t].S[8]);
-      jac_add(P, P, sums[t].P[8]);
-    }
-  } else {
-    const uint32_t t = g - n_inst;
-    S = sums[t].S[8];
-    P = sums[t].P[8];
-  }
-  const bool ok = rlc_pair_check(S, P, h_lines + (size_t)k * MILLER_STEPS, h_aff[k].inf != 0,
-                                 w_lines + (size_t)k * MILLER_STEPS, w_aff[k].inf != 0);
-  if (g < n_inst)
-    inst_pass[g] = ok;
-  else
-    tile_pass[g - n_inst] = ok;
+  if (weighted) return;
+  tile_pass[t] = (ok || !inst_ok) ? 1 : 0;
+  tile_loc[t] = (ok || !inst_ok) ? -1 : rlc_locate(e, ew, count);
 }
 
-// One lane per (tile, sub-tile) of tiles whose ciphertext AND tile checks failed: check the
-// sub-tile sum; a failing sub-tile appends its pending items to the leaf list.
-__global__ void __launch_bounds__(64) k_rlc_sub(
-    uint32_t n_tiles, const Tile* __restrict__ tiles, const TileSums* __restrict__ sums,
-    const uint8_t* __restrict__ inst_pass, const uint8_t* __restrict__ tile_pass,
-    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
-    const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
-    const int32_t* __restrict__ status, uint32_t* __restrict__ leaf_count,
-    uint32_t* __restrict__ leaves) {
-  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
-  if (g >= n_tiles * 8) return;
-  const uint32_t t = g >> 3, sub = g & 7;
+// One lane per tile: a tile whose ciphertext AND tile checks failed either had its single
+// wrong share located (REJECT it; the rest of the tile is valid) or goes to the sub-tile list.
+__global__ void __launch_bounds__(64) k_rlc_triage(
+    uint32_t n_tiles, const Tile* __restrict__ tiles, const uint8_t* __restrict__ inst_pass,
+    const uint8_t* __restrict__ tile_pass, const int32_t* __restrict__ tile_loc,
+    int32_t* __restrict__ status, uint32_t* __restrict__ sub_count,
+    uint32_t* __restrict__ sub_list) {
+  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= n_tiles) return;
   const Tile tile = tiles[t];
   if (inst_pass[tile.inst] || tile_pass[t]) return;
-  if (sub * 8 >= tile.count) return;
-  const uint32_t k = tile.inst;
-  const bool ok = rlc_pair_check(sums[t].S[sub], sums[t].P[sub], h_lines + (size_t)k * MILLER_STEPS,
-                                 h_aff[k].inf != 0, w_lines + (size_t)k * MILLER_STEPS,
-                                 w_aff[k].inf != 0);
-  if (ok) return;
-  const uint32_t lo = tile.first + sub * 8;
-  const uint32_t hi = min(tile.first + tile.count, lo + 8);
+  const int32_t loc = tile_loc[t];
+  if (loc >= 0 && status[tile.first + loc] == HBTC_RLC_PENDING) {
+    status[tile.first + loc] = HBTC_REJECT;
+    return;
+  }
+  sub_list[atomicAdd(sub_count, 1u)] = t;
+}
+
+// 16 lanes per listed tile: its 8 sub-tiles x (plain, weighted).  A failing sub-tile with one
+// wrong share is located; one with more appends its pending items to the leaf list.
+__global__ void __launch_bounds__(64) k_rlc_sub(
+    const uint32_t* __restrict__ sub_count, const uint32_t* __restrict__ sub_list,
+    const Tile* __restrict__ tiles, const TileSums* __restrict__ sums,
+    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
+    const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
+    int32_t* __restrict__ status, uint32_t* __restrict__ leaf_count,
+    uint32_t* __restrict__ leaves) {
+  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+  const uint32_t entry = g >> 4, sub = (g >> 1) & 7u;
+  const bool weighted = (g & 1u) != 0;
+  bool active = entry < *sub_count;
+  uint32_t k = 0, lo = 0, hi = 0;
+  G1J S, P;
+  jac_set_inf(S);
+  jac_set_inf(P);
+  if (active) {
+    const uint32_t t = sub_list[entry];
+    const Tile tile = tiles[t];
+    k = tile.inst;
+    lo = tile.first + sub * 8;
+    hi = min(tile.first + tile.count, lo + 8);
+    active = lo < hi;
+    if (active) {
+      S = weighted ? sums[t].SW[sub] : sums[t].S[sub];
+      P = weighted ? sums[t].PW[sub] : sums[t].P[sub];
+    }
+  }
+  Fq12 e;
+  bool ok = true;
+  if (active)
+    ok = rlc_pair_value(e, S, P, h_lines + (size_t)k * MILLER_STEPS, h_aff[k].inf != 0,
+                        w_lines + (size_t)k * MILLER_STEPS, w_aff[k].inf != 0);
+  else
+    fq12_one(e);
+  Fq12 ew;
+  fq12_shfl_xor1(ew, e);
+  if (!active || weighted || ok) return;
+  const int32_t loc = rlc_locate(e, ew, hi - lo);
+  if (loc >= 0 && status[lo + loc] == HBTC_RLC_PENDING) {
+    status[lo + loc] = HBTC_REJECT;
+    return;
+  }
   for (uint32_t i = lo; i < hi; ++i)
     if (status[i] == HBTC_RLC_PENDING) {
       const uint32_t pos = atomicAdd(leaf_count, 1u);
@@ -247,8 +364,8 @@ __global__ void __launch_bounds__(64) k_rlc_sub(
     }
 }
 
-// Exact per-share check for the compacted leaf list (items of failing sub-tiles): the same
-// arithmetic as k_dec_verify, with per-lane instance (vector line loads).
+// Exact per-share check for the compacted leaf list (items of sub-tiles with >= 2 wrong
+// shares): the same arithmetic as k_dec_verify, with per-lane instance (vector line loads).
 __global__ void __launch_bounds__(64) k_rlc_leaves(
     const uint32_t* __restrict__ leaf_count, const uint32_t* __restrict__ leaves,
     const uint32_t* __restrict__ idx, const uint8_t* __restrict__ shares,
@@ -317,21 +434,31 @@ hipError_t launch_rlc_check_groups(hipStream_t s, uint32_t n_inst, uint32_t n_ti
                                    const TileSums* sums, const G2A* h_aff, const Line* h_lines,
                                    const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
                                    const int32_t* w_status, uint8_t* inst_pass,
-                                   uint8_t* tile_pass) {
-  const uint64_t n = (uint64_t)n_inst + n_tiles;
+                                   uint8_t* tile_pass, int32_t* tile_loc) {
+  const uint64_t n = 2 * (uint64_t)n_tiles + n_inst;
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_rlc_check_groups, dim3(rlc_blocks(n, 64)), dim3(64), 0, s, n_inst, n_tiles,
                      tiles, inst_tiles, sums, h_aff, h_lines, w_aff, w_lines, h_status, w_status,
-                     inst_pass, tile_pass);
+                     inst_pass, tile_pass, tile_loc);
   return hipGetLastError();
 }
-hipError_t launch_rlc_sub(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const TileSums* sums,
-                          const uint8_t* inst_pass, const uint8_t* tile_pass, const G2A* h_aff,
-                          const Line* h_lines, const G2A* w_aff, const Line* w_lines,
-                          const int32_t* status, uint32_t* leaf_count, uint32_t* leaves) {
+hipError_t launch_rlc_triage(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                             const uint8_t* inst_pass, const uint8_t* tile_pass,
+                             const int32_t* tile_loc, int32_t* status, uint32_t* sub_count,
+                             uint32_t* sub_list) {
   if (n_tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rlc_sub, dim3(rlc_blocks((uint64_t)n_tiles * 8, 64)), dim3(64), 0, s, n_tiles,
-                     tiles, sums, inst_pass, tile_pass, h_aff, h_lines, w_aff, w_lines, status,
+  hipLaunchKernelGGL(k_rlc_triage, dim3(rlc_blocks(n_tiles, 64)), dim3(64), 0, s, n_tiles, tiles,
+                     inst_pass, tile_pass, tile_loc, status, sub_count, sub_list);
+  return hipGetLastError();
+}
+hipError_t launch_rlc_sub(hipStream_t s, uint32_t max_tiles, const uint32_t* sub_count,
+                          const uint32_t* sub_list, const Tile* tiles, const TileSums* sums,
+                          const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
+                          const Line* w_lines, int32_t* status, uint32_t* leaf_count,
+                          uint32_t* leaves) {
+  if (max_tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rlc_sub, dim3(rlc_blocks((uint64_t)max_tiles * 16, 64)), dim3(64), 0, s,
+                     sub_count, sub_list, tiles, sums, h_aff, h_lines, w_aff, w_lines, status,
                      leaf_count, leaves);
   return hipGetLastError();
 }

@@ -153,8 +153,10 @@ int hbtc_combine_sigs_dev(hbtc_ctx* ctx, uint32_t n_inst, const uint32_t* offset
 /* ---- verification strategy ----------------------------------------------------------------- */
 /* HBTC_MODE_RLC (default): shares of one instance are checked together by a random linear
  * combination (fresh 64-bit ChaCha20 scalars per call, prime-order points only), failing groups
- * are split ciphertext -> 64 -> 8 -> 1 share, single shares get the exact pairing check.  The
- * decisions equal the per-share decisions except with probability <= 2^-64 per group check.
+ * are split ciphertext -> 64 -> 8 -> 1 share; a group with exactly one wrong share is resolved
+ * by a position-weighted second combination (the wrong share located without per-share
+ * pairings), the rest get the exact pairing check.  The decisions equal the per-share decisions
+ * except with probability <= 2^-64 per group check (<= 2^-58 per located group).
  * HBTC_MODE_PER_SHARE: every share gets its own 2-pair pairing check (the reference's count).
  * Applies to hbtc_verify_dec_shares[_dev]. */
 #define HBTC_MODE_PER_SHARE 0
@@ -165,7 +167,7 @@ int hbtc_rlc_last_leaves(hbtc_ctx* ctx, uint32_t* leaves);
 
 /* ---- kernel timing (HIP events on the context's stream) ---------------------------------- */
 /* Families: "prepare", "dec_verify", "sig_verify", "pair_verify", "lagrange", "combine",
- * "mul", "rlc_items", "rlc_groups", "rlc_sub", "rlc_leaves", "rlc_finalize".  Reading
+ * "mul", "rlc_items", "rlc_groups", "rlc_triage", "rlc_sub", "rlc_leaves", "rlc_finalize".  Reading
  * synchronises the stream. */
 int hbtc_timing_enable(hbtc_ctx* ctx, int enable);
 int hbtc_timing_read(hbtc_ctx* ctx, const char* family, double* total_ms, uint64_t* launches);

@@ -109,7 +109,9 @@ int main() {
   const unsigned long long comb2 = hbtc_fqm_count;
 
   // RLC item: decode + r*d + r*pk (64-bit double-and-add, r with 32 of 64 bits set, the mean)
-  // + the two reduction-tree additions the item's lane performs on average (63 adds / 64 lanes)
+  // + the item's share of the plain + position-weighted reduction tree of its tile: per side
+  // 3 * 63 Jacobian additions and 57 doublings (merges of halves of size s cost 3 adds and
+  // log2(s) doublings), two sides, over 64 items
   hbtc_fqm_count = 0;
   G1A d2;
   g1_decompress(d2, w1);
@@ -117,10 +119,15 @@ int main() {
   G1J rd, rp;
   jac_mul_u64(rd, d2, r64);
   jac_mul_u64(rp, gen1, r64);
+  const unsigned long long rlc_item_mults = hbtc_fqm_count;
+  hbtc_fqm_count = 0;
   G1J ts;
   jac_add(ts, rd, rp);
-  jac_add(ts, ts, rd);
-  const unsigned long long rlc_item = hbtc_fqm_count;
+  const unsigned long long jadd = hbtc_fqm_count;
+  hbtc_fqm_count = 0;
+  jac_dbl(ts, ts);
+  const unsigned long long jdbl = hbtc_fqm_count;
+  const unsigned long long rlc_item = rlc_item_mults + (2 * (189 * jadd + 57 * jdbl) + 63) / 64;
   // group check: two normalisations + 2-pair Miller loop + final exponentiation
   hbtc_fqm_count = 0;
   G1A sa, pa;
