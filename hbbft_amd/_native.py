@@ -9,7 +9,9 @@ import os
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libhbtc.so")
+# HBTC_LIB_PATH selects another build of the same library (kernel-variant experiments)
+LIB_PATH = os.environ.get("HBTC_LIB_PATH") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "libhbtc.so")
 
 # ---- status codes (include/hbtc.h) ------------------------------------------------------------
 ACCEPT = 0

@@ -261,6 +261,30 @@ HDN void jac_mul_u64(Jac<F>& r, const Aff<F>& q, uint64_t k) {
   r = acc;
 }
 
+// [a] p + [b] q for 32-bit a, b (joint MSB-first double-and-add, p and q affine)
+template <class F>
+HDN void jac_mul2_u32(Jac<F>& r, const Aff<F>& p, uint32_t a, const Aff<F>& q, uint32_t b) {
+  Jac<F> acc;
+  jac_set_inf(acc);
+  const uint32_t m = a | b;
+  const int top = m ? 31 - __builtin_clz(m) : -1;
+  for (int bit = top; bit >= 0; --bit) {
+    jac_dbl(acc, acc);
+    if ((a >> bit) & 1u) jac_add_aff(acc, acc, p);
+    if ((b >> bit) & 1u) jac_add_aff(acc, acc, q);
+  }
+  r = acc;
+}
+
+// GLV endomorphism of G1: phi(x, y) = (beta x, y) = [-x^2] (x, y) on the r-order subgroup
+HD void g1_phi(G1A& r, const G1A& p) {
+  Fq beta;
+  fq_set(beta, G1_BETA);
+  fq_mul(r.x, p.x, beta);
+  r.y = p.y;
+  r.inf = p.inf;
+}
+
 // [k] q for a Jacobian base and 64-bit k
 template <class F>
 HDN void jac_mul_u64_jac(Jac<F>& r, const Jac<F>& q, uint64_t k) {

@@ -24,6 +24,7 @@ struct DevBuf {
 struct Keyset {
   G1A* pk = nullptr;
   int32_t* st = nullptr;
+  PtXY* tab = nullptr;  // fixed-base tables (n * PK_TAB_WIN * 256 points, ~98 KB per share)
   uint32_t n = 0;
 };
 
@@ -302,8 +303,8 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   uint32_t* sub_count = counters + 1;
   HB_CHECK(c, hipMemsetAsync(counters, 0, 2 * sizeof(uint32_t), c->stream));
   HB_TRY(timed(c, "rlc_items", [&] {
-    return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n,
-                            key, sums, d_status);
+    return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->tab,
+                            ks->n, key, sums, d_status);
   }));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
   HB_TRY(timed(c, "rlc_groups", [&] {
@@ -470,6 +471,7 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
   for (auto& kv : c->keysets) {
     (void)hipFree(kv.second.pk);
     (void)hipFree(kv.second.st);
+    (void)hipFree(kv.second.tab);
   }
   for (Span& sp : c->spans) {
     (void)hipEventDestroy(sp.a);
@@ -503,6 +505,12 @@ int hbtc_keyset_load(hbtc_ctx* c, const uint8_t* pk_c48, uint32_t n, uint32_t* k
   HB_TRY(timed(c, "prepare", [&] {
     return launch_g1_decode(c->stream, (const uint8_t*)d_in, n, ks.pk, ks.st);
   }));
+  HB_CHECK(c, hipMalloc(&ks.tab, sizeof(PtXY) * (size_t)n * PK_TAB_WIN * 256));
+  Fq* tab_ws;
+  HB_TRY(wst(c, "pktab.ws", (size_t)n * PK_TAB_WIN * 512, &tab_ws));
+  HB_TRY(timed(c, "prepare", [&] {
+    return launch_pk_table(c->stream, ks.pk, ks.st, n, ks.tab, tab_ws);
+  }));
   std::vector<int32_t> st(n);
   HB_TRY(download(c, st.data(), ks.st, sizeof(int32_t) * n));
   HB_TRY(sync(c));
@@ -523,6 +531,7 @@ int hbtc_keyset_free(hbtc_ctx* c, uint32_t keyset_id) {
   HB_TRY(sync(c));
   (void)hipFree(it->second.pk);
   (void)hipFree(it->second.st);
+  (void)hipFree(it->second.tab);
   c->keysets.erase(it);
   return HBTC_OK;
 }

@@ -30,9 +30,20 @@ struct TileSums {
   G1J PW[9];  // sum pos_i r_i pk_i
 };
 
+// Fixed-base table of every public-key share (built once per key set, resident in HBM):
+// tab[(i * PK_TAB_WIN + w) * 256 + v] = v * 2^(8w) * pk_i (affine, v >= 1), so [a] pk_i for a
+// 32-bit a is PK_TAB_WIN = 4 mixed additions and no doublings.
+constexpr int PK_TAB_WIN = 4;
+struct PtXY {
+  Fq x, y;
+};
+
+hipError_t launch_pk_table(hipStream_t s, const G1A* pk, const int32_t* pk_status, uint32_t n,
+                           PtXY* tab, Fq* ws);
 hipError_t launch_rlc_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* shares, const G1A* pk, const int32_t* pk_status,
-                            uint32_t n_pk, RlcKey key, TileSums* sums, int32_t* status);
+                            const PtXY* pk_tab, uint32_t n_pk, RlcKey key, TileSums* sums,
+                            int32_t* status);
 hipError_t launch_rlc_check_groups(hipStream_t s, uint32_t n_inst, uint32_t n_tiles,
                                    const Tile* tiles, const uint32_t* inst_tiles,
                                    const TileSums* sums, const G2A* h_aff, const Line* h_lines,

@@ -106,6 +106,59 @@ __global__ void __launch_bounds__(64) k_g2_prepare(const uint8_t* __restrict__ i
   }
 }
 
+// Fixed-base tables of the key set (PK_TAB_WIN windows of 8 bits): one lane per (share i,
+// window w) walks v * B for B = 2^(8w) pk_i, v = 1..255, in Jacobian coordinates and
+// normalises the 255 points with one batched inversion (ws: 512 Fq per lane).
+__global__ void __launch_bounds__(64) k_pk_table(const G1A* __restrict__ pk,
+                                                 const int32_t* __restrict__ pk_status,
+                                                 uint32_t n, PtXY* __restrict__ tab,
+                                                 Fq* __restrict__ ws) {
+  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+  if (g >= n * PK_TAB_WIN) return;
+  const uint32_t i = g / PK_TAB_WIN, win = g % PK_TAB_WIN;
+  PtXY* out = tab + (size_t)g * 256;
+  Fq* zs = ws + (size_t)g * 512;  // [0, 256): Z_v, [256, 512): prefix products
+  const G1A p = pk[i];
+  if (pk_status[i] != HBTC_ACCEPT || p.inf) return;  // never read (items check pk first)
+  G1J b;
+  jac_from_aff(b, p);
+  for (uint32_t j = 0; j < 8 * win; ++j) jac_dbl(b, b);
+  G1A base;
+  jac_to_aff(base, b);
+  G1J acc;
+  jac_set_inf(acc);
+  Fq pre;
+  fq_one(pre);
+  for (int v = 1; v < 256; ++v) {
+    jac_add_aff(acc, acc, base);  // v B != O: v 2^(8w) < r
+    out[v].x = acc.x;
+    out[v].y = acc.y;
+    zs[v] = acc.z;
+    fq_mul(pre, pre, acc.z);
+    zs[256 + v] = pre;
+  }
+  Fq inv;
+  fq_inv(inv, pre);
+  for (int v = 255; v >= 1; --v) {
+    Fq zi, zi2, t;
+    if (v > 1)
+      fq_mul(zi, inv, zs[256 + v - 1]);
+    else
+      zi = inv;
+    fq_mul(inv, inv, zs[v]);
+    fq_sqr(zi2, zi);
+    PtXY e = out[v];
+    fq_mul(t, e.x, zi2);
+    fq_canon(e.x, t);
+    fq_mul(zi2, zi2, zi);
+    fq_mul(t, e.y, zi2);
+    fq_canon(e.y, t);
+    out[v] = e;
+  }
+  fq_zero(out[0].x);
+  fq_zero(out[0].y);
+}
+
 #endif  // part 1
 
 // ------------------------------------------------------------------------------ share checks
@@ -400,6 +453,14 @@ hipError_t launch_g1_decode(hipStream_t s, const uint8_t* in, uint32_t n, G1A* o
                             int32_t* status) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_g1_decode, dim3(blocks_for(n, 64)), dim3(64), 0, s, in, n, out, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_pk_table(hipStream_t s, const G1A* pk, const int32_t* pk_status, uint32_t n,
+                           PtXY* tab, Fq* ws) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pk_table, dim3(blocks_for((uint64_t)n * PK_TAB_WIN, 64)), dim3(64), 0, s, pk,
+                     pk_status, n, tab, ws);
   return hipGetLastError();
 }
 

@@ -26,8 +26,9 @@
 //     k_rlc_triage        failing, unlocated tiles -> compact list
 //     k_rlc_sub           (plain, weighted) checks of their 8-share sub-tiles, located likewise
 //     k_rlc_leaves        the exact per-share check for sub-tiles with >= 2 wrong shares
-// Work per share in the honest case: decode + two 64-bit scalar multiplications in G1
-// (r_i d_i, r_i pk_i) + a share of the wave's reduction tree; the pairing work is per group.
+// Work per share in the honest case: decode + r_i d_i (a joint 32-bit double-and-add through
+// the GLV endomorphism) + r_i pk_i (8 mixed additions from the key set's fixed-base table) + a
+// share of the wave's reduction tree; the pairing work is per group.
 #include "hbtc_kernels.h"
 
 #ifndef HBTC_PART
@@ -89,6 +90,10 @@ struct RlcTableLines {
   const Line* l;
   __device__ __forceinline__ void load(Line& out, int j) const { out = l[j]; }
 };
+
+#ifndef HBTC_CHECK_WAVES
+#define HBTC_CHECK_WAVES 1  // minimum waves per SIMD for the pairing-check kernels
+#endif
 
 #if HBTC_IN_PART(7)
 // T = e(S, H) * e(-P, w) for aggregated Jacobian S, P (per-lane instance: vector line loads);
@@ -181,17 +186,48 @@ __device__ void rlc_reduce(G1J* redA, G1J* redB, const G1J& q, uint32_t lane, G1
   __syncthreads();  // the arrays are reused by the next reduction
 }
 
-// One wave per tile: decode every share, draw r_i, compute r_i d_i and r_i pk_i (64-bit
-// double-and-add on G1, Jacobian), then the plain and weighted group sums.  Items that cannot
-// be checked (decode error, unknown sender) get their final status here and contribute the
-// identity; a ciphertext whose own H / w failed to decode is resolved by k_rlc_finalize.
-// Needs nothing from the per-ciphertext preparation, so it runs concurrently with
-// k_g2_prepare on another stream.
-__global__ void __launch_bounds__(64) k_rlc_items(
+// [a] pk + [b] phi(pk) from the key set's fixed-base table (8 mixed additions, no doublings).
+__device__ void rlc_pk_mul(G1J& r, const PtXY* __restrict__ tab, uint32_t a, uint32_t b) {
+  jac_set_inf(r);
+#pragma unroll
+  for (int w = 0; w < PK_TAB_WIN; ++w) {
+    const uint32_t va = (a >> (8 * w)) & 0xffu, vb = (b >> (8 * w)) & 0xffu;
+    if (va) {
+      const PtXY e = tab[w * 256 + va];
+      G1A q;
+      q.x = e.x;
+      q.y = e.y;
+      q.inf = 0;
+      jac_add_aff(r, r, q);
+    }
+    if (vb) {
+      const PtXY e = tab[w * 256 + vb];
+      G1A q, pq;
+      q.x = e.x;
+      q.y = e.y;
+      q.inf = 0;
+      g1_phi(pq, q);
+      jac_add_aff(r, r, pq);
+    }
+  }
+}
+
+// One wave per tile: decode every share, draw r_i = a_i + b_i mu (a_i, b_i the two 32-bit
+// halves of a ChaCha20 word, mu the eigenvalue of the GLV endomorphism phi: 2^64 distinct
+// residues mod r), compute r_i d_i = [a] d + [b] phi(d) (joint 32-bit
+// double-and-add) and r_i pk_i from the fixed-base table, then the plain and weighted group
+// sums.  Items that cannot be checked (decode error, unknown sender) get their final status
+// here and contribute the identity; a ciphertext whose own H / w failed to decode is resolved
+// by k_rlc_finalize.  Needs nothing from the per-ciphertext preparation, so it runs
+// concurrently with k_g2_prepare on another stream.
+#ifndef HBTC_ITEMS_WAVES
+#define HBTC_ITEMS_WAVES 1  // minimum waves per SIMD the register allocation must allow
+#endif
+__global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
     const uint8_t* __restrict__ shares, const G1A* __restrict__ pk,
-    const int32_t* __restrict__ pk_status, uint32_t n_pk, RlcKey key,
-    TileSums* __restrict__ sums, int32_t* __restrict__ status) {
+    const int32_t* __restrict__ pk_status, const PtXY* __restrict__ pk_tab, uint32_t n_pk,
+    RlcKey key, TileSums* __restrict__ sums, int32_t* __restrict__ status) {
   __shared__ G1J redA[64];
   __shared__ G1J redB[64];
   const Tile tile = tiles[blockIdx.x];
@@ -215,8 +251,11 @@ __global__ void __launch_bounds__(64) k_rlc_items(
         st = HBTC_DECODE_ERR;
       } else {
         const uint64_t r = rlc_scalar(key, item);
-        jac_mul_u64(S, d, r);
-        jac_mul_u64(P, pk[id], r);
+        const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
+        G1A pd;
+        g1_phi(pd, d);
+        jac_mul2_u32(S, d, ra, pd, rb);
+        if (!pk[id].inf) rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb);
       }
     }
     status[item] = st;
@@ -233,7 +272,7 @@ __global__ void __launch_bounds__(64) k_rlc_items(
 // wave.  Lanes [2 n_tiles, 2 n_tiles + n_inst): ciphertext-level checks (sum of the tile sums).
 // All run in one launch (one round of pairing latency); a tile whose ciphertext passes is
 // resolved by the ciphertext verdict in k_rlc_triage.
-__global__ void __launch_bounds__(64) k_rlc_check_groups(
+__global__ void __launch_bounds__(64, HBTC_CHECK_WAVES) k_rlc_check_groups(
     uint32_t n_inst, uint32_t n_tiles, const Tile* __restrict__ tiles,
     const uint32_t* __restrict__ inst_tiles, const TileSums* __restrict__ sums,
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
@@ -314,7 +353,7 @@ __global__ void __launch_bounds__(64) k_rlc_triage(
 
 // 16 lanes per listed tile: its 8 sub-tiles x (plain, weighted).  A failing sub-tile with one
 // wrong share is located; one with more appends its pending items to the leaf list.
-__global__ void __launch_bounds__(64) k_rlc_sub(
+__global__ void __launch_bounds__(64, HBTC_CHECK_WAVES) k_rlc_sub(
     const uint32_t* __restrict__ sub_count, const uint32_t* __restrict__ sub_list,
     const Tile* __restrict__ tiles, const TileSums* __restrict__ sums,
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
@@ -366,7 +405,7 @@ __global__ void __launch_bounds__(64) k_rlc_sub(
 
 // Exact per-share check for the compacted leaf list (items of sub-tiles with >= 2 wrong
 // shares): the same arithmetic as k_dec_verify, with per-lane instance (vector line loads).
-__global__ void __launch_bounds__(64) k_rlc_leaves(
+__global__ void __launch_bounds__(64, HBTC_CHECK_WAVES) k_rlc_leaves(
     const uint32_t* __restrict__ leaf_count, const uint32_t* __restrict__ leaves,
     const uint32_t* __restrict__ idx, const uint8_t* __restrict__ shares,
     const G1A* __restrict__ pk, const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
@@ -413,10 +452,11 @@ static inline uint32_t rlc_blocks(uint64_t n, uint32_t bs) { return (uint32_t)((
 #if HBTC_IN_PART(6)
 hipError_t launch_rlc_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* shares, const G1A* pk, const int32_t* pk_status,
-                            uint32_t n_pk, RlcKey key, TileSums* sums, int32_t* status) {
+                            const PtXY* pk_tab, uint32_t n_pk, RlcKey key, TileSums* sums,
+                            int32_t* status) {
   if (n_tiles == 0) return hipSuccess;
   hipLaunchKernelGGL(k_rlc_items, dim3(n_tiles), dim3(64), 0, s, tiles, idx, shares, pk, pk_status,
-                     n_pk, key, sums, status);
+                     pk_tab, n_pk, key, sums, status);
   return hipGetLastError();
 }
 hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n_tiles, const Tile* tiles,

@@ -110,6 +110,22 @@ int ht_g1_mul(const uint8_t* in48, const uint8_t* k32, uint8_t* out48) {
   store_words(out48, w, 12);
   return 0;
 }
+// [a] P + [b] phi(P) with 32-bit a, b (the RLC item's r_i d_i, hbtc_rlc.hip)
+int ht_g1_mul_glv32(const uint8_t* in48, uint32_t a, uint32_t b, uint8_t* out48) {
+  uint32_t w[12];
+  load_words(w, in48, 12);
+  G1A p;
+  if (!g1_decompress(p, w)) return -1;
+  G1A pp;
+  g1_phi(pp, p);
+  G1J r;
+  jac_mul2_u32(r, p, a, pp, b);
+  G1A o;
+  jac_to_aff(o, r);
+  g1_compress(w, o);
+  store_words(out48, w, 12);
+  return 0;
+}
 int ht_g2_mul(const uint8_t* in96, const uint8_t* k32, uint8_t* out96) {
   uint32_t w[24];
   load_words(w, in96, 24);

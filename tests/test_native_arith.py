@@ -62,6 +62,22 @@ def test_codec_and_mul_roundtrip(ht):
         assert ht.ht_g2_mul(g2, ks, o2) == 0 and o2.raw == B.g2_compress(Q)
 
 
+def test_glv_split_scalar_of_rlc_items(ht):
+    """r_i d_i = [a] d + [b] phi(d) equals [a + b mu] d with mu = -x^2 mod r (the eigenvalue of
+    phi(x, y) = (beta x, y) on G1): the RLC scalars are a + b mu for the two 32-bit halves of a
+    ChaCha20 word, and distinct (a, b) give distinct residues mod r."""
+    rng = random.Random(5)
+    mu = (-(B.X * B.X)) % B.R
+    cases = [(0, 0), (1, 0), (0, 1), (0xffffffff, 0xffffffff), (1, 0xffffffff)]
+    cases += [(rng.getrandbits(32), rng.getrandbits(32)) for _ in range(4)]
+    ht.ht_g1_mul_glv32.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p]
+    for a, b in cases:
+        P = B.g1_mul(B.G1_GEN, rng.randrange(1, B.R))
+        o = buf(48)
+        assert ht.ht_g1_mul_glv32(B.g1_compress(P), a, b, o) == 0
+        assert o.raw == B.g1_compress(B.g1_mul(P, (a + b * mu) % B.R)), (a, b)
+
+
 def test_miller_loop_value_matches_oracle(ht):
     o = buf(576)
     assert ht.ht_miller(B.g1_compress(B.G1_GEN), B.g2_compress(B.G2_GEN), o) == 0

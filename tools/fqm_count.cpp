@@ -108,17 +108,26 @@ int main() {
   jac_add(acc2, qj, m2);
   const unsigned long long comb2 = hbtc_fqm_count;
 
-  // RLC item: decode + r*d + r*pk (64-bit double-and-add, r with 32 of 64 bits set, the mean)
+  // RLC item: decode + r*d = [a] d + [b] phi(d) (joint 32-bit double-and-add, a and b with
+  // 16 of 32 bits set, the mean) + r*pk (8 mixed additions from the fixed-base table + 4 phi)
   // + the item's share of the plain + position-weighted reduction tree of its tile: per side
   // 3 * 63 Jacobian additions and 57 doublings (merges of halves of size s cost 3 adds and
   // log2(s) doublings), two sides, over 64 items
   hbtc_fqm_count = 0;
   G1A d2;
   g1_decompress(d2, w1);
-  const uint64_t r64 = 0xa5a5a5a55a5a5a5aull;  // popcount 32
-  G1J rd, rp;
-  jac_mul_u64(rd, d2, r64);
-  jac_mul_u64(rp, gen1, r64);
+  const uint32_t ra = 0xa5a55a5au, rb = 0x5a5aa5a5u;  // popcount 16 each
+  G1J rd;
+  G1A pd;
+  g1_phi(pd, d2);
+  jac_mul2_u32(rd, d2, ra, pd, rb);
+  G1J rp = rd;  // a generic accumulator for the 4 + 4 table additions
+  for (int w = 0; w < 4; ++w) {
+    jac_add_aff(rp, rp, gen1);
+    G1A pq;
+    g1_phi(pq, gen1);
+    jac_add_aff(rp, rp, pq);
+  }
   const unsigned long long rlc_item_mults = hbtc_fqm_count;
   hbtc_fqm_count = 0;
   G1J ts;
