@@ -1,6 +1,7 @@
 # Build recipes.  The product is hbbft_amd/libhbtc.so (gfx950 HIP kernels + host C++ behind the
 # C ABI of include/hbtc.h).  The kernel file is compiled once per kernel group (HBTC_PART=1..5)
-# so the groups build in parallel (`make -j8 lib`).
+# so the groups build in parallel (`make -j8 lib`); hbtc_rlc.hip (parts 6-7) and hbtc_msm.hip
+# (parts 8-9) likewise.
 #   hosttest : the kernel arithmetic headers compiled for the HOST (tests/native, test-only)
 #   oracle   : the C restatement of threshold_crypto (oracle/c, test + CPU-baseline only)
 HIPCC ?= /opt/rocm/bin/hipcc
@@ -11,9 +12,11 @@ CSRC := hbbft_amd/csrc
 HDRS := $(wildcard $(CSRC)/*.h) include/hbtc.h
 BUILD := build
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC)
-PARTS := 1 2 3 4 5
+PARTS := 1 2 3 4
 RLC_PARTS := 6 7
-KOBJS := $(foreach p,$(PARTS),$(BUILD)/hbtc_kernels.p$(p).o) $(foreach p,$(RLC_PARTS),$(BUILD)/hbtc_rlc.p$(p).o)
+MSM_PARTS := 8 9
+KOBJS := $(foreach p,$(PARTS),$(BUILD)/hbtc_kernels.p$(p).o) $(foreach p,$(RLC_PARTS),$(BUILD)/hbtc_rlc.p$(p).o) \
+         $(foreach p,$(MSM_PARTS),$(BUILD)/hbtc_msm.p$(p).o)
 LIB := hbbft_amd/libhbtc.so
 
 .PHONY: all lib hosttest oracle clean resources roofline-constants
@@ -32,6 +35,9 @@ $(BUILD)/hbtc_rlc.p6.o: $(CSRC)/hbtc_rlc.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=6 -DHBTC_INLINE_ALL -c $< -o $@
 
 $(BUILD)/hbtc_rlc.p%.o: $(CSRC)/hbtc_rlc.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
+
+$(BUILD)/hbtc_msm.p%.o: $(CSRC)/hbtc_msm.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
 
 $(BUILD)/hbtc_api.o: $(CSRC)/hbtc_api.hip $(HDRS) | $(BUILD)

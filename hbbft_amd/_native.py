@@ -67,6 +67,10 @@ SIGNATURES = {
     "hbtc_verify_sig_shares_dev": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P]),
     "hbtc_combine_dec_dev": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P]),
     "hbtc_combine_sigs_dev": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P, _P]),
+    "hbtc_combine_dec_verified_dev": (_I32, [_P, _U32, _P, _P, _P, _P, _U32, _P, _P]),
+    "hbtc_combine_sigs_verified_dev": (_I32, [_P, _U32, _P, _P, _P, _P, _U32, _P, _P, _P]),
+    "hbtc_g1_msm": (_I32, [_P, _U32, _U32, _P, _P, _P, _P]),
+    "hbtc_g2_msm": (_I32, [_P, _U32, _U32, _P, _P, _P, _P]),
     "hbtc_set_verify_mode": (_I32, [_P, _I32]),
     "hbtc_rlc_last_leaves": (_I32, [_P, ctypes.POINTER(_U32)]),
     "hbtc_timing_enable": (_I32, [_P, _I32]),
@@ -259,6 +263,26 @@ class Context:
 
     def g2_mul(self, bases, scalars):
         return self._mul(self.lib.hbtc_g2_mul, 96, bases, scalars)
+
+    # ---- multi-scalar multiplication
+    def _msm(self, fn, size, n_msm, n, points, scalars):
+        pts = _join(points, size)
+        sc = np.frombuffer(b"".join(int(k).to_bytes(32, "little") for k in scalars),
+                           dtype=np.uint8).copy() if not isinstance(scalars, np.ndarray) else \
+            np.ascontiguousarray(scalars, dtype=np.uint8).reshape(-1)
+        if pts.size != size * n_msm * n or sc.size != 32 * n_msm * n:
+            raise ValueError("expected %d points and scalars" % (n_msm * n))
+        out = np.zeros(size * n_msm, np.uint8)
+        st = np.empty(n_msm, np.int32)
+        self._check(fn(self.h, n_msm, n, _ptr(pts), _ptr(sc), _ptr(out), _ptr(st)), "msm")
+        return [bytes(out[size * m:size * m + size]) for m in range(n_msm)], st
+
+    def g1_msm(self, n_msm, n, points, scalars):
+        """n_msm MSMs of n terms (points/scalars item-major [m][i]); returns ([48 B], status)."""
+        return self._msm(self.lib.hbtc_g1_msm, 48, n_msm, n, points, scalars)
+
+    def g2_msm(self, n_msm, n, points, scalars):
+        return self._msm(self.lib.hbtc_g2_msm, 96, n_msm, n, points, scalars)
 
     # ---- device memory (benchmarks)
     def dev_alloc(self, nbytes):

@@ -413,7 +413,7 @@ HD void fq_to_be_words(uint32_t* w, const Fq& a) {
 enum : uint32_t { FLAG_COMPRESSED = 0x80u, FLAG_INFINITY = 0x40u, FLAG_LARGEST = 0x20u };
 
 // G1Compressed::into_affine.  w = the 48 input bytes as 12 little-endian-loaded words.
-HDN bool g1_decompress(G1A& out, const uint32_t* w_in) {
+HDN bool g1_decompress(G1A& out, const uint32_t* w_in, bool check_subgroup = true) {
   uint32_t w[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) w[i] = w_in[i];
@@ -447,10 +447,10 @@ HDN bool g1_decompress(G1A& out, const uint32_t* w_in) {
   out.x = x;
   fq_canon(out.y, y);
   fq_canon(out.x, out.x);
-  return g1_in_subgroup(out);
+  return !check_subgroup || g1_in_subgroup(out);
 }
 
-HDN bool g2_decompress(G2A& out, const uint32_t* w_in) {
+HDN bool g2_decompress(G2A& out, const uint32_t* w_in, bool check_subgroup = true) {
   uint32_t w[24];
 #pragma unroll
   for (int i = 0; i < 24; ++i) w[i] = w_in[i];
@@ -486,7 +486,7 @@ HDN bool g2_decompress(G2A& out, const uint32_t* w_in) {
   fq_canon(out.x.c1, x.c1);
   fq_canon(out.y.c0, y.c0);
   fq_canon(out.y.c1, y.c1);
-  return g2_in_subgroup(out);
+  return !check_subgroup || g2_in_subgroup(out);
 }
 
 // G1Compressed::from_affine -> 12 words (to be stored little-endian => BE bytes)

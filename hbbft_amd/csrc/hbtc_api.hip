@@ -2,6 +2,7 @@
 // tables, workspaces, batch shaping (tiles) and kernel timing.  Device work lives in
 // hbtc_kernels.hip.  Every entry point validates its arguments and fails loudly (negative
 // return + hbtc_last_error) — there is no CPU fallback anywhere in the product path.
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -353,11 +354,69 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   });
 }
 
+// Window width of a batch of n-term MSMs: minimise ceil(256/c) * (mixed adds + bucket adds) in
+// Fqm (mixed add 11, full add 16, segment scaling ~15 per bit per 8 buckets).
+uint32_t msm_window(uint32_t n) {
+  uint32_t best = 4;
+  double best_cost = 1e300;
+  for (uint32_t c = 4; c <= 13; ++c) {
+    const double B = double(1u << (c - 1)), W = double((256 + c - 1) / c);
+    const double cost = W * (11.0 * n + 16.0 * B + (B / 8) * 15.0 * c) + W * c * 7.0;
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = c;
+    }
+  }
+  return best;
+}
+
+MsmPlan msm_plan(uint32_t n_msm, uint32_t n) {
+  MsmPlan p;
+  p.n_msm = n_msm;
+  p.n = n;
+  p.c = msm_window(n);
+  p.W = (256 + p.c - 1) / p.c;
+  return p;
+}
+
+// Digits, bucket lists and the bucket reduction of a planned batch (points already decoded into
+// `pts`), ordered on `st`.  `tag` prefixes the workspace names.
+template <class F>
+int msm_run(hbtc_ctx* c, hipStream_t st, const MsmPlan& p, const uint32_t* d_scalars,
+            const Aff<F>* d_pts, const uint32_t* sel_cnt, uint32_t t, const uint32_t* d_bad,
+            const uint32_t* d_dup, int32_t* d_status, uint8_t* d_out, uint8_t* d_parity) {
+  const uint64_t terms = (uint64_t)p.n_msm * p.n;
+  const uint64_t mw = (uint64_t)p.n_msm * p.W;
+  const uint32_t B = 1u << (p.c - 1), S = B / 8;
+  int16_t* d_digits;
+  uint32_t *d_list, *d_roff;
+  Jac<F>*d_part, *d_wsum;
+  HB_TRY(wst(c, "msm.digits", terms * p.W, &d_digits));
+  HB_TRY(wst(c, "msm.list", terms * p.W, &d_list));
+  HB_TRY(wst(c, "msm.roff", mw * (B + 1), &d_roff));
+  HB_TRY(ws(c, "msm.part", mw * S * sizeof(Jac<F>), (void**)&d_part));
+  HB_TRY(ws(c, "msm.wsum", mw * sizeof(Jac<F>), (void**)&d_wsum));
+  HB_TRY(timed_on(c, st, "comb_digits", [&] {
+    return launch_msm_digits(st, p, d_scalars, d_digits, d_list, d_roff);
+  }));
+  return timed_on(c, st, "combine", [&] {
+    if constexpr (sizeof(F) == sizeof(Fq))
+      return launch_msm_reduce_g1(st, p, d_pts, d_list, d_roff, d_part, d_wsum, sel_cnt, t, d_bad,
+                                  d_dup, d_status, d_out);
+    else
+      return launch_msm_reduce_g2(st, p, d_pts, d_list, d_roff, d_part, d_wsum, sel_cnt, t, d_bad,
+                                  d_dup, d_status, d_out, d_parity);
+  });
+}
+
 // Lagrange combine on s_comb: ordered after everything already on the main stream (its inputs),
-// overlapped with whatever the main stream does next.
+// overlapped with whatever the main stream does next.  The first t items of every instance are
+// combined; with d_item_status, the first t items whose status is ACCEPT (hbbft combines only
+// verified shares: coin.rs:185-191 iterates `received_shares`, td.rs:184 `shares`, both holding
+// verified shares only).
 int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets,
                 const uint32_t* d_idx, const uint8_t* d_pts, uint32_t t, uint8_t* d_out,
-                uint8_t* d_parity, int32_t* d_inst_status) {
+                uint8_t* d_parity, int32_t* d_inst_status, const int32_t* d_item_status = nullptr) {
   uint32_t n_items;
   HB_TRY(check_offsets(c, n_inst, offsets, &n_items));
   if (n_inst == 0) return HBTC_OK;
@@ -369,38 +428,42 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
   void* p;
   HB_TRY(stage_upload(c, "comb.offsets", offsets, ((size_t)n_inst + 1) * 4, sc, &p));
   uint32_t* d_off = static_cast<uint32_t*>(p);
-  // Lagrange coefficients over a dense (instance, t) grid; an instance with fewer than t
-  // items reads a zero-filled dummy window (its status is NOT_ENOUGH_SHARES regardless).
-  std::vector<uint32_t> h_first(n_inst);
-  bool any_short = false;
-  for (uint32_t k = 0; k < n_inst; ++k) {
-    const bool enough = offsets[k + 1] - offsets[k] >= t;
-    any_short |= !enough;
-    h_first[k] = enough ? offsets[k] : n_items;
-  }
-  const uint32_t* idx_for_lagrange = d_idx;
-  if (any_short) {
-    uint32_t* d_idx2;
-    HB_TRY(wst(c, "comb.idx2", (size_t)n_items + t, &d_idx2));
-    if (n_items)
-      HB_CHECK(c, hipMemcpyAsync(d_idx2, d_idx, (size_t)n_items * 4, hipMemcpyDeviceToDevice, sc));
-    HB_CHECK(c, hipMemsetAsync(d_idx2 + n_items, 0, (size_t)t * 4, sc));
-    idx_for_lagrange = d_idx2;
-  }
-  HB_TRY(stage_upload(c, "comb.first", h_first.data(), (size_t)n_inst * 4, sc, &p));
-  uint32_t* d_first = static_cast<uint32_t*>(p);
+  const uint64_t terms = (uint64_t)n_inst * t;
+  uint32_t *d_sel_pos, *d_sel_idx, *d_sel_cnt, *d_dup, *d_bad;
   Fr* d_lambda;
-  uint32_t* d_dup;
-  HB_TRY(wst(c, "comb.lambda", (size_t)n_inst * t, &d_lambda));
+  HB_TRY(wst(c, "comb.sel_pos", terms, &d_sel_pos));
+  HB_TRY(wst(c, "comb.sel_idx", terms, &d_sel_idx));
+  HB_TRY(wst(c, "comb.sel_cnt", n_inst, &d_sel_cnt));
   HB_TRY(wst(c, "comb.dup", n_inst, &d_dup));
+  HB_TRY(wst(c, "comb.bad", n_inst, &d_bad));
+  HB_TRY(wst(c, "comb.lambda", terms, &d_lambda));
   HB_CHECK(c, hipMemsetAsync(d_dup, 0, (size_t)n_inst * 4, sc));
+  HB_CHECK(c, hipMemsetAsync(d_bad, 0, (size_t)n_inst * 4, sc));
   HB_TRY(timed_on(c, sc, "lagrange", [&] {
-    return launch_lagrange(sc, d_first, n_inst, t, idx_for_lagrange, d_lambda, d_dup);
+    hipError_t e = launch_select(sc, n_inst, d_off, t, d_item_status, d_idx, d_sel_pos, d_sel_idx,
+                                 d_sel_cnt);
+    if (e != hipSuccess) return e;
+    return launch_lagrange_sel(sc, n_inst, t, d_sel_idx, d_lambda, d_dup);
   }));
-  return timed_on(c, sc, "combine", [&] {
-    return launch_combine(sc, group, n_inst, d_off, t, d_pts, d_lambda, d_dup, d_inst_status,
-                          d_out, d_parity);
-  });
+  const MsmPlan plan = msm_plan(n_inst, t);
+  if (group == 1) {
+    G1A* d_aff;
+    HB_TRY(wst(c, "comb.g1", terms, &d_aff));
+    HB_TRY(timed_on(c, sc, "comb_decode", [&] {
+      return launch_msm_decode_g1(sc, n_inst, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status, d_aff,
+                                  d_bad);
+    }));
+    return msm_run<Fq>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
+                       d_inst_status, d_out, nullptr);
+  }
+  G2A* d_aff;
+  HB_TRY(wst(c, "comb.g2", terms, &d_aff));
+  HB_TRY(timed_on(c, sc, "comb_decode", [&] {
+    return launch_msm_decode_g2(sc, n_inst, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status, d_aff,
+                                d_bad);
+  }));
+  return msm_run<Fq2>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
+                      d_inst_status, d_out, d_parity);
 }
 
 int point_mul_host(hbtc_ctx* c, int group, uint32_t n, const uint8_t* base,
@@ -738,6 +801,123 @@ int hbtc_combine_sigs_dev(hbtc_ctx* c, uint32_t n_inst, const uint32_t* offsets,
   Guard g(c);
   return combine_dev(c, 2, n_inst, offsets, d_idx, d_sig, t, d_out_sig, d_out_parity,
                      d_inst_status);
+}
+
+int hbtc_combine_dec_verified_dev(hbtc_ctx* c, uint32_t n_ct, const uint32_t* offsets,
+                                  const uint32_t* d_idx, const uint8_t* d_share,
+                                  const int32_t* d_status, uint32_t t, uint8_t* d_out_g,
+                                  int32_t* d_inst_status) {
+  if (!c || !d_status) return HBTC_ERR_ARG;
+  Guard g(c);
+  return combine_dev(c, 1, n_ct, offsets, d_idx, d_share, t, d_out_g, nullptr, d_inst_status,
+                     d_status);
+}
+
+int hbtc_combine_sigs_verified_dev(hbtc_ctx* c, uint32_t n_inst, const uint32_t* offsets,
+                                   const uint32_t* d_idx, const uint8_t* d_sig,
+                                   const int32_t* d_status, uint32_t t, uint8_t* d_out_sig,
+                                   uint8_t* d_out_parity, int32_t* d_inst_status) {
+  if (!c || !d_status) return HBTC_ERR_ARG;
+  Guard g(c);
+  return combine_dev(c, 2, n_inst, offsets, d_idx, d_sig, t, d_out_sig, d_out_parity,
+                     d_inst_status, d_status);
+}
+
+namespace {
+// k mod r for a 256-bit little-endian scalar (k < 2^256 < 3r: at most two subtractions)
+void scalar_mod_r(uint32_t* out, const uint8_t* in) {
+  static const uint32_t R[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                                0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+  uint32_t k[8];
+  memcpy(k, in, 32);
+  for (int rep = 0; rep < 2; ++rep) {
+    bool ge = true;
+    for (int i = 7; i >= 0; --i)
+      if (k[i] != R[i]) {
+        ge = k[i] > R[i];
+        break;
+      }
+    if (!ge) break;
+    uint64_t borrow = 0;
+    for (int i = 0; i < 8; ++i) {
+      const uint64_t d = (uint64_t)k[i] - R[i] - borrow;
+      k[i] = (uint32_t)d;
+      borrow = (d >> 63) & 1u;
+    }
+  }
+  memcpy(out, k, 32);
+}
+
+// Batched MSMs from host buffers, chunked over MSMs so the digit/list workspaces stay bounded.
+int msm_host(hbtc_ctx* c, int group, uint32_t n_msm, uint32_t n, const uint8_t* pts,
+             const uint8_t* scalars, uint8_t* out, int32_t* status) {
+  if (n_msm == 0) return HBTC_OK;
+  if (n == 0) return fail(c, HBTC_ERR_ARG, "n must be >= 1");
+  const size_t pb = group == 1 ? 48 : 96;
+  const MsmPlan full = msm_plan(n_msm, n);
+  const uint64_t cap_terms = (1ull << 27) / full.W;
+  const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_msm, cap_terms / n));
+  hipStream_t sc = c->s_comb;
+  HB_TRY(sync(c));
+  std::vector<uint32_t> red((size_t)chunk * n * 8), cnt(chunk, n);
+  for (uint32_t m0 = 0; m0 < n_msm; m0 += chunk) {
+    const uint32_t mc = std::min(chunk, n_msm - m0);
+    const uint64_t terms = (uint64_t)mc * n;
+    for (uint64_t i = 0; i < terms; ++i)
+      scalar_mod_r(&red[i * 8], scalars + ((uint64_t)m0 * n + i) * 32);
+    void *d_pts, *d_sc, *d_out, *d_st, *d_cnt;
+    HB_TRY(ws(c, "msm.in_pts", terms * pb, &d_pts));
+    HB_TRY(ws(c, "msm.in_sc", terms * 32, &d_sc));
+    HB_TRY(ws(c, "msm.out", (size_t)mc * pb, &d_out));
+    HB_TRY(ws(c, "msm.st", (size_t)mc * 4, &d_st));
+    HB_CHECK(c, hipMemcpyAsync(d_pts, pts + (uint64_t)m0 * n * pb, terms * pb,
+                               hipMemcpyHostToDevice, sc));
+    HB_CHECK(c, hipMemcpyAsync(d_sc, red.data(), terms * 32, hipMemcpyHostToDevice, sc));
+    HB_TRY(stage_upload(c, "msm.cnt", cnt.data(), (size_t)mc * 4, sc, &d_cnt));
+    uint32_t* d_bad;
+    HB_TRY(wst(c, "msm.bad", mc, &d_bad));
+    HB_CHECK(c, hipMemsetAsync(d_bad, 0, (size_t)mc * 4, sc));
+    const MsmPlan p = msm_plan(mc, n);
+    if (group == 1) {
+      G1A* d_aff;
+      HB_TRY(wst(c, "msm.g1", terms, &d_aff));
+      HB_TRY(timed_on(c, sc, "comb_decode", [&] {
+        return launch_msm_decode_g1(sc, mc, n, (const uint8_t*)d_pts, nullptr,
+                                    (const uint32_t*)d_cnt, nullptr, d_aff, d_bad);
+      }));
+      HB_TRY(msm_run<Fq>(c, sc, p, (const uint32_t*)d_sc, d_aff, (const uint32_t*)d_cnt, n, d_bad,
+                         nullptr, (int32_t*)d_st, (uint8_t*)d_out, nullptr));
+    } else {
+      G2A* d_aff;
+      HB_TRY(wst(c, "msm.g2", terms, &d_aff));
+      HB_TRY(timed_on(c, sc, "comb_decode", [&] {
+        return launch_msm_decode_g2(sc, mc, n, (const uint8_t*)d_pts, nullptr,
+                                    (const uint32_t*)d_cnt, nullptr, d_aff, d_bad);
+      }));
+      HB_TRY(msm_run<Fq2>(c, sc, p, (const uint32_t*)d_sc, d_aff, (const uint32_t*)d_cnt, n, d_bad,
+                          nullptr, (int32_t*)d_st, (uint8_t*)d_out, nullptr));
+    }
+    HB_CHECK(c, hipMemcpyAsync(out + (uint64_t)m0 * pb, d_out, (size_t)mc * pb,
+                               hipMemcpyDeviceToHost, sc));
+    HB_CHECK(c, hipMemcpyAsync(status + m0, d_st, (size_t)mc * 4, hipMemcpyDeviceToHost, sc));
+    HB_CHECK(c, hipStreamSynchronize(sc));
+  }
+  return HBTC_OK;
+}
+}  // namespace
+
+int hbtc_g1_msm(hbtc_ctx* c, uint32_t n_msm, uint32_t n, const uint8_t* pts_c48,
+                const uint8_t* scalars_le32, uint8_t* out_c48, int32_t* status) {
+  if (!c || (n_msm && (!pts_c48 || !scalars_le32 || !out_c48 || !status))) return HBTC_ERR_ARG;
+  Guard g(c);
+  return msm_host(c, 1, n_msm, n, pts_c48, scalars_le32, out_c48, status);
+}
+
+int hbtc_g2_msm(hbtc_ctx* c, uint32_t n_msm, uint32_t n, const uint8_t* pts_c96,
+                const uint8_t* scalars_le32, uint8_t* out_c96, int32_t* status) {
+  if (!c || (n_msm && (!pts_c96 || !scalars_le32 || !out_c96 || !status))) return HBTC_ERR_ARG;
+  Guard g(c);
+  return msm_host(c, 2, n_msm, n, pts_c96, scalars_le32, out_c96, status);
 }
 
 int hbtc_set_verify_mode(hbtc_ctx* c, int mode) {

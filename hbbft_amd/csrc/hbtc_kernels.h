@@ -84,10 +84,34 @@ hipError_t launch_pair_verify(hipStream_t s, uint32_t n, const uint8_t* a1, cons
 hipError_t launch_point_mul(hipStream_t s, int group, uint32_t n, const uint8_t* base,
                             uint32_t base_stride, const uint8_t* scalars, uint8_t* out,
                             int32_t* status);
-hipError_t launch_lagrange(hipStream_t s, const uint32_t* first, uint32_t n_inst, uint32_t t,
-                           const uint32_t* idx, Fr* lambda, uint32_t* dup);
-hipError_t launch_combine(hipStream_t s, int group, uint32_t n_inst, const uint32_t* offsets,
-                          uint32_t t, const uint8_t* pts, const Fr* lambda, const uint32_t* dup,
-                          int32_t* inst_status, uint8_t* out, uint8_t* parity);
+
+// ---- batched Pippenger MSM + Lagrange combine (hbtc_msm.hip)
+// n_msm MSMs of n terms each; signed c-bit digits over W = ceil(256 / c) windows, 2^(c-1)
+// buckets per window in segments of 8 (c >= 4).
+struct MsmPlan {
+  uint32_t n_msm, n, c, W;
+};
+hipError_t launch_select(hipStream_t s, uint32_t n_inst, const uint32_t* offsets, uint32_t t,
+                         const int32_t* status, const uint32_t* idx, uint32_t* sel_pos,
+                         uint32_t* sel_idx, uint32_t* sel_cnt);
+hipError_t launch_lagrange_sel(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_idx,
+                               Fr* lambda, uint32_t* dup);
+hipError_t launch_msm_digits(hipStream_t s, const MsmPlan& p, const uint32_t* scalars,
+                             int16_t* digits, uint32_t* list, uint32_t* roff);
+hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, const uint8_t* pts_c,
+                                const uint32_t* sel_pos, const uint32_t* sel_cnt,
+                                const int32_t* item_status, G1A* pts, uint32_t* bad);
+hipError_t launch_msm_reduce_g1(hipStream_t s, const MsmPlan& p, const G1A* pts,
+                                const uint32_t* list, const uint32_t* roff, G1J* part, G1J* wsum,
+                                const uint32_t* sel_cnt, uint32_t t, const uint32_t* bad,
+                                const uint32_t* dup, int32_t* status, uint8_t* out);
+hipError_t launch_msm_decode_g2(hipStream_t s, uint32_t n_msm, uint32_t n, const uint8_t* pts_c,
+                                const uint32_t* sel_pos, const uint32_t* sel_cnt,
+                                const int32_t* item_status, G2A* pts, uint32_t* bad);
+hipError_t launch_msm_reduce_g2(hipStream_t s, const MsmPlan& p, const G2A* pts,
+                                const uint32_t* list, const uint32_t* roff, G2J* part, G2J* wsum,
+                                const uint32_t* sel_cnt, uint32_t t, const uint32_t* bad,
+                                const uint32_t* dup, int32_t* status, uint8_t* out,
+                                uint8_t* parity);
 
 }  // namespace hbtc

@@ -338,112 +338,6 @@ template __global__ void k_point_mul<Fq2, 24>(uint32_t, const uint8_t*, uint32_t
 
 #endif  // part 1
 
-#if HBTC_IN_PART(5)
-// ------------------------------------------------------------------------------ combine
-// Lagrange coefficients at 0 of the first t abscissae x = idx + 1 of every instance:
-// lambda_i = prod_{j != i} x_j / (x_j - x_i).  One lane per (instance, i); a repeated x sets
-// the instance's duplicate flag (threshold_crypto's DuplicateEntry).
-__global__ void __launch_bounds__(256) k_lagrange(const uint32_t* __restrict__ first,
-                                                  uint32_t n_inst, uint32_t t,
-                                                  const uint32_t* __restrict__ idx,
-                                                  Fr* __restrict__ lambda,
-                                                  uint32_t* __restrict__ dup) {
-  const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (g >= (uint64_t)n_inst * t) return;
-  const uint32_t k = (uint32_t)(g / t), i = (uint32_t)(g % t);
-  const uint32_t* ix = idx + first[k];
-  const uint32_t xi_raw = ix[i];
-  Fr xi, num, den;
-  fr_from_u64(xi, (uint64_t)xi_raw + 1);
-  limbs_set_const<8>(num, FR_ONE);
-  limbs_set_const<8>(den, FR_ONE);
-  bool is_dup = false;
-  for (uint32_t j = 0; j < t; ++j) {
-    if (j == i) continue;
-    const uint32_t xj_raw = ix[j];
-    is_dup |= (xj_raw == xi_raw);
-    Fr xj, d;
-    fr_from_u64(xj, (uint64_t)xj_raw + 1);
-    fr_mul(num, num, xj);
-    fr_sub(d, xj, xi);
-    fr_mul(den, den, d);
-  }
-  if (is_dup) atomicOr(&dup[k], 1u);
-  Fr inv, l, lc;
-  fr_inv(inv, den);
-  fr_mul(l, num, inv);
-  fr_from_mont(lc, l);
-  lambda[g] = lc;
-}
-
-// sum_i lambda_i * P_i over the first t items of each instance; one workgroup per instance,
-// LDS tree reduction of Jacobian partial sums, lane 0 normalises and encodes.
-template <class F, int NW, int BS>
-__global__ void __launch_bounds__(BS) k_combine(const uint32_t* __restrict__ offsets, uint32_t t,
-                                                const uint8_t* __restrict__ pts,
-                                                const Fr* __restrict__ lambda,
-                                                const uint32_t* __restrict__ dup,
-                                                int32_t* __restrict__ inst_status,
-                                                uint8_t* __restrict__ out,
-                                                uint8_t* __restrict__ parity) {
-  __shared__ Jac<F> red[BS];
-  __shared__ uint32_t bad;
-  const uint32_t k = blockIdx.x, tid = threadIdx.x;
-  if (tid == 0) bad = 0;
-  __syncthreads();
-  const uint32_t first = offsets[k];
-  const bool enough = offsets[k + 1] - first >= t;
-  Jac<F> acc;
-  jac_set_inf(acc);
-  if (enough) {
-    for (uint32_t i = tid; i < t; i += BS) {
-      uint32_t w[NW];
-      load_words(w, pts, (size_t)first + i, NW);
-      Aff<F> p;
-      if (!pt_decompress(p, w)) {
-        atomicOr(&bad, 1u);
-        continue;
-      }
-      Jac<F> m;
-      jac_mul_fr(m, p, lambda[(size_t)k * t + i]);
-      jac_add(acc, acc, m);
-    }
-  }
-  red[tid] = acc;
-  __syncthreads();
-  for (uint32_t s = BS / 2; s > 0; s >>= 1) {
-    if (tid < s) {
-      Jac<F> a = red[tid], b = red[tid + s];
-      jac_add(a, a, b);
-      red[tid] = a;
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    const int32_t st = !enough ? HBTC_NOT_ENOUGH_SHARES
-                       : bad   ? HBTC_DECODE_ERR
-                       : dup[k] ? HBTC_DUPLICATE_ENTRY
-                                : HBTC_ACCEPT;
-    inst_status[k] = st;
-    Aff<F> a;
-    jac_to_aff(a, red[0]);
-    uint32_t w[NW];
-    pt_compress(w, a);
-    if (st != HBTC_ACCEPT)
-      for (int j = 0; j < NW; ++j) w[j] = 0;
-    store_words(out, k, w, NW);
-    if (parity) parity[k] = (st == HBTC_ACCEPT) ? (uint8_t)point_parity(a) : 0;
-  }
-}
-
-template __global__ void k_combine<Fq, 12, 256>(const uint32_t*, uint32_t, const uint8_t*,
-                                                const Fr*, const uint32_t*, int32_t*, uint8_t*,
-                                                uint8_t*);
-template __global__ void k_combine<Fq2, 24, 128>(const uint32_t*, uint32_t, const uint8_t*,
-                                                 const Fr*, const uint32_t*, int32_t*, uint8_t*,
-                                                 uint8_t*);
-
-#endif  // part 5
 
 // ------------------------------------------------------------------------------ launchers
 static inline uint32_t blocks_for(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
@@ -528,29 +422,5 @@ hipError_t launch_point_mul(hipStream_t s, int group, uint32_t n, const uint8_t*
 
 #endif  // part 1
 
-#if HBTC_IN_PART(5)
-hipError_t launch_lagrange(hipStream_t s, const uint32_t* first, uint32_t n_inst, uint32_t t,
-                           const uint32_t* idx, Fr* lambda, uint32_t* dup) {
-  const uint64_t n = (uint64_t)n_inst * t;
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_lagrange, dim3(blocks_for(n, 256)), dim3(256), 0, s, first, n_inst, t, idx,
-                     lambda, dup);
-  return hipGetLastError();
-}
-
-hipError_t launch_combine(hipStream_t s, int group, uint32_t n_inst, const uint32_t* offsets,
-                          uint32_t t, const uint8_t* pts, const Fr* lambda, const uint32_t* dup,
-                          int32_t* inst_status, uint8_t* out, uint8_t* parity) {
-  if (n_inst == 0) return hipSuccess;
-  if (group == 1)
-    hipLaunchKernelGGL((k_combine<Fq, 12, 256>), dim3(n_inst), dim3(256), 0, s, offsets, t, pts,
-                       lambda, dup, inst_status, out, parity);
-  else
-    hipLaunchKernelGGL((k_combine<Fq2, 24, 128>), dim3(n_inst), dim3(128), 0, s, offsets, t, pts,
-                       lambda, dup, inst_status, out, parity);
-  return hipGetLastError();
-}
-
-#endif  // part 5
 
 }  // namespace hbtc

@@ -1,0 +1,489 @@
+// Batched Pippenger multi-scalar multiplication on gfx950, and the Lagrange combines built on it.
+//
+// Replaces threshold_crypto's `interpolate` as called by PublicKeySet::combine_signatures
+// (src/coin.rs:190) and PublicKeySet::decrypt (src/threshold_decryption.rs:184): the reference
+// computes sum_i lambda_i * P_i with t independent 255-bit double-and-add multiplications
+// (≈ 383 group operations per term).  Here every combine is one MSM of t terms, and a batch of
+// combines (one per coin instance / ciphertext) is one launch sequence:
+//
+//   k_select     first t items of each instance (optionally: the first t ACCEPTED items, i.e.
+//                the shares hbbft would hold in its verified-share map)         1 wave / instance
+//   k_lagrange   lambda_i at 0 over the selected abscissae x = idx + 1, duplicate detection
+//   k_msm_decode decode the selected compressed points to affine (subgroup check skipped for
+//                items the verifier already accepted: it decoded and checked them)
+//   k_msm_recode signed c-bit digits of every scalar (digits in [-2^(c-1), 2^(c-1)])
+//   k_msm_sort   per (msm, window): counting sort of the terms by |digit| (bucket), largest
+//                bucket first; LDS histogram + scan, one workgroup per (msm, window)
+//   k_msm_buckets per (msm, window, 8-bucket segment): running-sum bucket reduction over the
+//                sorted list (mixed additions of affine points), = sum_b b * B_b restricted to
+//                the segment
+//   k_msm_wsum   per (msm, window): sum of its segments
+//   k_msm_final  per msm: Horner over the windows (c doublings per window), normalise, encode,
+//                instance status (+ Signature::parity for G2)
+//
+// Cost per MSM of n terms: ceil(256/c) * (n mixed adds + 2^(c-1) full adds) + 255 doublings;
+// c is chosen on the host to minimise it (n = 334: c = 6, ≈ 17k adds instead of ≈ 128k).
+// Work is spread over (msm, window, segment) threads, so a batch of 1000 combines of 334
+// terms runs ≈ 172k independent lanes.
+//
+// Data layout in HBM (all per batch, dense):
+//   pts    [m][i]         Aff<F> (canonical Montgomery x, y, infinity flag)
+//   digits [m][w][i]      int16
+//   list   [m][w][pos]    u32: term index | sign << 31, grouped by bucket, largest first
+//   roff   [m][w][r]      u32 start of bucket rank r (rank 0 = bucket 2^(c-1)), r = 0..B
+//   part   [m][w][s]      Jac<F> segment partial sums;  wsum [m][w] Jac<F>
+#include "hbtc_kernels.h"
+
+#ifndef HBTC_PART
+#define HBTC_PART 0
+#endif
+#define HBTC_IN_PART(n) (HBTC_PART == 0 || HBTC_PART == (n))
+
+namespace hbtc {
+
+namespace {
+__device__ __forceinline__ void msm_load_words(uint32_t* w, const uint8_t* base, size_t item,
+                                               int nwords) {
+  const uint4* q = reinterpret_cast<const uint4*>(base + item * (size_t)(nwords * 4));
+  for (int i = 0; i < nwords / 4; ++i) {
+    const uint4 v = q[i];
+    w[4 * i] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+}
+__device__ __forceinline__ void msm_store_words(uint8_t* base, size_t item, const uint32_t* w,
+                                                int nwords) {
+  uint4* q = reinterpret_cast<uint4*>(base + item * (size_t)(nwords * 4));
+  for (int i = 0; i < nwords / 4; ++i)
+    q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+__device__ __forceinline__ bool msm_decompress(G1A& p, const uint32_t* w, bool chk) {
+  return g1_decompress(p, w, chk);
+}
+__device__ __forceinline__ bool msm_decompress(G2A& p, const uint32_t* w, bool chk) {
+  return g2_decompress(p, w, chk);
+}
+__device__ __forceinline__ void msm_compress(uint32_t* w, const G1A& p) { g1_compress(w, p); }
+__device__ __forceinline__ void msm_compress(uint32_t* w, const G2A& p) { g2_compress(w, p); }
+__device__ __forceinline__ uint32_t msm_parity(const G1A&) { return 0; }
+__device__ __forceinline__ uint32_t msm_parity(const G2A& p) { return g2_parity(p); }
+
+// [k] p for a small k (< 2^16), Jacobian base, MSB-first
+template <class F>
+__device__ __forceinline__ void jac_mul_small(Jac<F>& r, const Jac<F>& p, uint32_t k) {
+  Jac<F> acc;
+  jac_set_inf(acc);
+  const int top = k ? 31 - __builtin_clz(k) : -1;
+  for (int b = top; b >= 0; --b) {
+    jac_dbl(acc, acc);
+    if ((k >> b) & 1u) jac_add(acc, acc, p);
+  }
+  r = acc;
+}
+}  // namespace
+
+#if HBTC_IN_PART(8)
+// ------------------------------------------------------------------ selection + Lagrange
+// The first t items of instance k in item order (the caller orders items by node index, as
+// hbbft's BTreeMap iteration does); with `status`, only items whose status is ACCEPT count.
+__global__ void __launch_bounds__(64) k_select(const uint32_t* __restrict__ offsets,
+                                               uint32_t t, const int32_t* __restrict__ status,
+                                               const uint32_t* __restrict__ idx,
+                                               uint32_t* __restrict__ sel_pos,
+                                               uint32_t* __restrict__ sel_idx,
+                                               uint32_t* __restrict__ sel_cnt) {
+  const uint32_t k = blockIdx.x, lane = threadIdx.x;
+  const uint32_t a = offsets[k], b = offsets[k + 1];
+  const size_t o = (size_t)k * t;
+  uint32_t found = 0;
+  for (uint32_t base = a; base < b && found < t; base += 64) {
+    const uint32_t i = base + lane;
+    const bool ok = i < b && (!status || status[i] == HBTC_ACCEPT);
+    const uint64_t mask = __ballot(ok);
+    const uint32_t slot = found + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    if (ok && slot < t) {
+      sel_pos[o + slot] = i;
+      sel_idx[o + slot] = idx[i];
+    }
+    found += (uint32_t)__popcll(mask);
+  }
+  const uint32_t cnt = found < t ? found : t;
+  for (uint32_t s = cnt + lane; s < t; s += 64) {
+    sel_pos[o + s] = 0xffffffffu;
+    sel_idx[o + s] = 0xffffffffu - s;  // distinct fillers: no spurious duplicate flag
+  }
+  if (lane == 0) sel_cnt[k] = cnt;
+}
+
+// lambda_i = prod_{j != i} x_j / (x_j - x_i) over the selected abscissae (dense [k][t]); one lane
+// per (instance, i).  A repeated x sets the instance's duplicate flag (DuplicateEntry).
+__global__ void __launch_bounds__(256) k_lagrange_sel(uint32_t n_inst, uint32_t t,
+                                                      const uint32_t* __restrict__ sel_idx,
+                                                      Fr* __restrict__ lambda,
+                                                      uint32_t* __restrict__ dup) {
+  const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (uint64_t)n_inst * t) return;
+  const uint32_t k = (uint32_t)(g / t), i = (uint32_t)(g % t);
+  const uint32_t* ix = sel_idx + (size_t)k * t;
+  const uint32_t xi_raw = ix[i];
+  Fr xi, num, den;
+  fr_from_u64(xi, (uint64_t)xi_raw + 1);
+  limbs_set_const<8>(num, FR_ONE);
+  limbs_set_const<8>(den, FR_ONE);
+  bool is_dup = false;
+  for (uint32_t j = 0; j < t; ++j) {
+    if (j == i) continue;
+    const uint32_t xj_raw = ix[j];
+    is_dup |= (xj_raw == xi_raw);
+    Fr xj, d;
+    fr_from_u64(xj, (uint64_t)xj_raw + 1);
+    fr_mul(num, num, xj);
+    fr_sub(d, xj, xi);
+    fr_mul(den, den, d);
+  }
+  if (is_dup) atomicOr(&dup[k], 1u);
+  Fr inv, l, lc;
+  fr_inv(inv, den);
+  fr_mul(l, num, inv);
+  fr_from_mont(lc, l);
+  lambda[g] = lc;
+}
+
+// ------------------------------------------------------------------ digits and buckets
+// Signed c-bit digits of every (canonical, < 2^255) scalar: W = ceil(256 / c) windows,
+// digit_w in [-2^(c-1), 2^(c-1)], sum_w digit_w 2^(cw) = k.
+__global__ void __launch_bounds__(256) k_msm_recode(uint64_t n_terms, uint32_t n, uint32_t c,
+                                                    uint32_t W, const uint32_t* __restrict__ sc,
+                                                    int16_t* __restrict__ digits) {
+  const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= n_terms) return;
+  const uint64_t m = g / n, i = g % n;
+  const uint32_t* k = sc + g * 8;
+  uint32_t kw[9];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) kw[j] = k[j];
+  kw[8] = 0;
+  const uint32_t mask = (1u << c) - 1u, half = 1u << (c - 1);
+  uint32_t carry = 0;
+  int16_t* out = digits + (m * W) * n + i;
+  for (uint32_t w = 0; w < W; ++w) {
+    const uint32_t bit = w * c, wi = bit >> 5, sh = bit & 31;
+    uint64_t two = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)  // static indexing: kw stays in registers
+      if ((uint32_t)j == wi) two = ((uint64_t)kw[j + 1] << 32) | kw[j];
+    uint32_t v = (uint32_t)(two >> sh) & mask;
+    v += carry;
+    int32_t d;
+    if (v > half) {
+      d = (int32_t)v - (int32_t)(1u << c);
+      carry = 1;
+    } else {
+      d = (int32_t)v;
+      carry = 0;
+    }
+    out[(size_t)w * n] = (int16_t)d;
+  }
+}
+
+// Counting sort of one (msm, window)'s n digits by bucket |d| (rank r = B - |d|), 256 threads.
+constexpr uint32_t MSM_SORT_BS = 256;
+__global__ void __launch_bounds__(MSM_SORT_BS) k_msm_sort(uint32_t n, uint32_t c,
+                                                          const int16_t* __restrict__ digits,
+                                                          uint32_t* __restrict__ list,
+                                                          uint32_t* __restrict__ roff) {
+  extern __shared__ uint32_t cnt[];  // B counters, then MSM_SORT_BS chunk sums
+  uint32_t* part = cnt + (1u << (c - 1));
+  const uint32_t B = 1u << (c - 1), tid = threadIdx.x;
+  const size_t mw = blockIdx.x;
+  const int16_t* d = digits + mw * n;
+  for (uint32_t r = tid; r < B; r += MSM_SORT_BS) cnt[r] = 0;
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += MSM_SORT_BS) {
+    const int32_t v = d[i];
+    if (v) atomicAdd(&cnt[B - (uint32_t)(v < 0 ? -v : v)], 1u);
+  }
+  __syncthreads();
+  // exclusive scan: thread tid owns ranks [tid*ch, (tid+1)*ch)
+  const uint32_t ch = (B + MSM_SORT_BS - 1) / MSM_SORT_BS;
+  const uint32_t r0 = tid * ch, r1 = min(B, r0 + ch);
+  uint32_t s = 0;
+  for (uint32_t r = r0; r < r1; ++r) s += cnt[r];
+  part[tid] = s;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (uint32_t j = 0; j < MSM_SORT_BS; ++j) {
+      const uint32_t v = part[j];
+      part[j] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  uint32_t* ro = roff + mw * (B + 1);
+  uint32_t acc = part[tid];
+  for (uint32_t r = r0; r < r1; ++r) {
+    const uint32_t v = cnt[r];
+    cnt[r] = acc;  // becomes the scatter cursor
+    ro[r] = acc;
+    acc += v;
+  }
+  if (tid == MSM_SORT_BS - 1) ro[B] = acc;  // last chunk ends at the total (empty chunks: part)
+  __syncthreads();
+  uint32_t* L = list + mw * n;
+  for (uint32_t i = tid; i < n; i += MSM_SORT_BS) {
+    const int32_t v = d[i];
+    if (v) {
+      const uint32_t pos = atomicAdd(&cnt[B - (uint32_t)(v < 0 ? -v : v)], 1u);
+      L[pos] = i | (v < 0 ? 0x80000000u : 0u);
+    }
+  }
+}
+#endif  // part 8
+
+// ------------------------------------------------------------------ group kernels
+#if HBTC_IN_PART(8) || HBTC_IN_PART(9)
+template <class F, int NW>
+__global__ void __launch_bounds__(64) k_msm_decode(uint32_t n_inst, uint32_t t,
+                                                   const uint8_t* __restrict__ pts,
+                                                   const uint32_t* __restrict__ sel_pos,
+                                                   const uint32_t* __restrict__ sel_cnt,
+                                                   const int32_t* __restrict__ status,
+                                                   Aff<F>* __restrict__ out,
+                                                   uint32_t* __restrict__ bad) {
+  const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (g >= (uint64_t)n_inst * t) return;
+  const uint32_t k = (uint32_t)(g / t), i = (uint32_t)(g % t);
+  Aff<F> p;
+  fzero(p.x);
+  fzero(p.y);
+  p.inf = 1;
+  if (i < sel_cnt[k]) {
+    const uint32_t pos = sel_pos ? sel_pos[g] : (uint32_t)g;
+    uint32_t w[NW];
+    msm_load_words(w, pts, pos, NW);
+    // an item the verifier accepted was decoded and subgroup-checked by it
+    const bool chk = !(status && status[pos] == HBTC_ACCEPT);
+    if (!msm_decompress(p, w, chk)) {
+      atomicOr(&bad[k], 1u);
+      p.inf = 1;
+    }
+  }
+  out[g] = p;
+}
+
+// One lane per (msm, window, segment of 8 buckets): running-sum reduction over the segment's
+// sorted terms.  With rank r = B - b, tot = sum_r (8s + 8 - r) B_r = sum_b (b - base) B_b and
+// run = sum_b B_b, so the segment's share of sum_b b B_b is tot + [base] run.
+template <class F>
+__global__ void __launch_bounds__(64) k_msm_buckets(uint64_t n_lanes, uint32_t n, uint32_t c,
+                                                    uint32_t W, const Aff<F>* __restrict__ pts,
+                                                    const uint32_t* __restrict__ list,
+                                                    const uint32_t* __restrict__ roff,
+                                                    Jac<F>* __restrict__ part) {
+  const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (g >= n_lanes) return;
+  const uint32_t B = 1u << (c - 1), S = B / 8;
+  const uint32_t s = (uint32_t)(g % S);
+  const uint64_t mw = g / S;
+  const uint32_t* ro = roff + mw * (B + 1);
+  const uint32_t* L = list + mw * n;
+  const Aff<F>* P = pts + (mw / W) * n;
+  Jac<F> run, tot;
+  jac_set_inf(run);
+  jac_set_inf(tot);
+  uint32_t e = ro[8 * s];
+  for (uint32_t r = 8 * s; r < 8 * s + 8; ++r) {
+    const uint32_t end = ro[r + 1];
+    for (; e < end; ++e) {
+      const uint32_t v = L[e];
+      Aff<F> q = P[v & 0x7fffffffu];
+      if (v >> 31) fneg(q.y, q.y);
+      jac_add_aff(run, run, q);
+    }
+    jac_add(tot, tot, run);
+  }
+  const uint32_t base = B - 8 * s - 8;
+  if (base) {
+    Jac<F> m;
+    jac_mul_small(m, run, base);
+    jac_add(tot, tot, m);
+  }
+  part[g] = tot;
+}
+
+template <class F>
+__global__ void __launch_bounds__(64) k_msm_wsum(uint64_t n_mw, uint32_t S,
+                                                 const Jac<F>* __restrict__ part,
+                                                 Jac<F>* __restrict__ wsum) {
+  const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (g >= n_mw) return;
+  const Jac<F>* p = part + g * S;
+  Jac<F> acc = p[0];
+  for (uint32_t s = 1; s < S; ++s) jac_add(acc, acc, p[s]);
+  wsum[g] = acc;
+}
+
+// Horner over the windows, normalise and encode.  Combine mode (sel_cnt != nullptr): the
+// instance status (NOT_ENOUGH_SHARES > DECODE_ERR > DUPLICATE_ENTRY > ACCEPT), zero bytes for a
+// failed instance and the parity bit.  MSM mode: status DECODE_ERR if any term failed to decode.
+template <class F, int NW>
+__global__ void __launch_bounds__(64) k_msm_final(uint32_t n_msm, uint32_t c, uint32_t W,
+                                                  const Jac<F>* __restrict__ wsum,
+                                                  const uint32_t* __restrict__ sel_cnt,
+                                                  uint32_t t, const uint32_t* __restrict__ bad,
+                                                  const uint32_t* __restrict__ dup,
+                                                  int32_t* __restrict__ status,
+                                                  uint8_t* __restrict__ out,
+                                                  uint8_t* __restrict__ parity) {
+  const uint32_t m = blockIdx.x * 64 + threadIdx.x;
+  if (m >= n_msm) return;
+  const Jac<F>* ws = wsum + (size_t)m * W;
+  Jac<F> acc = ws[W - 1];
+  for (int w = (int)W - 2; w >= 0; --w) {
+    for (uint32_t j = 0; j < c; ++j) jac_dbl(acc, acc);
+    jac_add(acc, acc, ws[w]);
+  }
+  int32_t st = HBTC_ACCEPT;
+  if (sel_cnt && sel_cnt[m] < t)
+    st = HBTC_NOT_ENOUGH_SHARES;
+  else if (bad[m])
+    st = HBTC_DECODE_ERR;
+  else if (dup && dup[m])
+    st = HBTC_DUPLICATE_ENTRY;
+  status[m] = st;
+  Aff<F> a;
+  jac_to_aff(a, acc);
+  uint32_t w[NW];
+  msm_compress(w, a);
+  if (st != HBTC_ACCEPT)
+    for (int j = 0; j < NW; ++j) w[j] = 0;
+  msm_store_words(out, m, w, NW);
+  if (parity) parity[m] = (st == HBTC_ACCEPT) ? (uint8_t)msm_parity(a) : 0;
+}
+#endif
+
+#if HBTC_IN_PART(8)
+template __global__ void k_msm_decode<Fq, 12>(uint32_t, uint32_t, const uint8_t*, const uint32_t*,
+                                              const uint32_t*, const int32_t*, G1A*, uint32_t*);
+template __global__ void k_msm_buckets<Fq>(uint64_t, uint32_t, uint32_t, uint32_t, const G1A*,
+                                           const uint32_t*, const uint32_t*, G1J*);
+template __global__ void k_msm_wsum<Fq>(uint64_t, uint32_t, const G1J*, G1J*);
+template __global__ void k_msm_final<Fq, 12>(uint32_t, uint32_t, uint32_t, const G1J*,
+                                             const uint32_t*, uint32_t, const uint32_t*,
+                                             const uint32_t*, int32_t*, uint8_t*, uint8_t*);
+#endif
+#if HBTC_IN_PART(9)
+template __global__ void k_msm_decode<Fq2, 24>(uint32_t, uint32_t, const uint8_t*,
+                                               const uint32_t*, const uint32_t*, const int32_t*,
+                                               G2A*, uint32_t*);
+template __global__ void k_msm_buckets<Fq2>(uint64_t, uint32_t, uint32_t, uint32_t, const G2A*,
+                                            const uint32_t*, const uint32_t*, G2J*);
+template __global__ void k_msm_wsum<Fq2>(uint64_t, uint32_t, const G2J*, G2J*);
+template __global__ void k_msm_final<Fq2, 24>(uint32_t, uint32_t, uint32_t, const G2J*,
+                                              const uint32_t*, uint32_t, const uint32_t*,
+                                              const uint32_t*, int32_t*, uint8_t*, uint8_t*);
+#endif
+
+// ------------------------------------------------------------------ launchers
+static inline uint32_t msm_blocks(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
+
+#if HBTC_IN_PART(8)
+hipError_t launch_select(hipStream_t s, uint32_t n_inst, const uint32_t* offsets, uint32_t t,
+                         const int32_t* status, const uint32_t* idx, uint32_t* sel_pos,
+                         uint32_t* sel_idx, uint32_t* sel_cnt) {
+  if (n_inst == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_select, dim3(n_inst), dim3(64), 0, s, offsets, t, status, idx, sel_pos,
+                     sel_idx, sel_cnt);
+  return hipGetLastError();
+}
+
+hipError_t launch_lagrange_sel(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_idx,
+                               Fr* lambda, uint32_t* dup) {
+  const uint64_t n = (uint64_t)n_inst * t;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_lagrange_sel, dim3(msm_blocks(n, 256)), dim3(256), 0, s, n_inst, t, sel_idx,
+                     lambda, dup);
+  return hipGetLastError();
+}
+
+hipError_t launch_msm_digits(hipStream_t s, const MsmPlan& p, const uint32_t* scalars,
+                             int16_t* digits, uint32_t* list, uint32_t* roff) {
+  const uint64_t terms = (uint64_t)p.n_msm * p.n;
+  if (terms == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_msm_recode, dim3(msm_blocks(terms, 256)), dim3(256), 0, s, terms, p.n, p.c,
+                     p.W, scalars, digits);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const size_t lds = ((size_t)(1u << (p.c - 1)) + MSM_SORT_BS) * 4;
+  hipLaunchKernelGGL(k_msm_sort, dim3((uint32_t)((uint64_t)p.n_msm * p.W)), dim3(MSM_SORT_BS), lds,
+                     s, p.n, p.c, (const int16_t*)digits, list, roff);
+  return hipGetLastError();
+}
+#endif
+
+template <class F, int NW>
+static hipError_t launch_msm_reduce(hipStream_t s, const MsmPlan& p, const Aff<F>* pts,
+                                    const uint32_t* list, const uint32_t* roff, Jac<F>* part,
+                                    Jac<F>* wsum, const uint32_t* sel_cnt, uint32_t t,
+                                    const uint32_t* bad, const uint32_t* dup, int32_t* status,
+                                    uint8_t* out, uint8_t* parity) {
+  const uint32_t S = (1u << (p.c - 1)) / 8;
+  const uint64_t lanes = (uint64_t)p.n_msm * p.W * S;
+  hipLaunchKernelGGL((k_msm_buckets<F>), dim3(msm_blocks(lanes, 64)), dim3(64), 0, s, lanes, p.n,
+                     p.c, p.W, pts, list, roff, part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint64_t n_mw = (uint64_t)p.n_msm * p.W;
+  hipLaunchKernelGGL((k_msm_wsum<F>), dim3(msm_blocks(n_mw, 64)), dim3(64), 0, s, n_mw, S,
+                     (const Jac<F>*)part, wsum);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_msm_final<F, NW>), dim3(msm_blocks(p.n_msm, 64)), dim3(64), 0, s, p.n_msm,
+                     p.c, p.W, (const Jac<F>*)wsum, sel_cnt, t, bad, dup, status, out, parity);
+  return hipGetLastError();
+}
+
+#if HBTC_IN_PART(8)
+hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, const uint8_t* pts_c,
+                                const uint32_t* sel_pos, const uint32_t* sel_cnt,
+                                const int32_t* item_status, G1A* pts, uint32_t* bad) {
+  const uint64_t terms = (uint64_t)n_msm * n;
+  if (terms == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_msm_decode<Fq, 12>), dim3(msm_blocks(terms, 64)), dim3(64), 0, s, n_msm, n,
+                     pts_c, sel_pos, sel_cnt, item_status, pts, bad);
+  return hipGetLastError();
+}
+hipError_t launch_msm_reduce_g1(hipStream_t s, const MsmPlan& p, const G1A* pts,
+                                const uint32_t* list, const uint32_t* roff, G1J* part, G1J* wsum,
+                                const uint32_t* sel_cnt, uint32_t t, const uint32_t* bad,
+                                const uint32_t* dup, int32_t* status, uint8_t* out) {
+  if (p.n_msm == 0) return hipSuccess;
+  return launch_msm_reduce<Fq, 12>(s, p, pts, list, roff, part, wsum, sel_cnt, t, bad, dup, status,
+                                   out, nullptr);
+}
+#endif
+#if HBTC_IN_PART(9)
+hipError_t launch_msm_decode_g2(hipStream_t s, uint32_t n_msm, uint32_t n, const uint8_t* pts_c,
+                                const uint32_t* sel_pos, const uint32_t* sel_cnt,
+                                const int32_t* item_status, G2A* pts, uint32_t* bad) {
+  const uint64_t terms = (uint64_t)n_msm * n;
+  if (terms == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_msm_decode<Fq2, 24>), dim3(msm_blocks(terms, 64)), dim3(64), 0, s, n_msm,
+                     n, pts_c, sel_pos, sel_cnt, item_status, pts, bad);
+  return hipGetLastError();
+}
+hipError_t launch_msm_reduce_g2(hipStream_t s, const MsmPlan& p, const G2A* pts,
+                                const uint32_t* list, const uint32_t* roff, G2J* part, G2J* wsum,
+                                const uint32_t* sel_cnt, uint32_t t, const uint32_t* bad,
+                                const uint32_t* dup, int32_t* status, uint8_t* out,
+                                uint8_t* parity) {
+  if (p.n_msm == 0) return hipSuccess;
+  return launch_msm_reduce<Fq2, 24>(s, p, pts, list, roff, part, wsum, sel_cnt, t, bad, dup, status,
+                                    out, parity);
+}
+#endif
+
+}  // namespace hbtc

@@ -18,8 +18,8 @@
  *                                                                             src/messaging.rs:253-256
  *   hbtc_g1_mul/hbtc_g2_mul  batched scalar multiplication (Poly::commitment src/sync_key_gen.rs:366,
  *                            SecretKeyShare::sign src/coin.rs:142, decrypt_share src/threshold_decryption.rs:98)
- *   hbtc_hash_g2             threshold_crypto's hash_g2 (SHA3-256 -> ChaCha -> G2::rand), the
- *                            coin nonce hash behind src/coin.rs:142,151 (host + GPU cofactor clearing)
+ *   hbtc_g1_msm/hbtc_g2_msm  batched Pippenger MSMs (BivarCommitment::row / Commitment::evaluate,
+ *                            src/sync_key_gen.rs:345,366,493); the combines run on the same kernels
  *
  * Encodings are hbbft's wire encodings of the points (zcash compressed: G1 = 48 bytes, G2 =
  * 96 bytes with x.c1 first; flag bits 0x80 compressed, 0x40 infinity, 0x20 lexicographically
@@ -150,6 +150,30 @@ int hbtc_combine_sigs_dev(hbtc_ctx* ctx, uint32_t n_inst, const uint32_t* offset
                           const uint32_t* d_idx, const uint8_t* d_sig_c96, uint32_t t,
                           uint8_t* d_out_sig_c96, uint8_t* d_out_parity, int32_t* d_inst_status);
 
+/* Combine from the verified shares: as hbtc_combine_dec_dev / hbtc_combine_sigs_dev, but over the
+ * first t items of each instance whose d_status (written by hbtc_verify_*_dev on the same
+ * context) is HBTC_ACCEPT — the shares hbbft keeps after verification (coin.rs:185-191 combines
+ * `received_shares`, threshold_decryption.rs:184 `shares`; both hold verified shares only).
+ * Ordered after the verification on the context's streams; no host synchronisation. */
+int hbtc_combine_dec_verified_dev(hbtc_ctx* ctx, uint32_t n_ct, const uint32_t* offsets,
+                                  const uint32_t* d_idx, const uint8_t* d_share_c48,
+                                  const int32_t* d_status, uint32_t t, uint8_t* d_out_g_c48,
+                                  int32_t* d_inst_status);
+int hbtc_combine_sigs_verified_dev(hbtc_ctx* ctx, uint32_t n_inst, const uint32_t* offsets,
+                                   const uint32_t* d_idx, const uint8_t* d_sig_c96,
+                                   const int32_t* d_status, uint32_t t, uint8_t* d_out_sig_c96,
+                                   uint8_t* d_out_parity, int32_t* d_inst_status);
+
+/* ---- batched multi-scalar multiplication (Pippenger) -------------------------------------- */
+/* n_msm independent MSMs of n terms: out_m = sum_i k_{m,i} P_{m,i} (points item-major
+ * [m][i], 32-byte little-endian scalars, reduced mod r).  Used for commitments and bivariate
+ * commitment rows (BivarCommitment::row, Commitment::evaluate: src/sync_key_gen.rs:345,366,493)
+ * and by the combines.  status[m] = ACCEPT or DECODE_ERR (a point failed to decode). */
+int hbtc_g1_msm(hbtc_ctx* ctx, uint32_t n_msm, uint32_t n, const uint8_t* pts_c48,
+                const uint8_t* scalars_le32, uint8_t* out_c48, int32_t* status);
+int hbtc_g2_msm(hbtc_ctx* ctx, uint32_t n_msm, uint32_t n, const uint8_t* pts_c96,
+                const uint8_t* scalars_le32, uint8_t* out_c96, int32_t* status);
+
 /* ---- verification strategy ----------------------------------------------------------------- */
 /* HBTC_MODE_RLC (default): shares of one instance are checked together by a random linear
  * combination (fresh 64-bit ChaCha20 scalars per call, prime-order points only), failing groups
@@ -166,7 +190,8 @@ int hbtc_set_verify_mode(hbtc_ctx* ctx, int mode);
 int hbtc_rlc_last_leaves(hbtc_ctx* ctx, uint32_t* leaves);
 
 /* ---- kernel timing (HIP events on the context's stream) ---------------------------------- */
-/* Families: "prepare", "dec_verify", "sig_verify", "pair_verify", "lagrange", "combine",
+/* Families: "prepare", "dec_verify", "sig_verify", "pair_verify", "lagrange" (selection +
+ * Lagrange coefficients), "comb_decode", "comb_digits", "combine" (MSM bucket reduction),
  * "mul", "rlc_items", "rlc_groups", "rlc_triage", "rlc_sub", "rlc_leaves", "rlc_finalize".  Reading
  * synchronises the stream. */
 int hbtc_timing_enable(hbtc_ctx* ctx, int enable);
