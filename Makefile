@@ -15,8 +15,9 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC)
 PARTS := 1 2 3 4
 RLC_PARTS := 6 7
 MSM_PARTS := 8 9
+SKG_PARTS := 10
 KOBJS := $(foreach p,$(PARTS),$(BUILD)/hbtc_kernels.p$(p).o) $(foreach p,$(RLC_PARTS),$(BUILD)/hbtc_rlc.p$(p).o) \
-         $(foreach p,$(MSM_PARTS),$(BUILD)/hbtc_msm.p$(p).o)
+         $(foreach p,$(MSM_PARTS),$(BUILD)/hbtc_msm.p$(p).o) $(foreach p,$(SKG_PARTS),$(BUILD)/hbtc_skg.p$(p).o)
 LIB := hbbft_amd/libhbtc.so
 
 .PHONY: all lib hosttest oracle clean resources roofline-constants
@@ -38,6 +39,9 @@ $(BUILD)/hbtc_rlc.p%.o: $(CSRC)/hbtc_rlc.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
 
 $(BUILD)/hbtc_msm.p%.o: $(CSRC)/hbtc_msm.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
+
+$(BUILD)/hbtc_skg.p%.o: $(CSRC)/hbtc_skg.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
 
 $(BUILD)/hbtc_api.o: $(CSRC)/hbtc_api.hip $(HDRS) | $(BUILD)

@@ -71,6 +71,8 @@ SIGNATURES = {
     "hbtc_combine_sigs_verified_dev": (_I32, [_P, _U32, _P, _P, _P, _P, _U32, _P, _P, _P]),
     "hbtc_g1_msm": (_I32, [_P, _U32, _U32, _P, _P, _P, _P]),
     "hbtc_g2_msm": (_I32, [_P, _U32, _U32, _P, _P, _P, _P]),
+    "hbtc_skg_check_parts": (_I32, [_P, _U32, _U32, _U32, _P, _P, _P]),
+    "hbtc_skg_check_acks": (_I32, [_P, _U32, _U32, _U32, _P, _P, _P, _U32, _P, _P, _P, _P]),
     "hbtc_set_verify_mode": (_I32, [_P, _I32]),
     "hbtc_rlc_last_leaves": (_I32, [_P, ctypes.POINTER(_U32)]),
     "hbtc_timing_enable": (_I32, [_P, _I32]),
@@ -283,6 +285,43 @@ class Context:
 
     def g2_msm(self, n_msm, n, points, scalars):
         return self._msm(self.lib.hbtc_g2_msm, 96, n_msm, n, points, scalars)
+
+    # ---- SyncKeyGen
+    @staticmethod
+    def _fr_bytes(vals):
+        if isinstance(vals, np.ndarray):
+            return np.ascontiguousarray(vals, dtype=np.uint8).reshape(-1)
+        return np.frombuffer(b"".join(int(v).to_bytes(32, "little") for v in vals),
+                             dtype=np.uint8).copy()
+
+    def skg_check_parts(self, t, our_idx, commits, rows):
+        """commits: per Part the (t+1)(t+2)/2 compressed G1 points (coeff_pos order, packed);
+        rows: per Part t+1 Fr ints.  Returns the per-Part status array."""
+        m = (t + 1) * (t + 2) // 2
+        cm = _join(commits, 48)
+        n_parts = cm.size // (48 * m)
+        rb = self._fr_bytes([v for r in rows for v in r])
+        if rb.size != 32 * n_parts * (t + 1):
+            raise ValueError("expected %d row coefficients" % (n_parts * (t + 1)))
+        st = np.empty(n_parts, np.int32)
+        self._check(self.lib.hbtc_skg_check_parts(self.h, n_parts, t, our_idx, _ptr(cm), _ptr(rb),
+                                                  _ptr(st)), "hbtc_skg_check_parts")
+        return st
+
+    def skg_check_acks(self, t, our_idx, commits, rows, row_ok, ack_part, ack_sender, vals):
+        m = (t + 1) * (t + 2) // 2
+        cm = _join(commits, 48)
+        n_parts = cm.size // (48 * m)
+        rb = self._fr_bytes([v for r in rows for v in r]) if rows is not None else None
+        ok = np.ascontiguousarray(row_ok, dtype=np.uint8)
+        ap = np.ascontiguousarray(ack_part, dtype=np.uint32)
+        sd = np.ascontiguousarray(ack_sender, dtype=np.uint32)
+        vb = self._fr_bytes(vals)
+        st = np.empty(ap.size, np.int32)
+        self._check(self.lib.hbtc_skg_check_acks(self.h, n_parts, t, our_idx, _ptr(cm), _ptr(rb),
+                                                 _ptr(ok), ap.size, _ptr(ap), _ptr(sd), _ptr(vb),
+                                                 _ptr(st)), "hbtc_skg_check_acks")
+        return st
 
     # ---- device memory (benchmarks)
     def dev_alloc(self, nbytes):

@@ -384,7 +384,8 @@ MsmPlan msm_plan(uint32_t n_msm, uint32_t n) {
 template <class F>
 int msm_run(hbtc_ctx* c, hipStream_t st, const MsmPlan& p, const uint32_t* d_scalars,
             const Aff<F>* d_pts, const uint32_t* sel_cnt, uint32_t t, const uint32_t* d_bad,
-            const uint32_t* d_dup, int32_t* d_status, uint8_t* d_out, uint8_t* d_parity) {
+            const uint32_t* d_dup, int32_t* d_status, uint8_t* d_out, uint8_t* d_parity,
+            const uint32_t* d_pts_map = nullptr) {
   const uint64_t terms = (uint64_t)p.n_msm * p.n;
   const uint64_t mw = (uint64_t)p.n_msm * p.W;
   const uint32_t B = 1u << (p.c - 1), S = B / 8;
@@ -401,10 +402,10 @@ int msm_run(hbtc_ctx* c, hipStream_t st, const MsmPlan& p, const uint32_t* d_sca
   }));
   return timed_on(c, st, "combine", [&] {
     if constexpr (sizeof(F) == sizeof(Fq))
-      return launch_msm_reduce_g1(st, p, d_pts, d_list, d_roff, d_part, d_wsum, sel_cnt, t, d_bad,
+      return launch_msm_reduce_g1(st, p, d_pts, d_pts_map, d_list, d_roff, d_part, d_wsum, sel_cnt, t, d_bad,
                                   d_dup, d_status, d_out);
     else
-      return launch_msm_reduce_g2(st, p, d_pts, d_list, d_roff, d_part, d_wsum, sel_cnt, t, d_bad,
+      return launch_msm_reduce_g2(st, p, d_pts, d_pts_map, d_list, d_roff, d_part, d_wsum, sel_cnt, t, d_bad,
                                   d_dup, d_status, d_out, d_parity);
   });
 }
@@ -450,7 +451,7 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
     G1A* d_aff;
     HB_TRY(wst(c, "comb.g1", terms, &d_aff));
     HB_TRY(timed_on(c, sc, "comb_decode", [&] {
-      return launch_msm_decode_g1(sc, n_inst, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status, d_aff,
+      return launch_msm_decode_g1(sc, n_inst, t, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status, d_aff,
                                   d_bad);
     }));
     return msm_run<Fq>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
@@ -459,7 +460,7 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
   G2A* d_aff;
   HB_TRY(wst(c, "comb.g2", terms, &d_aff));
   HB_TRY(timed_on(c, sc, "comb_decode", [&] {
-    return launch_msm_decode_g2(sc, n_inst, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status, d_aff,
+    return launch_msm_decode_g2(sc, n_inst, t, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status, d_aff,
                                 d_bad);
   }));
   return msm_run<Fq2>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
@@ -848,24 +849,63 @@ void scalar_mod_r(uint32_t* out, const uint8_t* in) {
   memcpy(out, k, 32);
 }
 
-// Batched MSMs from host buffers, chunked over MSMs so the digit/list workspaces stay bounded.
+// n_msm MSMs of n terms on s_comb from device buffers: term i of MSM m is compressed item
+// m * stride + i (terms i >= stride: the generator), canonical scalars [m][n].  Writes the
+// compressed results and ACCEPT / DECODE_ERR per MSM.
+int msm_dev(hbtc_ctx* c, int group, uint32_t n_msm, uint32_t n, uint32_t stride,
+            const uint8_t* d_pts, const uint32_t* d_sc, uint8_t* d_out, int32_t* d_st) {
+  hipStream_t sc = c->s_comb;
+  const uint64_t terms = (uint64_t)n_msm * n;
+  std::vector<uint32_t> cnt(n_msm, n);
+  void* d_cnt;
+  HB_TRY(stage_upload(c, "msm.cnt", cnt.data(), (size_t)n_msm * 4, sc, &d_cnt));
+  uint32_t* d_bad;
+  HB_TRY(wst(c, "msm.bad", n_msm, &d_bad));
+  HB_CHECK(c, hipMemsetAsync(d_bad, 0, (size_t)n_msm * 4, sc));
+  const MsmPlan p = msm_plan(n_msm, n);
+  if (group == 1) {
+    G1A* d_aff;
+    HB_TRY(wst(c, "msm.g1", terms, &d_aff));
+    HB_TRY(timed_on(c, sc, "comb_decode", [&] {
+      return launch_msm_decode_g1(sc, n_msm, n, stride, d_pts, nullptr, (const uint32_t*)d_cnt,
+                                  nullptr, d_aff, d_bad);
+    }));
+    return msm_run<Fq>(c, sc, p, d_sc, d_aff, (const uint32_t*)d_cnt, n, d_bad, nullptr, d_st,
+                       d_out, nullptr);
+  }
+  G2A* d_aff;
+  HB_TRY(wst(c, "msm.g2", terms, &d_aff));
+  HB_TRY(timed_on(c, sc, "comb_decode", [&] {
+    return launch_msm_decode_g2(sc, n_msm, n, stride, d_pts, nullptr, (const uint32_t*)d_cnt,
+                                nullptr, d_aff, d_bad);
+  }));
+  return msm_run<Fq2>(c, sc, p, d_sc, d_aff, (const uint32_t*)d_cnt, n, d_bad, nullptr, d_st,
+                      d_out, nullptr);
+}
+
+// MSMs per chunk so that the digit / list workspaces stay near 2^27 entries.
+uint32_t msm_chunk(uint32_t n_msm, uint32_t n) {
+  const MsmPlan full = msm_plan(n_msm, n);
+  const uint64_t cap_terms = (1ull << 27) / full.W;
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_msm, cap_terms / n));
+}
+
+// Batched MSMs from host buffers, chunked over MSMs.
 int msm_host(hbtc_ctx* c, int group, uint32_t n_msm, uint32_t n, const uint8_t* pts,
              const uint8_t* scalars, uint8_t* out, int32_t* status) {
   if (n_msm == 0) return HBTC_OK;
   if (n == 0) return fail(c, HBTC_ERR_ARG, "n must be >= 1");
   const size_t pb = group == 1 ? 48 : 96;
-  const MsmPlan full = msm_plan(n_msm, n);
-  const uint64_t cap_terms = (1ull << 27) / full.W;
-  const uint32_t chunk = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_msm, cap_terms / n));
+  const uint32_t chunk = msm_chunk(n_msm, n);
   hipStream_t sc = c->s_comb;
   HB_TRY(sync(c));
-  std::vector<uint32_t> red((size_t)chunk * n * 8), cnt(chunk, n);
+  std::vector<uint32_t> red((size_t)chunk * n * 8);
   for (uint32_t m0 = 0; m0 < n_msm; m0 += chunk) {
     const uint32_t mc = std::min(chunk, n_msm - m0);
     const uint64_t terms = (uint64_t)mc * n;
     for (uint64_t i = 0; i < terms; ++i)
       scalar_mod_r(&red[i * 8], scalars + ((uint64_t)m0 * n + i) * 32);
-    void *d_pts, *d_sc, *d_out, *d_st, *d_cnt;
+    void *d_pts, *d_sc, *d_out, *d_st;
     HB_TRY(ws(c, "msm.in_pts", terms * pb, &d_pts));
     HB_TRY(ws(c, "msm.in_sc", terms * 32, &d_sc));
     HB_TRY(ws(c, "msm.out", (size_t)mc * pb, &d_out));
@@ -873,30 +913,8 @@ int msm_host(hbtc_ctx* c, int group, uint32_t n_msm, uint32_t n, const uint8_t* 
     HB_CHECK(c, hipMemcpyAsync(d_pts, pts + (uint64_t)m0 * n * pb, terms * pb,
                                hipMemcpyHostToDevice, sc));
     HB_CHECK(c, hipMemcpyAsync(d_sc, red.data(), terms * 32, hipMemcpyHostToDevice, sc));
-    HB_TRY(stage_upload(c, "msm.cnt", cnt.data(), (size_t)mc * 4, sc, &d_cnt));
-    uint32_t* d_bad;
-    HB_TRY(wst(c, "msm.bad", mc, &d_bad));
-    HB_CHECK(c, hipMemsetAsync(d_bad, 0, (size_t)mc * 4, sc));
-    const MsmPlan p = msm_plan(mc, n);
-    if (group == 1) {
-      G1A* d_aff;
-      HB_TRY(wst(c, "msm.g1", terms, &d_aff));
-      HB_TRY(timed_on(c, sc, "comb_decode", [&] {
-        return launch_msm_decode_g1(sc, mc, n, (const uint8_t*)d_pts, nullptr,
-                                    (const uint32_t*)d_cnt, nullptr, d_aff, d_bad);
-      }));
-      HB_TRY(msm_run<Fq>(c, sc, p, (const uint32_t*)d_sc, d_aff, (const uint32_t*)d_cnt, n, d_bad,
-                         nullptr, (int32_t*)d_st, (uint8_t*)d_out, nullptr));
-    } else {
-      G2A* d_aff;
-      HB_TRY(wst(c, "msm.g2", terms, &d_aff));
-      HB_TRY(timed_on(c, sc, "comb_decode", [&] {
-        return launch_msm_decode_g2(sc, mc, n, (const uint8_t*)d_pts, nullptr,
-                                    (const uint32_t*)d_cnt, nullptr, d_aff, d_bad);
-      }));
-      HB_TRY(msm_run<Fq2>(c, sc, p, (const uint32_t*)d_sc, d_aff, (const uint32_t*)d_cnt, n, d_bad,
-                          nullptr, (int32_t*)d_st, (uint8_t*)d_out, nullptr));
-    }
+    HB_TRY(msm_dev(c, group, mc, n, n, (const uint8_t*)d_pts, (const uint32_t*)d_sc,
+                   (uint8_t*)d_out, (int32_t*)d_st));
     HB_CHECK(c, hipMemcpyAsync(out + (uint64_t)m0 * pb, d_out, (size_t)mc * pb,
                                hipMemcpyDeviceToHost, sc));
     HB_CHECK(c, hipMemcpyAsync(status + m0, d_st, (size_t)mc * 4, hipMemcpyDeviceToHost, sc));
@@ -904,7 +922,287 @@ int msm_host(hbtc_ctx* c, int group, uint32_t n_msm, uint32_t n, const uint8_t* 
   }
   return HBTC_OK;
 }
+
+// ---- SyncKeyGen (hbtc_skg.hip): Fr helpers on the host (the same field.h code)
+void fr_set_zero(Fr& r) {
+  for (int i = 0; i < 8; ++i) r.v[i] = 0;
+}
+bool fr_load_canonical(Fr& r, const uint8_t* le32) {
+  memcpy(r.v, le32, 32);
+  return limbs_lt_const<8>(r, FR_R);
+}
+Fr fr_mont_of(const Fr& canon) {
+  Fr m;
+  fr_to_mont(m, canon);
+  return m;
+}
+Fr fr_random(hbtc_ctx* c) {
+  uint8_t b[32];
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t w = c->rd();
+    memcpy(b + 4 * i, &w, 4);
+  }
+  Fr k;
+  scalar_mod_r(k.v, b);
+  return k;
+}
+Fr fr_neg_canon(const Fr& mont) {  // -(a) as a canonical scalar, a in Montgomery form
+  Fr z, n, cn;
+  fr_set_zero(z);
+  fr_sub(n, z, mont);
+  fr_from_mont(cn, n);
+  return cn;
+}
+std::vector<uint32_t> skg_ij_table(uint32_t t1) {  // coeff_pos order: pos = j(j+1)/2 + i, i <= j
+  std::vector<uint32_t> ij;
+  ij.reserve((size_t)t1 * (t1 + 1) / 2);
+  for (uint32_t j = 0; j < t1; ++j)
+    for (uint32_t i = 0; i <= j; ++i) ij.push_back(i | (j << 16));
+  return ij;
+}
+bool is_g1_infinity_c48(const uint8_t* p) {
+  if (p[0] != 0xc0) return false;
+  for (int i = 1; i < 48; ++i)
+    if (p[i]) return false;
+  return true;
+}
+
+// "MSM == O" checks of n_chk equations over BivarCommitments: equation e uses commitment
+// blk[e] (device compressed commitments [part][M]), scalars s_ij from U (shared) and V_e
+// (Montgomery, stride v_stride), and the generator term tail_e (canonical).
+// result[e] = ACCEPT / REJECT / DECODE_ERR.
+int skg_checks(hbtc_ctx* c, uint32_t t1, const uint8_t* d_commit, uint32_t n_chk,
+               const uint32_t* blk, const Fr* U, const Fr* V, uint32_t v_stride, const Fr* tail,
+               int32_t* result) {
+  if (n_chk == 0) return HBTC_OK;
+  const uint32_t M = t1 * (t1 + 1) / 2, n = M + 1;
+  hipStream_t sc = c->s_comb;
+  const std::vector<uint32_t> ij = skg_ij_table(t1);
+  void *d_ij, *d_U;
+  HB_TRY(stage_upload(c, "skg.ij", ij.data(), ij.size() * 4, sc, &d_ij));
+  HB_TRY(stage_upload(c, "skg.U", U, (size_t)t1 * sizeof(Fr), sc, &d_U));
+  const uint32_t chunk = msm_chunk(n_chk, n);
+  std::vector<uint8_t> out((size_t)chunk * 48);
+  std::vector<int32_t> st(chunk);
+  for (uint32_t e0 = 0; e0 < n_chk; e0 += chunk) {
+    const uint32_t ec = std::min(chunk, n_chk - e0);
+    void *d_V, *d_tail, *d_sc, *d_out, *d_st, *d_pts;
+    HB_TRY(stage_upload(c, "skg.V", V + (size_t)e0 * v_stride,
+                        (size_t)((ec - 1) * v_stride + t1) * sizeof(Fr), sc, &d_V));
+    HB_TRY(stage_upload(c, "skg.tail", tail + e0, (size_t)ec * sizeof(Fr), sc, &d_tail));
+    HB_TRY(ws(c, "skg.sc", (size_t)ec * n * sizeof(Fr), &d_sc));
+    HB_TRY(ws(c, "skg.out", (size_t)ec * 48, &d_out));
+    HB_TRY(ws(c, "skg.st", (size_t)ec * 4, &d_st));
+    HB_TRY(timed_on(c, sc, "skg_scalars", [&] {
+      return launch_skg_sym_scalars(sc, ec, M, (const Fr*)d_U, 0, (const Fr*)d_V, v_stride,
+                                    (const uint32_t*)d_ij, (const Fr*)d_tail, (Fr*)d_sc);
+    }));
+    // the commitments of this chunk in equation order (device-to-device; contiguous blocks of
+    // one copy each when the equations are the Parts themselves)
+    const uint8_t* pts = d_commit + (size_t)blk[e0] * M * 48;
+    bool contiguous = true;
+    for (uint32_t e = 1; e < ec && contiguous; ++e) contiguous = blk[e0 + e] == blk[e0] + e;
+    if (!contiguous) {
+      HB_TRY(ws(c, "skg.pts", (size_t)ec * M * 48, &d_pts));
+      for (uint32_t e = 0; e < ec; ++e)
+        HB_CHECK(c, hipMemcpyAsync((uint8_t*)d_pts + (size_t)e * M * 48,
+                                   d_commit + (size_t)blk[e0 + e] * M * 48, (size_t)M * 48,
+                                   hipMemcpyDeviceToDevice, sc));
+      pts = (const uint8_t*)d_pts;
+    }
+    HB_TRY(msm_dev(c, 1, ec, n, M, pts, (const uint32_t*)d_sc, (uint8_t*)d_out, (int32_t*)d_st));
+    HB_CHECK(c, hipMemcpyAsync(out.data(), d_out, (size_t)ec * 48, hipMemcpyDeviceToHost, sc));
+    HB_CHECK(c, hipMemcpyAsync(st.data(), d_st, (size_t)ec * 4, hipMemcpyDeviceToHost, sc));
+    HB_CHECK(c, hipStreamSynchronize(sc));
+    for (uint32_t e = 0; e < ec; ++e)
+      result[e0 + e] = st[e] == HBTC_DECODE_ERR           ? HBTC_DECODE_ERR
+                       : is_g1_infinity_c48(&out[48 * e]) ? HBTC_ACCEPT
+                                                          : HBTC_REJECT;
+  }
+  return HBTC_OK;
+}
 }  // namespace
+
+int hbtc_skg_check_parts(hbtc_ctx* c, uint32_t n_parts, uint32_t t, uint32_t our_idx,
+                         const uint8_t* commit_c48, const uint8_t* rows_le32,
+                         int32_t* part_status) {
+  if (!c || (n_parts && (!commit_c48 || !rows_le32 || !part_status))) return HBTC_ERR_ARG;
+  if (t >= 0xffffu) return HBTC_ERR_ARG;
+  Guard g(c);
+  if (n_parts == 0) return HBTC_OK;
+  HB_TRY(sync(c));
+  const uint32_t t1 = t + 1, M = t1 * (t1 + 1) / 2;
+  // rho_i (fresh per call) and x^j with x = our_idx + 1, both Montgomery
+  std::vector<Fr> U(t1), V(t1);
+  Fr x, xp;
+  fr_from_u64(x, (uint64_t)our_idx + 1);
+  fr_from_u64(xp, 1);
+  for (uint32_t j = 0; j < t1; ++j) {
+    U[j] = fr_mont_of(fr_random(c));
+    V[j] = xp;
+    fr_mul(xp, xp, x);
+  }
+  // tail_p = -(sum_i rho_i a_{p,i}); a row coefficient >= r fails bincode's Fr decoding
+  // (InvalidPartMessage, sync_key_gen.rs:359-364)
+  std::vector<Fr> tail(n_parts);
+  std::vector<uint8_t> row_bad(n_parts, 0);
+  for (uint32_t p = 0; p < n_parts; ++p) {
+    Fr acc;
+    fr_set_zero(acc);
+    for (uint32_t i = 0; i < t1; ++i) {
+      Fr a;
+      if (!fr_load_canonical(a, rows_le32 + ((size_t)p * t1 + i) * 32)) {
+        row_bad[p] = 1;
+        break;
+      }
+      Fr prod;
+      fr_mul(prod, U[i], fr_mont_of(a));
+      fr_add(acc, acc, prod);
+    }
+    tail[p] = fr_neg_canon(acc);
+  }
+  void* d_commit;
+  HB_TRY(ws(c, "skg.commit", (size_t)n_parts * M * 48, &d_commit));
+  HB_CHECK(c, hipMemcpyAsync(d_commit, commit_c48, (size_t)n_parts * M * 48,
+                             hipMemcpyHostToDevice, c->s_comb));
+  std::vector<uint32_t> blk(n_parts);
+  for (uint32_t p = 0; p < n_parts; ++p) blk[p] = p;
+  HB_TRY(skg_checks(c, t1, (const uint8_t*)d_commit, n_parts, blk.data(), U.data(), V.data(), 0,
+                    tail.data(), part_status));
+  for (uint32_t p = 0; p < n_parts; ++p)
+    if (row_bad[p] && part_status[p] != HBTC_DECODE_ERR) part_status[p] = HBTC_REJECT;
+  return HBTC_OK;
+}
+
+int hbtc_skg_check_acks(hbtc_ctx* c, uint32_t n_parts, uint32_t t, uint32_t our_idx,
+                        const uint8_t* commit_c48, const uint8_t* rows_le32,
+                        const uint8_t* row_ok, uint32_t n_acks, const uint32_t* ack_part,
+                        const uint32_t* ack_sender, const uint8_t* vals_le32,
+                        int32_t* ack_status) {
+  if (!c || (n_acks && (!commit_c48 || !row_ok || !ack_part || !ack_sender || !vals_le32 ||
+                        !ack_status)))
+    return HBTC_ERR_ARG;
+  if (t >= 0xffffu) return HBTC_ERR_ARG;
+  Guard g(c);
+  if (n_acks == 0) return HBTC_OK;
+  const uint32_t t1 = t + 1, M = t1 * (t1 + 1) / 2;
+  std::vector<Fr> vals(n_acks);
+  std::vector<uint8_t> val_bad(n_acks, 0);
+  for (uint32_t a = 0; a < n_acks; ++a) {
+    if (ack_part[a] >= n_parts) return fail(c, HBTC_ERR_ARG, "ack_part out of range");
+    if (!fr_load_canonical(vals[a], vals_le32 + (size_t)a * 32)) val_bad[a] = 1;
+  }
+  HB_TRY(sync(c));
+  hipStream_t sc = c->s_comb;
+  // (1) Acks of Parts whose row this node verified: val == row(sender + 1)
+  bool any_row = false;
+  for (uint32_t p = 0; p < n_parts && !any_row; ++p) any_row = row_ok[p] != 0;
+  if (any_row) {
+    if (!rows_le32) return fail(c, HBTC_ERR_ARG, "rows_le32 is NULL");
+    std::vector<Fr> rows((size_t)n_parts * t1);
+    for (size_t k = 0; k < rows.size(); ++k) {
+      Fr a;
+      memcpy(a.v, rows_le32 + k * 32, 32);
+      rows[k] = fr_mont_of(a);
+    }
+    void *d_rows, *d_part, *d_snd, *d_vals, *d_st;
+    HB_TRY(upload(c, "skg.rows", rows.data(), rows.size() * sizeof(Fr), &d_rows));
+    HB_TRY(upload(c, "skg.ack_part", ack_part, (size_t)n_acks * 4, &d_part));
+    HB_TRY(upload(c, "skg.ack_snd", ack_sender, (size_t)n_acks * 4, &d_snd));
+    HB_TRY(upload(c, "skg.vals", vals.data(), (size_t)n_acks * sizeof(Fr), &d_vals));
+    HB_TRY(ws(c, "skg.ack_st", (size_t)n_acks * 4, &d_st));
+    HB_TRY(timed(c, "skg_ack_rows", [&] {
+      return launch_skg_ack_rows(c->stream, n_acks, t1, (const Fr*)d_rows,
+                                 (const uint32_t*)d_part, (const uint32_t*)d_snd,
+                                 (const Fr*)d_vals, (int32_t*)d_st);
+    }));
+    HB_TRY(download(c, ack_status, d_st, (size_t)n_acks * 4));
+    HB_TRY(sync(c));
+  }
+  // (2) Parts without a verified row: one random linear combination of their Acks each,
+  // sum_a rho_a evaluate(x, y_a) == [sum_a rho_a val_a] G1
+  std::vector<std::vector<uint32_t>> by_part(n_parts);
+  for (uint32_t a = 0; a < n_acks; ++a)
+    if (!row_ok[ack_part[a]] && !val_bad[a]) by_part[ack_part[a]].push_back(a);
+  std::vector<uint32_t> parts;
+  for (uint32_t p = 0; p < n_parts; ++p)
+    if (!by_part[p].empty()) parts.push_back(p);
+  if (!parts.empty()) {
+    std::vector<Fr> U(t1);
+    Fr x, xp;
+    fr_from_u64(x, (uint64_t)our_idx + 1);
+    fr_from_u64(xp, 1);
+    for (uint32_t j = 0; j < t1; ++j) {
+      U[j] = xp;
+      fr_mul(xp, xp, x);
+    }
+    void* d_commit;
+    HB_TRY(ws(c, "skg.commit", (size_t)n_parts * M * 48, &d_commit));
+    HB_CHECK(c, hipMemcpyAsync(d_commit, commit_c48, (size_t)n_parts * M * 48,
+                               hipMemcpyHostToDevice, sc));
+    auto powers = [&](uint32_t sender, Fr* out) {  // (sender + 1)^j, Montgomery
+      Fr y, yp;
+      fr_from_u64(y, (uint64_t)sender + 1);
+      fr_from_u64(yp, 1);
+      for (uint32_t j = 0; j < t1; ++j) {
+        out[j] = yp;
+        fr_mul(yp, yp, y);
+      }
+    };
+    std::vector<Fr> V(parts.size() * t1), tail(parts.size()), yp(t1);
+    for (size_t q = 0; q < parts.size(); ++q) {
+      Fr* Y = &V[q * t1];
+      for (uint32_t j = 0; j < t1; ++j) fr_set_zero(Y[j]);
+      Fr acc;
+      fr_set_zero(acc);
+      for (uint32_t a : by_part[parts[q]]) {
+        const Fr rho = fr_mont_of(fr_random(c));
+        powers(ack_sender[a], yp.data());
+        for (uint32_t j = 0; j < t1; ++j) {
+          Fr tm;
+          fr_mul(tm, rho, yp[j]);
+          fr_add(Y[j], Y[j], tm);
+        }
+        Fr tv;
+        fr_mul(tv, rho, fr_mont_of(vals[a]));
+        fr_add(acc, acc, tv);
+      }
+      tail[q] = fr_neg_canon(acc);
+    }
+    std::vector<int32_t> res(parts.size());
+    HB_TRY(skg_checks(c, t1, (const uint8_t*)d_commit, (uint32_t)parts.size(), parts.data(),
+                      U.data(), V.data(), t1, tail.data(), res.data()));
+    // (3) a failing combination: every Ack of that Part checked exactly
+    std::vector<uint32_t> exact, eblk;
+    for (size_t q = 0; q < parts.size(); ++q) {
+      for (uint32_t a : by_part[parts[q]]) {
+        if (res[q] == HBTC_ACCEPT) {
+          ack_status[a] = HBTC_ACCEPT;
+        } else if (res[q] == HBTC_DECODE_ERR) {
+          ack_status[a] = HBTC_DECODE_ERR;  // the Part's commitment itself does not decode
+        } else {
+          exact.push_back(a);
+          eblk.push_back(parts[q]);
+        }
+      }
+    }
+    if (!exact.empty()) {
+      std::vector<Fr> V2(exact.size() * t1), tail2(exact.size());
+      for (size_t e = 0; e < exact.size(); ++e) {
+        powers(ack_sender[exact[e]], &V2[e * t1]);
+        tail2[e] = fr_neg_canon(fr_mont_of(vals[exact[e]]));
+      }
+      std::vector<int32_t> res2(exact.size());
+      HB_TRY(skg_checks(c, t1, (const uint8_t*)d_commit, (uint32_t)exact.size(), eblk.data(),
+                        U.data(), V2.data(), t1, tail2.data(), res2.data()));
+      for (size_t e = 0; e < exact.size(); ++e)
+        ack_status[exact[e]] = res2[e] == HBTC_ACCEPT ? HBTC_ACCEPT : HBTC_REJECT;
+    }
+  }
+  for (uint32_t a = 0; a < n_acks; ++a)
+    if (val_bad[a]) ack_status[a] = HBTC_DECODE_ERR;
+  return HBTC_OK;
+}
 
 int hbtc_g1_msm(hbtc_ctx* c, uint32_t n_msm, uint32_t n, const uint8_t* pts_c48,
                 const uint8_t* scalars_le32, uint8_t* out_c48, int32_t* status) {

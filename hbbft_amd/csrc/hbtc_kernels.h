@@ -98,20 +98,30 @@ hipError_t launch_lagrange_sel(hipStream_t s, uint32_t n_inst, uint32_t t, const
                                Fr* lambda, uint32_t* dup);
 hipError_t launch_msm_digits(hipStream_t s, const MsmPlan& p, const uint32_t* scalars,
                              int16_t* digits, uint32_t* list, uint32_t* roff);
-hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, const uint8_t* pts_c,
-                                const uint32_t* sel_pos, const uint32_t* sel_cnt,
-                                const int32_t* item_status, G1A* pts, uint32_t* bad);
+hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
+                                const uint8_t* pts_c, const uint32_t* sel_pos,
+                                const uint32_t* sel_cnt, const int32_t* item_status, G1A* pts,
+                                uint32_t* bad);
 hipError_t launch_msm_reduce_g1(hipStream_t s, const MsmPlan& p, const G1A* pts,
-                                const uint32_t* list, const uint32_t* roff, G1J* part, G1J* wsum,
+                                const uint32_t* pts_map, const uint32_t* list, const uint32_t* roff, G1J* part, G1J* wsum,
                                 const uint32_t* sel_cnt, uint32_t t, const uint32_t* bad,
                                 const uint32_t* dup, int32_t* status, uint8_t* out);
-hipError_t launch_msm_decode_g2(hipStream_t s, uint32_t n_msm, uint32_t n, const uint8_t* pts_c,
-                                const uint32_t* sel_pos, const uint32_t* sel_cnt,
-                                const int32_t* item_status, G2A* pts, uint32_t* bad);
+hipError_t launch_msm_decode_g2(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
+                                const uint8_t* pts_c, const uint32_t* sel_pos,
+                                const uint32_t* sel_cnt, const int32_t* item_status, G2A* pts,
+                                uint32_t* bad);
 hipError_t launch_msm_reduce_g2(hipStream_t s, const MsmPlan& p, const G2A* pts,
-                                const uint32_t* list, const uint32_t* roff, G2J* part, G2J* wsum,
+                                const uint32_t* pts_map, const uint32_t* list, const uint32_t* roff, G2J* part, G2J* wsum,
                                 const uint32_t* sel_cnt, uint32_t t, const uint32_t* bad,
                                 const uint32_t* dup, int32_t* status, uint8_t* out,
                                 uint8_t* parity);
+
+// ---- SyncKeyGen (hbtc_skg.hip)
+hipError_t launch_skg_sym_scalars(hipStream_t s, uint32_t n_parts, uint32_t M, const Fr* U,
+                                  uint32_t u_stride, const Fr* V, uint32_t v_stride,
+                                  const uint32_t* ij, const Fr* tail, Fr* out);
+hipError_t launch_skg_ack_rows(hipStream_t s, uint32_t n_acks, uint32_t t1, const Fr* rows,
+                               const uint32_t* ack_part, const uint32_t* ack_sender,
+                               const Fr* vals, int32_t* status);
 
 }  // namespace hbtc

@@ -245,8 +245,22 @@ __global__ void __launch_bounds__(MSM_SORT_BS) k_msm_sort(uint32_t n, uint32_t c
 
 // ------------------------------------------------------------------ group kernels
 #if HBTC_IN_PART(8) || HBTC_IN_PART(9)
+__device__ __forceinline__ void msm_generator(G1A& p) {
+  fq_set(p.x, G1_GEN_X);
+  fq_set(p.y, G1_GEN_Y);
+  p.inf = 0;
+}
+__device__ __forceinline__ void msm_generator(G2A& p) {
+  fq2_set(p.x, G2_GEN_X);
+  fq2_set(p.y, G2_GEN_Y);
+  p.inf = 0;
+}
+
+// Term i of MSM k: the selected item sel_pos[k*t+i] (combines), else item k*stride+i of the
+// compressed array; terms i >= stride are the group generator (SyncKeyGen checks fold the
+// right-hand side [v]G into the MSM as one extra term).
 template <class F, int NW>
-__global__ void __launch_bounds__(64) k_msm_decode(uint32_t n_inst, uint32_t t,
+__global__ void __launch_bounds__(64) k_msm_decode(uint32_t n_inst, uint32_t t, uint32_t stride,
                                                    const uint8_t* __restrict__ pts,
                                                    const uint32_t* __restrict__ sel_pos,
                                                    const uint32_t* __restrict__ sel_cnt,
@@ -260,8 +274,10 @@ __global__ void __launch_bounds__(64) k_msm_decode(uint32_t n_inst, uint32_t t,
   fzero(p.x);
   fzero(p.y);
   p.inf = 1;
-  if (i < sel_cnt[k]) {
-    const uint32_t pos = sel_pos ? sel_pos[g] : (uint32_t)g;
+  if (!sel_pos && i >= stride) {
+    msm_generator(p);
+  } else if (i < sel_cnt[k]) {
+    const uint64_t pos = sel_pos ? (uint64_t)sel_pos[g] : (uint64_t)k * stride + i;
     uint32_t w[NW];
     msm_load_words(w, pts, pos, NW);
     // an item the verifier accepted was decoded and subgroup-checked by it
@@ -282,6 +298,7 @@ __global__ void __launch_bounds__(64) k_msm_buckets(uint64_t n_lanes, uint32_t n
                                                     uint32_t W, const Aff<F>* __restrict__ pts,
                                                     const uint32_t* __restrict__ list,
                                                     const uint32_t* __restrict__ roff,
+                                                    const uint32_t* __restrict__ pts_map,
                                                     Jac<F>* __restrict__ part) {
   const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
   if (g >= n_lanes) return;
@@ -290,7 +307,9 @@ __global__ void __launch_bounds__(64) k_msm_buckets(uint64_t n_lanes, uint32_t n
   const uint64_t mw = g / S;
   const uint32_t* ro = roff + mw * (B + 1);
   const uint32_t* L = list + mw * n;
-  const Aff<F>* P = pts + (mw / W) * n;
+  // pts_map: MSMs sharing one decoded point set (several Ack equations over one commitment)
+  const uint64_t blk = pts_map ? (uint64_t)pts_map[mw / W] : mw / W;
+  const Aff<F>* P = pts + blk * n;
   Jac<F> run, tot;
   jac_set_inf(run);
   jac_set_inf(tot);
@@ -366,21 +385,24 @@ __global__ void __launch_bounds__(64) k_msm_final(uint32_t n_msm, uint32_t c, ui
 #endif
 
 #if HBTC_IN_PART(8)
-template __global__ void k_msm_decode<Fq, 12>(uint32_t, uint32_t, const uint8_t*, const uint32_t*,
-                                              const uint32_t*, const int32_t*, G1A*, uint32_t*);
+template __global__ void k_msm_decode<Fq, 12>(uint32_t, uint32_t, uint32_t, const uint8_t*,
+                                              const uint32_t*, const uint32_t*, const int32_t*,
+                                              G1A*, uint32_t*);
 template __global__ void k_msm_buckets<Fq>(uint64_t, uint32_t, uint32_t, uint32_t, const G1A*,
-                                           const uint32_t*, const uint32_t*, G1J*);
+                                           const uint32_t*, const uint32_t*, const uint32_t*,
+                                           G1J*);
 template __global__ void k_msm_wsum<Fq>(uint64_t, uint32_t, const G1J*, G1J*);
 template __global__ void k_msm_final<Fq, 12>(uint32_t, uint32_t, uint32_t, const G1J*,
                                              const uint32_t*, uint32_t, const uint32_t*,
                                              const uint32_t*, int32_t*, uint8_t*, uint8_t*);
 #endif
 #if HBTC_IN_PART(9)
-template __global__ void k_msm_decode<Fq2, 24>(uint32_t, uint32_t, const uint8_t*,
+template __global__ void k_msm_decode<Fq2, 24>(uint32_t, uint32_t, uint32_t, const uint8_t*,
                                                const uint32_t*, const uint32_t*, const int32_t*,
                                                G2A*, uint32_t*);
 template __global__ void k_msm_buckets<Fq2>(uint64_t, uint32_t, uint32_t, uint32_t, const G2A*,
-                                            const uint32_t*, const uint32_t*, G2J*);
+                                            const uint32_t*, const uint32_t*, const uint32_t*,
+                                            G2J*);
 template __global__ void k_msm_wsum<Fq2>(uint64_t, uint32_t, const G2J*, G2J*);
 template __global__ void k_msm_final<Fq2, 24>(uint32_t, uint32_t, uint32_t, const G2J*,
                                               const uint32_t*, uint32_t, const uint32_t*,
@@ -426,14 +448,15 @@ hipError_t launch_msm_digits(hipStream_t s, const MsmPlan& p, const uint32_t* sc
 
 template <class F, int NW>
 static hipError_t launch_msm_reduce(hipStream_t s, const MsmPlan& p, const Aff<F>* pts,
-                                    const uint32_t* list, const uint32_t* roff, Jac<F>* part,
+                                    const uint32_t* pts_map, const uint32_t* list,
+                                    const uint32_t* roff, Jac<F>* part,
                                     Jac<F>* wsum, const uint32_t* sel_cnt, uint32_t t,
                                     const uint32_t* bad, const uint32_t* dup, int32_t* status,
                                     uint8_t* out, uint8_t* parity) {
   const uint32_t S = (1u << (p.c - 1)) / 8;
   const uint64_t lanes = (uint64_t)p.n_msm * p.W * S;
   hipLaunchKernelGGL((k_msm_buckets<F>), dim3(msm_blocks(lanes, 64)), dim3(64), 0, s, lanes, p.n,
-                     p.c, p.W, pts, list, roff, part);
+                     p.c, p.W, pts, list, roff, pts_map, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint64_t n_mw = (uint64_t)p.n_msm * p.W;
@@ -447,41 +470,43 @@ static hipError_t launch_msm_reduce(hipStream_t s, const MsmPlan& p, const Aff<F
 }
 
 #if HBTC_IN_PART(8)
-hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, const uint8_t* pts_c,
-                                const uint32_t* sel_pos, const uint32_t* sel_cnt,
-                                const int32_t* item_status, G1A* pts, uint32_t* bad) {
+hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
+                                const uint8_t* pts_c, const uint32_t* sel_pos,
+                                const uint32_t* sel_cnt, const int32_t* item_status, G1A* pts,
+                                uint32_t* bad) {
   const uint64_t terms = (uint64_t)n_msm * n;
   if (terms == 0) return hipSuccess;
   hipLaunchKernelGGL((k_msm_decode<Fq, 12>), dim3(msm_blocks(terms, 64)), dim3(64), 0, s, n_msm, n,
-                     pts_c, sel_pos, sel_cnt, item_status, pts, bad);
+                     stride, pts_c, sel_pos, sel_cnt, item_status, pts, bad);
   return hipGetLastError();
 }
 hipError_t launch_msm_reduce_g1(hipStream_t s, const MsmPlan& p, const G1A* pts,
-                                const uint32_t* list, const uint32_t* roff, G1J* part, G1J* wsum,
+                                const uint32_t* pts_map, const uint32_t* list, const uint32_t* roff, G1J* part, G1J* wsum,
                                 const uint32_t* sel_cnt, uint32_t t, const uint32_t* bad,
                                 const uint32_t* dup, int32_t* status, uint8_t* out) {
   if (p.n_msm == 0) return hipSuccess;
-  return launch_msm_reduce<Fq, 12>(s, p, pts, list, roff, part, wsum, sel_cnt, t, bad, dup, status,
+  return launch_msm_reduce<Fq, 12>(s, p, pts, pts_map, list, roff, part, wsum, sel_cnt, t, bad, dup, status,
                                    out, nullptr);
 }
 #endif
 #if HBTC_IN_PART(9)
-hipError_t launch_msm_decode_g2(hipStream_t s, uint32_t n_msm, uint32_t n, const uint8_t* pts_c,
-                                const uint32_t* sel_pos, const uint32_t* sel_cnt,
-                                const int32_t* item_status, G2A* pts, uint32_t* bad) {
+hipError_t launch_msm_decode_g2(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
+                                const uint8_t* pts_c, const uint32_t* sel_pos,
+                                const uint32_t* sel_cnt, const int32_t* item_status, G2A* pts,
+                                uint32_t* bad) {
   const uint64_t terms = (uint64_t)n_msm * n;
   if (terms == 0) return hipSuccess;
   hipLaunchKernelGGL((k_msm_decode<Fq2, 24>), dim3(msm_blocks(terms, 64)), dim3(64), 0, s, n_msm,
-                     n, pts_c, sel_pos, sel_cnt, item_status, pts, bad);
+                     n, stride, pts_c, sel_pos, sel_cnt, item_status, pts, bad);
   return hipGetLastError();
 }
 hipError_t launch_msm_reduce_g2(hipStream_t s, const MsmPlan& p, const G2A* pts,
-                                const uint32_t* list, const uint32_t* roff, G2J* part, G2J* wsum,
+                                const uint32_t* pts_map, const uint32_t* list, const uint32_t* roff, G2J* part, G2J* wsum,
                                 const uint32_t* sel_cnt, uint32_t t, const uint32_t* bad,
                                 const uint32_t* dup, int32_t* status, uint8_t* out,
                                 uint8_t* parity) {
   if (p.n_msm == 0) return hipSuccess;
-  return launch_msm_reduce<Fq2, 24>(s, p, pts, list, roff, part, wsum, sel_cnt, t, bad, dup, status,
+  return launch_msm_reduce<Fq2, 24>(s, p, pts, pts_map, list, roff, part, wsum, sel_cnt, t, bad, dup, status,
                                     out, parity);
 }
 #endif

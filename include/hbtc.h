@@ -18,6 +18,10 @@
  *                                                                             src/messaging.rs:253-256
  *   hbtc_g1_mul/hbtc_g2_mul  batched scalar multiplication (Poly::commitment src/sync_key_gen.rs:366,
  *                            SecretKeyShare::sign src/coin.rs:142, decrypt_share src/threshold_decryption.rs:98)
+ *   hbtc_skg_check_parts     SyncKeyGen::handle_part: row.commitment() == commit.row(x)
+ *                                                                             src/sync_key_gen.rs:366
+ *   hbtc_skg_check_acks      SyncKeyGen::handle_ack_or_err: commit.evaluate(x, y) == val * G1
+ *                                                                             src/sync_key_gen.rs:493
  *   hbtc_g1_msm/hbtc_g2_msm  batched Pippenger MSMs (BivarCommitment::row / Commitment::evaluate,
  *                            src/sync_key_gen.rs:345,366,493); the combines run on the same kernels
  *
@@ -174,6 +178,32 @@ int hbtc_g1_msm(hbtc_ctx* ctx, uint32_t n_msm, uint32_t n, const uint8_t* pts_c4
 int hbtc_g2_msm(hbtc_ctx* ctx, uint32_t n_msm, uint32_t n, const uint8_t* pts_c96,
                 const uint8_t* scalars_le32, uint8_t* out_c96, int32_t* status);
 
+/* ---- SyncKeyGen (DynamicHoneyBadger era change) ------------------------------------------- */
+/* A node's Part checks (SyncKeyGen::handle_part, src/sync_key_gen.rs:338-369): for every Part p,
+ * commit_c48[p] holds the (t+1)(t+2)/2 compressed G1 coefficients of its BivarCommitment in
+ * coeff_pos order (pos(i, j) = j(j+1)/2 + i, i <= j) and rows_le32[p] the t+1 coefficients
+ * (32-byte little-endian Fr) of the row this node decrypted from it.  part_status[p] = ACCEPT
+ * iff row.commitment() == commit.row(our_idx + 1) (:366), REJECT otherwise (InvalidPartMessage;
+ * also for a row coefficient >= r, which bincode's Fr decoding refuses), DECODE_ERR if a
+ * commitment point does not decode (serde would refuse the Part).  One random linear
+ * combination of the t+1 coefficient equations per Part (one Pippenger MSM, error <= 1/r). */
+int hbtc_skg_check_parts(hbtc_ctx* ctx, uint32_t n_parts, uint32_t t, uint32_t our_idx,
+                         const uint8_t* commit_c48, const uint8_t* rows_le32,
+                         int32_t* part_status);
+/* A node's Ack value checks (handle_ack_or_err, :493): Ack a (for Part ack_part[a], from node
+ * ack_sender[a], decrypted value vals_le32[a]) is ACCEPT iff
+ * commit.evaluate(our_idx + 1, ack_sender + 1) == val * G1, REJECT otherwise (ValueInvalid),
+ * DECODE_ERR for a value >= r (ValueDeserialization).  For a Part with row_ok[p] != 0 (its row
+ * passed hbtc_skg_check_parts) the check is the identical scalar equation val == row(y); the
+ * other Parts' Acks are checked by one random linear combination per Part with an exact per-Ack
+ * fallback.  The caller applies the checks that precede the value (NodeCount, SenderExist,
+ * DuplicateAck, ValueDecryption: :467-482) and calls this for the Acks that reach :493. */
+int hbtc_skg_check_acks(hbtc_ctx* ctx, uint32_t n_parts, uint32_t t, uint32_t our_idx,
+                        const uint8_t* commit_c48, const uint8_t* rows_le32,
+                        const uint8_t* row_ok, uint32_t n_acks, const uint32_t* ack_part,
+                        const uint32_t* ack_sender, const uint8_t* vals_le32,
+                        int32_t* ack_status);
+
 /* ---- verification strategy ----------------------------------------------------------------- */
 /* HBTC_MODE_RLC (default): shares of one instance are checked together by a random linear
  * combination (fresh 64-bit ChaCha20 scalars per call, prime-order points only), failing groups
@@ -191,7 +221,7 @@ int hbtc_rlc_last_leaves(hbtc_ctx* ctx, uint32_t* leaves);
 
 /* ---- kernel timing (HIP events on the context's stream) ---------------------------------- */
 /* Families: "prepare", "dec_verify", "sig_verify", "pair_verify", "lagrange" (selection +
- * Lagrange coefficients), "comb_decode", "comb_digits", "combine" (MSM bucket reduction),
+ * Lagrange coefficients), "comb_decode", "comb_digits", "combine" (MSM bucket reduction), "skg_scalars", "skg_ack_rows",
  * "mul", "rlc_items", "rlc_groups", "rlc_triage", "rlc_sub", "rlc_leaves", "rlc_finalize".  Reading
  * synchronises the stream. */
 int hbtc_timing_enable(hbtc_ctx* ctx, int enable);

@@ -8,7 +8,12 @@
 //   sig_share   one SignatureShare check: G2 decode + subgroup test, Miller loop with one
 //               precomputed table and one on-the-fly G2 argument, final exp (k_sig_verify)
 //   g2_prepare  per-instance G2 decode + 68-line precomputation           (k_g2_prepare)
-//   g1_combine_item  one G1 combine term: decode + 255-bit double-and-add  (k_combine<Fq>)
+//   g1_combine_item  one G1 combine term: decode + 255-bit double-and-add (the reference's
+//               interpolate; kept for comparison)
+//   g1_msm_combine   one G1 Lagrange combine of t = 334 verified shares as the batched
+//               Pippenger kernels run it (hbtc_msm.hip, c = 6): trusted decode (no subgroup
+//               test) per term, exact digit statistics of random scalars, bucket running sums,
+//               segment scaling, window sums, Horner doublings, normalisation
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -147,6 +152,52 @@ int main() {
   final_exponentiation(e, f);
   const unsigned long long rlc_group = hbtc_fqm_count;
 
+  // Pippenger combine (t = 334, c = 6, W = 43, B = 32, S = 4), exact digit counts
+  unsigned long long msm_combine = 0;
+  {
+    const int t = 334, c = 6, W = (256 + c - 1) / c, B = 1 << (c - 1), S = B / 8;
+    hbtc_fqm_count = 0;
+    G1A dp;
+    g1_decompress(dp, w1, false);
+    const unsigned long long dec_trusted = hbtc_fqm_count;
+    hbtc_fqm_count = 0;
+    G1J tj = pj;
+    jac_add_aff(tj, tj, gen1);
+    const unsigned long long madd = hbtc_fqm_count;
+    hbtc_fqm_count = 0;
+    G1A na;
+    jac_to_aff(na, pj);
+    const unsigned long long norm = hbtc_fqm_count;
+    unsigned long long n_madd = 0;
+    for (int i = 0; i < t; ++i) {
+      Fr kk;
+      rand_scalar(kk, g);
+      uint32_t carry = 0;
+      for (int w = 0; w < W; ++w) {
+        const int bit = w * c;
+        uint64_t two = 0;
+        const int wi = bit >> 5, sh = bit & 31;
+        two = ((uint64_t)(wi + 1 < 8 ? kk.v[wi + 1] : 0) << 32) | kk.v[wi];
+        uint32_t v = (uint32_t)(two >> sh) & ((1u << c) - 1u);
+        v += carry;
+        int d;
+        if (v > (uint32_t)B) { d = (int)v - (1 << c); carry = 1; } else { d = (int)v; carry = 0; }
+        n_madd += d != 0;
+      }
+    }
+    // per window: B running-sum closes + S segment adds of [base] run (base = B - 8s - 8 with
+    // its bits as doublings and popcount adds), S-1 window-sum adds; then W-1 Horner steps
+    unsigned long long seg = 0;
+    for (int s2 = 0; s2 < S; ++s2) {
+      const uint32_t base = B - 8 * s2 - 8;
+      if (!base) continue;
+      const int bits = 32 - __builtin_clz(base);
+      seg += bits * jdbl + (__builtin_popcount(base) + 1) * jadd;
+    }
+    msm_combine = t * dec_trusted + n_madd * madd +
+                  W * (B * jadd + seg + (S - 1) * jadd) + (W - 1) * (c * jdbl + jadd) + norm;
+  }
+
   printf("{\n");
   printf("  \"unit\": \"Fqm (12x32-bit-limb CIOS Montgomery multiplications; 288 v_mad_u64_u32 + 12 v_mul_lo_u32 each)\",\n");
   printf("  \"mul32_per_fqm\": 300,\n  \"mad_u64_u32_per_fqm\": 288,\n");
@@ -156,6 +207,7 @@ int main() {
   printf("  \"sig_share\": {\"decode\": %llu, \"miller_loop_fixed_var\": %llu, \"final_exp\": %llu, \"total\": %llu},\n",
          sig_decode, mlfv, fe, sig_decode + mlfv + fe);
   printf("  \"g1_combine_item\": %llu,\n  \"g2_combine_item\": %llu,\n", comb1, comb2);
+  printf("  \"g1_msm_combine\": %llu,\n", msm_combine);
   printf("  \"rlc_item\": %llu,\n  \"rlc_group_check\": %llu\n}\n", rlc_item, rlc_group);
   return 0;
 }
