@@ -1,0 +1,278 @@
+#!/usr/bin/env python3
+"""Secondary benchmark lines for the other SURVEY.md §8 configurations (one JSON line each).
+
+bench.py measures the headline metric on C3 (the configuration BASELINE.json's metric is quoted
+on).  This script measures the remaining hot-path configurations through the same C ABI, one
+GPU, synthetic seeded inputs generated on the device (setup outside the timed region), results
+checked against the construction after timing:
+
+  c2  Binary Agreement coins N=100: 100 coin instances x 100 SignatureShares verified
+      (PublicKeyShare::verify, src/coin.rs:151) + 100 G2 combines of the first t=34 verified
+      shares (combine_signatures + parity, src/coin.rs:185-191,173).  Inputs resident in HBM.
+  c4  N=10,000: I coin instances x 10^4 SignatureShares + I G2 Pippenger combines (t=3334).
+      SURVEY §8 shards the I=64 instances over 8 GPUs; this 1-GPU line runs --inst of them.
+  c5  SyncKeyGen N=1000, one node's view: 1000 Parts (row.commitment() == commit.row(x),
+      src/sync_key_gen.rs:366) then 10^6 Acks (commit.evaluate(x, y) == val*G1, :493).  The
+      SKG entry points take host buffers, so this line is PCIe-inclusive (2.7 GB of commitments
+      per Part batch); the Parts reuse --distinct bivariate polynomials (laid out per Part in
+      HBM as 1000 separate copies, so the device work and traffic are those of 1000 Parts).
+
+Usage: python bench_configs.py [--configs c2,c4,c5] [--steps K] [--warmup W]
+"""
+import argparse
+import ctypes
+import json
+import os
+import random
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from hbbft_amd import _native as N  # noqa: E402
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+G1_GEN = bytes.fromhex("97f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb")
+G2_GEN = bytes.fromhex("93e02b6052719f607dacd3a088274f65596bd0d09920b61ab5da61bbdc7f5049334cf11213945d57e5ac7d055d042b7e"
+                       "024aa2b2f08f0a91260805272dc51051c6e47ad4fa403b02b4510b647ae3d1770bac0326a805bbefd48056c8c121bdb8")
+SEED = 0x6862626674
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def fr_bytes(vals):
+    return np.frombuffer(b"".join(int(v).to_bytes(32, "little") for v in vals), dtype=np.uint8).copy()
+
+
+def key_shares(rng, n):
+    """sk_i = poly(i+1) for a random degree-f polynomial (messaging.rs:372-394)."""
+    f = (n - 1) // 3
+    coeffs = [rng.randrange(1, R) for _ in range(f + 1)]
+    sks = []
+    for i in range(n):
+        acc, x = 0, i + 1
+        for c in reversed(coeffs):
+            acc = (acc * x + c) % R
+        sks.append(acc)
+    return coeffs[0], sks
+
+
+def timed_steps(ctx, fn, steps, warmup):
+    ctx.timing_enable(True)
+    for _ in range(warmup):
+        fn()
+    ctx.sync()
+    ctx.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    ctx.sync()
+    return time.perf_counter() - t0
+
+
+def breakdown(ctx, steps, fams):
+    out = {}
+    for f in fams:
+        ms, n = ctx.timing_read(f)
+        if n:
+            out[f] = round(ms / steps, 3)
+    return out
+
+
+COIN_FAMS = ["prepare", "sig_verify", "lagrange", "comb_decode", "comb_digits", "combine"]
+
+
+def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01):
+    """c2 / c4: n_inst coin instances x n SignatureShares + n_inst combines (first t verified)."""
+    rng = random.Random(SEED + n)
+    t0 = time.time()
+    master, sks = key_shares(rng, n)
+    t = (n - 1) // 3 + 1
+    pk, st = ctx.g1_mul(G1_GEN, fr_bytes(sks))
+    assert not st.any()
+    ks, bad = ctx.keyset_load(pk)
+    assert bad == 0
+    hs = [rng.randrange(1, R) for _ in range(n_inst)]
+    H, _ = ctx.g2_mul(G2_GEN, fr_bytes(hs))
+    total = n * n_inst
+    scal = [sks[i] * h % R for h in hs for i in range(n)]
+    expected = np.zeros(total, np.int32)
+    for j in rng.sample(range(total), int(total * corrupt)):
+        scal[j] = (scal[j] + 1) % R
+        expected[j] = N.REJECT
+    sigs, st = ctx.g2_mul(G2_GEN, fr_bytes(scal))
+    assert not st.any()
+    offsets = np.arange(0, total + 1, n, dtype=np.uint32)
+    idx = np.tile(np.arange(n, dtype=np.uint32), n_inst)
+    d = {}
+    for k, arr in (("H", H), ("idx", idx), ("sigs", sigs)):
+        d[k] = ctx.dev_alloc(arr.nbytes)
+        ctx.dev_upload(d[k], arr)
+    d["status"] = ctx.dev_alloc(4 * total)
+    d["out"] = ctx.dev_alloc(96 * n_inst)
+    d["par"] = ctx.dev_alloc(n_inst)
+    d["cst"] = ctx.dev_alloc(4 * n_inst)
+    log("%s: setup %.1fs (%d shares)" % (name, time.time() - t0, total))
+    lib, h, off = ctx.lib, ctx.h, N._ptr(offsets)
+
+    def step():
+        ctx._check(lib.hbtc_verify_sig_shares_dev(h, ks, n_inst, d["H"], off, d["idx"], d["sigs"],
+                                                  d["status"]), "verify_sig_shares_dev")
+        ctx._check(lib.hbtc_combine_sigs_verified_dev(h, n_inst, off, d["idx"], d["sigs"], d["status"],
+                                                      t, d["out"], d["par"], d["cst"]),
+                   "combine_sigs_verified_dev")
+
+    elapsed = timed_steps(ctx, step, steps, warmup)
+    per = breakdown(ctx, steps, COIN_FAMS)
+    stv = np.empty(total, np.int32)
+    ctx.dev_download(stv, d["status"])
+    out = np.empty(96 * n_inst, np.uint8)
+    ctx.dev_download(out, d["out"])
+    cst = np.empty(n_inst, np.int32)
+    ctx.dev_download(cst, d["cst"])
+    want, _ = ctx.g2_mul(G2_GEN, fr_bytes([master * hh % R for hh in hs]))
+    mism = int((stv != expected).sum())
+    comb_ok = bool((cst == 0).all() and bytes(out) == bytes(want))
+    if mism or not comb_ok:
+        raise SystemExit("%s: results differ from the construction (%d mismatches, combine %s)"
+                         % (name, mism, comb_ok))
+    for p in d.values():
+        ctx.dev_free(p)
+    ctx.keyset_free(ks)
+    return {
+        "metric": "verified BLS12-381 SignatureShares/sec; combines/sec",
+        "value": round(total * steps / elapsed, 1), "unit": "shares/s", "n_gpus": 1,
+        "steps": steps, "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 3),
+        "higher_is_better": True, "dtype": "u32 (381-bit Montgomery limbs)",
+        "data": "synthetic (seeded key set, shares generated on device; %g%% wrong shares)" % (100 * corrupt),
+        "config": {"workload": "%s: %d coin instances x %d SignatureShares verified + %d G2 combines (t=%d)"
+                   % (name, n_inst, n, n_inst, t), "N": n, "t": t, "instances": n_inst},
+        "combines_per_s": round(n_inst * steps / elapsed, 2),
+        "kernel_ms_per_step": per, "mismatches": mism, "combine_ok": comb_ok,
+    }
+
+
+def bench_skg(ctx, n, n_parts, n_distinct, steps, warmup):
+    """c5: one node's SyncKeyGen view at N=n (t = (n-1)/3): n_parts Parts, then n_parts x n Acks."""
+    rng = random.Random(SEED + 5)
+    t0 = time.time()
+    t = (n - 1) // 3
+    t1, m = t + 1, (t + 1) * (t + 2) // 2
+    our = 17
+    x = our + 1
+    polys = [[rng.randrange(R) for _ in range(m)] for _ in range(n_distinct)]
+    commit_d = []
+    for b in polys:
+        c, st = ctx.g1_mul(G1_GEN, fr_bytes(b))
+        assert not st.any()
+        commit_d.append(c)
+    xp = [pow(x, j, R) for j in range(t1)]
+
+    def pos(i, j):
+        return j * (j + 1) // 2 + i if j >= i else i * (i + 1) // 2 + j
+
+    rows_d = [[sum(b[pos(i, j)] * xp[j] for j in range(t1)) % R for i in range(t1)] for b in polys]
+
+    def horner(row, y):
+        acc = 0
+        for c in reversed(row):
+            acc = (acc * y + c) % R
+        return acc
+
+    vals_d = [[horner(r, s + 1) for s in range(n)] for r in rows_d]
+    commits = np.concatenate([commit_d[p % n_distinct] for p in range(n_parts)])
+    rows = [list(rows_d[p % n_distinct]) for p in range(n_parts)]
+    bad_part = 7 % n_parts
+    rows[bad_part][t // 2] = (rows[bad_part][t // 2] + 1) % R
+    rows_b = fr_bytes([v for r in rows for v in r])
+    part_expect = np.full(n_parts, N.ACCEPT, np.int32)
+    part_expect[bad_part] = N.REJECT
+    n_acks = n_parts * n
+    ack_part = np.repeat(np.arange(n_parts, dtype=np.uint32), n)
+    ack_sender = np.tile(np.arange(n, dtype=np.uint32), n_parts)
+    vals_d_b = [fr_bytes(v).reshape(n, 32) for v in vals_d]
+    vals = np.concatenate([vals_d_b[p % n_distinct] for p in range(n_parts)]).reshape(n_acks, 32)
+    ack_expect = np.full(n_acks, N.ACCEPT, np.int32)
+    for a in rng.sample(range(n_acks), 100):  # tampered values (ValueInvalid)
+        v = (int.from_bytes(vals[a].tobytes(), "little") + 1) % R
+        vals[a] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)
+        ack_expect[a] = N.REJECT
+    vals = vals.reshape(-1)
+    log("c5: setup %.1fs (%d Parts x %d commitment points, %d Acks)"
+        % (time.time() - t0, n_parts, m, n_acks))
+    lib, h = ctx.lib, ctx.h
+    pst = np.empty(n_parts, np.int32)
+    ast = np.empty(n_acks, np.int32)
+    row_ok = np.empty(n_parts, np.uint8)
+    t_parts = [0.0]
+
+    def step():
+        a0 = time.perf_counter()
+        ctx._check(lib.hbtc_skg_check_parts(h, n_parts, t, our, N._ptr(commits), N._ptr(rows_b),
+                                            N._ptr(pst)), "skg_check_parts")
+        t_parts[0] += time.perf_counter() - a0
+        row_ok[:] = (pst == N.ACCEPT)
+        ctx._check(lib.hbtc_skg_check_acks(h, n_parts, t, our, N._ptr(commits), N._ptr(rows_b),
+                                           N._ptr(row_ok), n_acks, N._ptr(ack_part),
+                                           N._ptr(ack_sender), N._ptr(vals), N._ptr(ast)),
+                   "skg_check_acks")
+
+    for _ in range(warmup):
+        step()
+    t_parts[0] = 0.0
+    elapsed = timed_steps(ctx, step, steps, 0)
+    per = breakdown(ctx, steps, ["skg_scalars", "skg_ack_rows", "comb_decode", "comb_digits",
+                                 "combine", "mul"])
+    pm = int((pst != part_expect).sum())
+    am = int((ast != ack_expect).sum())
+    if pm or am:
+        raise SystemExit("c5: results differ from the construction (%d Part, %d Ack mismatches)" % (pm, am))
+    tp = t_parts[0] / steps
+    ta = elapsed / steps - tp
+    return {
+        "metric": "SyncKeyGen checks/sec: Parts/s and Acks/s (one node's view)",
+        "value": round(n_acks * steps / elapsed, 1), "unit": "acks/s (Parts + Acks of the era in the timed region)",
+        "n_gpus": 1, "steps": steps, "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 3),
+        "higher_is_better": True, "dtype": "u32 (381-bit Montgomery limbs)",
+        "data": "synthetic (%d distinct bivariate polynomials reused over %d Parts; 1 Part with a tampered row, 100 tampered Ack values); host buffers (PCIe-inclusive)"
+                % (n_distinct, n_parts),
+        "config": {"workload": "c5: SyncKeyGen N=%d: %d Parts (%d-point BivarCommitments) + %d Acks"
+                   % (n, n_parts, m, n_acks), "N": n, "t": t, "parts": n_parts, "acks": n_acks},
+        "parts_ms": round(tp * 1e3, 3), "acks_ms": round(ta * 1e3, 3),
+        "parts_per_s": round(n_parts / tp, 1), "acks_per_s": round(n_acks / ta, 1),
+        "kernel_ms_per_step": per, "mismatches": pm + am,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c2,c4,c5")
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--inst", type=int, default=64, help="c4 coin instances on this GPU")
+    ap.add_argument("--parts", type=int, default=1000, help="c5 Parts")
+    ap.add_argument("--distinct", type=int, default=4, help="c5 distinct bivariate polynomials")
+    args = ap.parse_args()
+    ctx = N.Context(0)
+    try:
+        for c in args.configs.split(","):
+            if c == "c2":
+                out = bench_coins(ctx, "c2", 100, 100, args.steps, args.warmup)
+            elif c == "c4":
+                out = bench_coins(ctx, "c4", 10000, args.inst, args.steps, args.warmup)
+            elif c == "c5":
+                out = bench_skg(ctx, 1000, args.parts, args.distinct, args.steps, args.warmup)
+            else:
+                raise SystemExit("unknown config " + c)
+            print(json.dumps(out), flush=True)
+    finally:
+        ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -953,7 +953,7 @@ Fr fr_neg_canon(const Fr& mont) {  // -(a) as a canonical scalar, a in Montgomer
   fr_from_mont(cn, n);
   return cn;
 }
-std::vector<uint32_t> skg_ij_table(uint32_t t1) {  // coeff_pos order: pos = j(j+1)/2 + i, i <= j
+static std::vector<uint32_t> skg_ij_table(uint32_t t1) {  // coeff_pos order: pos = j(j+1)/2 + i, i <= j
   std::vector<uint32_t> ij;
   ij.reserve((size_t)t1 * (t1 + 1) / 2);
   for (uint32_t j = 0; j < t1; ++j)
