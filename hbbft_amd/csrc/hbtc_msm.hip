@@ -290,9 +290,24 @@ __global__ void __launch_bounds__(64) k_msm_decode(uint32_t n_inst, uint32_t t, 
   out[g] = p;
 }
 
-// One lane per (msm, window, segment of 8 buckets): running-sum reduction over the segment's
-// sorted terms.  With rank r = B - b, tot = sum_r (8s + 8 - r) B_r = sum_b (b - base) B_b and
-// run = sum_b B_b, so the segment's share of sum_b b B_b is tot + [base] run.
+// Rank whose bucket holds sorted position p: the largest r < B with ro[r] <= p (ro[0] = 0 and
+// p < ro[B]).
+__device__ __forceinline__ uint32_t msm_rank(const uint32_t* ro, uint32_t B, uint32_t p) {
+  uint32_t lo = 0, hi = B;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (ro[mid] <= p) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// One lane per (msm, window, segment): S = B/8 segments split the window's sorted nonzero terms
+// into equal slices of the LIST (not of the buckets), so a window whose digits crowd into a few
+// buckets (the top window: k < 2^255 leaves it only a few bits) is shared by all S lanes instead
+// of serialising n additions on one.  Running-sum reduction over the slice's ranks
+// [r_lo, r_hi): tot = sum_r (r_hi - r) B'_r, run = sum_r B'_r (B'_r = the slice's part of
+// bucket rank r, bucket b = B - r), so the slice's share of sum_b b B_b is tot + [B - r_hi] run.
 template <class F>
 __global__ void __launch_bounds__(64) k_msm_buckets(uint64_t n_lanes, uint32_t n, uint32_t c,
                                                     uint32_t W, const Aff<F>* __restrict__ pts,
@@ -313,22 +328,28 @@ __global__ void __launch_bounds__(64) k_msm_buckets(uint64_t n_lanes, uint32_t n
   Jac<F> run, tot;
   jac_set_inf(run);
   jac_set_inf(tot);
-  uint32_t e = ro[8 * s];
-  for (uint32_t r = 8 * s; r < 8 * s + 8; ++r) {
-    const uint32_t end = ro[r + 1];
-    for (; e < end; ++e) {
-      const uint32_t v = L[e];
-      Aff<F> q = P[v & 0x7fffffffu];
-      if (v >> 31) fneg(q.y, q.y);
-      jac_add_aff(run, run, q);
+  const uint32_t total = ro[B];
+  const uint32_t p0 = (uint32_t)((uint64_t)total * s / S);
+  const uint32_t p1 = (uint32_t)((uint64_t)total * (s + 1) / S);
+  if (p0 < p1) {
+    const uint32_t r_last = msm_rank(ro, B, p1 - 1);
+    uint32_t e = p0;
+    for (uint32_t r = msm_rank(ro, B, p0); r <= r_last; ++r) {
+      const uint32_t end = min(ro[r + 1], p1);
+      for (; e < end; ++e) {
+        const uint32_t v = L[e];
+        Aff<F> q = P[v & 0x7fffffffu];
+        if (v >> 31) fneg(q.y, q.y);
+        jac_add_aff(run, run, q);
+      }
+      jac_add(tot, tot, run);
     }
-    jac_add(tot, tot, run);
-  }
-  const uint32_t base = B - 8 * s - 8;
-  if (base) {
-    Jac<F> m;
-    jac_mul_small(m, run, base);
-    jac_add(tot, tot, m);
+    const uint32_t base = B - r_last - 1;
+    if (base) {
+      Jac<F> m;
+      jac_mul_small(m, run, base);
+      jac_add(tot, tot, m);
+    }
   }
   part[g] = tot;
 }
