@@ -237,6 +237,15 @@ def main():
     dom = max((f for f in main_stream if breakdown[f][1]), key=lambda f: breakdown[f][0])
     dom_avg_s = breakdown[dom][0] / breakdown[dom][1] / 1e3
     achieved = fqm_per_launch[dom] / dom_avg_s * consts["mad_u64_u32_per_fqm"] / 1e12
+    # HBM traffic and VALU instruction count of the same kernel from the committed rocprofv3
+    # PMC passes of this command (tools/gpu_configs_pmc.sh -> tools/pmc_summary.py): separate
+    # FETCH_SIZE / WRITE_SIZE / SQ passes, FETCH_SIZE doubled per the gfx950 note.
+    traffic, pmc = None, {}
+    pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+    if os.path.exists(pmc_path):
+        pmc = json.load(open(pmc_path)).get("hbtc::k_" + dom, {})
+        if "hbm_read_bytes" in pmc and "hbm_write_bytes" in pmc:
+            traffic = pmc["hbm_read_bytes"] + pmc["hbm_write_bytes"]
     out = {
         "metric": "verified BLS12-381 shares/sec (whole node) at N=1000; combines/sec",
         "value": round(value, 1),
@@ -267,9 +276,13 @@ def main():
             "peak": MAD_U64_PEAK / 1e12,
             "unit": "T mad_u64_u32/s",
             "frac": round(achieved / (MAD_U64_PEAK / 1e12), 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch (HBM read + write, rocprofv3 PMC)",
             "fqm_per_launch": fqm_per_launch[dom],
             "kernel_ms_per_launch": round(dom_avg_s * 1e3, 3),
+            "pmc": {k: pmc[k] for k in ("vgpr", "scratch_bytes_per_lane", "valu_busy",
+                                        "hbm_read_bytes", "hbm_write_bytes") if k in pmc} or None,
+            "valu_insts_per_launch": pmc.get("counters_mean_per_dispatch", {}).get("SQ_INSTS_VALU"),
         },
     }
     if rank == 0 and not args.no_cpu:
