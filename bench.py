@@ -16,8 +16,9 @@ Multi-GPU (weak scaling): one process per GPU (torch.distributed.run), each rank
 own epoch shard of 1000 ciphertexts (shards are independent, SURVEY.md §8e: no data-path
 collective); gloo carries the barrier and the max-over-ranks time only.
 
-Prints ONE JSON line on rank 0 (contract in the task statement), with "roofline" (dominant
-kernel k_dec_verify, Fqm counted by tools/fqm_count.cpp -> bench/roofline_constants.json) and
+Prints ONE JSON line on rank 0 (contract in the task statement), with "roofline" (the longest
+critical-path kernel, k_rlc_items in the default RLC mode; Fqm counted by tools/fqm_count.cpp ->
+bench/roofline_constants.json; HBM traffic from the committed PMC passes) and
 "cpu_baseline" (the oracle's threshold_crypto restatement timed on this host).
 """
 import argparse
@@ -155,6 +156,23 @@ def cpu_baseline(ep, budget_s):
     return run_dec_share_baseline(ep, budget_s)
 
 
+def rank_seed(rank):
+    """Seed of a rank's epoch shard: ranks verify disjoint, independently generated epochs
+    (weak scaling, SURVEY.md §8e: no shared state besides the read-only key set)."""
+    return SEED + 7919 * rank
+
+
+def max_over_ranks(elapsed, dist):
+    """The job's time: barrier, then the MAX of the ranks' timed regions (gloo all-reduce)."""
+    if dist is None:
+        return elapsed
+    import torch
+    dist.barrier()
+    tt = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -175,14 +193,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as dist
         dist.init_process_group("gloo")
 
     ctx = N.Context(local)
     t0 = time.time()
     ctx.set_verify_mode(N.MODE_RLC if args.mode == "rlc" else N.MODE_PER_SHARE)
-    ep = Epoch(ctx, args.n, args.cts, SEED + 7919 * rank, corrupt_frac=args.corrupt)
+    ep = Epoch(ctx, args.n, args.cts, rank_seed(rank), corrupt_frac=args.corrupt)
     log("rank %d: setup %.1fs (%d shares)" % (rank, time.time() - t0, ep.total))
 
     ctx.timing_enable(True)
@@ -198,11 +215,7 @@ def main():
         ep.step(ctx)
     ctx.sync()
     elapsed = time.perf_counter() - t0
-    if dist:
-        dist.barrier()
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(elapsed, dist)
     fams = ["dec_verify", "rlc_items", "rlc_groups", "rlc_triage", "rlc_sub", "rlc_leaves",
             "rlc_finalize", "lagrange", "comb_decode", "comb_digits", "combine", "prepare"]
     breakdown = {f: ctx.timing_read(f) for f in fams}

@@ -69,13 +69,33 @@ def test_msm_small_vs_oracle(ctx, group):
 
 
 @pytest.mark.parametrize("group,n", [(1, 1), (1, 7), (1, 64), (1, 334), (1, 3000), (2, 34),
-                                     (2, 700)])
+                                     (2, 700), (1, 56000), (2, 4000)])
 def test_msm_identity(ctx, group, n):
-    """sum_i k_i (a_i G) == (sum_i k_i a_i) G across window widths c = 4 .. 10."""
+    """sum_i k_i (a_i G) == (sum_i k_i a_i) G across window widths c = 4 .. 12 (n = 56000 is a
+    SyncKeyGen Part's MSM at t = 333)."""
     rng = random.Random(1000 * group + n)
     n_msm = 4
     a = [rng.randrange(1, R) for _ in range(n_msm * n)]
     k = [rng.randrange(0, R) for _ in range(n_msm * n)]
+    pts = _gen(ctx, group, a)
+    msm = ctx.g1_msm if group == 1 else ctx.g2_msm
+    out, st = msm(n_msm, n, pts, k)
+    assert not st.any()
+    want = _gen(ctx, group, [sum(k[m * n + i] * a[m * n + i] for i in range(n)) % R
+                             for m in range(n_msm)])
+    assert out == want
+
+
+@pytest.mark.parametrize("group,n", [(1, 5000), (2, 1500)])
+def test_msm_crowded_buckets(ctx, group, n):
+    """Scalars K + i share every digit above the lowest windows, so each of those windows puts
+    all n terms into ONE bucket: the bucket pass must split that bucket's run over lanes (equal
+    slices of the sorted list) and still sum to sum_b b B_b."""
+    rng = random.Random(77 + group)
+    n_msm = 2
+    K = rng.randrange(R // 2, R - n)
+    a = [rng.randrange(1, R) for _ in range(n_msm * n)]
+    k = [K + (i % n) for i in range(n_msm * n)]
     pts = _gen(ctx, group, a)
     msm = ctx.g1_msm if group == 1 else ctx.g2_msm
     out, st = msm(n_msm, n, pts, k)
