@@ -47,7 +47,10 @@ $(BUILD)/hbtc_skg.p%.o: $(CSRC)/hbtc_skg.hip $(HDRS) | $(BUILD)
 $(BUILD)/hbtc_api.o: $(CSRC)/hbtc_api.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(KOBJS) $(BUILD)/hbtc_api.o
+$(BUILD)/hbtc_hash.o: $(CSRC)/hbtc_hash.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(KOBJS) $(BUILD)/hbtc_api.o $(BUILD)/hbtc_hash.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
 # per-kernel VGPR / scratch / occupancy report (one part at a time: make resources PART=2)

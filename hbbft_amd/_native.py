@@ -74,6 +74,11 @@ SIGNATURES = {
     "hbtc_skg_check_parts": (_I32, [_P, _U32, _U32, _U32, _P, _P, _P]),
     "hbtc_skg_check_acks": (_I32, [_P, _U32, _U32, _U32, _P, _P, _P, _U32, _P, _P, _P, _P]),
     "hbtc_set_verify_mode": (_I32, [_P, _I32]),
+    "hbtc_sha3_256": (_I32, [_P, _SZ, _P]),
+    "hbtc_hash_g2": (_I32, [_P, _SZ, _P]),
+    "hbtc_hash_g1_g2": (_I32, [_P, _P, _SZ, _P]),
+    "hbtc_hash_g2_batch": (_I32, [_U32, _P, _P, _P]),
+    "hbtc_hash_g1_g2_batch": (_I32, [_U32, _P, _P, _P, _P]),
     "hbtc_rlc_last_leaves": (_I32, [_P, ctypes.POINTER(_U32)]),
     "hbtc_timing_enable": (_I32, [_P, _I32]),
     "hbtc_timing_read": (_I32, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
@@ -106,6 +111,66 @@ def load():
 
 def device_count():
     return load().hbtc_device_count()
+
+
+def sha3_256(msg):
+    """SHA3-256 through the library (host code; no context or GPU needed)."""
+    m = bytes(msg)
+    out = ctypes.create_string_buffer(32)
+    if load().hbtc_sha3_256(m, len(m), out) != 0:
+        raise HbtcError("hbtc_sha3_256 failed")
+    return out.raw
+
+
+def hash_g2(msg):
+    """threshold_crypto's hash_g2(msg) as compressed G2 bytes (host code, no GPU)."""
+    m = bytes(msg)
+    out = ctypes.create_string_buffer(96)
+    if load().hbtc_hash_g2(m, len(m), out) != 0:
+        raise HbtcError("hbtc_hash_g2 failed")
+    return out.raw
+
+
+def hash_g1_g2(g1_c48, msg):
+    """threshold_crypto's hash_g1_g2(g1, msg) as compressed G2 bytes (host code, no GPU)."""
+    g, m = bytes(g1_c48), bytes(msg)
+    if len(g) != 48:
+        raise ValueError("g1 must be 48 compressed bytes")
+    out = ctypes.create_string_buffer(96)
+    if load().hbtc_hash_g1_g2(g, m, len(m), out) != 0:
+        raise HbtcError("hbtc_hash_g1_g2 failed")
+    return out.raw
+
+
+def _msg_batch(msgs):
+    ms = [bytes(m) for m in msgs]
+    off = np.zeros(len(ms) + 1, np.uint32)
+    off[1:] = np.cumsum([len(m) for m in ms])
+    buf = np.frombuffer(b"".join(ms) or b"\0", np.uint8).copy()
+    return buf, off
+
+
+def hash_g2_batch(msgs):
+    """hash_g2 of every message, over the host's cores; returns a list of 96-byte encodings."""
+    buf, off = _msg_batch(msgs)
+    n = off.size - 1
+    out = np.zeros(96 * max(n, 1), np.uint8)
+    if load().hbtc_hash_g2_batch(n, _ptr(buf), _ptr(off), _ptr(out)) != 0:
+        raise HbtcError("hbtc_hash_g2_batch failed")
+    return [bytes(out[96 * i:96 * i + 96]) for i in range(n)]
+
+
+def hash_g1_g2_batch(us, msgs):
+    """hash_g1_g2(u_i, v_i) for every ciphertext, over the host's cores."""
+    buf, off = _msg_batch(msgs)
+    n = off.size - 1
+    u = _join(us, 48)
+    if u.size != 48 * n:
+        raise ValueError("one 48-byte u per message")
+    out = np.zeros(96 * max(n, 1), np.uint8)
+    if load().hbtc_hash_g1_g2_batch(n, _ptr(u), _ptr(buf), _ptr(off), _ptr(out)) != 0:
+        raise HbtcError("hbtc_hash_g1_g2_batch failed")
+    return [bytes(out[96 * i:96 * i + 96]) for i in range(n)]
 
 
 def _u8(buf, item_bytes=None):

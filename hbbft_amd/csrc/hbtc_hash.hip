@@ -1,0 +1,263 @@
+// Host-side hash_g2 / hash_g1_g2 of threshold_crypto @ 0.1.0-rng-fix: the
+// per-instance hash that hbbft's coin nonce (src/coin.rs:151 via PublicKeyShare::verify) and
+// every ciphertext (src/threshold_decryption.rs:159 via verify_decryption_share) go through.
+// The GPU path receives H; this computes it once per instance on the host, as the north star
+// asks.  Algorithm (restated, [EXT-UNVERIFIED] like oracle/rand04.py, which it must match
+// byte for byte — tests/test_hash.py):
+//   seed   = sha3_256(msg) read as 8 big-endian u32 words
+//   rng    = rand 0.4 ChaChaRng::from_seed(seed): 20 rounds, key = seed, 128-bit block counter
+//            in words 12..15 from 0, output words in order; next_u64 = (first << 32) | second
+//   G2::rand: loop { x = Fq2 { c0: Fq::rand, c1: Fq::rand }  (6 u64 limbs, top 3 bits masked,
+//            rejected if >= p, the limbs ARE the Montgomery form); greatest = next_u32 & 1;
+//            p = get_point_from_x(x, greatest); if some: q = [h2] p; if q != O: return q }
+//   hash_g1_g2(g1, msg) = hash_g2((len(msg) > 64 ? sha3_256(msg) : msg) || compressed(g1))
+// The 384-bit Montgomery radix of pairing 0.14 (6 x 64) equals this library's (12 x 32), so
+// the drawn limbs are used as the Montgomery representation directly.
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "hbtc.h"
+#include "hbtc_kernels.h"
+
+namespace hbtc {
+namespace {
+
+// ------------------------------------------------------------------ SHA3-256 (FIPS 202)
+const uint64_t KECCAK_RC[24] = {
+    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808aull, 0x8000000080008000ull,
+    0x000000000000808bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+    0x000000000000008aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000aull,
+    0x000000008000808bull, 0x800000000000008bull, 0x8000000000008089ull, 0x8000000000008003ull,
+    0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800aull, 0x800000008000000aull,
+    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+const int KECCAK_ROT[25] = {0,  1,  62, 28, 27, 36, 44, 6,  55, 20, 3,  10, 43,
+                            25, 39, 41, 45, 15, 21, 8,  18, 2,  61, 56, 14};
+
+inline uint64_t rotl64(uint64_t v, int c) { return c ? (v << c) | (v >> (64 - c)) : v; }
+
+void keccak_f(uint64_t a[25]) {
+  for (int round = 0; round < 24; ++round) {
+    uint64_t c[5], b[25];
+    for (int x = 0; x < 5; ++x) c[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
+    for (int x = 0; x < 5; ++x) {
+      const uint64_t d = c[(x + 4) % 5] ^ rotl64(c[(x + 1) % 5], 1);
+      for (int y = 0; y < 25; y += 5) a[y + x] ^= d;
+    }
+    // rho + pi: b[y, 2x + 3y] = rot(a[x, y])
+    for (int x = 0; x < 5; ++x)
+      for (int y = 0; y < 5; ++y) b[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(a[x + 5 * y], KECCAK_ROT[x + 5 * y]);
+    for (int y = 0; y < 25; y += 5)
+      for (int x = 0; x < 5; ++x) a[y + x] = b[y + x] ^ (~b[y + (x + 1) % 5] & b[y + (x + 2) % 5]);
+    a[0] ^= KECCAK_RC[round];
+  }
+}
+
+void sha3_256(const uint8_t* msg, size_t len, uint8_t out[32]) {
+  const size_t rate = 136;
+  uint64_t a[25] = {0};
+  std::vector<uint8_t> buf(msg, msg + len);
+  buf.push_back(0x06);
+  while (buf.size() % rate) buf.push_back(0);
+  buf.back() |= 0x80;
+  for (size_t off = 0; off < buf.size(); off += rate) {
+    for (size_t i = 0; i < rate / 8; ++i) {
+      uint64_t v = 0;
+      for (int j = 7; j >= 0; --j) v = (v << 8) | buf[off + 8 * i + j];
+      a[i] ^= v;
+    }
+    keccak_f(a);
+  }
+  for (int i = 0; i < 32; ++i) out[i] = (uint8_t)(a[i / 8] >> (8 * (i % 8)));
+}
+
+// ------------------------------------------------------------------ rand 0.4 ChaChaRng
+struct ChaCha04 {
+  uint32_t state[16], buf[16];
+  int index = 16;
+  explicit ChaCha04(const uint32_t seed[8]) {
+    const uint32_t k[4] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+    for (int i = 0; i < 4; ++i) state[i] = k[i];
+    for (int i = 0; i < 8; ++i) state[4 + i] = seed[i];
+    for (int i = 12; i < 16; ++i) state[i] = 0;
+  }
+  static inline uint32_t rotl(uint32_t v, int c) { return (v << c) | (v >> (32 - c)); }
+  static inline void qr(uint32_t* s, int a, int b, int c, int d) {
+    s[a] += s[b]; s[d] = rotl(s[d] ^ s[a], 16);
+    s[c] += s[d]; s[b] = rotl(s[b] ^ s[c], 12);
+    s[a] += s[b]; s[d] = rotl(s[d] ^ s[a], 8);
+    s[c] += s[d]; s[b] = rotl(s[b] ^ s[c], 7);
+  }
+  void refill() {
+    uint32_t s[16];
+    memcpy(s, state, sizeof(s));
+    for (int i = 0; i < 10; ++i) {
+      qr(s, 0, 4, 8, 12); qr(s, 1, 5, 9, 13); qr(s, 2, 6, 10, 14); qr(s, 3, 7, 11, 15);
+      qr(s, 0, 5, 10, 15); qr(s, 1, 6, 11, 12); qr(s, 2, 7, 8, 13); qr(s, 3, 4, 9, 14);
+    }
+    for (int i = 0; i < 16; ++i) buf[i] = s[i] + state[i];
+    index = 0;
+    for (int i = 12; i < 16; ++i)  // 128-bit block counter
+      if (++state[i] != 0) break;
+  }
+  uint32_t next_u32() {
+    if (index == 16) refill();
+    return buf[index++];
+  }
+  uint64_t next_u64() {  // rand 0.4's default: the first word is the high half
+    const uint64_t hi = next_u32();
+    return (hi << 32) | next_u32();
+  }
+};
+
+// ff_derive Rand for Fq: the drawn limbs are the Montgomery representation
+void fq_rand(Fq& r, ChaCha04& rng) {
+  for (;;) {
+    uint64_t l[6];
+    for (int i = 0; i < 6; ++i) l[i] = rng.next_u64();
+    l[5] &= 0xffffffffffffffffull >> 3;
+    for (int i = 0; i < 6; ++i) {
+      r.v[2 * i] = (uint32_t)l[i];
+      r.v[2 * i + 1] = (uint32_t)(l[i] >> 32);
+    }
+    if (limbs_lt_const<12>(r, FQ_P)) return;
+  }
+}
+
+const Limbs<16> G2_COFACTOR = {{0x1c7238e5u, 0xcf1c38e3u, 0x786f0c70u, 0x1616ec6eu, 0x3a6691aeu,
+                                0x21537e29u, 0x4d9e82efu, 0xa628f1cbu, 0x2e5a7ddfu, 0xa68a205bu,
+                                0x47085abau, 0xcd91de45u, 0x2876a202u, 0x091d5079u, 0x5414e7f1u,
+                                0x05d543a9u}};
+
+// pairing 0.14 G2::rand over the seeded ChaChaRng
+void g2_rand(G2A& out, ChaCha04& rng) {
+  for (;;) {
+    Fq2 x;
+    fq_rand(x.c0, rng);
+    fq_rand(x.c1, rng);
+    const bool greatest = (rng.next_u32() & 1u) != 0;
+    // get_point_from_x: y = sqrt(x^3 + b), the larger of y, -y when `greatest`
+    Fq2 rhs, b, y;
+    fq2_sqr(rhs, x);
+    fq2_mul(rhs, rhs, x);
+    fq2_set(b, G2_B);
+    fq2_add(rhs, rhs, b);
+    if (!fq2_sqrt(y, rhs)) continue;
+    if (fq2_is_lex_largest(y) != greatest) fq2_neg(y, y);
+    G2A p;
+    fq_canon(p.x.c0, x.c0);
+    fq_canon(p.x.c1, x.c1);
+    fq_canon(p.y.c0, y.c0);
+    fq_canon(p.y.c1, y.c1);
+    p.inf = 0;
+    G2J q;
+    jac_mul_limbs<Fq2, 16>(q, p, G2_COFACTOR);  // scale_by_cofactor (full h2)
+    if (jac_is_inf(q)) continue;
+    jac_to_aff(out, q);
+    return;
+  }
+}
+
+void store_le_words(uint8_t* b, const uint32_t* w, int nwords) {
+  for (int i = 0; i < nwords; ++i)
+    for (int j = 0; j < 4; ++j) b[4 * i + j] = (uint8_t)(w[i] >> (8 * j));
+}
+
+void hash_g2_c96(const uint8_t* msg, size_t len, uint8_t* out96) {
+  uint8_t d[32];
+  sha3_256(msg, len, d);
+  uint32_t seed[8];
+  for (int i = 0; i < 8; ++i)
+    seed[i] = ((uint32_t)d[4 * i] << 24) | ((uint32_t)d[4 * i + 1] << 16) |
+              ((uint32_t)d[4 * i + 2] << 8) | d[4 * i + 3];
+  ChaCha04 rng(seed);
+  G2A h;
+  g2_rand(h, rng);
+  uint32_t w[24];
+  g2_compress(w, h);
+  store_le_words(out96, w, 24);  // little-endian words of the big-endian encoding
+}
+
+void hash_g1_g2_c96(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8_t* out96) {
+  std::vector<uint8_t> m;
+  if (len > 64) {
+    m.resize(32);
+    sha3_256(msg, len, m.data());
+  } else {
+    m.assign(msg, msg + len);
+  }
+  m.insert(m.end(), g1_c48, g1_c48 + 48);
+  hash_g2_c96(m.data(), m.size(), out96);
+}
+
+// Items [0, n) over the host's cores (a work counter; each item is independent).
+template <class F>
+void parallel_items(uint32_t n, F&& f) {
+  const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+  const uint32_t nt = std::min<uint32_t>(std::min<uint32_t>(hw, 64u), n);
+  std::atomic<uint32_t> next{0};
+  auto worker = [&] {
+    for (uint32_t i; (i = next.fetch_add(1)) < n;) f(i);
+  };
+  std::vector<std::thread> pool;
+  for (uint32_t t = 1; t < nt; ++t) pool.emplace_back(worker);
+  worker();
+  for (auto& th : pool) th.join();
+}
+
+bool offsets_ok(uint32_t n, const uint32_t* offsets) {
+  if (offsets[0] != 0) return false;
+  for (uint32_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return false;
+  return true;
+}
+
+}  // namespace
+}  // namespace hbtc
+
+extern "C" {
+
+int hbtc_sha3_256(const uint8_t* msg, size_t len, uint8_t* out32) {
+  if ((!msg && len) || !out32) return HBTC_ERR_ARG;
+  hbtc::sha3_256(msg, len, out32);
+  return HBTC_OK;
+}
+
+int hbtc_hash_g2(const uint8_t* msg, size_t len, uint8_t* out_c96) {
+  if ((!msg && len) || !out_c96) return HBTC_ERR_ARG;
+  hbtc::hash_g2_c96(msg, len, out_c96);
+  return HBTC_OK;
+}
+
+int hbtc_hash_g1_g2(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8_t* out_c96) {
+  if (!g1_c48 || (!msg && len) || !out_c96) return HBTC_ERR_ARG;
+  hbtc::hash_g1_g2_c96(g1_c48, msg, len, out_c96);
+  return HBTC_OK;
+}
+
+int hbtc_hash_g2_batch(uint32_t n, const uint8_t* msgs, const uint32_t* offsets,
+                       uint8_t* out_c96) {
+  if (n == 0) return HBTC_OK;
+  if (!offsets || !out_c96 || (!msgs && offsets[n]) || !hbtc::offsets_ok(n, offsets))
+    return HBTC_ERR_ARG;
+  hbtc::parallel_items(n, [&](uint32_t i) {
+    hbtc::hash_g2_c96(msgs + offsets[i], offsets[i + 1] - offsets[i], out_c96 + 96 * (size_t)i);
+  });
+  return HBTC_OK;
+}
+
+int hbtc_hash_g1_g2_batch(uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
+                          const uint32_t* offsets, uint8_t* out_c96) {
+  if (n == 0) return HBTC_OK;
+  if (!g1_c48 || !offsets || !out_c96 || (!msgs && offsets[n]) || !hbtc::offsets_ok(n, offsets))
+    return HBTC_ERR_ARG;
+  hbtc::parallel_items(n, [&](uint32_t i) {
+    hbtc::hash_g1_g2_c96(g1_c48 + 48 * (size_t)i, msgs + offsets[i], offsets[i + 1] - offsets[i],
+                         out_c96 + 96 * (size_t)i);
+  });
+  return HBTC_OK;
+}
+
+}  // extern "C"

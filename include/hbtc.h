@@ -122,6 +122,23 @@ int hbtc_combine_dec(hbtc_ctx* ctx, uint32_t n_ct, const uint32_t* offsets, cons
 int hbtc_verify_ciphertexts(hbtc_ctx* ctx, uint32_t n, const uint8_t* u_c48,
                             const uint8_t* H_c96, const uint8_t* w_c96, int32_t* status);
 
+/* ---- host hashes (no context, no GPU) ----------------------------------------------------- */
+/* threshold_crypto's crate-internal hash_g2(msg) -> compressed G2 (96 B), and hash_g1_g2(g1, msg)
+ * = hash_g2((|msg| > 64 ? sha3_256(msg) : msg) || g1_c48).  These produce the H that
+ * PublicKeyShare::verify (src/coin.rs:151: H = hash_g2(nonce)) and verify_decryption_share /
+ * Ciphertext::verify (src/threshold_decryption.rs:98,159: H = hash_g1_g2(u, v)) compute per
+ * call; the batch queue computes it once per instance and passes it to the verifiers.  Byte
+ * stream follows rand 0.4's ChaChaRng (parity unpinned). */
+int hbtc_sha3_256(const uint8_t* msg, size_t len, uint8_t* out32);
+int hbtc_hash_g2(const uint8_t* msg, size_t len, uint8_t* out_c96);
+int hbtc_hash_g1_g2(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8_t* out_c96);
+/* Batches over the host's cores: message i = msgs[offsets[i] .. offsets[i+1]) (offsets[0] == 0,
+ * non-decreasing); ciphertext i's u is g1_c48[48 i ..]. */
+int hbtc_hash_g2_batch(uint32_t n, const uint8_t* msgs, const uint32_t* offsets,
+                       uint8_t* out_c96);
+int hbtc_hash_g1_g2_batch(uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
+                          const uint32_t* offsets, uint8_t* out_c96);
+
 /* ---- batched scalar multiplication -------------------------------------------------------- */
 /* out_i = k_i * P_i with 32-byte little-endian scalars (any value < 2^256).  base_stride is 1
  * for one base per item or 0 for a single shared base.  status[i] = ACCEPT or DECODE_ERR. */
