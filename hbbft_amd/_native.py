@@ -79,6 +79,8 @@ SIGNATURES = {
     "hbtc_hash_g1_g2": (_I32, [_P, _P, _SZ, _P]),
     "hbtc_hash_g2_batch": (_I32, [_U32, _P, _P, _P]),
     "hbtc_hash_g1_g2_batch": (_I32, [_U32, _P, _P, _P, _P]),
+    "hbtc_hash_g2_batch_gpu": (_I32, [_P, _U32, _P, _P, _P]),
+    "hbtc_hash_g1_g2_batch_gpu": (_I32, [_P, _U32, _P, _P, _P, _P]),
     "hbtc_rlc_last_leaves": (_I32, [_P, ctypes.POINTER(_U32)]),
     "hbtc_timing_enable": (_I32, [_P, _I32]),
     "hbtc_timing_read": (_I32, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
@@ -233,6 +235,26 @@ class Context:
         if rc != 0:
             msg = self.lib.hbtc_last_error(self.h)
             raise HbtcError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+    # ---- hashes (cofactor clearing on this context's GPU)
+    def hash_g2_batch(self, msgs):
+        buf, off = _msg_batch(msgs)
+        n = off.size - 1
+        out = np.zeros(96 * max(n, 1), np.uint8)
+        self._check(self.lib.hbtc_hash_g2_batch_gpu(self.h, n, _ptr(buf), _ptr(off), _ptr(out)),
+                    "hbtc_hash_g2_batch_gpu")
+        return [bytes(out[96 * i:96 * i + 96]) for i in range(n)]
+
+    def hash_g1_g2_batch(self, us, msgs):
+        buf, off = _msg_batch(msgs)
+        n = off.size - 1
+        u = _join(us, 48)
+        if u.size != 48 * n:
+            raise ValueError("one 48-byte u per message")
+        out = np.zeros(96 * max(n, 1), np.uint8)
+        self._check(self.lib.hbtc_hash_g1_g2_batch_gpu(self.h, n, _ptr(u), _ptr(buf), _ptr(off),
+                                                       _ptr(out)), "hbtc_hash_g1_g2_batch_gpu")
+        return [bytes(out[96 * i:96 * i + 96]) for i in range(n)]
 
     # ---- key sets
     def keyset_load(self, pk_shares):

@@ -15,6 +15,19 @@
 
 using namespace hbtc;
 
+#include <functional>
+
+namespace hbtc {
+// hbtc_hash.hip: host hash_g2 pieces + the GPU cofactor clearing
+void hash_g2_c96(const uint8_t* msg, size_t len, uint8_t* out96);
+void g1_g2_message(const uint8_t* g1_c48, const uint8_t* msg, size_t len, std::vector<uint8_t>& m);
+void hash_g2_candidate(const uint8_t* msg, size_t len, G2A& p);
+void parallel_items(uint32_t n, const std::function<void(uint32_t)>& f);
+bool hash_offsets_ok(uint32_t n, const uint32_t* offsets);
+hipError_t launch_g2_clear_cofactor(hipStream_t s, uint32_t n, const G2A* in, uint8_t* out_c96,
+                                    int32_t* st);
+}  // namespace hbtc
+
 namespace {
 
 struct DevBuf {
@@ -1257,6 +1270,54 @@ int hbtc_timing_reset(hbtc_ctx* c) {
   HB_TRY(collect_spans(c));
   c->totals.clear();
   return HBTC_OK;
+}
+
+// ---- hashes with the cofactor clearing on the GPU (the host draws the candidates)
+static int hash_batch_gpu(hbtc_ctx* c, uint32_t n, const std::vector<std::vector<uint8_t>>& msgs,
+                          uint8_t* out_c96) {
+  std::vector<G2A> cand(n);
+  parallel_items(n, [&](uint32_t i) { hash_g2_candidate(msgs[i].data(), msgs[i].size(), cand[i]); });
+  HB_TRY(sync(c));
+  void* d_cand;
+  uint8_t* d_out;
+  int32_t* d_st;
+  HB_TRY(stage_upload(c, "hash.cand", cand.data(), (size_t)n * sizeof(G2A), c->stream, &d_cand));
+  HB_TRY(wst(c, "hash.out", (size_t)n * 96, &d_out));
+  HB_TRY(wst(c, "hash.st", n, &d_st));
+  HB_CHECK(c, launch_g2_clear_cofactor(c->stream, n, (const G2A*)d_cand, d_out, d_st));
+  std::vector<int32_t> st(n);
+  HB_CHECK(c, hipMemcpyAsync(out_c96, d_out, (size_t)n * 96, hipMemcpyDeviceToHost, c->stream));
+  HB_CHECK(c, hipMemcpyAsync(st.data(), d_st, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  HB_TRY(sync(c));
+  for (uint32_t i = 0; i < n; ++i)  // [h2] P = O: G2::rand draws again (host, exact)
+    if (st[i]) hash_g2_c96(msgs[i].data(), msgs[i].size(), out_c96 + 96 * (size_t)i);
+  return HBTC_OK;
+}
+
+int hbtc_hash_g2_batch_gpu(hbtc_ctx* c, uint32_t n, const uint8_t* msgs, const uint32_t* offsets,
+                           uint8_t* out_c96) {
+  if (!c) return HBTC_ERR_ARG;
+  if (n == 0) return HBTC_OK;
+  if (!offsets || !out_c96 || (!msgs && offsets[n]) || !hash_offsets_ok(n, offsets))
+    return HBTC_ERR_ARG;
+  Guard g(c);
+  std::vector<std::vector<uint8_t>> m(n);
+  for (uint32_t i = 0; i < n; ++i) m[i].assign(msgs + offsets[i], msgs + offsets[i + 1]);
+  return hash_batch_gpu(c, n, m, out_c96);
+}
+
+int hbtc_hash_g1_g2_batch_gpu(hbtc_ctx* c, uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
+                              const uint32_t* offsets, uint8_t* out_c96) {
+  if (!c) return HBTC_ERR_ARG;
+  if (n == 0) return HBTC_OK;
+  if (!g1_c48 || !offsets || !out_c96 || (!msgs && offsets[n]) || !hash_offsets_ok(n, offsets))
+    return HBTC_ERR_ARG;
+  Guard g(c);
+  std::vector<std::vector<uint8_t>> m(n);
+  parallel_items(n, [&](uint32_t i) {
+    g1_g2_message(g1_c48 + 48 * (size_t)i, msgs + offsets[i], offsets[i + 1] - offsets[i], m[i]);
+  });
+  return hash_batch_gpu(c, n, m, out_c96);
 }
 
 }  // extern "C"

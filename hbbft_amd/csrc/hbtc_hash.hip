@@ -15,7 +15,9 @@
 // the drawn limbs are used as the Montgomery representation directly.
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -131,27 +133,33 @@ const Limbs<16> G2_COFACTOR = {{0x1c7238e5u, 0xcf1c38e3u, 0x786f0c70u, 0x1616ec6
                                 0x47085abau, 0xcd91de45u, 0x2876a202u, 0x091d5079u, 0x5414e7f1u,
                                 0x05d543a9u}};
 
+// One draw of G2::rand's loop: x, greatest, get_point_from_x.  False if x^3 + b is not a square
+// (the loop draws again).
+bool g2_rand_candidate(G2A& p, ChaCha04& rng) {
+  Fq2 x;
+  fq_rand(x.c0, rng);
+  fq_rand(x.c1, rng);
+  const bool greatest = (rng.next_u32() & 1u) != 0;
+  Fq2 rhs, b, y;
+  fq2_sqr(rhs, x);
+  fq2_mul(rhs, rhs, x);
+  fq2_set(b, G2_B);
+  fq2_add(rhs, rhs, b);
+  if (!fq2_sqrt(y, rhs)) return false;
+  if (fq2_is_lex_largest(y) != greatest) fq2_neg(y, y);
+  fq_canon(p.x.c0, x.c0);
+  fq_canon(p.x.c1, x.c1);
+  fq_canon(p.y.c0, y.c0);
+  fq_canon(p.y.c1, y.c1);
+  p.inf = 0;
+  return true;
+}
+
 // pairing 0.14 G2::rand over the seeded ChaChaRng
 void g2_rand(G2A& out, ChaCha04& rng) {
   for (;;) {
-    Fq2 x;
-    fq_rand(x.c0, rng);
-    fq_rand(x.c1, rng);
-    const bool greatest = (rng.next_u32() & 1u) != 0;
-    // get_point_from_x: y = sqrt(x^3 + b), the larger of y, -y when `greatest`
-    Fq2 rhs, b, y;
-    fq2_sqr(rhs, x);
-    fq2_mul(rhs, rhs, x);
-    fq2_set(b, G2_B);
-    fq2_add(rhs, rhs, b);
-    if (!fq2_sqrt(y, rhs)) continue;
-    if (fq2_is_lex_largest(y) != greatest) fq2_neg(y, y);
     G2A p;
-    fq_canon(p.x.c0, x.c0);
-    fq_canon(p.x.c1, x.c1);
-    fq_canon(p.y.c0, y.c0);
-    fq_canon(p.y.c1, y.c1);
-    p.inf = 0;
+    if (!g2_rand_candidate(p, rng)) continue;
     G2J q;
     jac_mul_limbs<Fq2, 16>(q, p, G2_COFACTOR);  // scale_by_cofactor (full h2)
     if (jac_is_inf(q)) continue;
@@ -165,13 +173,19 @@ void store_le_words(uint8_t* b, const uint32_t* w, int nwords) {
     for (int j = 0; j < 4; ++j) b[4 * i + j] = (uint8_t)(w[i] >> (8 * j));
 }
 
-void hash_g2_c96(const uint8_t* msg, size_t len, uint8_t* out96) {
+void seed_of(const uint8_t* msg, size_t len, uint32_t seed[8]) {
   uint8_t d[32];
   sha3_256(msg, len, d);
-  uint32_t seed[8];
   for (int i = 0; i < 8; ++i)
     seed[i] = ((uint32_t)d[4 * i] << 24) | ((uint32_t)d[4 * i + 1] << 16) |
               ((uint32_t)d[4 * i + 2] << 8) | d[4 * i + 3];
+}
+
+}  // namespace
+
+void hash_g2_c96(const uint8_t* msg, size_t len, uint8_t* out96) {
+  uint32_t seed[8];
+  seed_of(msg, len, seed);
   ChaCha04 rng(seed);
   G2A h;
   g2_rand(h, rng);
@@ -180,8 +194,8 @@ void hash_g2_c96(const uint8_t* msg, size_t len, uint8_t* out96) {
   store_le_words(out96, w, 24);  // little-endian words of the big-endian encoding
 }
 
-void hash_g1_g2_c96(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8_t* out96) {
-  std::vector<uint8_t> m;
+void g1_g2_message(const uint8_t* g1_c48, const uint8_t* msg, size_t len,
+                   std::vector<uint8_t>& m) {
   if (len > 64) {
     m.resize(32);
     sha3_256(msg, len, m.data());
@@ -189,13 +203,30 @@ void hash_g1_g2_c96(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8
     m.assign(msg, msg + len);
   }
   m.insert(m.end(), g1_c48, g1_c48 + 48);
+}
+
+void hash_g1_g2_c96(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8_t* out96) {
+  std::vector<uint8_t> m;
+  g1_g2_message(g1_c48, msg, len, m);
   hash_g2_c96(m.data(), m.size(), out96);
 }
 
+// The first on-curve candidate of hash_g2(msg) (before [h2]); the GPU clears the cofactor.
+void hash_g2_candidate(const uint8_t* msg, size_t len, G2A& p) {
+  uint32_t seed[8];
+  seed_of(msg, len, seed);
+  ChaCha04 rng(seed);
+  while (!g2_rand_candidate(p, rng)) {
+  }
+}
+
 // Items [0, n) over the host's cores (a work counter; each item is independent).
-template <class F>
-void parallel_items(uint32_t n, F&& f) {
-  const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+void parallel_items(uint32_t n, const std::function<void(uint32_t)>& f) {
+  uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+  if (const char* e = getenv("OMP_NUM_THREADS")) {  // the process's CPU share, when given
+    const long v = strtol(e, nullptr, 10);
+    if (v > 0) hw = std::min<uint32_t>(hw, (uint32_t)v);
+  }
   const uint32_t nt = std::min<uint32_t>(std::min<uint32_t>(hw, 64u), n);
   std::atomic<uint32_t> next{0};
   auto worker = [&] {
@@ -207,14 +238,44 @@ void parallel_items(uint32_t n, F&& f) {
   for (auto& th : pool) th.join();
 }
 
-bool offsets_ok(uint32_t n, const uint32_t* offsets) {
+bool hash_offsets_ok(uint32_t n, const uint32_t* offsets) {
   if (offsets[0] != 0) return false;
   for (uint32_t i = 0; i < n; ++i)
     if (offsets[i + 1] < offsets[i]) return false;
   return true;
 }
 
-}  // namespace
+// [h2] P for candidates P (one lane each) -> compressed G2 words; st = 1 if [h2] P = O (the
+// host then continues G2::rand's loop itself).
+__global__ void __launch_bounds__(64) k_g2_clear_cofactor(uint32_t n, const G2A* __restrict__ in,
+                                                          Limbs<16> h2,
+                                                          uint32_t* __restrict__ out_w,
+                                                          int32_t* __restrict__ st) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  G2J q;
+  jac_mul_limbs<Fq2, 16>(q, in[i], h2);
+  if (jac_is_inf(q)) {
+    st[i] = 1;
+    return;
+  }
+  G2A a;
+  jac_to_aff(a, q);
+  uint32_t w[24];
+  g2_compress(w, a);
+  uint4* o = reinterpret_cast<uint4*>(out_w + 24 * (size_t)i);
+  for (int k = 0; k < 6; ++k) o[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+  st[i] = 0;
+}
+
+hipError_t launch_g2_clear_cofactor(hipStream_t s, uint32_t n, const G2A* in, uint8_t* out_c96,
+                                    int32_t* st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_g2_clear_cofactor, dim3((n + 63) / 64), dim3(64), 0, s, n, in,
+                     G2_COFACTOR, reinterpret_cast<uint32_t*>(out_c96), st);
+  return hipGetLastError();
+}
+
 }  // namespace hbtc
 
 extern "C" {
@@ -240,7 +301,7 @@ int hbtc_hash_g1_g2(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8
 int hbtc_hash_g2_batch(uint32_t n, const uint8_t* msgs, const uint32_t* offsets,
                        uint8_t* out_c96) {
   if (n == 0) return HBTC_OK;
-  if (!offsets || !out_c96 || (!msgs && offsets[n]) || !hbtc::offsets_ok(n, offsets))
+  if (!offsets || !out_c96 || (!msgs && offsets[n]) || !hbtc::hash_offsets_ok(n, offsets))
     return HBTC_ERR_ARG;
   hbtc::parallel_items(n, [&](uint32_t i) {
     hbtc::hash_g2_c96(msgs + offsets[i], offsets[i + 1] - offsets[i], out_c96 + 96 * (size_t)i);
@@ -251,7 +312,7 @@ int hbtc_hash_g2_batch(uint32_t n, const uint8_t* msgs, const uint32_t* offsets,
 int hbtc_hash_g1_g2_batch(uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
                           const uint32_t* offsets, uint8_t* out_c96) {
   if (n == 0) return HBTC_OK;
-  if (!g1_c48 || !offsets || !out_c96 || (!msgs && offsets[n]) || !hbtc::offsets_ok(n, offsets))
+  if (!g1_c48 || !offsets || !out_c96 || (!msgs && offsets[n]) || !hbtc::hash_offsets_ok(n, offsets))
     return HBTC_ERR_ARG;
   hbtc::parallel_items(n, [&](uint32_t i) {
     hbtc::hash_g1_g2_c96(g1_c48 + 48 * (size_t)i, msgs + offsets[i], offsets[i + 1] - offsets[i],

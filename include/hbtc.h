@@ -138,6 +138,12 @@ int hbtc_hash_g2_batch(uint32_t n, const uint8_t* msgs, const uint32_t* offsets,
                        uint8_t* out_c96);
 int hbtc_hash_g1_g2_batch(uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
                           const uint32_t* offsets, uint8_t* out_c96);
+/* The same batches with the full-cofactor multiplication [h2] P (the dominant cost: a 507-bit G2
+ * scalar multiplication per hash) on the context's GPU; the host draws the candidates P. */
+int hbtc_hash_g2_batch_gpu(hbtc_ctx* ctx, uint32_t n, const uint8_t* msgs, const uint32_t* offsets,
+                           uint8_t* out_c96);
+int hbtc_hash_g1_g2_batch_gpu(hbtc_ctx* ctx, uint32_t n, const uint8_t* g1_c48,
+                              const uint8_t* msgs, const uint32_t* offsets, uint8_t* out_c96);
 
 /* ---- batched scalar multiplication -------------------------------------------------------- */
 /* out_i = k_i * P_i with 32-byte little-endian scalars (any value < 2^256).  base_stride is 1
