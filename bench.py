@@ -43,6 +43,9 @@ SEED = 0x6862626674
 # measured v_mad_u64_u32 lane-op throughput on MI355X (tools/microbench/intmul.hip,
 # profiles/r01_intmul_microbench.txt): the VALU integer-multiply roofline of the Fqm kernels
 MAD_U64_PEAK = 29.51e12
+# timing family -> kernel (hbtc_api.hip timed() families, rocprofv3 names)
+KERNEL_NAME = {"dec_verify": "k_dec_verify", "rlc_items": "k_rlc_items",
+               "rlc_groups": "k_rlc_check_groups", "rlc_leaves": "k_rlc_leaves"}
 
 
 def log(*a):
@@ -256,7 +259,7 @@ def main():
     traffic, pmc = None, {}
     pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
     if os.path.exists(pmc_path):
-        pmc = json.load(open(pmc_path)).get("hbtc::k_" + dom, {})
+        pmc = json.load(open(pmc_path)).get("hbtc::" + KERNEL_NAME[dom], {})
         if "hbm_read_bytes" in pmc and "hbm_write_bytes" in pmc:
             traffic = pmc["hbm_read_bytes"] + pmc["hbm_write_bytes"]
     out = {
@@ -284,7 +287,7 @@ def main():
         "kernel_ms_per_step": per_step,
         "roofline": {
             "bound": "valu-int (v_mad_u64_u32)",
-            "kernel": "k_" + dom,
+            "kernel": KERNEL_NAME[dom],
             "achieved": round(achieved, 3),
             "peak": MAD_U64_PEAK / 1e12,
             "unit": "T mad_u64_u32/s",

@@ -221,7 +221,7 @@ __device__ void rlc_pk_mul(G1J& r, const PtXY* __restrict__ tab, uint32_t a, uin
 // by k_rlc_finalize.  Needs nothing from the per-ciphertext preparation, so it runs
 // concurrently with k_g2_prepare on another stream.
 #ifndef HBTC_ITEMS_WAVES
-#define HBTC_ITEMS_WAVES 1  // minimum waves per SIMD the register allocation must allow
+#define HBTC_ITEMS_WAVES 2  // minimum waves per SIMD the register allocation must allow (1: 153 ms, 2: 86 ms, 3: 161 ms per C3 launch)
 #endif
 __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
