@@ -72,10 +72,16 @@ class CoinEpoch:
         {key: [step per queued event]}."""
         ni = self.ni
         keys = [k for k in self.inst if self.inst[k].events]
+        # state at the start of the flush: a failed deferred combine replays from here
+        snap = {k: (dict(self.inst[k].received), self.inst[k].had_input, self.inst[k].terminated)
+                for k in keys}
         counts, idx, sigs, where = [], [], [], {}
         for k in keys:
             st = self.inst[k]
             c = 0
+            if st.terminated:  # coin.rs:105: nothing after termination is looked at
+                counts.append(0)
+                continue
             for e_i, ev in enumerate(st.events):
                 share = None
                 sender = None
@@ -98,7 +104,7 @@ class CoinEpoch:
         results, pending = {}, []
         for k in keys:
             results[k] = self._replay(k, verdict, pending)
-        self._finish_combines(pending, results, verdict)
+        self._finish_combines(pending, results, verdict, snap)
         for k in keys:
             self.inst[k].events = []
         return results
@@ -173,7 +179,7 @@ class CoinEpoch:
                 res[j] = (None, bool(par[j]))
         return res
 
-    def _finish_combines(self, pending, results, verdict):
+    def _finish_combines(self, pending, results, verdict, snap):
         if not pending:
             return
         res = self._combine([p[0] for p in pending], [p[2] for p in pending])
@@ -183,9 +189,10 @@ class CoinEpoch:
                 step["output"] = parity
             else:
                 failed.add(k)
-        for k in failed:  # rare: redo this instance with synchronous combines (exact retry semantics)
-            st = self.inst[k]
-            st.received, st.had_input, st.terminated = {}, False, False
+        for k in failed:  # rare: redo this flush of the instance with synchronous combines,
+            st = self.inst[k]  # from its state at the start of the flush (coin.rs:163-181 retries)
+            received, had_input, terminated = snap[k]
+            st.received, st.had_input, st.terminated = dict(received), had_input, terminated
             results[k] = self._replay(k, verdict, [], sync=True)
 
 
@@ -219,33 +226,40 @@ class DecryptionEpoch:
     def flush(self):
         ni = self.ni
         keys = [k for k in self.inst if self.inst[k].events]
-        # the ciphertext each instance will know by the end of its queue
+        # every queued ciphertext of an instance that has none yet: set_ciphertext leaves the
+        # instance without one after an invalid ciphertext (td.rs:94-105), so a later valid one
+        # in the same queue is accepted
+        ct_ev = []
+        for k in keys:
+            st = self.inst[k]
+            if st.ct is None:
+                ct_ev += [(k, e_i, ev[1]) for e_i, ev in enumerate(st.events) if ev[0] == "ct"]
+        ct_ok = {}
+        if ct_ev:
+            vs = self.ctx.verify_ciphertexts([c[0] for _, _, c in ct_ev], [c[3] for _, _, c in ct_ev],
+                                             [c[2] for _, _, c in ct_ev])
+            for (k, e_i, _), v in zip(ct_ev, vs):
+                ct_ok[(k, e_i)] = int(v) == N.ACCEPT
+        # the ciphertext each instance will know by the end of its queue: the stored one, else
+        # the first valid queued one
         ct_of = {}
-        new_cts = []
         for k in keys:
             st = self.inst[k]
             ct = st.ct
-            for ev in st.events:
-                if ev[0] == "ct" and ct is None:
-                    ct = ev[1]
-                    new_cts.append((k, ct))
+            if ct is None:
+                ct = next((ev[1] for e_i, ev in enumerate(st.events)
+                           if ev[0] == "ct" and ct_ok.get((k, e_i), False)), None)
             ct_of[k] = ct
-        ct_ok = {}
-        if new_cts:
-            vs = self.ctx.verify_ciphertexts([c[0] for _, c in new_cts], [c[3] for _, c in new_cts],
-                                             [c[2] for _, c in new_cts])
-            for (k, c), v in zip(new_cts, vs):
-                ct_ok[k] = int(v) == N.ACCEPT
-        # every share that may be checked against that ciphertext: stored ones + queued ones
+        # shares that will be checked against that ciphertext: the stored (still unverified)
+        # ones when it is set in this flush (remove_invalid_shares, td.rs:136-149), and every
+        # queued message of an instance that has not terminated (td.rs:121-128)
         vkeys, counts, idx, shares, where = [], [], [], [], {}
         for k in keys:
             st, ct = self.inst[k], ct_of[k]
-            if ct is None or (st.ct is None and not ct_ok.get(k, False)):
+            if ct is None or st.terminated:
                 continue
-            cand = [("stored", s, sh) for s, sh in st.shares.items()]
+            cand = [("stored", s, sh) for s, sh in st.shares.items()] if st.ct is None else []
             cand += [("ev%d" % e_i, ev[1], ev[2]) for e_i, ev in enumerate(st.events) if ev[0] == "msg"]
-            if ni.is_validator() and st.our_share is not None:
-                cand.append(("own", ni.our_id, st.our_share))
             c = 0
             for tag, sender, sh in cand:
                 if sender in ni.index:
@@ -253,8 +267,9 @@ class DecryptionEpoch:
                     idx.append(ni.index[sender])
                     shares.append(sh)
                     c += 1
-            vkeys.append(k)
-            counts.append(c)
+            if c:
+                vkeys.append(k)
+                counts.append(c)
         verdict = {}
         if idx:
             status = self.ctx.verify_dec_shares(ni.keyset, [ct_of[k][3] for k in vkeys],
@@ -294,7 +309,7 @@ class DecryptionEpoch:
                 if st.ct is not None:
                     steps.append(_step(error="MultipleInputs"))
                     continue
-                if not ct_ok.get(k, False):
+                if not ct_ok.get((k, e_i), False):
                     steps.append(_step(error="InvalidCiphertext"))
                     continue
                 st.ct = ev[1]

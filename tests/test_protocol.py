@@ -108,9 +108,11 @@ def coin_scenario(rng, n, n_inst):
     return ids, sks, pks, mpk, our, insts
 
 
-def run_coin(ctx, rng, n=7, n_inst=3, n_flush=2):
+def run_coin(ctx, rng, n=7, n_inst=3, n_flush=2, wrong_master=False):
     ids, sks, pks, mpk, our, insts = coin_scenario(rng, n, n_inst)
     f = (n - 1) // 3
+    if wrong_master:  # every combine fails the master check: VerificationFailed, retried per share
+        mpk = cb.g1_mul(G1, 12345)
     ks, _ = ctx.keyset_load(pks)
     ni = P.NetInfo(ids, our, ks, master_pk=mpk)
     ep = P.CoinEpoch(ctx, ni)
@@ -137,7 +139,10 @@ def run_coin(ctx, rng, n=7, n_inst=3, n_flush=2):
         ref = RULES.Coin(ids, our, f, own, verify, comb, lambda sig, H=H: bool(cb.pairing_eq(mpk, H, G1, sig)))
         want = ref.run(events)
         assert got[k] == want, (k, events)
-        assert any(s["output"] is not None for s in want)
+        if wrong_master:
+            assert sum(s["error"] == "VerificationFailed" for s in want) >= 2
+        else:
+            assert any(s["output"] is not None for s in want)
 
 
 def run_decryption(ctx, rng, n=7, n_ct=3, n_flush=2):
@@ -155,8 +160,9 @@ def run_decryption(ctx, rng, n=7, n_ct=3, n_flush=2):
         v = bytes(rng.randrange(256) for _ in range(24))
         H = cb.hash_g1_g2(u, v)
         w = cb.g2_mul(H, r)
+        w_bad = cb.g2_mul(H, r + 1)  # invalid ciphertext: set_ciphertext -> InvalidCiphertext
         if k == 2:
-            w = cb.g2_mul(H, r + 1)  # invalid ciphertext: set_ciphertext -> InvalidCiphertext
+            w = w_bad
         shares = {ids[i]: cb.g1_mul(u, sks[i]) for i in range(n)}
         for b in rng.sample(ids, 2):
             shares[b] = cb.g1_mul(u, sks[0] + 5)
@@ -164,7 +170,10 @@ def run_decryption(ctx, rng, n=7, n_ct=3, n_flush=2):
         events.append(("msg", "zz_unknown", shares[ids[0]]))
         events.append(("msg", ids[2], shares[ids[2]]))
         rng.shuffle(events)
-        events.insert(rng.randrange(len(events) + 1), ("ct", (u, v, w, H)))
+        pos = rng.randrange(len(events) + 1)
+        events.insert(pos, ("ct", (u, v, w, H)))
+        if k == 1:  # an invalid ciphertext queued before the valid one: the valid one is accepted
+            events.insert(rng.randrange(pos + 1), ("ct", (u, v, w_bad, H)))
         own = cb.g1_mul(u, sks[ids.index(our)])
         cases[k] = (own, events)
         ep.add(k, own)
@@ -207,6 +216,13 @@ def test_decryption_queue_matches_reference_rules_cpu(seed):
     run_decryption(OracleCtx(), random.Random(seed))
 
 
+@pytest.mark.parametrize("seed", [11, 12])
+def test_coin_queue_failed_combine_retries_cpu(seed):
+    """A deferred combine that fails keeps the shares and the input of earlier flushes
+    (coin.rs:163-181 retries on every later share)."""
+    run_coin(OracleCtx(), random.Random(seed), n_flush=3, wrong_master=True)
+
+
 @pytest.fixture(scope="module")
 def gctx():
     c = N.Context(0)
@@ -218,6 +234,11 @@ def gctx():
 @pytest.mark.parametrize("seed", [5, 6, 7])
 def test_coin_queue_matches_reference_rules_gpu(gctx, seed):
     run_coin(gctx, random.Random(seed), n=10, n_inst=4, n_flush=3)
+
+
+@pytest.mark.gpu
+def test_coin_queue_failed_combine_retries_gpu(gctx):
+    run_coin(gctx, random.Random(13), n=10, n_inst=3, n_flush=3, wrong_master=True)
 
 
 @pytest.mark.gpu
