@@ -13,11 +13,12 @@ HDRS := $(wildcard $(CSRC)/*.h) include/hbtc.h
 BUILD := build
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC)
 PARTS := 1 2 3 4
-RLC_PARTS := 6 7
+RLC_PARTS := 6
 MSM_PARTS := 8 9
 SKG_PARTS := 10
 KOBJS := $(foreach p,$(PARTS),$(BUILD)/hbtc_kernels.p$(p).o) $(foreach p,$(RLC_PARTS),$(BUILD)/hbtc_rlc.p$(p).o) \
-         $(foreach p,$(MSM_PARTS),$(BUILD)/hbtc_msm.p$(p).o) $(foreach p,$(SKG_PARTS),$(BUILD)/hbtc_skg.p$(p).o)
+         $(foreach p,$(MSM_PARTS),$(BUILD)/hbtc_msm.p$(p).o) $(foreach p,$(SKG_PARTS),$(BUILD)/hbtc_skg.p$(p).o) \
+         $(BUILD)/hbtc_check.o
 LIB := hbbft_amd/libhbtc.so
 
 .PHONY: all lib hosttest oracle clean resources roofline-constants
@@ -44,6 +45,9 @@ $(BUILD)/hbtc_msm.p%.o: $(CSRC)/hbtc_msm.hip $(HDRS) | $(BUILD)
 $(BUILD)/hbtc_skg.p%.o: $(CSRC)/hbtc_skg.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
 
+$(BUILD)/hbtc_check.o: $(CSRC)/hbtc_check.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(BUILD)/hbtc_api.o: $(CSRC)/hbtc_api.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -60,8 +64,8 @@ resources:
 	  -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs|AGPRs|Scratch|Occupancy|Spill"
 
 hosttest: tests/native/libhbtc_hosttest.so
-tests/native/libhbtc_hosttest.so: tests/native/hbtc_hosttest.cpp $(HDRS)
-	$(CLANGXX) -O2 -std=c++17 -shared -fPIC -I$(CSRC) $< -o $@
+tests/native/libhbtc_hosttest.so: tests/native/hbtc_hosttest.cpp tests/native/gt_sim.cpp $(HDRS)
+	$(CLANGXX) -O2 -std=c++17 -shared -fPIC -pthread -I$(CSRC) tests/native/hbtc_hosttest.cpp tests/native/gt_sim.cpp -o $@
 
 oracle: oracle/c/libtcoracle.so
 oracle/c/libtcoracle.so: oracle/c/tc_oracle.c

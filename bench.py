@@ -17,7 +17,7 @@ own epoch shard of 1000 ciphertexts (shards are independent, SURVEY.md §8e: no 
 collective); gloo carries the barrier and the max-over-ranks time only.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with "roofline" (the longest
-critical-path kernel, k_rlc_items in the default RLC mode; Fqm counted by tools/fqm_count.cpp ->
+critical-path kernel of the default RLC mode; Fqm counted by tools/fqm_count.cpp ->
 bench/roofline_constants.json; HBM traffic from the committed PMC passes) and
 "cpu_baseline" (the oracle's threshold_crypto restatement timed on this host).
 """
@@ -45,7 +45,7 @@ SEED = 0x6862626674
 MAD_U64_PEAK = 29.51e12
 # timing family -> kernel (hbtc_api.hip timed() families, rocprofv3 names)
 KERNEL_NAME = {"dec_verify": "k_dec_verify", "rlc_items": "k_rlc_items",
-               "rlc_groups": "k_rlc_check_groups", "rlc_leaves": "k_rlc_leaves"}
+               "chk_tiles": "k_chk_tiles", "chk_subs": "k_chk_subs", "chk_leaves": "k_chk_leaves"}
 
 
 def log(*a):
@@ -111,9 +111,13 @@ class Epoch:
             p = ctx.dev_alloc(arr.nbytes)
             ctx.dev_upload(p, arr)
             self.d[name] = p
-        self.d["status"] = ctx.dev_alloc(4 * total)
-        self.d["g"] = ctx.dev_alloc(48 * n_ct)
-        self.d["cst"] = ctx.dev_alloc(4 * n_ct)
+        # two sets of outputs, alternated per step: epoch k+1's verification writes one status
+        # array while epoch k's combine still reads the other (hbtc.h ordering rules)
+        for j in range(2):
+            self.d["status%d" % j] = ctx.dev_alloc(4 * total)
+            self.d["g%d" % j] = ctx.dev_alloc(48 * n_ct)
+            self.d["cst%d" % j] = ctx.dev_alloc(4 * n_ct)
+        self.cur = 0
         self.total = total
         self.host_shares = shares
 
@@ -124,22 +128,26 @@ class Epoch:
         epoch's verification, so they overlap the NEXT epoch's verification (pipelined epochs);
         the timed region ends when the last combine is done."""
         lib, h, d = ctx.lib, ctx.h, self.d
+        self.cur ^= 1
+        j = self.cur
         off = N._ptr(self.offsets)
         ctx._check(lib.hbtc_verify_dec_shares_dev(h, self.keyset, self.n_ct, d["H"], d["w"], off,
-                                                  d["idx"], d["shares"], d["status"]),
+                                                  d["idx"], d["shares"], d["status%d" % j]),
                    "verify_dec_shares_dev")
         ctx._check(lib.hbtc_combine_dec_verified_dev(h, self.n_ct, off, d["idx"], d["shares"],
-                                                     d["status"], self.t, d["g"], d["cst"]),
+                                                     d["status%d" % j], self.t, d["g%d" % j],
+                                                     d["cst%d" % j]),
                    "combine_dec_verified_dev")
 
     def check(self, ctx):
+        j = self.cur  # the last step's outputs
         st = np.empty(self.total, np.int32)
-        ctx.dev_download(st, self.d["status"])
+        ctx.dev_download(st, self.d["status%d" % j])
         mism = int((st != self.expected).sum())
         g = np.empty(48 * self.n_ct, np.uint8)
-        ctx.dev_download(g, self.d["g"])
+        ctx.dev_download(g, self.d["g%d" % j])
         cst = np.empty(self.n_ct, np.int32)
-        ctx.dev_download(cst, self.d["cst"])
+        ctx.dev_download(cst, self.d["cst%d" % j])
         want, _ = ctx.g1_mul(G1_GEN, scalars_bytes([self.master_sk * r % R for r in self.rs]))
         comb_ok = bool((cst == 0).all() and bytes(g) == bytes(want))
         return mism, comb_ok, int((st == N.ACCEPT).sum())
@@ -219,8 +227,8 @@ def main():
     ctx.sync()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, dist)
-    fams = ["dec_verify", "rlc_items", "rlc_groups", "rlc_triage", "rlc_sub", "rlc_leaves",
-            "rlc_finalize", "lagrange", "comb_decode", "comb_digits", "combine", "prepare"]
+    fams = ["dec_verify", "rlc_items", "chk_tiles", "chk_subs", "chk_leaves", "rlc_finalize",
+            "lagrange", "comb_decode", "comb_digits", "combine", "prepare"]
     breakdown = {f: ctx.timing_read(f) for f in fams}
     leaves = ctx.rlc_last_leaves() if args.mode == "rlc" else ep.total
     mism, comb_ok, n_acc = ep.check(ctx)
@@ -241,15 +249,17 @@ def main():
     fqm_per_launch = {
         "dec_verify": consts["dec_share"]["total"] * ep.total,
         "rlc_items": consts["rlc_item"] * ep.total,
-        "rlc_groups": consts["rlc_group_check"] * (ep.n_ct + 2 * n_tiles),
-        "rlc_leaves": consts["dec_share"]["total"] * leaves,
+        # a tile unit = the plain and the weighted 2-pair check (serial Fqm count of one check;
+        # the cooperative kernel issues more lane-level work than this)
+        "chk_tiles": consts["rlc_group_check"] * 2 * n_tiles,
+        "chk_leaves": consts["dec_share"]["total"] * leaves,
         "combine": consts.get("g1_msm_combine", 0) * ep.n_ct,
     }
     per_step = {f: round(breakdown[f][0] / args.steps, 3) for f in fams if breakdown[f][1]}
     # The dominant kernel is chosen among the main-stream (critical-path) families: the
     # combine runs concurrently on its own stream, so its event span includes the time it
     # shares the CUs with the verify chain and is not a launch duration.
-    main_stream = ("dec_verify", "rlc_items", "rlc_groups", "rlc_leaves")
+    main_stream = ("dec_verify", "rlc_items", "chk_tiles", "chk_leaves")
     dom = max((f for f in main_stream if breakdown[f][1]), key=lambda f: breakdown[f][0])
     dom_avg_s = breakdown[dom][0] / breakdown[dom][1] / 1e3
     achieved = fqm_per_launch[dom] / dom_avg_s * consts["mad_u64_u32_per_fqm"] / 1e12
@@ -257,7 +267,7 @@ def main():
     # PMC passes of this command (tools/gpu_configs_pmc.sh -> tools/pmc_summary.py): separate
     # FETCH_SIZE / WRITE_SIZE / SQ passes, FETCH_SIZE doubled per the gfx950 note.
     traffic, pmc = None, {}
-    pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+    pmc_path = os.path.join(ROOT, "profiles", "r02_pmc_summary.json")
     if os.path.exists(pmc_path):
         pmc = json.load(open(pmc_path)).get("hbtc::" + KERNEL_NAME[dom], {})
         if "hbm_read_bytes" in pmc and "hbm_write_bytes" in pmc:

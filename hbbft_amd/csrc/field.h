@@ -45,6 +45,7 @@
 #endif
 
 #include "bls_constants.h"
+#include "fq_fips.h"
 
 #ifndef HBTC_FQ_UNROLL
 #define HBTC_FQ_UNROLL 1
@@ -225,15 +226,24 @@ extern unsigned long long hbtc_fqm_count;
 #define HBTC_COUNT_FQ_MUL() ((void)0)
 #endif
 
-#if defined(HBTC_FQMUL_CALL) && defined(__HIP_DEVICE_COMPILE__)
-// One out-of-line copy of the Montgomery product with its operands passed in VGPRs: callers
-// then keep only their own live values, which lets light group arithmetic run several waves
-// per SIMD (the call costs ~40 moves against ~600 instructions of multiply).
+// Device multiplication: product scanning with carry-out MACs (fq_fips.h; 0.58-0.62 of the
+// v_mad_u64_u32 roofline at 4-8 waves/SIMD vs 0.43-0.48 for the rolled CIOS loop, and 1.8x
+// lower single-wave latency: profiles/r02_fqbench.txt).  The product is ~660 instructions, so
+// by default every call site calls ONE out-of-line copy (operands and result in VGPRs): the
+// tower and curve code inlines dozens of products per loop body, and inlined copies put a G2
+// scalar-multiplication loop at ~55k instructions, far past the instruction cache.  A
+// translation unit whose hot loops hold few product sites (the cooperative GT kernels,
+// hbtc_check.hip) defines HBTC_FQMUL_INLINE; HBTC_FQMUL_CIOS selects round 1's CIOS loop.
+#if defined(__HIP_DEVICE_COMPILE__)
 __device__ __attribute__((noinline)) Fq fq_mul_call(Fq a, Fq b) {
   Fq r;
-  mont_mul<12, HBTC_FQ_UNROLL>(r, a, b, FQ_P, FQ_NP);
+  mont_mul_fips(r.v, a.v, b.v, FQ_P, FQ_NP);
   return r;
 }
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && defined(HBTC_FQMUL_INLINE)
+HD void fq_mul(Fq& r, const Fq& a, const Fq& b) { mont_mul_fips(r.v, a.v, b.v, FQ_P, FQ_NP); }
+#elif defined(__HIP_DEVICE_COMPILE__) && !defined(HBTC_FQMUL_CIOS)
 HD void fq_mul(Fq& r, const Fq& a, const Fq& b) { r = fq_mul_call(a, b); }
 #else
 HD void fq_mul(Fq& r, const Fq& a, const Fq& b) {
@@ -242,6 +252,14 @@ HD void fq_mul(Fq& r, const Fq& a, const Fq& b) {
 }
 #endif
 HD void fq_sqr(Fq& r, const Fq& a) { fq_mul(r, a, a); }
+// Product through the single out-of-line copy on the device (code-size-bound callers).
+HD void fq_mul_ol(Fq& r, const Fq& a, const Fq& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  r = fq_mul_call(a, b);
+#else
+  fq_mul(r, a, b);
+#endif
+}
 
 // canonical value in [0, p)
 HD void fq_canon(Fq& r, const Fq& a) {

@@ -1,0 +1,521 @@
+// Wavefront-cooperative pairing arithmetic for gfx950: one GT / Fq12 value spread over a
+// group of 6 lanes, one Fq2 coefficient per lane.
+//
+// Replaces the single-lane Miller loop + final exponentiation (pairing.h) for the pairing
+// checks of PublicKeyShare::verify_decryption_share (/root/reference/src/
+// threshold_decryption.rs:159) and PublicKeyShare::verify (src/coin.rs:151) as batched by
+// hbtc_rlc.hip.  A single lane holding a whole Fq12 (144 VGPRs) plus temporaries spills to
+// scratch and runs the ~17k Fq multiplications of a check serially; here a check's state
+// is 24 VGPRs per lane and each Fq12 operation's Fq2 products run on 6 lanes at once.
+//
+// Basis.  Fq12 = Fq2[w] / (w^6 - xi), xi = 1 + u: f = sum_{k<6} f_k w^k.  It is the tower
+// Fq6[w]/(w^2 - v), Fq6 = Fq2[v]/(v^3 - xi) of field.h flattened (v = w^2):
+//     f_0 = c0.c0, f_1 = c1.c0, f_2 = c0.c1, f_3 = c1.c1, f_4 = c0.c2, f_5 = c1.c2.
+// Lane l of a wave holds coefficient k = l mod 6 of group g = l / 6; lanes 60..63 form a
+// partial group whose results are never used (they take part in every exchange so the
+// exchanges stay in converged control flow).
+//
+// Operations (Fq2 products on the critical path of one lane, vs the serial tower):
+//     mul        f_k = sum_i a_i b_{k-i} (xi on wrap)            6 Fq2 mul   (18 Fq2 on 1 lane)
+//     sqr        symmetric terms, doubled                         4 Fq2 mul   (12)
+//     line mul   f*(A + B w^2 + Y w^3)                            2 Fq2 + 1 Fq2xFq
+//     cyclotomic Granger-Scott over the pairs (k, k+3)             2 Fq2 mul   (6)
+//     frobenius  conj^j(f_k) * xi^(k (p^j - 1)/6)                 1 Fq2 mul
+// Values are exchanged with ds_bpermute (no LDS storage, no barriers: a group never spans
+// two waves).  Every lane of a group executes the same instruction stream; data-dependent
+// choices are selects.
+#pragma once
+#include "pairing.h"
+
+namespace hbtc {
+namespace gt {
+
+// ------------------------------------------------------------------------------ lane plumbing
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint32_t shfl(uint32_t v, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+__device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
+__device__ __forceinline__ void fetch(Fq& r, const Fq& x, uint32_t src) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = shfl(x.v[i], src);
+}
+#else
+// Host build (tests/native): the cooperative code runs on host threads, one per lane, that
+// meet at every exchange (tests/native/gt_sim.cpp provides the simulator).
+uint32_t lane_id();
+uint32_t shfl(uint32_t v, uint32_t src);
+bool wave_any(bool p);
+void fetch_words(uint32_t* r, const uint32_t* x, int n, uint32_t src);
+inline void fetch(Fq& r, const Fq& x, uint32_t src) { fetch_words(r.v, x.v, 12, src); }
+#endif
+HD void fetch2(Fq2& r, const Fq2& x, uint32_t src) {
+  fetch(r.c0, x.c0, src);
+  fetch(r.c1, x.c1, src);
+}
+
+// position of the calling lane inside its group
+struct Pos {
+  uint32_t k;     // coefficient index 0..5
+  uint32_t base;  // lane holding coefficient 0
+};
+HD Pos pos() {
+  const uint32_t l = lane_id();
+  const uint32_t g = l / 6u;
+  return Pos{l - 6u * g, 6u * g};
+}
+HD uint32_t src(const Pos& ps, uint32_t k) { return ps.base + k; }
+
+HD void fq_sel(Fq& r, bool c, const Fq& a, const Fq& b) {  // r = c ? a : b
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+}
+HD void fq2_sel(Fq2& r, bool c, const Fq2& a, const Fq2& b) {
+  fq_sel(r.c0, c, a.c0, b.c0);
+  fq_sel(r.c1, c, a.c1, b.c1);
+}
+// r = t ? xi * a : a
+HD void fq2_xi_if(Fq2& r, bool t, const Fq2& a) {
+  Fq2 x;
+  fq2_mul_xi(x, a);
+  fq2_sel(r, t, x, a);
+}
+
+// Fq2 product (Karatsuba) with ONE Fq multiplication site in a rolled 3-step loop: with the
+// ~660-instruction product-scanning multiply inlined, three sites per Fq2 product put the
+// cooperative kernels far past the instruction cache; the operand selects cost ~10%.
+HD void mul2(Fq2& r, const Fq2& a, const Fq2& b) {
+  Fq sa, sb;
+  fq_add(sa, a.c0, a.c1);
+  fq_add(sb, b.c0, b.c1);
+  Fq t0, t1, t2;
+#pragma unroll 1
+  for (uint32_t t = 0; t < 3; ++t) {
+    Fq x, y, q;
+    fq_sel(x, t == 0, a.c0, t == 1 ? a.c1 : sa);
+    fq_sel(y, t == 0, b.c0, t == 1 ? b.c1 : sb);
+    fq_mul(q, x, y);
+    fq_sel(t0, t == 0, q, t0);
+    fq_sel(t1, t == 1, q, t1);
+    t2 = q;
+  }
+  fq_sub(r.c0, t0, t1);
+  fq_sub(t2, t2, t0);
+  fq_sub(r.c1, t2, t1);
+}
+// a * (y + 0u): two Fq products through the same single site
+HD void mul2_fq(Fq2& r, const Fq2& a, const Fq& y) {
+  Fq t0;
+#pragma unroll 1
+  for (uint32_t t = 0; t < 2; ++t) {
+    Fq q;
+    fq_mul(q, t == 0 ? a.c0 : a.c1, y);
+    fq_sel(t0, t == 0, q, t0);
+    r.c1 = q;
+  }
+  r.c0 = t0;
+}
+
+// ------------------------------------------------------------------------------ GT operations
+// Out-of-line on the device: the glue of the final exponentiation and the location search
+// call these a few dozen times per check, so one copy each keeps the kernels inside the
+// instruction cache; their by-reference operands cost ~100 dwords of stack traffic per call
+// against ~10^4 instructions of work.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GTN __device__ __attribute__((noinline))
+#else
+#define GTN static inline
+#endif
+
+// f = a * b
+GTN void mul(Fq2& f, const Fq2& a, const Fq2& b, const Pos& ps) {
+  Fq2 acc;
+  fq2_zero(acc);
+#pragma unroll 1
+  for (uint32_t i = 0; i < 6; ++i) {
+    const bool wrap = i > ps.k;
+    const uint32_t j = wrap ? ps.k + 6 - i : ps.k - i;
+    Fq2 ai, bj, z;
+    fetch2(ai, a, src(ps, i));
+    fetch2(bj, b, src(ps, j));
+    mul2(z, ai, bj);
+    fq2_xi_if(z, wrap, z);
+    fq2_add(acc, acc, z);
+  }
+  f = acc;
+}
+
+// f = a^2: the unordered pairs {i, j} with i + j = k (mod 6), cross terms doubled.  Per lane
+// 4 (even k) or 3 (odd k) terms, packed one byte each: i | j << 3 | xi << 6 | double << 7,
+// 0xff = no term.
+constexpr uint32_t sqr_word(uint32_t k) {
+  uint32_t w = 0xffffffffu;
+  int t = 0;
+  for (uint32_t i = 0; i < 6; ++i)
+    for (uint32_t j = i; j < 6; ++j)
+      if ((i + j) % 6 == k) {
+        const uint32_t e = i | (j << 3) | (i + j >= 6 ? 64u : 0u) | (i != j ? 128u : 0u);
+        w = (w & ~(0xffu << (8 * t))) | (e << (8 * t));
+        ++t;
+      }
+  return w;
+}
+static_assert(sqr_word(0) == 0x5be2e900u && sqr_word(1) == 0xffe3ea88u &&
+                  sqr_word(5) == 0xff9aa1a8u,
+              "squaring term table: (0,0) (1,5)x2 (2,4)x2 (3,3)x | (0,1)2 (2,5)x2 (3,4)x2");
+HD uint32_t sqr_terms(uint32_t k) {
+  uint32_t w = sqr_word(0);
+  w = k == 1 ? sqr_word(1) : w;
+  w = k == 2 ? sqr_word(2) : w;
+  w = k == 3 ? sqr_word(3) : w;
+  w = k == 4 ? sqr_word(4) : w;
+  w = k == 5 ? sqr_word(5) : w;
+  return w;
+}
+
+HD void sqr(Fq2& f, const Fq2& a, const Pos& ps) {
+  const uint32_t terms = sqr_terms(ps.k);
+  Fq2 acc;
+  fq2_zero(acc);
+#pragma unroll 1
+  for (uint32_t t = 0; t < 4; ++t) {
+    const uint32_t e = (terms >> (8 * t)) & 0xffu;
+    const bool none = e == 0xffu;
+    Fq2 ai, aj, z;
+    fetch2(ai, a, src(ps, e & 7u));
+    fetch2(aj, a, src(ps, (e >> 3) & 7u));
+    mul2(z, ai, aj);
+    fq2_xi_if(z, ((e >> 6) & 1u) && !none, z);
+    Fq2 z2;
+    fq2_dbl(z2, z);
+    fq2_sel(z, ((e >> 7) & 1u) && !none, z2, z);
+    fq2_add(z2, acc, z);
+    fq2_sel(acc, none, acc, z2);
+  }
+  f = acc;
+}
+
+// f = f * (A + B w^2 + Y w^3) for a Miller-loop line evaluated at a G1 point (scaled by a
+// subfield factor).  A, B in Fq2 and Y in Fq are not materialised: they sit on the lanes that
+// computed them — A = (pa on lane a, pa on lane a+1), B = (pb on lane b, pb on lane b+1),
+// Y = py on lane y — and each term fetches its operand, which keeps a Miller step's live set
+// small.  use = false makes the line 1 (A = 1, B = Y = 0: the caller zeroes pa, pb, py).
+HD void mul_line(Fq2& f, const Fq& pa, uint32_t a, const Fq& pb, uint32_t b, const Fq& py,
+                 uint32_t y, bool use, const Pos& ps) {
+  const uint32_t k = ps.k;
+  Fq2 acc;
+  fq2_zero(acc);
+#pragma unroll 1
+  for (uint32_t t = 0; t < 3; ++t) {
+    // term t: f_k A, f_{k-2} B (xi if k < 2), f_{k-3} Y (xi if k < 3)
+    const uint32_t fk = t == 0 ? k : (t == 1 ? (k >= 2 ? k - 2 : k + 4) : (k >= 3 ? k - 3 : k + 3));
+    Fq2 x, q, z;
+    fetch2(x, f, src(ps, fk));
+    Fq o0, o1;
+    fq_sel(o0, t == 0, pa, t == 1 ? pb : py);
+    fq_sel(o1, t == 0, pa, pb);
+    const uint32_t l0 = t == 0 ? a : (t == 1 ? b : y);
+    fetch(q.c0, o0, src(ps, l0));
+    fetch(q.c1, o1, src(ps, l0 + 1));
+    if (t == 0 && !use) fq_one(q.c0);
+    if (t == 2) fq_zero(q.c1);
+    mul2(z, x, q);
+    fq2_xi_if(z, (t == 1 && k < 2) || (t == 2 && k < 3), z);
+    fq2_add(acc, acc, z);
+  }
+  f = acc;
+}
+
+HD void conj(Fq2& f, const Pos& ps) {
+  Fq2 n;
+  fq2_neg(n, f);
+  fq2_sel(f, (ps.k & 1u) != 0, n, f);
+}
+
+// f = phi^j(f), j = 1, 2, 3
+GTN void frob(Fq2& f, int j, const Pos& ps) {
+  const uint32_t* tab = j == 1 ? GT_FROB_1 : (j == 2 ? GT_FROB_2 : GT_FROB_3);
+  Fq2 g, x;
+  // the table row of this lane's coefficient (selects: no per-lane memory indexing)
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint32_t a = tab[i], b = tab[12 + i];
+#pragma unroll
+    for (uint32_t c = 1; c < 6; ++c) {
+      a = ps.k == c ? tab[24 * c + i] : a;
+      b = ps.k == c ? tab[24 * c + 12 + i] : b;
+    }
+    g.c0.v[i] = a;
+    g.c1.v[i] = b;
+  }
+  if (j & 1)
+    fq2_conj(x, f);
+  else
+    x = f;
+  mul2(f, x, g);
+}
+
+// Granger-Scott squaring of a cyclotomic element, Fq12 seen as Fq4^3 over the coefficient
+// pairs (k, k+3): lane k < 3 forms a^2 + xi b^2 and lane k + 3 forms 2ab (a = f_k,
+// b = f_{k+3}); each output then needs one partner value:
+//     z_0 = 3 T_0 - 2 f_0   z_1 = 3 xi T_5 + 2 f_1   z_2 = 3 T_1 - 2 f_2
+//     z_3 = 3 T_3 + 2 f_3   z_4 = 3 T_2 - 2 f_4      z_5 = 3 T_4 + 2 f_5
+HD void cyc_sqr(Fq2& f, const Pos& ps) {
+  const bool lo = ps.k < 3;
+  Fq2 partner;
+  fetch2(partner, f, src(ps, lo ? ps.k + 3 : ps.k - 3));
+  // lo lanes: a*a then b*b (a = f, b = partner); hi lanes: a*b (partner * f), then unused
+  Fq2 z0, z1;
+#pragma unroll 1
+  for (uint32_t t = 0; t < 2; ++t) {
+    Fq2 x, y, r, first;
+    fq2_sel(first, lo, f, partner);
+    fq2_sel(x, t == 0, first, partner);
+    fq2_sel(y, t == 0, f, partner);
+    mul2(r, x, y);
+    fq2_sel(z0, t == 0, r, z0);
+    z1 = r;
+  }
+  Fq2 T, t1;
+  fq2_mul_xi(t1, z1);
+  fq2_add(t1, z0, t1);  // a^2 + xi b^2
+  Fq2 t2;
+  fq2_dbl(t2, z0);      // 2ab
+  fq2_sel(T, lo, t1, t2);
+  // route T: lane k reads T from lane s(k) = {0, 5, 1, 3, 2, 4}[k]
+  const uint32_t sk = ps.k == 0 ? 0u : ps.k == 1 ? 5u : ps.k == 2 ? 1u : ps.k == 3 ? 3u : ps.k == 4 ? 2u : 4u;
+  Fq2 Ts;
+  fetch2(Ts, T, src(ps, sk));
+  fq2_xi_if(Ts, ps.k == 1, Ts);
+  Fq2 three, two;
+  fq2_dbl(three, Ts);
+  fq2_add(three, three, Ts);
+  fq2_dbl(two, f);
+  Fq2 plus, minus;
+  fq2_add(plus, three, two);
+  fq2_sub(minus, three, two);
+  fq2_sel(f, (ps.k & 1u) != 0, plus, minus);
+}
+
+// Group-wide AND of a per-lane predicate.
+HD bool group_all(bool ok, const Pos& ps) {
+  uint32_t acc = 1;
+#pragma unroll
+  for (uint32_t c = 0; c < 6; ++c) acc &= shfl(ok ? 1u : 0u, src(ps, c));
+  return acc != 0;
+}
+
+HD bool is_one(const Fq2& f, const Pos& ps) {
+  Fq2 one;
+  fq2_one(one);
+  const bool ok = ps.k == 0 ? fq2_eq(f, one) : fq2_is_zero(f);
+  return group_all(ok, ps);
+}
+
+HD bool equal(const Fq2& a, const Fq2& b, const Pos& ps) { return group_all(fq2_eq(a, b), ps); }
+
+HD void set_one(Fq2& f, const Pos& ps) {
+  Fq2 one, zero;
+  fq2_one(one);
+  fq2_zero(zero);
+  fq2_sel(f, ps.k == 0, one, zero);
+}
+
+// y^x for cyclotomic y (x < 0: y^|x| then conjugate)
+GTN void exp_by_x(Fq2& r, const Fq2& y, const Pos& ps) {
+  Fq2 acc = y;
+#pragma unroll 1
+  for (int bit = 62; bit >= 0; --bit) {
+    cyc_sqr(acc, ps);
+    if ((BLS_X_ABS >> bit) & 1ull) mul(acc, acc, y, ps);
+  }
+  conj(acc, ps);
+  r = acc;
+}
+
+// a^(p-2) (Fermat inversion), square-and-multiply over the constant exponent
+HD void fq_inv_fermat(Fq& r, const Fq& a) {
+  Fq acc;
+  fq_one(acc);
+#pragma unroll 1
+  for (int w = 11; w >= 0; --w) {
+    const uint32_t word = EXP_P_MINUS_2[w];
+#pragma unroll 1
+    for (int b = 31; b >= 0; --b) {
+      fq_sqr(acc, acc);
+      if ((word >> b) & 1u) fq_mul(acc, acc, a);  // uniform: the exponent is a constant
+    }
+  }
+  r = acc;
+}
+
+// f^(p^6 - 1) = conj(f)^2 / N with N = f conj(f) in Fq6 (coefficients 0, 2, 4 = its
+// v-basis digits n0, n1, n2); N^-1 = (t0 + t1 v + t2 v^2) / d with
+//   t0 = n0^2 - xi n1 n2,  t1 = xi n2^2 - n0 n1,  t2 = n1^2 - n0 n2,  d = n0 t0 + xi (n2 t1 + n1 t2)
+// computed on lanes 0, 2, 4 (one t each), d^-1 in Fq2 through one Fq inversion.
+HD void easy_part(Fq2& r, const Fq2& f, const Pos& ps) {
+  Fq2 cf = f;
+  conj(cf, ps);
+  Fq2 N;
+  mul(N, f, cf, ps);
+  Fq2 n0, n1, n2;
+  fetch2(n0, N, src(ps, 0));
+  fetch2(n1, N, src(ps, 2));
+  fetch2(n2, N, src(ps, 4));
+  const uint32_t k = ps.k;
+  // t_m = tx * x * x' - ty * y * y'
+  Fq2 z0, z1;
+#pragma unroll 1
+  for (uint32_t t = 0; t < 2; ++t) {
+    Fq2 x, y, q, sx, px, py;
+    // the square term, then the product term: (n1 n2), (n0 n1), (n0 n2)
+    fq2_sel(sx, k == 2, n2, n0);
+    fq2_sel(sx, k == 4, n1, sx);
+    fq2_sel(px, k == 0, n1, n0);
+    fq2_sel(py, k == 2, n1, n2);
+    fq2_sel(x, t == 0, sx, px);
+    fq2_sel(y, t == 0, sx, py);
+    mul2(q, x, y);
+    fq2_sel(z0, t == 0, q, z0);
+    z1 = q;
+  }
+  fq2_xi_if(z0, k == 2, z0);
+  fq2_xi_if(z1, k == 0, z1);
+  Fq2 tm;
+  fq2_sub(tm, z0, z1);
+  // d: lane 0 n0 t0, lane 2 xi n2 t1, lane 4 xi n1 t2
+  Fq2 m, u;
+  fq2_sel(m, k == 2, n2, n0);
+  fq2_sel(m, k == 4, n1, m);
+  mul2(u, m, tm);
+  fq2_xi_if(u, k != 0, u);
+  Fq2 d, d2, d4;
+  fetch2(d, u, src(ps, 0));
+  fetch2(d2, u, src(ps, 2));
+  fetch2(d4, u, src(ps, 4));
+  fq2_add(d, d, d2);
+  fq2_add(d, d, d4);
+  // d^-1 = conj(d) / (d0^2 + d1^2)
+  Fq nrm, t1;
+  fq_sqr(nrm, d.c0);
+  fq_sqr(t1, d.c1);
+  fq_add(nrm, nrm, t1);
+  Fq inv;
+  fq_inv_fermat(inv, nrm);
+  Fq2 dinv;
+  fq_mul(dinv.c0, d.c0, inv);
+  fq_mul(t1, d.c1, inv);
+  fq_neg(dinv.c1, t1);
+  Fq2 ninv, zero;
+  mul2(ninv, tm, dinv);
+  fq2_zero(zero);
+  fq2_sel(ninv, (k & 1u) == 0, ninv, zero);
+  Fq2 c2;
+  sqr(c2, cf, ps);
+  mul(r, c2, ninv, ps);
+}
+
+// Final exponentiation (easy part, then the hard part by the Hayashida-Hayasaka-Teruya
+// x-chain, which yields the cube of the standard pairing: equality decisions are unchanged
+// since gcd(3, r) = 1) — the chain of pairing.h's final_exponentiation.
+HD void final_exp(Fq2& out, const Fq2& f, const Pos& ps) {
+  Fq2 r, t0;
+  easy_part(r, f, ps);
+  t0 = r;
+  frob(t0, 2, ps);
+  mul(r, t0, r, ps);
+  Fq2 y0, y1, y2;
+  y0 = r;
+  cyc_sqr(y0, ps);
+  exp_by_x(y1, r, ps);
+  y2 = r;
+  conj(y2, ps);
+  mul(y1, y1, y2, ps);
+  exp_by_x(y2, y1, ps);
+  conj(y1, ps);
+  mul(y1, y1, y2, ps);
+  exp_by_x(y2, y1, ps);
+  frob(y1, 1, ps);
+  mul(y1, y1, y2, ps);
+  mul(r, r, y0, ps);
+  exp_by_x(y0, y1, ps);
+  exp_by_x(y2, y0, ps);
+  y0 = y1;
+  frob(y0, 2, ps);
+  conj(y1, ps);
+  mul(y1, y1, y2, ps);
+  mul(y1, y1, y0, ps);
+  mul(out, r, y1, ps);
+}
+
+// ------------------------------------------------------------------------------ Miller loop
+// One G1 argument of a pairing product with a precomputed line table (pairing.h Line: the
+// affine-normalised line a + b xP v + yP v w at step j).  With P Jacobian (X, Y, Z) the
+// line times Z^3 (an Fq factor, removed by the final exponentiation) is
+//     Z^3 a + (X Z) b w^2 + Y w^3
+// so the loop needs no inversion.  An unused pair (P or Q at infinity) contributes 1.
+struct MillerArg {
+  const Line* lines;  // MILLER_STEPS lines of the G2 argument
+  G1J P;              // the G1 argument (sign already applied)
+  bool use;
+};
+
+// f = prod_{pairs} f_{|x|,Q}(P), conjugated (x < 0).  Per step the 8 Fq products that scale
+// the two lines run on separate lanes (lane k: product k; lanes 0, 1: products 6, 7).
+HD void miller2(Fq2& f, const MillerArg& m1, const MillerArg& m2, const Pos& ps) {
+  const uint32_t k = ps.k;
+  // per-pair scalars Z^3, X Z, Y (zero when unused: the line becomes 1 below)
+  // lane k's round-1 product: k = 0,1 a1.c{k} Z1^3; 2,3 b1.c{k-2} X1Z1; 4,5 a2.c{k-4} Z2^3.
+  // lanes 0, 1 round 2: b2.c{k} X2Z2.  Lane 0 keeps Y1, the others Y2.
+  Fq s1, s2, ymine, zero;
+  fq_zero(zero);
+  {
+    const bool second = k >= 4;
+    const G1J& P = second ? m2.P : m1.P;
+    Fq z2, z3, xz;
+    fq_sqr(z2, P.z);
+    fq_mul(z3, z2, P.z);
+    fq_mul(xz, P.x, P.z);
+    fq_sel(s1, k < 2 || second, z3, xz);
+    fq_sel(s1, second ? m2.use : m1.use, s1, zero);
+    fq_mul(s2, m2.P.x, m2.P.z);
+    fq_sel(s2, m2.use, s2, zero);
+    fq_sel(ymine, k == 0, m1.P.y, m2.P.y);
+    fq_sel(ymine, k == 0 ? m1.use : m2.use, ymine, zero);
+  }
+  const Line* l1c = k < 4 ? m1.lines : m2.lines;
+  const uint32_t c1 = k < 4 ? k : k - 4;       // Fq component of the Line (a.c0 a.c1 b.c0 b.c1)
+  const uint32_t c2 = 2 + (k & 1u);            // round-2 component (b2)
+  set_one(f, ps);
+  int j = 0;
+  bool first = true;
+#pragma unroll 1
+  for (int bit = 62; bit >= 0; --bit) {
+    const bool add = ((BLS_X_ABS >> bit) & 1ull) != 0;
+#pragma unroll 1
+    for (int rep = 0; rep < (add ? 2 : 1); ++rep) {
+      if (rep == 0 && !first) sqr(f, f, ps);
+      first = false;
+      const Fq* L1 = reinterpret_cast<const Fq*>(l1c + j);
+      const Fq* L2 = reinterpret_cast<const Fq*>(m2.lines + j);
+      Fq p1, p2;
+#pragma unroll 1
+      for (uint32_t t = 0; t < 2; ++t) {
+        Fq q;
+        fq_mul(q, t == 0 ? L1[c1] : L2[c2], t == 0 ? s1 : s2);
+        fq_sel(p1, t == 0, q, p1);
+        p2 = q;
+      }
+      // line 1: A1 = p1@{0,1}, B1 = p1@{2,3}, Y1 = ymine@0; line 2: A2 = p1@{4,5},
+      // B2 = p2@{0,1}, Y2 = ymine@1
+      mul_line(f, p1, 0, p1, 2, ymine, 0, m1.use, ps);
+      mul_line(f, p1, 4, p2, 0, ymine, 1, m2.use, ps);
+      ++j;
+    }
+  }
+  conj(f, ps);
+}
+
+}  // namespace gt
+}  // namespace hbtc

@@ -72,6 +72,23 @@ struct hbtc_ctx {
   std::map<std::string, DevBuf> bufs;
   int verify_mode = HBTC_MODE_RLC;
   const uint32_t* last_leaf_count = nullptr;  // device counter of the last RLC call
+  // Device ranges that combines enqueued on s_comb still read, each with the event recorded
+  // after that combine: main-stream work that writes an overlapping range waits on it first
+  // (combines run concurrently with the NEXT verification; hbtc.h: *_dev calls are ordered).
+  struct PendingRead {
+    uintptr_t lo, hi;
+    hipEvent_t ev;
+  };
+  std::vector<PendingRead> comb_reads;
+  // the decoded shares of the last RLC DecryptionShare verification (reused by a combine of
+  // the same item arrays: no second decode / subgroup check)
+  struct LastDec {
+    const int32_t* status = nullptr;
+    const uint8_t* shares = nullptr;
+    uint32_t n_items = 0;
+    const G1A* dec = nullptr;
+  } last_dec;
+  int dec_flip = 0;
   std::random_device rd;
   bool timing = false;
   std::vector<Span> spans;
@@ -147,6 +164,45 @@ int sync(hbtc_ctx* c) {
 int stream_after(hbtc_ctx* c, hipStream_t waiter, hipStream_t on, hipEvent_t ev) {
   HB_CHECK(c, hipEventRecord(ev, on));
   HB_CHECK(c, hipStreamWaitEvent(waiter, ev, 0));
+  return HBTC_OK;
+}
+
+// Main-stream work about to write [p, p + bytes): wait for every pending combine that reads
+// an overlapping range; forget combines that have completed.
+int guard_write(hbtc_ctx* c, const void* p, size_t bytes) {
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + bytes;
+  auto& v = c->comb_reads;
+  for (size_t i = 0; i < v.size();) {
+    if (hipEventQuery(v[i].ev) == hipSuccess) {
+      (void)hipEventDestroy(v[i].ev);
+      v[i] = v.back();
+      v.pop_back();
+      continue;
+    }
+    if (v[i].lo < hi && lo < v[i].hi) HB_CHECK(c, hipStreamWaitEvent(c->stream, v[i].ev, 0));
+    ++i;
+  }
+  return HBTC_OK;
+}
+
+// A combine just enqueued on s_comb reads these ranges until it completes.
+int note_comb_reads(hbtc_ctx* c, std::initializer_list<std::pair<const void*, size_t>> ranges) {
+  hipEvent_t ev;
+  HB_CHECK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HB_CHECK(c, hipEventRecord(ev, c->s_comb));
+  bool first = true;
+  for (const auto& r : ranges) {
+    if (!r.first || !r.second) continue;
+    hipEvent_t e = ev;
+    if (!first) {  // one event per entry: entries are destroyed independently
+      HB_CHECK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      HB_CHECK(c, hipEventRecord(e, c->s_comb));
+    }
+    first = false;
+    const uintptr_t lo = reinterpret_cast<uintptr_t>(r.first);
+    c->comb_reads.push_back({lo, lo + r.second, e});
+  }
+  if (first) (void)hipEventDestroy(ev);
   return HBTC_OK;
 }
 
@@ -285,6 +341,8 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   Tile* tiles;
   uint32_t n_tiles;
   if (c->verify_mode == HBTC_MODE_PER_SHARE) {
+    HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
+    if (c->last_dec.status == d_status) c->last_dec = {};
     HB_TRY(prepare_g2(c, "H", d_H, n_ct, &h_aff, &h_st, &h_lines));
     HB_TRY(prepare_g2(c, "W", d_w, n_ct, &w_aff, &w_st, &w_lines));
     HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles));
@@ -298,18 +356,19 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   HB_TRY(stream_after(c, c->s_prep, c->stream, c->ev_main));
   HB_TRY(prepare_g2(c, "H", d_H, n_ct, &h_aff, &h_st, &h_lines, c->s_prep));
   HB_TRY(prepare_g2(c, "W", d_w, n_ct, &w_aff, &w_st, &w_lines, c->s_prep));
-  uint32_t* inst_tiles;
-  HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles, &inst_tiles));
+  HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles));
   RlcKey key;
   for (int i = 0; i < 8; ++i) key.k[i] = c->rd();
   TileSums* sums;
-  uint8_t *inst_pass, *tile_pass;
-  int32_t* tile_loc;
+  G1A* dec;
   uint32_t *counters, *sub_list, *leaves;
   HB_TRY(wst(c, "rlc.sums", n_tiles, &sums));
-  HB_TRY(wst(c, "rlc.inst_pass", n_ct, &inst_pass));
-  HB_TRY(wst(c, "rlc.tile_pass", n_tiles, &tile_pass));
-  HB_TRY(wst(c, "rlc.tile_loc", n_tiles, &tile_loc));
+  // two alternating buffers: a combine of the previous call may still read the other one
+  c->dec_flip ^= 1;
+  HB_TRY(wst(c, c->dec_flip ? "rlc.dec1" : "rlc.dec0", n_items, &dec));
+  HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
+  HB_TRY(guard_write(c, dec, (size_t)n_items * sizeof(G1A)));
+  c->last_dec = {d_status, d_share, n_items, dec};
   HB_TRY(wst(c, "rlc.counters", 2, &counters));  // [0] leaves, [1] sub-tile list
   HB_TRY(wst(c, "rlc.sub_list", n_tiles, &sub_list));
   HB_TRY(wst(c, "rlc.leaves", (size_t)2 * n_items, &leaves));
@@ -318,24 +377,19 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   HB_CHECK(c, hipMemsetAsync(counters, 0, 2 * sizeof(uint32_t), c->stream));
   HB_TRY(timed(c, "rlc_items", [&] {
     return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->tab,
-                            ks->n, key, sums, d_status);
+                            ks->n, key, sums, dec, d_status);
   }));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
-  HB_TRY(timed(c, "rlc_groups", [&] {
-    return launch_rlc_check_groups(c->stream, n_ct, n_tiles, tiles, inst_tiles, sums, h_aff,
-                                   h_lines, w_aff, w_lines, h_st, w_st, inst_pass, tile_pass,
-                                   tile_loc);
+  HB_TRY(timed(c, "chk_tiles", [&] {
+    return launch_chk_tiles(c->stream, n_tiles, tiles, sums, h_aff, h_lines, w_aff, w_lines, h_st,
+                            w_st, d_status, sub_count, sub_list);
   }));
-  HB_TRY(timed(c, "rlc_triage", [&] {
-    return launch_rlc_triage(c->stream, n_tiles, tiles, inst_pass, tile_pass, tile_loc, d_status,
-                             sub_count, sub_list);
+  HB_TRY(timed(c, "chk_subs", [&] {
+    return launch_chk_subs(c->stream, n_tiles, sub_count, sub_list, tiles, sums, h_aff, h_lines,
+                           w_aff, w_lines, d_status, leaf_count, leaves);
   }));
-  HB_TRY(timed(c, "rlc_sub", [&] {
-    return launch_rlc_sub(c->stream, n_tiles, sub_count, sub_list, tiles, sums, h_aff, h_lines,
-                          w_aff, w_lines, d_status, leaf_count, leaves);
-  }));
-  HB_TRY(timed(c, "rlc_leaves", [&] {
-    return launch_rlc_leaves(c->stream, n_items, leaf_count, leaves, d_idx, d_share, ks->pk, h_aff,
+  HB_TRY(timed(c, "chk_leaves", [&] {
+    return launch_chk_leaves(c->stream, n_items, leaf_count, leaves, d_idx, dec, ks->pk, h_aff,
                              h_lines, w_aff, w_lines, d_status);
   }));
   c->last_leaf_count = leaf_count;
@@ -354,6 +408,8 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   if (n_items == 0) return HBTC_OK;
   if (!aligned16(d_H) || !aligned16(d_sig))
     return fail(c, HBTC_ERR_ARG, "item arrays must be 16-byte aligned");
+  HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
+  if (c->last_dec.status == d_status) c->last_dec = {};
   G2A* h_aff;
   int32_t* h_st;
   Line* h_lines;
@@ -460,24 +516,37 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
     return launch_lagrange_sel(sc, n_inst, t, d_sel_idx, d_lambda, d_dup);
   }));
   const MsmPlan plan = msm_plan(n_inst, t);
+  const size_t pb = group == 1 ? 48 : 96;
   if (group == 1) {
+    // the decoded shares of the verification that produced d_item_status, when it is the last
+    // RLC DecryptionShare call over these very arrays
+    const auto& ld = c->last_dec;
+    const G1A* dec = (d_item_status && ld.status == d_item_status && ld.shares == d_pts &&
+                      ld.n_items == n_items)
+                         ? ld.dec
+                         : nullptr;
     G1A* d_aff;
     HB_TRY(wst(c, "comb.g1", terms, &d_aff));
     HB_TRY(timed_on(c, sc, "comb_decode", [&] {
-      return launch_msm_decode_g1(sc, n_inst, t, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status, d_aff,
-                                  d_bad);
+      return launch_msm_decode_g1(sc, n_inst, t, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status,
+                                  dec, d_aff, d_bad);
     }));
-    return msm_run<Fq>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
-                       d_inst_status, d_out, nullptr);
+    HB_TRY(msm_run<Fq>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
+                       d_inst_status, d_out, nullptr));
+    return note_comb_reads(c, {{d_idx, (size_t)n_items * 4}, {d_pts, n_items * pb},
+                               {d_item_status, d_item_status ? (size_t)n_items * 4 : 0},
+                               {dec, dec ? n_items * sizeof(G1A) : 0}});
   }
   G2A* d_aff;
   HB_TRY(wst(c, "comb.g2", terms, &d_aff));
   HB_TRY(timed_on(c, sc, "comb_decode", [&] {
-    return launch_msm_decode_g2(sc, n_inst, t, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status, d_aff,
-                                d_bad);
+    return launch_msm_decode_g2(sc, n_inst, t, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status,
+                                nullptr, d_aff, d_bad);
   }));
-  return msm_run<Fq2>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
-                      d_inst_status, d_out, d_parity);
+  HB_TRY(msm_run<Fq2>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
+                      d_inst_status, d_out, d_parity));
+  return note_comb_reads(c, {{d_idx, (size_t)n_items * 4}, {d_pts, n_items * pb},
+                             {d_item_status, d_item_status ? (size_t)n_items * 4 : 0}});
 }
 
 int point_mul_host(hbtc_ctx* c, int group, uint32_t n, const uint8_t* base,
@@ -554,6 +623,7 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
     (void)hipEventDestroy(sp.a);
     (void)hipEventDestroy(sp.b);
   }
+  for (auto& r : c->comb_reads) (void)hipEventDestroy(r.ev);
   for (auto& kv : c->stages) {
     if (kv.second.h) (void)hipHostFree(kv.second.h);
     if (kv.second.ev) (void)hipEventDestroy(kv.second.ev);
@@ -766,8 +836,10 @@ int hbtc_dev_free(hbtc_ctx* c, void* d_ptr) {
 int hbtc_dev_upload(hbtc_ctx* c, void* d_dst, const void* h_src, size_t bytes) {
   if (!c) return HBTC_ERR_ARG;
   Guard g(c);
+  HB_TRY(guard_write(c, d_dst, bytes));  // a combine still reading the old contents
   HB_CHECK(c, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, c->stream));
-  return sync(c);
+  HB_CHECK(c, hipStreamSynchronize(c->stream));
+  return HBTC_OK;
 }
 
 int hbtc_dev_download(hbtc_ctx* c, void* h_dst, const void* d_src, size_t bytes) {
@@ -881,7 +953,7 @@ int msm_dev(hbtc_ctx* c, int group, uint32_t n_msm, uint32_t n, uint32_t stride,
     HB_TRY(wst(c, "msm.g1", terms, &d_aff));
     HB_TRY(timed_on(c, sc, "comb_decode", [&] {
       return launch_msm_decode_g1(sc, n_msm, n, stride, d_pts, nullptr, (const uint32_t*)d_cnt,
-                                  nullptr, d_aff, d_bad);
+                                  nullptr, nullptr, d_aff, d_bad);
     }));
     return msm_run<Fq>(c, sc, p, d_sc, d_aff, (const uint32_t*)d_cnt, n, d_bad, nullptr, d_st,
                        d_out, nullptr);
@@ -890,7 +962,7 @@ int msm_dev(hbtc_ctx* c, int group, uint32_t n_msm, uint32_t n, uint32_t stride,
   HB_TRY(wst(c, "msm.g2", terms, &d_aff));
   HB_TRY(timed_on(c, sc, "comb_decode", [&] {
     return launch_msm_decode_g2(sc, n_msm, n, stride, d_pts, nullptr, (const uint32_t*)d_cnt,
-                                nullptr, d_aff, d_bad);
+                                nullptr, nullptr, d_aff, d_bad);
   }));
   return msm_run<Fq2>(c, sc, p, d_sc, d_aff, (const uint32_t*)d_cnt, n, d_bad, nullptr, d_st,
                       d_out, nullptr);

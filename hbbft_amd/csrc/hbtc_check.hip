@@ -1,0 +1,274 @@
+// Pairing-product checks of the RLC batch verification (hbtc_rlc.hip) on the cooperative GT
+// arithmetic of gt6.h: one check per 6-lane group, two checks (a "unit") per 12 lanes, five
+// units per wave.
+//
+// Replaces, for batches, the per-share PublicKeyShare::verify_decryption_share
+// (/root/reference/src/threshold_decryption.rs:159): for a group G of shares of one
+// ciphertext, T = e(sum r_i d_i, H) e(-sum r_i pk_i, w) == 1 iff (except with probability
+// 2^-64) every share of G is valid; T_w, the same with position-weighted r_i, locates a single
+// wrong share as the p with T_w == T^p (hbtc_rlc.hip explains both).
+//
+// Levels:
+//   k_chk_tiles   every 64-share tile: (plain, weighted) unit; a failing tile's single wrong
+//                 share is located, a tile with more goes to the sub-tile list
+//   k_chk_subs    the 8 sub-tiles of each listed tile, likewise; an unlocated sub-tile sends
+//                 its pending shares to the leaf list
+//   k_chk_leaves  two exact per-share checks per unit (decoded shares from k_rlc_items)
+// A unit's two groups run the same instruction stream; the location search is split between
+// them (the plain group tries positions [0, half), the weighted group [half, count) starting
+// from T^half), with a wave-wide early exit once every failing unit has its answer.
+// few product sites per hot loop (gt6.h's rolled Fq2 product): inline the multiplication
+#define HBTC_FQMUL_INLINE
+#include "gt6.h"
+#include "hbtc_kernels.h"
+
+namespace hbtc {
+
+using gt::Pos;
+
+#ifndef HBTC_GT_WAVES
+#define HBTC_GT_WAVES 2  // minimum waves per SIMD the check kernels' register budget must allow
+#endif
+
+namespace {
+
+constexpr uint32_t UNITS_PER_WAVE = 5;
+
+struct UnitLane {
+  uint32_t unit;     // 0..4 (5: the idle lanes 60..63)
+  uint32_t side;     // 0: first group of the unit, 1: second
+  uint32_t partner;  // the same coefficient's lane in the other group
+  Pos ps;
+};
+
+__device__ __forceinline__ UnitLane unit_lane() {
+  const uint32_t l = gt::lane_id();
+  UnitLane u;
+  u.unit = l / 12u;
+  u.side = (l / 6u) & 1u;
+  u.partner = u.side ? l - 6u : l + 6u;
+  u.ps = gt::pos();
+  return u;
+}
+
+__device__ __forceinline__ G1J g1j_of(const G1A& a) {
+  G1J r;
+  jac_from_aff(r, a);
+  return r;
+}
+
+// e = FE( f_{|x|,H}(S) * f_{|x|,w}(-P) ): the pairing-product value of one group.
+__device__ __forceinline__ void pair_value(Fq2& e, const G1J& S, bool use1, const Line* hl, const G1J& P,
+                           bool use2, const Line* wl, const Pos& ps) {
+  gt::MillerArg m1{hl, S, use1};
+  gt::MillerArg m2{wl, P, use2};
+  fq_neg(m2.P.y, P.y);
+  Fq2 f;
+  gt::miller2(f, m1, m2, ps);
+  gt::final_exp(e, f, ps);
+}
+
+// Single-error location for a failing unit: smallest p < count with Tw == T^p, or -1.  The
+// group on side 0 tries [0, half), side 1 tries [half, count) from T^half (half = 2^lg).
+// Every lane of the wave runs the loop; `need` is false on units that passed or are idle.
+__device__ __forceinline__ int32_t locate(const Fq2& T, const Fq2& Tw, uint32_t count, int lg, bool need,
+                          const UnitLane& ul) {
+  const uint32_t half = 1u << lg;
+  Fq2 acc;
+  gt::set_one(acc, ul.ps);
+  if (ul.side) {
+    acc = T;
+#pragma unroll 1
+    for (int i = 0; i < lg; ++i) gt::cyc_sqr(acc, ul.ps);
+  }
+  const uint32_t p0 = ul.side ? half : 0u;
+  int32_t found = -1;
+#pragma unroll 1
+  for (uint32_t q = 0; q < half; ++q) {
+    const bool live = need && found < 0 && p0 + q < count;
+    if (!gt::wave_any(live)) break;
+    if (gt::equal(acc, Tw, ul.ps) && live) found = (int32_t)(p0 + q);
+    gt::mul(acc, acc, T, ul.ps);
+  }
+  // combine the two halves (side 0's answer first: the smaller position)
+  const int32_t other = (int32_t)gt::shfl((uint32_t)found, ul.partner);
+  const int32_t f0 = ul.side ? other : found, f1 = ul.side ? found : other;
+  return f0 >= 0 ? f0 : f1;
+}
+
+// T (plain, side 0) and Tw (weighted, side 1) on both groups of a unit, the plain verdict.
+__device__ __forceinline__ bool unit_values(Fq2& T, Fq2& Tw, const Fq2& e, const UnitLane& ul) {
+  Fq2 other;
+  gt::fetch2(other, e, ul.partner);
+  gt::fq2_sel(T, ul.side == 0, e, other);
+  gt::fq2_sel(Tw, ul.side == 0, other, e);
+  return gt::is_one(T, ul.ps);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ level 1: tiles
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_tiles(
+    uint32_t n_tiles, const Tile* __restrict__ tiles, const TileSums* __restrict__ sums,
+    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
+    const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
+    const int32_t* __restrict__ h_status, const int32_t* __restrict__ w_status,
+    int32_t* __restrict__ status, uint32_t* __restrict__ sub_count,
+    uint32_t* __restrict__ sub_list) {
+  const UnitLane ul = unit_lane();
+  const uint32_t t = blockIdx.x * UNITS_PER_WAVE + ul.unit;
+  const bool active = ul.unit < UNITS_PER_WAVE && t < n_tiles;
+  uint32_t k = 0, first = 0, count = 0;
+  bool inst_ok = false;
+  G1J S, P;
+  jac_set_inf(S);
+  jac_set_inf(P);
+  if (active) {
+    const Tile tile = tiles[t];
+    k = tile.inst;
+    first = tile.first;
+    count = tile.count;
+    inst_ok = h_status[k] == HBTC_ACCEPT && w_status[k] == HBTC_ACCEPT;
+    S = ul.side ? sums[t].SW[8] : sums[t].S[8];
+    P = ul.side ? sums[t].PW[8] : sums[t].P[8];
+  }
+  const bool use1 = inst_ok && !jac_is_inf(S) && !h_aff[k].inf;
+  const bool use2 = inst_ok && !jac_is_inf(P) && !w_aff[k].inf;
+  Fq2 e, T, Tw;
+  pair_value(e, S, use1, h_lines + (size_t)k * MILLER_STEPS, P, use2,
+             w_lines + (size_t)k * MILLER_STEPS, ul.ps);
+  const bool pass = unit_values(T, Tw, e, ul);
+  const bool fail = active && inst_ok && !pass;
+  const int32_t loc = locate(T, Tw, count, 5, fail, ul);
+  if (!fail || ul.side != 0 || ul.ps.k != 0) return;
+  // undecodable H / w or a passing tile: k_rlc_finalize decides the pending items
+  if (loc >= 0 && status[first + loc] == HBTC_RLC_PENDING) {
+    status[first + loc] = HBTC_REJECT;
+    return;
+  }
+  sub_list[atomicAdd(sub_count, 1u)] = t;
+}
+
+// ------------------------------------------------------------------------------ level 2: sub-tiles
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_subs(
+    const uint32_t* __restrict__ sub_count, const uint32_t* __restrict__ sub_list,
+    const Tile* __restrict__ tiles, const TileSums* __restrict__ sums,
+    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
+    const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
+    int32_t* __restrict__ status, uint32_t* __restrict__ leaf_count,
+    uint32_t* __restrict__ leaves) {
+  const uint32_t n_units = *sub_count * 8u;
+  if (blockIdx.x * UNITS_PER_WAVE >= n_units) return;  // wave-uniform: the grid is sized for the worst case
+  const UnitLane ul = unit_lane();
+  const uint32_t u = blockIdx.x * UNITS_PER_WAVE + ul.unit;
+  bool active = ul.unit < UNITS_PER_WAVE && u < n_units;
+  uint32_t k = 0, lo = 0, hi = 0;
+  G1J S, P;
+  jac_set_inf(S);
+  jac_set_inf(P);
+  if (active) {
+    const uint32_t t = sub_list[u >> 3], sub = u & 7u;
+    const Tile tile = tiles[t];
+    k = tile.inst;
+    lo = tile.first + sub * 8u;
+    hi = min(tile.first + tile.count, lo + 8u);
+    active = lo < hi;
+    if (active) {
+      S = ul.side ? sums[t].SW[sub] : sums[t].S[sub];
+      P = ul.side ? sums[t].PW[sub] : sums[t].P[sub];
+    }
+  }
+  // listed tiles belong to ciphertexts whose H and w decoded (k_chk_tiles)
+  const bool use1 = active && !jac_is_inf(S) && !h_aff[k].inf;
+  const bool use2 = active && !jac_is_inf(P) && !w_aff[k].inf;
+  Fq2 e, T, Tw;
+  pair_value(e, S, use1, h_lines + (size_t)k * MILLER_STEPS, P, use2,
+             w_lines + (size_t)k * MILLER_STEPS, ul.ps);
+  const bool pass = unit_values(T, Tw, e, ul);
+  const bool fail = active && !pass;
+  const int32_t loc = locate(T, Tw, hi - lo, 2, fail, ul);
+  if (!fail || ul.side != 0 || ul.ps.k != 0) return;
+  if (loc >= 0 && status[lo + loc] == HBTC_RLC_PENDING) {
+    status[lo + loc] = HBTC_REJECT;
+    return;
+  }
+  for (uint32_t i = lo; i < hi; ++i)
+    if (status[i] == HBTC_RLC_PENDING) {
+      const uint32_t pos = atomicAdd(leaf_count, 1u);
+      leaves[2 * pos] = i;
+      leaves[2 * pos + 1] = k;
+    }
+}
+
+// ------------------------------------------------------------------------------ level 3: leaves
+// e(d_i, H_k) e(-pk_i, w_k) == 1 for two listed shares per unit.
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_leaves(
+    const uint32_t* __restrict__ leaf_count, const uint32_t* __restrict__ leaves,
+    const uint32_t* __restrict__ idx, const G1A* __restrict__ dec, const G1A* __restrict__ pk,
+    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
+    const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
+    int32_t* __restrict__ status) {
+  const uint32_t n = *leaf_count;
+  if (blockIdx.x * 2 * UNITS_PER_WAVE >= n) return;
+  const UnitLane ul = unit_lane();
+  const uint32_t li = (blockIdx.x * UNITS_PER_WAVE + ul.unit) * 2u + ul.side;
+  const bool active = ul.unit < UNITS_PER_WAVE && li < n;
+  uint32_t item = 0, k = 0;
+  G1J S, P;
+  jac_set_inf(S);
+  jac_set_inf(P);
+  if (active) {
+    item = leaves[2 * li];
+    k = leaves[2 * li + 1];
+    S = g1j_of(dec[item]);
+    P = g1j_of(pk[idx[item]]);
+  }
+  const bool use1 = active && !jac_is_inf(S) && !h_aff[k].inf;
+  const bool use2 = active && !jac_is_inf(P) && !w_aff[k].inf;
+  Fq2 e;
+  pair_value(e, S, use1, h_lines + (size_t)k * MILLER_STEPS, P, use2,
+             w_lines + (size_t)k * MILLER_STEPS, ul.ps);
+  const bool ok = gt::is_one(e, ul.ps);
+  if (active && ul.ps.k == 0) status[item] = ok ? HBTC_ACCEPT : HBTC_REJECT;
+}
+
+// ------------------------------------------------------------------------------ launchers
+static inline uint32_t unit_blocks(uint64_t units) {
+  return (uint32_t)((units + UNITS_PER_WAVE - 1) / UNITS_PER_WAVE);
+}
+
+hipError_t launch_chk_tiles(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                            const TileSums* sums, const G2A* h_aff, const Line* h_lines,
+                            const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
+                            const int32_t* w_status, int32_t* status, uint32_t* sub_count,
+                            uint32_t* sub_list) {
+  if (n_tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_chk_tiles, dim3(unit_blocks(n_tiles)), dim3(64), 0, s, n_tiles, tiles, sums,
+                     h_aff, h_lines, w_aff, w_lines, h_status, w_status, status, sub_count,
+                     sub_list);
+  return hipGetLastError();
+}
+
+hipError_t launch_chk_subs(hipStream_t s, uint32_t max_tiles, const uint32_t* sub_count,
+                           const uint32_t* sub_list, const Tile* tiles, const TileSums* sums,
+                           const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
+                           const Line* w_lines, int32_t* status, uint32_t* leaf_count,
+                           uint32_t* leaves) {
+  if (max_tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_chk_subs, dim3(unit_blocks((uint64_t)max_tiles * 8)), dim3(64), 0, s,
+                     sub_count, sub_list, tiles, sums, h_aff, h_lines, w_aff, w_lines, status,
+                     leaf_count, leaves);
+  return hipGetLastError();
+}
+
+hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t* leaf_count,
+                             const uint32_t* leaves, const uint32_t* idx, const G1A* dec,
+                             const G1A* pk, const G2A* h_aff, const Line* h_lines,
+                             const G2A* w_aff, const Line* w_lines, int32_t* status) {
+  if (max_leaves == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_chk_leaves, dim3(unit_blocks(((uint64_t)max_leaves + 1) / 2)), dim3(64), 0,
+                     s, leaf_count, leaves, idx, dec, pk, h_aff, h_lines, w_aff, w_lines, status);
+  return hipGetLastError();
+}
+
+}  // namespace hbtc

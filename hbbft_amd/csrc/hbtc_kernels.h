@@ -43,28 +43,24 @@ hipError_t launch_pk_table(hipStream_t s, const G1A* pk, const int32_t* pk_statu
 hipError_t launch_rlc_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* shares, const G1A* pk, const int32_t* pk_status,
                             const PtXY* pk_tab, uint32_t n_pk, RlcKey key, TileSums* sums,
-                            int32_t* status);
-hipError_t launch_rlc_check_groups(hipStream_t s, uint32_t n_inst, uint32_t n_tiles,
-                                   const Tile* tiles, const uint32_t* inst_tiles,
-                                   const TileSums* sums, const G2A* h_aff, const Line* h_lines,
-                                   const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
-                                   const int32_t* w_status, uint8_t* inst_pass,
-                                   uint8_t* tile_pass, int32_t* tile_loc);
-hipError_t launch_rlc_triage(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
-                             const uint8_t* inst_pass, const uint8_t* tile_pass,
-                             const int32_t* tile_loc, int32_t* status, uint32_t* sub_count,
-                             uint32_t* sub_list);
-hipError_t launch_rlc_sub(hipStream_t s, uint32_t max_tiles, const uint32_t* sub_count,
-                          const uint32_t* sub_list, const Tile* tiles, const TileSums* sums,
-                          const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
-                          const Line* w_lines, int32_t* status, uint32_t* leaf_count,
-                          uint32_t* leaves);
-hipError_t launch_rlc_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t* leaf_count,
-                             const uint32_t* leaves, const uint32_t* idx, const uint8_t* shares,
-                             const G1A* pk, const G2A* h_aff, const Line* h_lines,
-                             const G2A* w_aff, const Line* w_lines, int32_t* status);
+                            G1A* dec, int32_t* status);
 hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
                                const int32_t* h_status, const int32_t* w_status, int32_t* status);
+// the pairing-product checks (hbtc_check.hip, cooperative GT arithmetic of gt6.h)
+hipError_t launch_chk_tiles(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                            const TileSums* sums, const G2A* h_aff, const Line* h_lines,
+                            const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
+                            const int32_t* w_status, int32_t* status, uint32_t* sub_count,
+                            uint32_t* sub_list);
+hipError_t launch_chk_subs(hipStream_t s, uint32_t max_tiles, const uint32_t* sub_count,
+                           const uint32_t* sub_list, const Tile* tiles, const TileSums* sums,
+                           const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
+                           const Line* w_lines, int32_t* status, uint32_t* leaf_count,
+                           uint32_t* leaves);
+hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t* leaf_count,
+                             const uint32_t* leaves, const uint32_t* idx, const G1A* dec,
+                             const G1A* pk, const G2A* h_aff, const Line* h_lines,
+                             const G2A* w_aff, const Line* w_lines, int32_t* status);
 
 hipError_t launch_g1_decode(hipStream_t s, const uint8_t* in, uint32_t n, G1A* out,
                             int32_t* status);
@@ -100,16 +96,16 @@ hipError_t launch_msm_digits(hipStream_t s, const MsmPlan& p, const uint32_t* sc
                              int16_t* digits, uint32_t* list, uint32_t* roff);
 hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
                                 const uint8_t* pts_c, const uint32_t* sel_pos,
-                                const uint32_t* sel_cnt, const int32_t* item_status, G1A* pts,
-                                uint32_t* bad);
+                                const uint32_t* sel_cnt, const int32_t* item_status,
+                                const G1A* dec, G1A* pts, uint32_t* bad);
 hipError_t launch_msm_reduce_g1(hipStream_t s, const MsmPlan& p, const G1A* pts,
                                 const uint32_t* pts_map, const uint32_t* list, const uint32_t* roff, G1J* part, G1J* wsum,
                                 const uint32_t* sel_cnt, uint32_t t, const uint32_t* bad,
                                 const uint32_t* dup, int32_t* status, uint8_t* out);
 hipError_t launch_msm_decode_g2(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
                                 const uint8_t* pts_c, const uint32_t* sel_pos,
-                                const uint32_t* sel_cnt, const int32_t* item_status, G2A* pts,
-                                uint32_t* bad);
+                                const uint32_t* sel_cnt, const int32_t* item_status,
+                                const G2A* dec, G2A* pts, uint32_t* bad);
 hipError_t launch_msm_reduce_g2(hipStream_t s, const MsmPlan& p, const G2A* pts,
                                 const uint32_t* pts_map, const uint32_t* list, const uint32_t* roff, G2J* part, G2J* wsum,
                                 const uint32_t* sel_cnt, uint32_t t, const uint32_t* bad,

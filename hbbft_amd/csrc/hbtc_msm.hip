@@ -265,6 +265,7 @@ __global__ void __launch_bounds__(64) k_msm_decode(uint32_t n_inst, uint32_t t, 
                                                    const uint32_t* __restrict__ sel_pos,
                                                    const uint32_t* __restrict__ sel_cnt,
                                                    const int32_t* __restrict__ status,
+                                                   const Aff<F>* __restrict__ dec,
                                                    Aff<F>* __restrict__ out,
                                                    uint32_t* __restrict__ bad) {
   const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
@@ -278,13 +279,18 @@ __global__ void __launch_bounds__(64) k_msm_decode(uint32_t n_inst, uint32_t t, 
     msm_generator(p);
   } else if (i < sel_cnt[k]) {
     const uint64_t pos = sel_pos ? (uint64_t)sel_pos[g] : (uint64_t)k * stride + i;
-    uint32_t w[NW];
-    msm_load_words(w, pts, pos, NW);
-    // an item the verifier accepted was decoded and subgroup-checked by it
-    const bool chk = !(status && status[pos] == HBTC_ACCEPT);
-    if (!msm_decompress(p, w, chk)) {
-      atomicOr(&bad[k], 1u);
-      p.inf = 1;
+    // an item the verifier accepted was decoded and subgroup-checked by it; with its decoded
+    // form at hand (the RLC item pass keeps it) nothing is decoded again
+    const bool accepted = status && status[pos] == HBTC_ACCEPT;
+    if (accepted && dec) {
+      p = dec[pos];
+    } else {
+      uint32_t w[NW];
+      msm_load_words(w, pts, pos, NW);
+      if (!msm_decompress(p, w, !accepted)) {
+        atomicOr(&bad[k], 1u);
+        p.inf = 1;
+      }
     }
   }
   out[g] = p;
@@ -408,7 +414,7 @@ __global__ void __launch_bounds__(64) k_msm_final(uint32_t n_msm, uint32_t c, ui
 #if HBTC_IN_PART(8)
 template __global__ void k_msm_decode<Fq, 12>(uint32_t, uint32_t, uint32_t, const uint8_t*,
                                               const uint32_t*, const uint32_t*, const int32_t*,
-                                              G1A*, uint32_t*);
+                                              const G1A*, G1A*, uint32_t*);
 template __global__ void k_msm_buckets<Fq>(uint64_t, uint32_t, uint32_t, uint32_t, const G1A*,
                                            const uint32_t*, const uint32_t*, const uint32_t*,
                                            G1J*);
@@ -420,7 +426,7 @@ template __global__ void k_msm_final<Fq, 12>(uint32_t, uint32_t, uint32_t, const
 #if HBTC_IN_PART(9)
 template __global__ void k_msm_decode<Fq2, 24>(uint32_t, uint32_t, uint32_t, const uint8_t*,
                                                const uint32_t*, const uint32_t*, const int32_t*,
-                                               G2A*, uint32_t*);
+                                               const G2A*, G2A*, uint32_t*);
 template __global__ void k_msm_buckets<Fq2>(uint64_t, uint32_t, uint32_t, uint32_t, const G2A*,
                                             const uint32_t*, const uint32_t*, const uint32_t*,
                                             G2J*);
@@ -493,12 +499,12 @@ static hipError_t launch_msm_reduce(hipStream_t s, const MsmPlan& p, const Aff<F
 #if HBTC_IN_PART(8)
 hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
                                 const uint8_t* pts_c, const uint32_t* sel_pos,
-                                const uint32_t* sel_cnt, const int32_t* item_status, G1A* pts,
-                                uint32_t* bad) {
+                                const uint32_t* sel_cnt, const int32_t* item_status,
+                                const G1A* dec, G1A* pts, uint32_t* bad) {
   const uint64_t terms = (uint64_t)n_msm * n;
   if (terms == 0) return hipSuccess;
   hipLaunchKernelGGL((k_msm_decode<Fq, 12>), dim3(msm_blocks(terms, 64)), dim3(64), 0, s, n_msm, n,
-                     stride, pts_c, sel_pos, sel_cnt, item_status, pts, bad);
+                     stride, pts_c, sel_pos, sel_cnt, item_status, dec, pts, bad);
   return hipGetLastError();
 }
 hipError_t launch_msm_reduce_g1(hipStream_t s, const MsmPlan& p, const G1A* pts,
@@ -513,12 +519,12 @@ hipError_t launch_msm_reduce_g1(hipStream_t s, const MsmPlan& p, const G1A* pts,
 #if HBTC_IN_PART(9)
 hipError_t launch_msm_decode_g2(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
                                 const uint8_t* pts_c, const uint32_t* sel_pos,
-                                const uint32_t* sel_cnt, const int32_t* item_status, G2A* pts,
-                                uint32_t* bad) {
+                                const uint32_t* sel_cnt, const int32_t* item_status,
+                                const G2A* dec, G2A* pts, uint32_t* bad) {
   const uint64_t terms = (uint64_t)n_msm * n;
   if (terms == 0) return hipSuccess;
   hipLaunchKernelGGL((k_msm_decode<Fq2, 24>), dim3(msm_blocks(terms, 64)), dim3(64), 0, s, n_msm,
-                     n, stride, pts_c, sel_pos, sel_cnt, item_status, pts, bad);
+                     n, stride, pts_c, sel_pos, sel_cnt, item_status, dec, pts, bad);
   return hipGetLastError();
 }
 hipError_t launch_msm_reduce_g2(hipStream_t s, const MsmPlan& p, const G2A* pts,

@@ -20,12 +20,13 @@
 // == 1 with a nonzero exponent on a wrong share, i.e. with probability <= 2^-64 per p (the same
 // argument as the plain check), <= |G| 2^-64 <= 2^-58 per located group; such groups are split.
 //
-// Levels:
-//     k_rlc_check_groups  ciphertext checks + (plain, weighted) checks of every 64-share tile;
-//                         a failing tile with one wrong share is located right there
-//     k_rlc_triage        failing, unlocated tiles -> compact list
-//     k_rlc_sub           (plain, weighted) checks of their 8-share sub-tiles, located likewise
-//     k_rlc_leaves        the exact per-share check for sub-tiles with >= 2 wrong shares
+// This file holds the per-item pass (k_rlc_items: decode, r_i, the tile and sub-tile sums)
+// and the final decision (k_rlc_finalize); the pairing-product checks of those sums run on
+// the cooperative GT arithmetic in hbtc_check.hip:
+//     k_chk_tiles   (plain, weighted) checks of every 64-share tile; a failing tile with one
+//                   wrong share is located right there, the others are listed
+//     k_chk_subs    the 8-share sub-tiles of listed tiles, located likewise
+//     k_chk_leaves  the exact per-share check for sub-tiles with >= 2 wrong shares
 // Work per share in the honest case: decode + r_i d_i (a joint 32-bit double-and-add through
 // the GLV endomorphism) + r_i pk_i (8 mixed additions from the key set's fixed-base table) + a
 // share of the wave's reduction tree; the pairing work is per group.
@@ -85,69 +86,6 @@ __device__ uint64_t rlc_scalar(const RlcKey& key, uint64_t item) {
     }
   return ((uint64_t)hi << 32) | lo;
 }
-
-struct RlcTableLines {
-  const Line* l;
-  __device__ __forceinline__ void load(Line& out, int j) const { out = l[j]; }
-};
-
-#ifndef HBTC_CHECK_WAVES
-#define HBTC_CHECK_WAVES 1  // minimum waves per SIMD for the pairing-check kernels
-#endif
-
-#if HBTC_IN_PART(7)
-// T = e(S, H) * e(-P, w) for aggregated Jacobian S, P (per-lane instance: vector line loads);
-// returns T == 1.
-__device__ bool rlc_pair_value(Fq12& e, const G1J& S, const G1J& P, const Line* hl, bool h_inf,
-                               const Line* wl, bool w_inf) {
-  G1A s, p;
-  jac_to_aff(s, S);
-  jac_to_aff(p, P);
-  const bool use1 = !s.inf && !h_inf, use2 = !p.inf && !w_inf;
-  if (!use1 && !use2) {
-    fq12_one(e);
-    return true;
-  }
-  G1A np;
-  aff_neg(np, p);
-  Fq12 f;
-  miller_loop_2(f, RlcTableLines{hl}, s, use1, RlcTableLines{wl}, np, use2);
-  final_exponentiation(e, f);
-  return fq12_is_one(e);
-}
-
-// Exchange a GT value with the partner lane (lane ^ 1) of the wave.
-__device__ __forceinline__ void fq_shfl_xor1(Fq& r, const Fq& a) {
-#pragma unroll
-  for (int i = 0; i < 12; ++i) r.v[i] = (uint32_t)__shfl_xor((int)a.v[i], 1);
-}
-__device__ __forceinline__ void fq12_shfl_xor1(Fq12& r, const Fq12& a) {
-  fq_shfl_xor1(r.c0.c0.c0, a.c0.c0.c0);
-  fq_shfl_xor1(r.c0.c0.c1, a.c0.c0.c1);
-  fq_shfl_xor1(r.c0.c1.c0, a.c0.c1.c0);
-  fq_shfl_xor1(r.c0.c1.c1, a.c0.c1.c1);
-  fq_shfl_xor1(r.c0.c2.c0, a.c0.c2.c0);
-  fq_shfl_xor1(r.c0.c2.c1, a.c0.c2.c1);
-  fq_shfl_xor1(r.c1.c0.c0, a.c1.c0.c0);
-  fq_shfl_xor1(r.c1.c0.c1, a.c1.c0.c1);
-  fq_shfl_xor1(r.c1.c1.c0, a.c1.c1.c0);
-  fq_shfl_xor1(r.c1.c1.c1, a.c1.c1.c1);
-  fq_shfl_xor1(r.c1.c2.c0, a.c1.c2.c0);
-  fq_shfl_xor1(r.c1.c2.c1, a.c1.c2.c1);
-}
-
-// Smallest p < count with Tw == T^p, or -1 (T != 1: the group failed).
-__device__ __attribute__((noinline)) int32_t rlc_locate(const Fq12& T, const Fq12& Tw,
-                                                        uint32_t count) {
-  Fq12 acc;
-  fq12_one(acc);
-  for (uint32_t p = 0; p < count; ++p) {
-    if (fq12_eq(acc, Tw)) return (int32_t)p;
-    fq12_mul(acc, acc, T);
-  }
-  return -1;
-}
-#endif  // part 7
 
 #if HBTC_IN_PART(6)
 // ------------------------------------------------------------------------------ per item
@@ -227,7 +165,8 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
     const uint8_t* __restrict__ shares, const G1A* __restrict__ pk,
     const int32_t* __restrict__ pk_status, const PtXY* __restrict__ pk_tab, uint32_t n_pk,
-    RlcKey key, TileSums* __restrict__ sums, int32_t* __restrict__ status) {
+    RlcKey key, TileSums* __restrict__ sums, G1A* __restrict__ dec,
+    int32_t* __restrict__ status) {
   __shared__ G1J redA[64];
   __shared__ G1J redB[64];
   const Tile tile = tiles[blockIdx.x];
@@ -250,6 +189,7 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
       if (!g1_decompress(d, w)) {
         st = HBTC_DECODE_ERR;
       } else {
+        dec[item] = d;  // for the exact leaf checks and the combine (no second decode)
         const uint64_t r = rlc_scalar(key, item);
         const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
         G1A pd;
@@ -265,169 +205,6 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
   rlc_reduce(redA, redB, P, lane, ts->P, ts->PW);
 }
 #endif  // part 6
-
-#if HBTC_IN_PART(7)
-// ------------------------------------------------------------------------------ group checks
-// Lanes [0, 2 n_tiles): tile g/2, plain (g even) and weighted (g odd) sums — partners in one
-// wave.  Lanes [2 n_tiles, 2 n_tiles + n_inst): ciphertext-level checks (sum of the tile sums).
-// All run in one launch (one round of pairing latency); a tile whose ciphertext passes is
-// resolved by the ciphertext verdict in k_rlc_triage.
-__global__ void __launch_bounds__(64, HBTC_CHECK_WAVES) k_rlc_check_groups(
-    uint32_t n_inst, uint32_t n_tiles, const Tile* __restrict__ tiles,
-    const uint32_t* __restrict__ inst_tiles, const TileSums* __restrict__ sums,
-    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
-    const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
-    const int32_t* __restrict__ h_status, const int32_t* __restrict__ w_status,
-    uint8_t* __restrict__ inst_pass, uint8_t* __restrict__ tile_pass,
-    int32_t* __restrict__ tile_loc) {
-  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
-  const uint32_t n_tl = 2 * n_tiles;
-  const bool active = g < n_tl + n_inst;
-  const bool is_tile = g < n_tl;
-  const bool weighted = (g & 1u) != 0;
-  const uint32_t t = g >> 1;
-  uint32_t k = 0, count = 0;
-  bool inst_ok = false;
-  G1J S, P;
-  jac_set_inf(S);
-  jac_set_inf(P);
-  if (active) {
-    if (is_tile) {
-      const Tile tile = tiles[t];
-      k = tile.inst;
-      count = tile.count;
-    } else {
-      k = g - n_tl;
-    }
-    inst_ok = h_status[k] == HBTC_ACCEPT && w_status[k] == HBTC_ACCEPT;
-    if (inst_ok) {
-      if (is_tile) {
-        S = weighted ? sums[t].SW[8] : sums[t].S[8];
-        P = weighted ? sums[t].PW[8] : sums[t].P[8];
-      } else {
-        for (uint32_t u = inst_tiles[k]; u < inst_tiles[k + 1]; ++u) {
-          jac_add(S, S, sums[u].S[8]);
-          jac_add(P, P, sums[u].P[8]);
-        }
-      }
-    }
-  }
-  Fq12 e;
-  bool ok = true;
-  if (active && inst_ok)
-    ok = rlc_pair_value(e, S, P, h_lines + (size_t)k * MILLER_STEPS, h_aff[k].inf != 0,
-                        w_lines + (size_t)k * MILLER_STEPS, w_aff[k].inf != 0);
-  else
-    fq12_one(e);
-  Fq12 ew;
-  fq12_shfl_xor1(ew, e);  // the plain lane receives its partner's weighted value
-  if (!active) return;
-  // undecodable H / w: no group work; k_rlc_finalize marks the items INSTANCE_ERR
-  if (!is_tile) {
-    inst_pass[k] = (ok || !inst_ok) ? 1 : 0;
-    return;
-  }
-  if (weighted) return;
-  tile_pass[t] = (ok || !inst_ok) ? 1 : 0;
-  tile_loc[t] = (ok || !inst_ok) ? -1 : rlc_locate(e, ew, count);
-}
-
-// One lane per tile: a tile whose ciphertext AND tile checks failed either had its single
-// wrong share located (REJECT it; the rest of the tile is valid) or goes to the sub-tile list.
-__global__ void __launch_bounds__(64) k_rlc_triage(
-    uint32_t n_tiles, const Tile* __restrict__ tiles, const uint8_t* __restrict__ inst_pass,
-    const uint8_t* __restrict__ tile_pass, const int32_t* __restrict__ tile_loc,
-    int32_t* __restrict__ status, uint32_t* __restrict__ sub_count,
-    uint32_t* __restrict__ sub_list) {
-  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
-  if (t >= n_tiles) return;
-  const Tile tile = tiles[t];
-  if (inst_pass[tile.inst] || tile_pass[t]) return;
-  const int32_t loc = tile_loc[t];
-  if (loc >= 0 && status[tile.first + loc] == HBTC_RLC_PENDING) {
-    status[tile.first + loc] = HBTC_REJECT;
-    return;
-  }
-  sub_list[atomicAdd(sub_count, 1u)] = t;
-}
-
-// 16 lanes per listed tile: its 8 sub-tiles x (plain, weighted).  A failing sub-tile with one
-// wrong share is located; one with more appends its pending items to the leaf list.
-__global__ void __launch_bounds__(64, HBTC_CHECK_WAVES) k_rlc_sub(
-    const uint32_t* __restrict__ sub_count, const uint32_t* __restrict__ sub_list,
-    const Tile* __restrict__ tiles, const TileSums* __restrict__ sums,
-    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
-    const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
-    int32_t* __restrict__ status, uint32_t* __restrict__ leaf_count,
-    uint32_t* __restrict__ leaves) {
-  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
-  const uint32_t entry = g >> 4, sub = (g >> 1) & 7u;
-  const bool weighted = (g & 1u) != 0;
-  bool active = entry < *sub_count;
-  uint32_t k = 0, lo = 0, hi = 0;
-  G1J S, P;
-  jac_set_inf(S);
-  jac_set_inf(P);
-  if (active) {
-    const uint32_t t = sub_list[entry];
-    const Tile tile = tiles[t];
-    k = tile.inst;
-    lo = tile.first + sub * 8;
-    hi = min(tile.first + tile.count, lo + 8);
-    active = lo < hi;
-    if (active) {
-      S = weighted ? sums[t].SW[sub] : sums[t].S[sub];
-      P = weighted ? sums[t].PW[sub] : sums[t].P[sub];
-    }
-  }
-  Fq12 e;
-  bool ok = true;
-  if (active)
-    ok = rlc_pair_value(e, S, P, h_lines + (size_t)k * MILLER_STEPS, h_aff[k].inf != 0,
-                        w_lines + (size_t)k * MILLER_STEPS, w_aff[k].inf != 0);
-  else
-    fq12_one(e);
-  Fq12 ew;
-  fq12_shfl_xor1(ew, e);
-  if (!active || weighted || ok) return;
-  const int32_t loc = rlc_locate(e, ew, hi - lo);
-  if (loc >= 0 && status[lo + loc] == HBTC_RLC_PENDING) {
-    status[lo + loc] = HBTC_REJECT;
-    return;
-  }
-  for (uint32_t i = lo; i < hi; ++i)
-    if (status[i] == HBTC_RLC_PENDING) {
-      const uint32_t pos = atomicAdd(leaf_count, 1u);
-      leaves[2 * pos] = i;
-      leaves[2 * pos + 1] = k;
-    }
-}
-
-// Exact per-share check for the compacted leaf list (items of sub-tiles with >= 2 wrong
-// shares): the same arithmetic as k_dec_verify, with per-lane instance (vector line loads).
-__global__ void __launch_bounds__(64, HBTC_CHECK_WAVES) k_rlc_leaves(
-    const uint32_t* __restrict__ leaf_count, const uint32_t* __restrict__ leaves,
-    const uint32_t* __restrict__ idx, const uint8_t* __restrict__ shares,
-    const G1A* __restrict__ pk, const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
-    const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
-    int32_t* __restrict__ status) {
-  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
-  if (g >= *leaf_count) return;
-  const uint32_t item = leaves[2 * g], k = leaves[2 * g + 1];
-  uint32_t w[12];
-  rlc_load_words(w, shares, item, 12);
-  G1A s;
-  g1_decompress(s, w);  // decoded fine in k_rlc_items
-  G1A npk;
-  aff_neg(npk, pk[idx[item]]);
-  const bool h_inf = h_aff[k].inf != 0, w_inf = w_aff[k].inf != 0;
-  Fq12 f, e;
-  miller_loop_2(f, RlcTableLines{h_lines + (size_t)k * MILLER_STEPS}, s, !s.inf && !h_inf,
-                RlcTableLines{w_lines + (size_t)k * MILLER_STEPS}, npk, !npk.inf && !w_inf);
-  final_exponentiation(e, f);
-  status[item] = fq12_is_one(e) ? HBTC_ACCEPT : HBTC_REJECT;
-}
-#endif  // part 7
 
 #if HBTC_IN_PART(6)
 // Every item still pending passed some group check: ACCEPT.  Items of a ciphertext whose own
@@ -453,10 +230,10 @@ static inline uint32_t rlc_blocks(uint64_t n, uint32_t bs) { return (uint32_t)((
 hipError_t launch_rlc_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* shares, const G1A* pk, const int32_t* pk_status,
                             const PtXY* pk_tab, uint32_t n_pk, RlcKey key, TileSums* sums,
-                            int32_t* status) {
+                            G1A* dec, int32_t* status) {
   if (n_tiles == 0) return hipSuccess;
   hipLaunchKernelGGL(k_rlc_items, dim3(n_tiles), dim3(64), 0, s, tiles, idx, shares, pk, pk_status,
-                     pk_tab, n_pk, key, sums, status);
+                     pk_tab, n_pk, key, sums, dec, status);
   return hipGetLastError();
 }
 hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
@@ -467,50 +244,5 @@ hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n_tiles, const Tile* tile
   return hipGetLastError();
 }
 #endif  // part 6
-
-#if HBTC_IN_PART(7)
-hipError_t launch_rlc_check_groups(hipStream_t s, uint32_t n_inst, uint32_t n_tiles,
-                                   const Tile* tiles, const uint32_t* inst_tiles,
-                                   const TileSums* sums, const G2A* h_aff, const Line* h_lines,
-                                   const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
-                                   const int32_t* w_status, uint8_t* inst_pass,
-                                   uint8_t* tile_pass, int32_t* tile_loc) {
-  const uint64_t n = 2 * (uint64_t)n_tiles + n_inst;
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rlc_check_groups, dim3(rlc_blocks(n, 64)), dim3(64), 0, s, n_inst, n_tiles,
-                     tiles, inst_tiles, sums, h_aff, h_lines, w_aff, w_lines, h_status, w_status,
-                     inst_pass, tile_pass, tile_loc);
-  return hipGetLastError();
-}
-hipError_t launch_rlc_triage(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
-                             const uint8_t* inst_pass, const uint8_t* tile_pass,
-                             const int32_t* tile_loc, int32_t* status, uint32_t* sub_count,
-                             uint32_t* sub_list) {
-  if (n_tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rlc_triage, dim3(rlc_blocks(n_tiles, 64)), dim3(64), 0, s, n_tiles, tiles,
-                     inst_pass, tile_pass, tile_loc, status, sub_count, sub_list);
-  return hipGetLastError();
-}
-hipError_t launch_rlc_sub(hipStream_t s, uint32_t max_tiles, const uint32_t* sub_count,
-                          const uint32_t* sub_list, const Tile* tiles, const TileSums* sums,
-                          const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
-                          const Line* w_lines, int32_t* status, uint32_t* leaf_count,
-                          uint32_t* leaves) {
-  if (max_tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rlc_sub, dim3(rlc_blocks((uint64_t)max_tiles * 16, 64)), dim3(64), 0, s,
-                     sub_count, sub_list, tiles, sums, h_aff, h_lines, w_aff, w_lines, status,
-                     leaf_count, leaves);
-  return hipGetLastError();
-}
-hipError_t launch_rlc_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t* leaf_count,
-                             const uint32_t* leaves, const uint32_t* idx, const uint8_t* shares,
-                             const G1A* pk, const G2A* h_aff, const Line* h_lines,
-                             const G2A* w_aff, const Line* w_lines, int32_t* status) {
-  if (max_leaves == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rlc_leaves, dim3(rlc_blocks(max_leaves, 64)), dim3(64), 0, s, leaf_count,
-                     leaves, idx, shares, pk, h_aff, h_lines, w_aff, w_lines, status);
-  return hipGetLastError();
-}
-#endif  // part 7
 
 }  // namespace hbtc

@@ -39,7 +39,10 @@
  *
  * Threading: one context per GPU; calls on one context are serialised by an internal mutex.
  * Host entry points block until the results are on the host; *_dev entry points take
- * device pointers (from hbtc_dev_alloc) and are ordered on the context's HIP stream.
+ * device pointers (from hbtc_dev_alloc) and are ordered as issued: combines run on a side
+ * stream, concurrently with the verification issued after them, and any later call that
+ * writes a device range a pending combine still reads (a status array, an upload into the
+ * share buffer) first waits for that combine.
  * The caller owns every buffer; nothing is retained after a call returns.
  */
 #ifndef HBTC_H
@@ -229,11 +232,12 @@ int hbtc_skg_check_acks(hbtc_ctx* ctx, uint32_t n_parts, uint32_t t, uint32_t ou
 
 /* ---- verification strategy ----------------------------------------------------------------- */
 /* HBTC_MODE_RLC (default): shares of one instance are checked together by a random linear
- * combination (fresh 64-bit ChaCha20 scalars per call, prime-order points only), failing groups
- * are split ciphertext -> 64 -> 8 -> 1 share; a group with exactly one wrong share is resolved
- * by a position-weighted second combination (the wrong share located without per-share
- * pairings), the rest get the exact pairing check.  The decisions equal the per-share decisions
- * except with probability <= 2^-64 per group check (<= 2^-58 per located group).
+ * combination (fresh 64-bit ChaCha20 scalars per call, prime-order points only) in groups of
+ * 64 consecutive shares; failing groups are split 64 -> 8 -> 1 share; a group with exactly one
+ * wrong share is resolved by a position-weighted second combination (the wrong share located
+ * without per-share pairings), the rest get the exact pairing check.  The decisions equal the
+ * per-share decisions except with probability <= 2^-64 per group check (<= 2^-58 per located
+ * group).
  * HBTC_MODE_PER_SHARE: every share gets its own 2-pair pairing check (the reference's count).
  * Applies to hbtc_verify_dec_shares[_dev]. */
 #define HBTC_MODE_PER_SHARE 0
@@ -245,7 +249,7 @@ int hbtc_rlc_last_leaves(hbtc_ctx* ctx, uint32_t* leaves);
 /* ---- kernel timing (HIP events on the context's stream) ---------------------------------- */
 /* Families: "prepare", "dec_verify", "sig_verify", "pair_verify", "lagrange" (selection +
  * Lagrange coefficients), "comb_decode", "comb_digits", "combine" (MSM bucket reduction), "skg_scalars", "skg_ack_rows",
- * "mul", "rlc_items", "rlc_groups", "rlc_triage", "rlc_sub", "rlc_leaves", "rlc_finalize".  Reading
+ * "mul", "rlc_items", "chk_tiles", "chk_subs", "chk_leaves", "rlc_finalize".  Reading
  * synchronises the stream. */
 int hbtc_timing_enable(hbtc_ctx* ctx, int enable);
 int hbtc_timing_read(hbtc_ctx* ctx, const char* family, double* total_ms, uint64_t* launches);
