@@ -217,10 +217,12 @@ HD void mul_line(Fq2& f, const Fq& pa, uint32_t a, const Fq& pb, uint32_t b, con
     fq_sel(o1, t == 0, pa, pb);
     const uint32_t l0 = t == 0 ? a : (t == 1 ? b : y);
     fetch(q.c0, o0, src(ps, l0));
-    fetch(q.c1, o1, src(ps, l0 + 1));
+    fetch(q.c1, o1, src(ps, l0 + 1));  // unused for t == 2
     if (t == 0 && !use) fq_one(q.c0);
-    if (t == 2) fq_zero(q.c1);
-    mul2(z, x, q);
+    if (t == 2)  // Y in Fq: two products (t is the same on every lane: a uniform branch)
+      mul2_fq(z, x, q.c0);
+    else
+      mul2(z, x, q);
     fq2_xi_if(z, (t == 1 && k < 2) || (t == 2 && k < 3), z);
     fq2_add(acc, acc, z);
   }
@@ -257,31 +259,35 @@ GTN void frob(Fq2& f, int j, const Pos& ps) {
 }
 
 // Granger-Scott squaring of a cyclotomic element, Fq12 seen as Fq4^3 over the coefficient
-// pairs (k, k+3): lane k < 3 forms a^2 + xi b^2 and lane k + 3 forms 2ab (a = f_k,
-// b = f_{k+3}); each output then needs one partner value:
+// pairs (k, k+3), a = f_k, b = f_{k+3}: (a + b s)^2 = (a^2 + xi b^2) + 2ab s with s = w^3.
+// Karatsuba across the pair: lane k + 3 forms m = ab, lane k forms q = (a + b)(a + xi b), so
+// a^2 + xi b^2 = q - m - xi m — ONE Fq2 product per lane.  Then each output needs one value:
 //     z_0 = 3 T_0 - 2 f_0   z_1 = 3 xi T_5 + 2 f_1   z_2 = 3 T_1 - 2 f_2
 //     z_3 = 3 T_3 + 2 f_3   z_4 = 3 T_2 - 2 f_4      z_5 = 3 T_4 + 2 f_5
+// with T_k = a^2 + xi b^2 on lanes k < 3 and 2ab on lanes k >= 3.
 HD void cyc_sqr(Fq2& f, const Pos& ps) {
   const bool lo = ps.k < 3;
+  const uint32_t pk = lo ? ps.k + 3 : ps.k - 3;
   Fq2 partner;
-  fetch2(partner, f, src(ps, lo ? ps.k + 3 : ps.k - 3));
-  // lo lanes: a*a then b*b (a = f, b = partner); hi lanes: a*b (partner * f), then unused
-  Fq2 z0, z1;
-#pragma unroll 1
-  for (uint32_t t = 0; t < 2; ++t) {
-    Fq2 x, y, r, first;
-    fq2_sel(first, lo, f, partner);
-    fq2_sel(x, t == 0, first, partner);
-    fq2_sel(y, t == 0, f, partner);
-    mul2(r, x, y);
-    fq2_sel(z0, t == 0, r, z0);
-    z1 = r;
+  fetch2(partner, f, src(ps, pk));
+  Fq2 x, y, r;
+  {
+    Fq2 b = lo ? partner : f, a = lo ? f : partner, xb, apb, apxb;
+    fq2_mul_xi(xb, b);
+    fq2_add(apb, a, b);
+    fq2_add(apxb, a, xb);
+    fq2_sel(x, lo, apb, a);
+    fq2_sel(y, lo, apxb, b);
   }
-  Fq2 T, t1;
-  fq2_mul_xi(t1, z1);
-  fq2_add(t1, z0, t1);  // a^2 + xi b^2
+  mul2(r, x, y);  // lo: (a + b)(a + xi b); hi: ab
+  Fq2 m;
+  fetch2(m, r, src(ps, pk));  // lo lanes take ab from their partner
+  Fq2 T, t1, xm;
+  fq2_mul_xi(xm, m);
+  fq2_sub(t1, r, m);
+  fq2_sub(t1, t1, xm);    // a^2 + xi b^2
   Fq2 t2;
-  fq2_dbl(t2, z0);      // 2ab
+  fq2_dbl(t2, r);         // 2ab
   fq2_sel(T, lo, t1, t2);
   // route T: lane k reads T from lane s(k) = {0, 5, 1, 3, 2, 4}[k]
   const uint32_t sk = ps.k == 0 ? 0u : ps.k == 1 ? 5u : ps.k == 2 ? 1u : ps.k == 3 ? 3u : ps.k == 4 ? 2u : 4u;
@@ -334,20 +340,89 @@ GTN void exp_by_x(Fq2& r, const Fq2& y, const Pos& ps) {
   r = acc;
 }
 
-// a^(p-2) (Fermat inversion), square-and-multiply over the constant exponent
-HD void fq_inv_fermat(Fq& r, const Fq& a) {
-  Fq acc;
-  fq_one(acc);
+// Inversion in Fq by the binary extended Euclidean algorithm (variable time: every input is
+// public), about a quarter of the instruction count of the Fermat power a^(p-2).
+// Invariants x1 A = u, x2 A = v (mod p) with A the canonical input, u, v odd after the first
+// step; each iteration subtracts the smaller of u, v from the larger and strips the difference's
+// factors of two (up to 31 per iteration: x <- x / 2^k mod p as (x + m p) / 2^k with
+// m = -x p^-1 mod 2^k, the Montgomery digit).  The loop is wave-uniform: lanes that finished
+// keep their state until every lane has.  Montgomery in, Montgomery out: for the input aR the
+// loop finds x = (aR)^-1 and the result is x R^3 R^-1 = a^-1 R.
+HD void half_k(Fq& x, uint32_t k) {  // x / 2^k mod p for x < p, 0 <= k <= 31  (result < p)
+  const uint32_t mask = k ? (0xffffffffu >> (32 - k)) : 0u;
+  const uint32_t m = (x.v[0] * FQ_NP) & mask;
+  uint32_t t[13];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    c += (uint64_t)m * FQ_P[i] + x.v[i];
+    t[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  t[12] = (uint32_t)c;
+#pragma unroll
+  for (int i = 0; i < 12; ++i)
+    x.v[i] = k ? ((t[i] >> k) | (t[i + 1] << (32 - k))) : t[i];
+  fq_canon(x, x);  // (x + m p) / 2^k < 2p
+}
+HD uint32_t ctz31(const Fq& a) {
+  const uint32_t w = a.v[0];
+  return w ? (uint32_t)__builtin_ctz(w) : 31u;
+}
+HD void shr_k(Fq& a, uint32_t k) {
+#pragma unroll
+  for (int i = 0; i < 11; ++i) a.v[i] = k ? ((a.v[i] >> k) | (a.v[i + 1] << (32 - k))) : a.v[i];
+  a.v[11] = a.v[11] >> k;
+}
+HD void fq_inv_binary(Fq& r, const Fq& a_mont) {
+  Fq u, v, x1, x2, one;
+  fq_canon(u, a_mont);
+  limbs_set_const<12>(v, FQ_P);
+  limbs_zero<12>(x1);
+  x1.v[0] = 1;
+  limbs_zero<12>(x2);
+  limbs_zero<12>(one);
+  one.v[0] = 1;
+  bool zero = limbs_is_zero<12>(u);
+  {  // make u odd
+    uint32_t k = ctz31(u);
 #pragma unroll 1
-  for (int w = 11; w >= 0; --w) {
-    const uint32_t word = EXP_P_MINUS_2[w];
-#pragma unroll 1
-    for (int b = 31; b >= 0; --b) {
-      fq_sqr(acc, acc);
-      if ((word >> b) & 1u) fq_mul(acc, acc, a);  // uniform: the exponent is a constant
+    for (int rep = 0; rep < 13 && k && !zero; ++rep) {
+      shr_k(u, k);
+      half_k(x1, k);
+      k = ctz31(u);
     }
   }
-  r = acc;
+  bool done = zero || limbs_eq<12>(u, one);
+#pragma unroll 1
+  for (int it = 0; it < 2 * 384; ++it) {
+    if (!wave_any(!done)) break;
+    Fq duv, dvu, d, xd, t;
+    const bool ge = limbs_sub<12>(duv, u, v) == 0;  // u >= v
+    limbs_sub<12>(dvu, v, u);
+    fq_sel(d, ge, duv, dvu);
+    // xd = ge ? x1 - x2 : x2 - x1 (mod p, canonical)
+    Fq xa, xb;
+    fq_sel(xa, ge, x1, x2);
+    fq_sel(xb, ge, x2, x1);
+    const uint32_t bw = limbs_sub<12>(xd, xa, xb);
+    limbs_add_const<12>(t, xd, FQ_P);
+    fq_sel(xd, bw != 0, t, xd);
+    uint32_t k = ctz31(d);
+    shr_k(d, k);
+    half_k(xd, k);
+    if (!done) {
+      fq_sel(u, ge, d, u);
+      fq_sel(x1, ge, xd, x1);
+      fq_sel(v, ge, v, d);
+      fq_sel(x2, ge, x2, xd);
+    }
+    done = done || limbs_eq<12>(u, one) || limbs_eq<12>(v, one);
+  }
+  Fq x, r3;
+  fq_sel(x, limbs_eq<12>(u, one), x1, x2);
+  limbs_set_const<12>(r3, FQ_R3);
+  fq_mul(r, x, r3);
 }
 
 // f^(p^6 - 1) = conj(f)^2 / N with N = f conj(f) in Fq6 (coefficients 0, 2, 4 = its
@@ -402,7 +477,7 @@ HD void easy_part(Fq2& r, const Fq2& f, const Pos& ps) {
   fq_sqr(t1, d.c1);
   fq_add(nrm, nrm, t1);
   Fq inv;
-  fq_inv_fermat(inv, nrm);
+  fq_inv_binary(inv, nrm);
   Fq2 dinv;
   fq_mul(dinv.c0, d.c0, inv);
   fq_mul(t1, d.c1, inv);

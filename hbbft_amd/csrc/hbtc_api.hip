@@ -308,20 +308,23 @@ int get_keyset(hbtc_ctx* c, uint32_t id, Keyset** ks) {
   return HBTC_OK;
 }
 
-// Decode + line tables for n per-instance G2 arguments (named workspace prefix `tag`).
-int prepare_g2(hbtc_ctx* c, const char* tag, const uint8_t* d_c96, uint32_t n, G2A** aff,
+// Decode + line tables for the per-instance G2 arguments: d0 (n items) and, when d1 is given,
+// d1 (n more) in one launch pair; outputs for d1 start at index n.
+int prepare_g2(hbtc_ctx* c, const uint8_t* d0, const uint8_t* d1, uint32_t n, G2A** aff,
                int32_t** st, Line** lines, hipStream_t on = nullptr) {
   hipStream_t strm = on ? on : c->stream;
-  std::string t(tag);
+  const uint32_t m = d1 ? 2 * n : n;
   Fq2* wsp;
-  HB_TRY(wst(c, (t + ".aff").c_str(), n, aff));
-  HB_TRY(wst(c, (t + ".st").c_str(), n, st));
-  HB_TRY(wst(c, (t + ".lines").c_str(), (size_t)n * MILLER_STEPS, lines));
-  HB_TRY(wst(c, (t + ".ws").c_str(), (size_t)n * 2 * MILLER_STEPS, &wsp));
+  HB_TRY(wst(c, "g2.aff", m, aff));
+  HB_TRY(wst(c, "g2.st", m, st));
+  HB_TRY(wst(c, "g2.lines", (size_t)m * MILLER_STEPS, lines));
+  HB_TRY(wst(c, "g2.ws", (size_t)m * 3 * MILLER_STEPS, &wsp));
   G2A* a = *aff;
   int32_t* s = *st;
   Line* l = *lines;
-  return timed_on(c, strm, "prepare", [&] { return launch_g2_prepare(strm, d_c96, n, a, l, wsp, s); });
+  return timed_on(c, strm, "prepare", [&] {
+    return launch_g2_prepare(strm, d0, n, d1, d1 ? n : 0, a, l, wsp, s);
+  });
 }
 
 // ---------------------------------------------------------------- device-pointer cores
@@ -343,8 +346,10 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   if (c->verify_mode == HBTC_MODE_PER_SHARE) {
     HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
     if (c->last_dec.status == d_status) c->last_dec = {};
-    HB_TRY(prepare_g2(c, "H", d_H, n_ct, &h_aff, &h_st, &h_lines));
-    HB_TRY(prepare_g2(c, "W", d_w, n_ct, &w_aff, &w_st, &w_lines));
+    HB_TRY(prepare_g2(c, d_H, d_w, n_ct, &h_aff, &h_st, &h_lines));
+    w_aff = h_aff + n_ct;
+    w_st = h_st + n_ct;
+    w_lines = h_lines + (size_t)n_ct * MILLER_STEPS;
     HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles));
     return timed(c, "dec_verify", [&] {
       return launch_dec_verify(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n,
@@ -354,8 +359,10 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   // RLC batch verification with hierarchical fallback (hbtc_rlc.hip).  The per-ciphertext G2
   // preparation runs on s_prep concurrently with the item pass; the checks wait for both.
   HB_TRY(stream_after(c, c->s_prep, c->stream, c->ev_main));
-  HB_TRY(prepare_g2(c, "H", d_H, n_ct, &h_aff, &h_st, &h_lines, c->s_prep));
-  HB_TRY(prepare_g2(c, "W", d_w, n_ct, &w_aff, &w_st, &w_lines, c->s_prep));
+  HB_TRY(prepare_g2(c, d_H, d_w, n_ct, &h_aff, &h_st, &h_lines, c->s_prep));
+  w_aff = h_aff + n_ct;
+  w_st = h_st + n_ct;
+  w_lines = h_lines + (size_t)n_ct * MILLER_STEPS;
   HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles));
   RlcKey key;
   for (int i = 0; i < 8; ++i) key.k[i] = c->rd();
@@ -413,7 +420,7 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   G2A* h_aff;
   int32_t* h_st;
   Line* h_lines;
-  HB_TRY(prepare_g2(c, "H", d_H, n_inst, &h_aff, &h_st, &h_lines));
+  HB_TRY(prepare_g2(c, d_H, nullptr, n_inst, &h_aff, &h_st, &h_lines));
   Tile* tiles;
   uint32_t n_tiles;
   HB_TRY(make_tiles(c, n_inst, offsets, &tiles, &n_tiles));
@@ -500,7 +507,8 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
   uint32_t* d_off = static_cast<uint32_t*>(p);
   const uint64_t terms = (uint64_t)n_inst * t;
   uint32_t *d_sel_pos, *d_sel_idx, *d_sel_cnt, *d_dup, *d_bad;
-  Fr* d_lambda;
+  Fr *d_lambda, *d_lws;
+  HB_TRY(wst(c, "comb.lws", terms, &d_lws));
   HB_TRY(wst(c, "comb.sel_pos", terms, &d_sel_pos));
   HB_TRY(wst(c, "comb.sel_idx", terms, &d_sel_idx));
   HB_TRY(wst(c, "comb.sel_cnt", n_inst, &d_sel_cnt));
@@ -513,7 +521,7 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
     hipError_t e = launch_select(sc, n_inst, d_off, t, d_item_status, d_idx, d_sel_pos, d_sel_idx,
                                  d_sel_cnt);
     if (e != hipSuccess) return e;
-    return launch_lagrange_sel(sc, n_inst, t, d_sel_idx, d_lambda, d_dup);
+    return launch_lagrange_sel(sc, n_inst, t, d_sel_idx, d_lambda, d_lws, d_dup);
   }));
   const MsmPlan plan = msm_plan(n_inst, t);
   const size_t pb = group == 1 ? 48 : 96;
@@ -528,8 +536,10 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
     G1A* d_aff;
     HB_TRY(wst(c, "comb.g1", terms, &d_aff));
     HB_TRY(timed_on(c, sc, "comb_decode", [&] {
+      if (dec)  // every selected item is ACCEPTed and was decoded by the verification
+        return launch_msm_gather_g1(sc, n_inst, t, d_sel_pos, d_sel_cnt, dec, d_aff);
       return launch_msm_decode_g1(sc, n_inst, t, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status,
-                                  dec, d_aff, d_bad);
+                                  nullptr, d_aff, d_bad);
     }));
     HB_TRY(msm_run<Fq>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
                        d_inst_status, d_out, nullptr));

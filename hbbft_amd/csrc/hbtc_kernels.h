@@ -64,8 +64,10 @@ hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t*
 
 hipError_t launch_g1_decode(hipStream_t s, const uint8_t* in, uint32_t n, G1A* out,
                             int32_t* status);
-hipError_t launch_g2_prepare(hipStream_t s, const uint8_t* in, uint32_t n, G2A* aff, Line* lines,
-                             Fq2* ws, int32_t* status);
+// Decode + affine-normalised line tables of n0 + n1 G2 arguments (two input arrays, outputs
+// contiguous); ws holds 3 * MILLER_STEPS Fq2 per argument.
+hipError_t launch_g2_prepare(hipStream_t s, const uint8_t* in0, uint32_t n0, const uint8_t* in1,
+                             uint32_t n1, G2A* aff, Line* lines, Fq2* ws, int32_t* status);
 hipError_t launch_dec_verify(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
                              const uint32_t* idx, const uint8_t* shares, const G1A* pk,
                              const int32_t* pk_status, uint32_t n_pk, const G2A* h_aff,
@@ -90,10 +92,13 @@ struct MsmPlan {
 hipError_t launch_select(hipStream_t s, uint32_t n_inst, const uint32_t* offsets, uint32_t t,
                          const int32_t* status, const uint32_t* idx, uint32_t* sel_pos,
                          uint32_t* sel_idx, uint32_t* sel_cnt);
+// lambda: n_inst * t canonical coefficients; ws: n_inst * t Fr of workspace
 hipError_t launch_lagrange_sel(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_idx,
-                               Fr* lambda, uint32_t* dup);
+                               Fr* lambda, Fr* ws, uint32_t* dup);
 hipError_t launch_msm_digits(hipStream_t s, const MsmPlan& p, const uint32_t* scalars,
                              int16_t* digits, uint32_t* list, uint32_t* roff);
+hipError_t launch_msm_gather_g1(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_pos,
+                                const uint32_t* sel_cnt, const G1A* dec, G1A* pts);
 hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
                                 const uint8_t* pts_c, const uint32_t* sel_pos,
                                 const uint32_t* sel_cnt, const int32_t* item_status,

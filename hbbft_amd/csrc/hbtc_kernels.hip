@@ -85,25 +85,60 @@ __global__ void __launch_bounds__(64) k_g1_decode(const uint8_t* __restrict__ in
   status[i] = ok ? HBTC_ACCEPT : HBTC_DECODE_ERR;
 }
 
-// Decode a fixed per-instance G2 argument (H = hash_g2(nonce), or w) and precompute its 68
-// affine-normalised Miller-loop lines (pairing.h).  One lane per instance.
-__global__ void __launch_bounds__(64) k_g2_prepare(const uint8_t* __restrict__ in, uint32_t n,
-                                                   G2A* __restrict__ aff,
-                                                   Line* __restrict__ lines,
-                                                   Fq2* __restrict__ ws,
-                                                   int32_t* __restrict__ status) {
-  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= n) return;
+// Decode the fixed per-instance G2 arguments (H = hash_g2(nonce), and w for ciphertexts) and
+// walk their Miller-loop steps: one lane per argument, both argument sets in ONE launch
+// (in0: n0 items, in1: n1 items; outputs [0, n0) then [n0, n0 + n1)).  The 68 projective
+// lines (A, B, C) go to the workspace; k_g2_norm scales them affine in parallel.
+__global__ void __launch_bounds__(64) k_g2_steps(const uint8_t* __restrict__ in0, uint32_t n0,
+                                                 const uint8_t* __restrict__ in1, uint32_t n1,
+                                                 G2A* __restrict__ aff, Fq2* __restrict__ ws,
+                                                 int32_t* __restrict__ status) {
+  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+  if (g >= n0 + n1) return;
   uint32_t w[24];
-  load_words(w, in, i, 24);
+  load_words(w, g < n0 ? in0 : in1, g < n0 ? g : g - n0, 24);
   G2A q;
   const bool ok = g2_decompress(q, w);
-  aff[i] = q;
-  status[i] = ok ? HBTC_ACCEPT : HBTC_DECODE_ERR;
-  if (ok && !q.inf) {
-    Fq2* cs = ws + (size_t)i * 2 * MILLER_STEPS;
-    g2_precompute_lines_ws(lines + (size_t)i * MILLER_STEPS, cs, cs + MILLER_STEPS, q);
+  aff[g] = q;
+  status[g] = ok ? HBTC_ACCEPT : HBTC_DECODE_ERR;
+  if (!ok || q.inf) return;
+  Fq2* out = ws + (size_t)g * 3 * MILLER_STEPS;
+  G2J T;
+  jac_from_aff(T, q);
+  int j = 0;
+  for (int bit = 62; bit >= 0; --bit) {
+    Fq2 A, B, C;
+    g2_dbl_step(T, A, B, C);
+    out[3 * j] = A;
+    out[3 * j + 1] = B;
+    out[3 * j + 2] = C;
+    ++j;
+    if ((BLS_X_ABS >> bit) & 1ull) {
+      g2_add_step(T, q, A, B, C);
+      out[3 * j] = A;
+      out[3 * j + 1] = B;
+      out[3 * j + 2] = C;
+      ++j;
+    }
   }
+}
+
+// One lane per (argument, step): the affine-normalised line (A / C, B / C) (pairing.h Line).
+__global__ void __launch_bounds__(64) k_g2_norm(uint32_t n, const G2A* __restrict__ aff,
+                                                const int32_t* __restrict__ status,
+                                                const Fq2* __restrict__ ws,
+                                                Line* __restrict__ lines) {
+  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+  if (g >= n * MILLER_STEPS) return;
+  const uint32_t a = g / MILLER_STEPS;
+  if (status[a] != HBTC_ACCEPT || aff[a].inf) return;  // never read: the pair is unused
+  const Fq2* in = ws + (size_t)g * 3;
+  Fq2 ci;
+  fq2_inv(ci, in[2]);
+  Line l;
+  fq2_mul(l.a, in[0], ci);
+  fq2_mul(l.b, in[1], ci);
+  lines[g] = l;
 }
 
 // Fixed-base tables of the key set (PK_TAB_WIN windows of 8 bits): one lane per (share i,
@@ -358,11 +393,16 @@ hipError_t launch_pk_table(hipStream_t s, const G1A* pk, const int32_t* pk_statu
   return hipGetLastError();
 }
 
-hipError_t launch_g2_prepare(hipStream_t s, const uint8_t* in, uint32_t n, G2A* aff, Line* lines,
-                             Fq2* ws, int32_t* status) {
+hipError_t launch_g2_prepare(hipStream_t s, const uint8_t* in0, uint32_t n0, const uint8_t* in1,
+                             uint32_t n1, G2A* aff, Line* lines, Fq2* ws, int32_t* status) {
+  const uint32_t n = n0 + n1;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_g2_prepare, dim3(blocks_for(n, 64)), dim3(64), 0, s, in, n, aff, lines, ws,
+  hipLaunchKernelGGL(k_g2_steps, dim3(blocks_for(n, 64)), dim3(64), 0, s, in0, n0, in1, n1, aff, ws,
                      status);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_g2_norm, dim3(blocks_for((uint64_t)n * MILLER_STEPS, 64)), dim3(64), 0, s, n,
+                     aff, status, ws, lines);
   return hipGetLastError();
 }
 

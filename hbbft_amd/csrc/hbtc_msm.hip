@@ -117,38 +117,101 @@ __global__ void __launch_bounds__(64) k_select(const uint32_t* __restrict__ offs
   if (lane == 0) sel_cnt[k] = cnt;
 }
 
-// lambda_i = prod_{j != i} x_j / (x_j - x_i) over the selected abscissae (dense [k][t]); one lane
-// per (instance, i).  A repeated x sets the instance's duplicate flag (DuplicateEntry).
-__global__ void __launch_bounds__(256) k_lagrange_sel(uint32_t n_inst, uint32_t t,
-                                                      const uint32_t* __restrict__ sel_idx,
-                                                      Fr* __restrict__ lambda,
+// Lagrange coefficients at 0 of the selected x_i = idx_i + 1 (Montgomery Fr), three passes:
+//   k_lagrange_x    x_i in Montgomery form (one lane per term)
+//   k_lagrange_den  q_i = x_i * prod_{j != i} (x_j - x_i): O(t) per term, one lane per term;
+//                   x_j == x_i for j != i is a DuplicateEntry (threshold_crypto interpolate)
+//   k_lagrange_inv  one workgroup per instance: P = prod_j x_j and a batched inversion of the
+//                   q_i (chunk products, one inversion, backward walk), lambda_i = P / q_i
+// (round 1 spent ~1,500 Fr products per coefficient: a conversion inside the O(t) loop and a
+// Fermat inversion per coefficient).
+__global__ void __launch_bounds__(256) k_lagrange_x(uint64_t n, const uint32_t* __restrict__ sel_idx,
+                                                    Fr* __restrict__ x) {
+  const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= n) return;
+  Fr v;
+  fr_from_u64(v, (uint64_t)sel_idx[g] + 1);
+  x[g] = v;
+}
+
+__global__ void __launch_bounds__(256) k_lagrange_den(uint32_t n_inst, uint32_t t,
+                                                      const Fr* __restrict__ x,
+                                                      Fr* __restrict__ q,
                                                       uint32_t* __restrict__ dup) {
   const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (g >= (uint64_t)n_inst * t) return;
   const uint32_t k = (uint32_t)(g / t), i = (uint32_t)(g % t);
-  const uint32_t* ix = sel_idx + (size_t)k * t;
-  const uint32_t xi_raw = ix[i];
-  Fr xi, num, den;
-  fr_from_u64(xi, (uint64_t)xi_raw + 1);
-  limbs_set_const<8>(num, FR_ONE);
+  const Fr* xk = x + (size_t)k * t;
+  const Fr xi = xk[i];
+  Fr den;
   limbs_set_const<8>(den, FR_ONE);
   bool is_dup = false;
   for (uint32_t j = 0; j < t; ++j) {
     if (j == i) continue;
-    const uint32_t xj_raw = ix[j];
-    is_dup |= (xj_raw == xi_raw);
-    Fr xj, d;
-    fr_from_u64(xj, (uint64_t)xj_raw + 1);
-    fr_mul(num, num, xj);
+    const Fr xj = xk[j];
+    is_dup |= limbs_eq<8>(xj, xi);
+    Fr d;
     fr_sub(d, xj, xi);
     fr_mul(den, den, d);
   }
   if (is_dup) atomicOr(&dup[k], 1u);
-  Fr inv, l, lc;
-  fr_inv(inv, den);
-  fr_mul(l, num, inv);
-  fr_from_mont(lc, l);
-  lambda[g] = lc;
+  Fr qi;
+  fr_mul(qi, xi, den);
+  q[g] = qi;
+}
+
+constexpr uint32_t LG_BS = 256;
+__global__ void __launch_bounds__(LG_BS) k_lagrange_inv(uint32_t t, Fr* __restrict__ x,
+                                                        Fr* __restrict__ q_lambda) {
+  __shared__ Fr C[LG_BS];   // product of q over chunk u
+  __shared__ Fr E[LG_BS];   // product of q over the chunks before u
+  __shared__ Fr IE[LG_BS];  // (E[u] * C[u])^-1
+  __shared__ Fr X[LG_BS];   // product of x over chunk u; X[0] then holds P = prod x
+  const uint32_t tid = threadIdx.x;
+  Fr* q = q_lambda + (size_t)blockIdx.x * t;
+  Fr* xw = x + (size_t)blockIdx.x * t;
+  const uint32_t chunk = (t + LG_BS - 1) / LG_BS;
+  const uint32_t lo = min(t, tid * chunk), hi = min(t, lo + chunk);
+  Fr pq, px;
+  limbs_set_const<8>(pq, FR_ONE);
+  limbs_set_const<8>(px, FR_ONE);
+  for (uint32_t i = lo; i < hi; ++i) {
+    fr_mul(px, px, xw[i]);
+    xw[i] = pq;  // x_i is no longer needed: keep q's in-chunk exclusive prefix instead
+    fr_mul(pq, pq, q[i]);
+  }
+  C[tid] = pq;
+  X[tid] = px;
+  __syncthreads();
+  if (tid == 0) {  // 3 * 256 products + one inversion, serial: small next to the O(t^2) pass
+    Fr acc, P;
+    limbs_set_const<8>(acc, FR_ONE);
+    limbs_set_const<8>(P, FR_ONE);
+    for (uint32_t u = 0; u < LG_BS; ++u) {
+      E[u] = acc;
+      fr_mul(acc, acc, C[u]);
+      fr_mul(P, P, X[u]);
+    }
+    Fr run;
+    fr_inv(run, acc);
+    for (int u = LG_BS - 1; u >= 0; --u) {
+      IE[u] = run;
+      fr_mul(run, run, C[u]);
+    }
+    X[0] = P;
+  }
+  __syncthreads();
+  const Fr P = X[0], e = E[tid];
+  Fr inv_incl = IE[tid];  // inverse of the prefix of q through item i (starting at the chunk end)
+  for (uint32_t i = hi; i-- > lo;) {
+    Fr excl, qi_inv, l, lc;
+    fr_mul(excl, e, xw[i]);          // prefix of q before item i
+    fr_mul(qi_inv, inv_incl, excl);  // 1 / q_i
+    fr_mul(inv_incl, inv_incl, q[i]);
+    fr_mul(l, P, qi_inv);            // prod_{j != i} x_j / prod_{j != i} (x_j - x_i)
+    fr_from_mont(lc, l);
+    q[i] = lc;
+  }
 }
 
 // ------------------------------------------------------------------ digits and buckets
@@ -295,6 +358,29 @@ __global__ void __launch_bounds__(64) k_msm_decode(uint32_t n_inst, uint32_t t, 
   }
   out[g] = p;
 }
+
+#if HBTC_IN_PART(8)
+// The selected terms of a combine over VERIFIED items whose decoded form the verification kept
+// (k_rlc_items): a plain gather, no decode and no subgroup check.
+__global__ void __launch_bounds__(256) k_msm_gather(uint32_t n_inst, uint32_t t,
+                                                    const uint32_t* __restrict__ sel_pos,
+                                                    const uint32_t* __restrict__ sel_cnt,
+                                                    const G1A* __restrict__ dec,
+                                                    G1A* __restrict__ out) {
+  const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (uint64_t)n_inst * t) return;
+  const uint32_t k = (uint32_t)(g / t), i = (uint32_t)(g % t);
+  G1A p;
+  if (i < sel_cnt[k]) {
+    p = dec[sel_pos[g]];
+  } else {
+    fzero(p.x);
+    fzero(p.y);
+    p.inf = 1;
+  }
+  out[g] = p;
+}
+#endif  // part 8
 
 // Rank whose bucket holds sorted position p: the largest r < B with ro[r] <= p (ro[0] = 0 and
 // p < ro[B]).
@@ -450,11 +536,17 @@ hipError_t launch_select(hipStream_t s, uint32_t n_inst, const uint32_t* offsets
 }
 
 hipError_t launch_lagrange_sel(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_idx,
-                               Fr* lambda, uint32_t* dup) {
+                               Fr* lambda, Fr* ws, uint32_t* dup) {
   const uint64_t n = (uint64_t)n_inst * t;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_lagrange_sel, dim3(msm_blocks(n, 256)), dim3(256), 0, s, n_inst, t, sel_idx,
-                     lambda, dup);
+  hipLaunchKernelGGL(k_lagrange_x, dim3(msm_blocks(n, 256)), dim3(256), 0, s, n, sel_idx, ws);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_lagrange_den, dim3(msm_blocks(n, 256)), dim3(256), 0, s, n_inst, t, ws, lambda,
+                     dup);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_lagrange_inv, dim3(n_inst), dim3(LG_BS), 0, s, t, ws, lambda);
   return hipGetLastError();
 }
 
@@ -497,6 +589,14 @@ static hipError_t launch_msm_reduce(hipStream_t s, const MsmPlan& p, const Aff<F
 }
 
 #if HBTC_IN_PART(8)
+hipError_t launch_msm_gather_g1(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_pos,
+                                const uint32_t* sel_cnt, const G1A* dec, G1A* pts) {
+  const uint64_t terms = (uint64_t)n_inst * t;
+  if (terms == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_msm_gather, dim3(msm_blocks(terms, 256)), dim3(256), 0, s, n_inst, t, sel_pos,
+                     sel_cnt, dec, pts);
+  return hipGetLastError();
+}
 hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
                                 const uint8_t* pts_c, const uint32_t* sel_pos,
                                 const uint32_t* sel_cnt, const int32_t* item_status,

@@ -108,3 +108,16 @@ def test_gt_pairing_check_infinity_pairs(ht):
                        ((inf1, Q, P, Q), 1)):
         rc, f, e, rs, sf, se = _check(ht, *args, z1=3, z2=5)
         assert rc == want and e == se and rs == (1 if want == 7 else 0)
+
+
+def test_binary_gcd_inversion(ht):
+    """fq_inv_binary (the final exponentiation's one inversion) on edge values and random ones,
+    several lanes at once (lanes finish at different iterations of the wave-uniform loop)."""
+    rng = random.Random(11)
+    vals = [1, 2, B.P - 1, B.P - 2, 3, 1 << 200, (1 << 380) + 1, 0x10000000000000000]
+    vals += [rng.randrange(1, B.P) for _ in range(8)]
+    raw = b"".join(v.to_bytes(48, "big") for v in vals)
+    out = ctypes.create_string_buffer(48 * len(vals))
+    assert ht.ht_fq_inv_binary(len(vals), raw, out) == 0
+    for i, v in enumerate(vals):
+        assert int.from_bytes(out.raw[48 * i:48 * i + 48], "big") == pow(v, -1, B.P), hex(v)
