@@ -84,10 +84,21 @@ def breakdown(ctx, steps, fams):
     return out
 
 
-COIN_FAMS = ["prepare", "sig_verify", "lagrange", "comb_decode", "comb_digits", "combine"]
+COIN_FAMS = ["prepare", "sig_verify", "sig_items", "sig_lines", "chk_tiles", "chk_subs",
+             "chk_leaves", "rlc_finalize", "lagrange", "comb_decode", "comb_digits", "combine"]
 
 
-def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01):
+def corrupt_positions(rng, n, n_inst, frac, mode):
+    """Wrong shares: `uniform` = a fraction of all shares at random; `senders` = the f Byzantine
+    senders (f = (n-1)/3, a random set) sign wrongly in every instance (~33%: BFT's worst case)."""
+    total = n * n_inst
+    if mode == "senders":
+        liars = set(rng.sample(range(n), (n - 1) // 3))
+        return [k * n + i for k in range(n_inst) for i in range(n) if i in liars]
+    return rng.sample(range(total), int(total * frac))
+
+
+def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode="uniform"):
     """c2 / c4: n_inst coin instances x n SignatureShares + n_inst combines (first t verified)."""
     rng = random.Random(SEED + n)
     t0 = time.time()
@@ -102,7 +113,7 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01):
     total = n * n_inst
     scal = [sks[i] * h % R for h in hs for i in range(n)]
     expected = np.zeros(total, np.int32)
-    for j in rng.sample(range(total), int(total * corrupt)):
+    for j in corrupt_positions(rng, n, n_inst, corrupt, corrupt_mode):
         scal[j] = (scal[j] + 1) % R
         expected[j] = N.REJECT
     sigs, st = ctx.g2_mul(G2_GEN, fr_bytes(scal))
@@ -113,28 +124,34 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01):
     for k, arr in (("H", H), ("idx", idx), ("sigs", sigs)):
         d[k] = ctx.dev_alloc(arr.nbytes)
         ctx.dev_upload(d[k], arr)
-    d["status"] = ctx.dev_alloc(4 * total)
-    d["out"] = ctx.dev_alloc(96 * n_inst)
-    d["par"] = ctx.dev_alloc(n_inst)
-    d["cst"] = ctx.dev_alloc(4 * n_inst)
+    for j in range(2):  # alternated per step: epoch k+1 verifies while epoch k combines
+        d["status%d" % j] = ctx.dev_alloc(4 * total)
+        d["out%d" % j] = ctx.dev_alloc(96 * n_inst)
+        d["par%d" % j] = ctx.dev_alloc(n_inst)
+        d["cst%d" % j] = ctx.dev_alloc(4 * n_inst)
     log("%s: setup %.1fs (%d shares)" % (name, time.time() - t0, total))
     lib, h, off = ctx.lib, ctx.h, N._ptr(offsets)
+    cur = [0]
 
     def step():
+        cur[0] ^= 1
+        j = cur[0]
         ctx._check(lib.hbtc_verify_sig_shares_dev(h, ks, n_inst, d["H"], off, d["idx"], d["sigs"],
-                                                  d["status"]), "verify_sig_shares_dev")
-        ctx._check(lib.hbtc_combine_sigs_verified_dev(h, n_inst, off, d["idx"], d["sigs"], d["status"],
-                                                      t, d["out"], d["par"], d["cst"]),
+                                                  d["status%d" % j]), "verify_sig_shares_dev")
+        ctx._check(lib.hbtc_combine_sigs_verified_dev(h, n_inst, off, d["idx"], d["sigs"],
+                                                      d["status%d" % j], t, d["out%d" % j],
+                                                      d["par%d" % j], d["cst%d" % j]),
                    "combine_sigs_verified_dev")
 
     elapsed = timed_steps(ctx, step, steps, warmup)
     per = breakdown(ctx, steps, COIN_FAMS)
+    j = cur[0]
     stv = np.empty(total, np.int32)
-    ctx.dev_download(stv, d["status"])
+    ctx.dev_download(stv, d["status%d" % j])
     out = np.empty(96 * n_inst, np.uint8)
-    ctx.dev_download(out, d["out"])
+    ctx.dev_download(out, d["out%d" % j])
     cst = np.empty(n_inst, np.int32)
-    ctx.dev_download(cst, d["cst"])
+    ctx.dev_download(cst, d["cst%d" % j])
     want, _ = ctx.g2_mul(G2_GEN, fr_bytes([master * hh % R for hh in hs]))
     mism = int((stv != expected).sum())
     comb_ok = bool((cst == 0).all() and bytes(out) == bytes(want))
@@ -149,7 +166,10 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01):
         "value": round(total * steps / elapsed, 1), "unit": "shares/s", "n_gpus": 1,
         "steps": steps, "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 3),
         "higher_is_better": True, "dtype": "u32 (381-bit Montgomery limbs)",
-        "data": "synthetic (seeded key set, shares generated on device; %g%% wrong shares)" % (100 * corrupt),
+        "data": "synthetic (seeded key set, shares generated on device; %s)"
+                % ("%g%% wrong shares" % (100 * corrupt) if corrupt_mode == "uniform"
+                   else "f = %d Byzantine senders sign wrongly in every instance" % ((n - 1) // 3)),
+        "mode": "rlc" if ctx_mode[0] == N.MODE_RLC else "per_share",
         "config": {"workload": "%s: %d coin instances x %d SignatureShares verified + %d G2 combines (t=%d)"
                    % (name, n_inst, n, n_inst, t), "N": n, "t": t, "instances": n_inst},
         "combines_per_s": round(n_inst * steps / elapsed, 2),
@@ -249,6 +269,9 @@ def bench_skg(ctx, n, n_parts, n_distinct, steps, warmup):
     }
 
 
+ctx_mode = [None]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c2,c4,c5")
@@ -257,14 +280,21 @@ def main():
     ap.add_argument("--inst", type=int, default=64, help="c4 coin instances on this GPU")
     ap.add_argument("--parts", type=int, default=1000, help="c5 Parts")
     ap.add_argument("--distinct", type=int, default=4, help="c5 distinct bivariate polynomials")
+    ap.add_argument("--mode", choices=["rlc", "per_share"], default="rlc")
+    ap.add_argument("--corrupt", type=float, default=0.01)
+    ap.add_argument("--corrupt-mode", choices=["uniform", "senders"], default="uniform")
     args = ap.parse_args()
     ctx = N.Context(0)
+    ctx_mode[0] = N.MODE_RLC if args.mode == "rlc" else N.MODE_PER_SHARE
+    ctx.set_verify_mode(ctx_mode[0])
     try:
         for c in args.configs.split(","):
             if c == "c2":
-                out = bench_coins(ctx, "c2", 100, 100, args.steps, args.warmup)
+                out = bench_coins(ctx, "c2", 100, 100, args.steps, args.warmup, args.corrupt,
+                                  args.corrupt_mode)
             elif c == "c4":
-                out = bench_coins(ctx, "c4", 10000, args.inst, args.steps, args.warmup)
+                out = bench_coins(ctx, "c4", 10000, args.inst, args.steps, args.warmup, args.corrupt,
+                                  args.corrupt_mode)
             elif c == "c5":
                 out = bench_skg(ctx, 1000, args.parts, args.distinct, args.steps, args.warmup)
             else:

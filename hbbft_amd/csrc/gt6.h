@@ -197,12 +197,15 @@ HD void sqr(Fq2& f, const Fq2& a, const Pos& ps) {
 }
 
 // f = f * (A + B w^2 + Y w^3) for a Miller-loop line evaluated at a G1 point (scaled by a
-// subfield factor).  A, B in Fq2 and Y in Fq are not materialised: they sit on the lanes that
-// computed them — A = (pa on lane a, pa on lane a+1), B = (pb on lane b, pb on lane b+1),
-// Y = py on lane y — and each term fetches its operand, which keeps a Miller step's live set
-// small.  use = false makes the line 1 (A = 1, B = Y = 0: the caller zeroes pa, pb, py).
-HD void mul_line(Fq2& f, const Fq& pa, uint32_t a, const Fq& pb, uint32_t b, const Fq& py,
-                 uint32_t y, bool use, const Pos& ps) {
+// subfield factor).  The coefficients are not materialised: they sit on the lanes that computed
+// them — B = (pb on lane b, pb on lane b+1), Y = py on lane y (Fq) or (py on y, py on y+1)
+// (Fq2 when Y2) — and A is either (pa on lane a, pa on lane a+1) or, with A_DIRECT, the Fq2
+// value Ad every lane already holds.  Each term fetches its operand, which keeps a Miller
+// step's live set small.  use = false makes the line 1 (A = 1, B = Y = 0: the caller zeroes
+// pa / Ad, pb, py).
+template <bool A_DIRECT, bool Y2>
+HD void mul_line_t(Fq2& f, const Fq& pa, uint32_t a, const Fq2& Ad, const Fq& pb, uint32_t b,
+                   const Fq& py, uint32_t y, bool use, const Pos& ps) {
   const uint32_t k = ps.k;
   Fq2 acc;
   fq2_zero(acc);
@@ -214,12 +217,16 @@ HD void mul_line(Fq2& f, const Fq& pa, uint32_t a, const Fq& pb, uint32_t b, con
     fetch2(x, f, src(ps, fk));
     Fq o0, o1;
     fq_sel(o0, t == 0, pa, t == 1 ? pb : py);
-    fq_sel(o1, t == 0, pa, pb);
+    fq_sel(o1, t == 0, pa, t == 1 ? pb : py);
     const uint32_t l0 = t == 0 ? a : (t == 1 ? b : y);
     fetch(q.c0, o0, src(ps, l0));
-    fetch(q.c1, o1, src(ps, l0 + 1));  // unused for t == 2
-    if (t == 0 && !use) fq_one(q.c0);
-    if (t == 2)  // Y in Fq: two products (t is the same on every lane: a uniform branch)
+    fetch(q.c1, o1, src(ps, l0 + 1));  // unused for an Fq Y
+    if (A_DIRECT && t == 0) q = Ad;
+    if (t == 0 && !use) {
+      fq_one(q.c0);
+      fq_zero(q.c1);
+    }
+    if (!Y2 && t == 2)  // Y in Fq: two products (t is the same on every lane: a uniform branch)
       mul2_fq(z, x, q.c0);
     else
       mul2(z, x, q);
@@ -227,6 +234,11 @@ HD void mul_line(Fq2& f, const Fq& pa, uint32_t a, const Fq& pb, uint32_t b, con
     fq2_add(acc, acc, z);
   }
   f = acc;
+}
+HD void mul_line(Fq2& f, const Fq& pa, uint32_t a, const Fq& pb, uint32_t b, const Fq& py,
+                 uint32_t y, bool use, const Pos& ps) {
+  Fq2 unused;
+  mul_line_t<false, false>(f, pa, a, unused, pb, b, py, y, use, ps);
 }
 
 HD void conj(Fq2& f, const Pos& ps) {
@@ -525,24 +537,29 @@ HD void final_exp(Fq2& out, const Fq2& f, const Pos& ps) {
 }
 
 // ------------------------------------------------------------------------------ Miller loop
-// One G1 argument of a pairing product with a precomputed line table (pairing.h Line: the
-// affine-normalised line a + b xP v + yP v w at step j).  With P Jacobian (X, Y, Z) the
-// line times Z^3 (an Fq factor, removed by the final exponentiation) is
+// One argument of a pairing product.  Either (PROJ = false) a precomputed affine-normalised line
+// table of the G2 argument (pairing.h Line: a + b xP v + yP v w at step j) with the G1 point P
+// Jacobian — the line times Z^3 (an Fq factor, removed by the final exponentiation) is
 //     Z^3 a + (X Z) b w^2 + Y w^3
-// so the loop needs no inversion.  An unused pair (P or Q at infinity) contributes 1.
+// so the loop needs no inversion — or (PROJ = true, second argument only) a projective table of
+// (A, B, C) per step (g2_dbl_step / g2_add_step of a G2 point that varies per check) with the
+// G1 point affine (Z = 1): the line is A + B xP w^2 + C yP w^3.  An unused pair (an argument at
+// infinity) contributes 1.
 struct MillerArg {
-  const Line* lines;  // MILLER_STEPS lines of the G2 argument
-  G1J P;              // the G1 argument (sign already applied)
+  const Line* lines;   // affine-normalised table (PROJ = false)
+  const Fq2* plines;   // projective (A, B, C) table, 3 * MILLER_STEPS Fq2 (PROJ = true)
+  G1J P;               // the G1 argument (sign already applied)
   bool use;
 };
 
-// f = prod_{pairs} f_{|x|,Q}(P), conjugated (x < 0).  Per step the 8 Fq products that scale
-// the two lines run on separate lanes (lane k: product k; lanes 0, 1: products 6, 7).
-HD void miller2(Fq2& f, const MillerArg& m1, const MillerArg& m2, const Pos& ps) {
+// f = prod_{pairs} f_{|x|,Q}(P), conjugated (x < 0).  Per step the 8 Fq products that scale the
+// two lines run on separate lanes (lane k: product k; lanes 0, 1: products 6, 7).
+template <bool PROJ2>
+HD void miller2_t(Fq2& f, const MillerArg& m1, const MillerArg& m2, const Pos& ps) {
   const uint32_t k = ps.k;
-  // per-pair scalars Z^3, X Z, Y (zero when unused: the line becomes 1 below)
-  // lane k's round-1 product: k = 0,1 a1.c{k} Z1^3; 2,3 b1.c{k-2} X1Z1; 4,5 a2.c{k-4} Z2^3.
-  // lanes 0, 1 round 2: b2.c{k} X2Z2.  Lane 0 keeps Y1, the others Y2.
+  // Round-1 product of lane k: k = 0,1 a1.c{k} Z1^3; 2,3 b1.c{k-2} X1Z1; 4,5 a2.c{k-4} Z2^3
+  // (PROJ2: B2.c{k-4} x2).  Lanes 0, 1, round 2: b2.c{k} X2Z2 (PROJ2: C2.c{k} y2).  Lane 0
+  // keeps Y1, the others Y2 (unused with PROJ2).  Unused pairs get zero scalars.
   Fq s1, s2, ymine, zero;
   fq_zero(zero);
   {
@@ -553,15 +570,18 @@ HD void miller2(Fq2& f, const MillerArg& m1, const MillerArg& m2, const Pos& ps)
     fq_mul(z3, z2, P.z);
     fq_mul(xz, P.x, P.z);
     fq_sel(s1, k < 2 || second, z3, xz);
+    if (PROJ2 && second) s1 = m2.P.x;
     fq_sel(s1, second ? m2.use : m1.use, s1, zero);
-    fq_mul(s2, m2.P.x, m2.P.z);
+    if (PROJ2)
+      s2 = m2.P.y;
+    else
+      fq_mul(s2, m2.P.x, m2.P.z);
     fq_sel(s2, m2.use, s2, zero);
     fq_sel(ymine, k == 0, m1.P.y, m2.P.y);
     fq_sel(ymine, k == 0 ? m1.use : m2.use, ymine, zero);
   }
-  const Line* l1c = k < 4 ? m1.lines : m2.lines;
-  const uint32_t c1 = k < 4 ? k : k - 4;       // Fq component of the Line (a.c0 a.c1 b.c0 b.c1)
-  const uint32_t c2 = 2 + (k & 1u);            // round-2 component (b2)
+  const uint32_t c1 = k < 4 ? k : (PROJ2 ? k - 2 : k - 4);  // Fq component: a.c0 a.c1 b.c0 b.c1 / A B C
+  const uint32_t c2 = (PROJ2 ? 4 : 2) + (k & 1u);            // round-2 component (b2 / C2)
   set_one(f, ps);
   int j = 0;
   bool first = true;
@@ -572,24 +592,37 @@ HD void miller2(Fq2& f, const MillerArg& m1, const MillerArg& m2, const Pos& ps)
     for (int rep = 0; rep < (add ? 2 : 1); ++rep) {
       if (rep == 0 && !first) sqr(f, f, ps);
       first = false;
-      const Fq* L1 = reinterpret_cast<const Fq*>(l1c + j);
-      const Fq* L2 = reinterpret_cast<const Fq*>(m2.lines + j);
+      const Fq* L1 = reinterpret_cast<const Fq*>(m1.lines + j);
+      const Fq* L2 = PROJ2 ? reinterpret_cast<const Fq*>(m2.plines + 3 * j)
+                           : reinterpret_cast<const Fq*>(m2.lines + j);
+      const Fq* Lr1 = k < 4 ? L1 : L2;
       Fq p1, p2;
 #pragma unroll 1
       for (uint32_t t = 0; t < 2; ++t) {
         Fq q;
-        fq_mul(q, t == 0 ? L1[c1] : L2[c2], t == 0 ? s1 : s2);
+        fq_mul(q, t == 0 ? Lr1[c1] : L2[c2], t == 0 ? s1 : s2);
         fq_sel(p1, t == 0, q, p1);
         p2 = q;
       }
-      // line 1: A1 = p1@{0,1}, B1 = p1@{2,3}, Y1 = ymine@0; line 2: A2 = p1@{4,5},
-      // B2 = p2@{0,1}, Y2 = ymine@1
+      // line 1: A1 = p1@{0,1}, B1 = p1@{2,3}, Y1 = ymine@0
       mul_line(f, p1, 0, p1, 2, ymine, 0, m1.use, ps);
-      mul_line(f, p1, 4, p2, 0, ymine, 1, m2.use, ps);
+      if (PROJ2) {
+        // line 2: A2 from the table, B2 = p1@{4,5} (B x2), Y2 = p2@{0,1} (C y2)
+        Fq2 A2;
+        A2.c0 = L2[0];
+        A2.c1 = L2[1];
+        mul_line_t<true, true>(f, p1, 0, A2, p1, 4, p2, 0, m2.use, ps);
+      } else {
+        // line 2: A2 = p1@{4,5}, B2 = p2@{0,1}, Y2 = ymine@1
+        mul_line(f, p1, 4, p2, 0, ymine, 1, m2.use, ps);
+      }
       ++j;
     }
   }
   conj(f, ps);
+}
+HD void miller2(Fq2& f, const MillerArg& m1, const MillerArg& m2, const Pos& ps) {
+  miller2_t<false>(f, m1, m2, ps);
 }
 
 }  // namespace gt

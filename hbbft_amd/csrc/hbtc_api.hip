@@ -86,7 +86,8 @@ struct hbtc_ctx {
     const int32_t* status = nullptr;
     const uint8_t* shares = nullptr;
     uint32_t n_items = 0;
-    const G1A* dec = nullptr;
+    const G1A* dec = nullptr;   // DecryptionShares (G1)
+    const G2A* dec2 = nullptr;  // SignatureShares (G2)
   } last_dec;
   int dec_flip = 0;
   std::random_device rd;
@@ -375,7 +376,7 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   HB_TRY(wst(c, c->dec_flip ? "rlc.dec1" : "rlc.dec0", n_items, &dec));
   HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
   HB_TRY(guard_write(c, dec, (size_t)n_items * sizeof(G1A)));
-  c->last_dec = {d_status, d_share, n_items, dec};
+  c->last_dec = {d_status, d_share, n_items, dec, nullptr};
   HB_TRY(wst(c, "rlc.counters", 2, &counters));  // [0] leaves, [1] sub-tile list
   HB_TRY(wst(c, "rlc.sub_list", n_tiles, &sub_list));
   HB_TRY(wst(c, "rlc.leaves", (size_t)2 * n_items, &leaves));
@@ -420,13 +421,78 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   G2A* h_aff;
   int32_t* h_st;
   Line* h_lines;
-  HB_TRY(prepare_g2(c, d_H, nullptr, n_inst, &h_aff, &h_st, &h_lines));
   Tile* tiles;
   uint32_t n_tiles;
+  if (c->verify_mode == HBTC_MODE_PER_SHARE) {
+    HB_TRY(prepare_g2(c, d_H, nullptr, n_inst, &h_aff, &h_st, &h_lines));
+    HB_TRY(make_tiles(c, n_inst, offsets, &tiles, &n_tiles));
+    return timed(c, "sig_verify", [&] {
+      return launch_sig_verify(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->n,
+                               h_aff, h_st, h_lines, d_status);
+    });
+  }
+  // RLC batch verification (hbtc_sig.hip): H's line tables on s_prep beside the item pass; the
+  // G2 sums' projective line tables before each check level.
+  HB_TRY(stream_after(c, c->s_prep, c->stream, c->ev_main));
+  HB_TRY(prepare_g2(c, d_H, nullptr, n_inst, &h_aff, &h_st, &h_lines, c->s_prep));
   HB_TRY(make_tiles(c, n_inst, offsets, &tiles, &n_tiles));
-  return timed(c, "sig_verify", [&] {
-    return launch_sig_verify(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->n,
-                             h_aff, h_st, h_lines, d_status);
+  RlcKey key;
+  for (int i = 0; i < 8; ++i) key.k[i] = c->rd();
+  constexpr uint32_t LEAF_CHUNK = 1u << 15;
+  const size_t n_tables = std::max<size_t>((size_t)16 * n_tiles, LEAF_CHUNK);
+  SigTileSums* sums;
+  G2A* dec;
+  Fq2* tables;
+  uint32_t *inf, *counters, *sub_list, *leaves;
+  HB_TRY(wst(c, "sig.sums", n_tiles, &sums));
+  c->dec_flip ^= 1;
+  HB_TRY(wst(c, c->dec_flip ? "sig.dec1" : "sig.dec0", n_items, &dec));
+  HB_TRY(guard_write(c, dec, (size_t)n_items * sizeof(G2A)));
+  c->last_dec = {d_status, d_sig, n_items, nullptr, dec};
+  HB_TRY(wst(c, "sig.tables", n_tables * PLINES_FQ2, &tables));
+  HB_TRY(wst(c, "sig.inf", n_tables, &inf));
+  HB_TRY(wst(c, "sig.counters", 2, &counters));
+  HB_TRY(wst(c, "sig.sub_list", n_tiles, &sub_list));
+  HB_TRY(wst(c, "sig.leaves", (size_t)2 * n_items, &leaves));
+  uint32_t* leaf_count = counters;
+  uint32_t* sub_count = counters + 1;
+  HB_CHECK(c, hipMemsetAsync(counters, 0, 2 * sizeof(uint32_t), c->stream));
+  HB_TRY(timed(c, "sig_items", [&] {
+    return launch_sig_items(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->tab,
+                            ks->n, key, sums, dec, d_status);
+  }));
+  HB_TRY(timed(c, "sig_lines", [&] {
+    return launch_plines(c->stream, 0, 2 * n_tiles, 0, nullptr, nullptr, tiles, sums, dec, tables,
+                         inf);
+  }));
+  HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
+  HB_TRY(timed(c, "chk_tiles", [&] {
+    return launch_sigchk_tiles(c->stream, n_tiles, tiles, sums, tables, inf, h_aff, h_lines, h_st,
+                               d_status, sub_count, sub_list);
+  }));
+  HB_TRY(timed(c, "sig_lines", [&] {
+    return launch_plines(c->stream, 1, 16 * n_tiles, 0, sub_count, sub_list, tiles, sums, dec,
+                         tables, inf);
+  }));
+  HB_TRY(timed(c, "chk_subs", [&] {
+    return launch_sigchk_subs(c->stream, n_tiles, sub_count, sub_list, tiles, sums, tables, inf,
+                              h_aff, h_lines, d_status, leaf_count, leaves);
+  }));
+  // leaves in chunks: launches past the device-side count exit at once
+  for (uint32_t base = 0; base < n_items; base += LEAF_CHUNK) {
+    const uint32_t chunk = std::min(LEAF_CHUNK, n_items - base);
+    HB_TRY(timed(c, "sig_lines", [&] {
+      return launch_plines(c->stream, 2, chunk, base, leaf_count, leaves, tiles, sums, dec, tables,
+                           inf);
+    }));
+    HB_TRY(timed(c, "chk_leaves", [&] {
+      return launch_sigchk_leaves(c->stream, base, chunk, leaf_count, leaves, d_idx, ks->pk, tables,
+                                  inf, h_aff, h_lines, d_status);
+    }));
+  }
+  c->last_leaf_count = leaf_count;
+  return timed(c, "rlc_finalize", [&] {
+    return launch_rlc_finalize(c->stream, n_tiles, tiles, h_st, h_st, d_status);
   });
 }
 
@@ -547,16 +613,23 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
                                {d_item_status, d_item_status ? (size_t)n_items * 4 : 0},
                                {dec, dec ? n_items * sizeof(G1A) : 0}});
   }
+  const auto& ld = c->last_dec;
+  const G2A* dec2 = (d_item_status && ld.status == d_item_status && ld.shares == d_pts &&
+                     ld.n_items == n_items)
+                        ? ld.dec2
+                        : nullptr;
   G2A* d_aff;
   HB_TRY(wst(c, "comb.g2", terms, &d_aff));
   HB_TRY(timed_on(c, sc, "comb_decode", [&] {
+    if (dec2) return launch_msm_gather_g2(sc, n_inst, t, d_sel_pos, d_sel_cnt, dec2, d_aff);
     return launch_msm_decode_g2(sc, n_inst, t, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status,
                                 nullptr, d_aff, d_bad);
   }));
   HB_TRY(msm_run<Fq2>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
                       d_inst_status, d_out, d_parity));
   return note_comb_reads(c, {{d_idx, (size_t)n_items * 4}, {d_pts, n_items * pb},
-                             {d_item_status, d_item_status ? (size_t)n_items * 4 : 0}});
+                             {d_item_status, d_item_status ? (size_t)n_items * 4 : 0},
+                             {dec2, dec2 ? n_items * sizeof(G2A) : 0}});
 }
 
 int point_mul_host(hbtc_ctx* c, int group, uint32_t n, const uint8_t* base,

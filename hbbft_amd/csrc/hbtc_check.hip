@@ -60,8 +60,8 @@ __device__ __forceinline__ G1J g1j_of(const G1A& a) {
 // e = FE( f_{|x|,H}(S) * f_{|x|,w}(-P) ): the pairing-product value of one group.
 __device__ __forceinline__ void pair_value(Fq2& e, const G1J& S, bool use1, const Line* hl, const G1J& P,
                            bool use2, const Line* wl, const Pos& ps) {
-  gt::MillerArg m1{hl, S, use1};
-  gt::MillerArg m2{wl, P, use2};
+  gt::MillerArg m1{hl, nullptr, S, use1};
+  gt::MillerArg m2{wl, nullptr, P, use2};
   fq_neg(m2.P.y, P.y);
   Fq2 f;
   gt::miller2(f, m1, m2, ps);
@@ -232,6 +232,147 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_leaves(
   if (active && ul.ps.k == 0) status[item] = ok ? HBTC_ACCEPT : HBTC_REJECT;
 }
 
+// ------------------------------------------------------------------------------ SignatureShares
+// e(sum r_i pk_i, H) e(-G1, sum r_i sigma_i) == 1: the first pair over H's precomputed lines,
+// the second over the group's projective line table (hbtc_sig.hip k_plines) at the fixed -G1.
+namespace {
+__device__ __forceinline__ void sig_pair_value(Fq2& e, const G1J& P, bool use1, const Line* hl,
+                                               const Fq2* table, bool use2, const Pos& ps) {
+  G1J ng;
+  fq_set(ng.x, G1_GEN_X);
+  fq_set(ng.y, G1_GEN_Y);
+  fq_neg(ng.y, ng.y);
+  fq_one(ng.z);
+  gt::MillerArg m1{hl, nullptr, P, use1};
+  gt::MillerArg m2{nullptr, table, ng, use2};
+  Fq2 f;
+  gt::miller2_t<true>(f, m1, m2, ps);
+  gt::final_exp(e, f, ps);
+}
+}  // namespace
+
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_tiles(
+    uint32_t n_tiles, const Tile* __restrict__ tiles, const SigTileSums* __restrict__ sums,
+    const Fq2* __restrict__ tables, const uint32_t* __restrict__ inf,
+    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
+    const int32_t* __restrict__ h_status, int32_t* __restrict__ status,
+    uint32_t* __restrict__ sub_count, uint32_t* __restrict__ sub_list) {
+  const UnitLane ul = unit_lane();
+  const uint32_t t = blockIdx.x * UNITS_PER_WAVE + ul.unit;
+  const bool active = ul.unit < UNITS_PER_WAVE && t < n_tiles;
+  uint32_t k = 0, first = 0, count = 0, g = 0;
+  bool inst_ok = false, inf2 = true;
+  G1J P;
+  jac_set_inf(P);
+  if (active) {
+    const Tile tile = tiles[t];
+    k = tile.inst;
+    first = tile.first;
+    count = tile.count;
+    inst_ok = h_status[k] == HBTC_ACCEPT;
+    P = ul.side ? sums[t].PW[8] : sums[t].P[8];
+    g = 2 * t + ul.side;
+    inf2 = inf[g] != 0;
+  }
+  const bool use1 = inst_ok && !jac_is_inf(P) && !h_aff[k].inf;
+  const bool use2 = inst_ok && !inf2;
+  Fq2 e, T, Tw;
+  sig_pair_value(e, P, use1, h_lines + (size_t)k * MILLER_STEPS, tables + (size_t)g * PLINES_FQ2,
+                 use2, ul.ps);
+  const bool pass = unit_values(T, Tw, e, ul);
+  const bool fail = active && inst_ok && !pass;
+  const int32_t loc = locate(T, Tw, count, 5, fail, ul);
+  if (!fail || ul.side != 0 || ul.ps.k != 0) return;
+  if (loc >= 0 && status[first + loc] == HBTC_RLC_PENDING) {
+    status[first + loc] = HBTC_REJECT;
+    return;
+  }
+  sub_list[atomicAdd(sub_count, 1u)] = t;
+}
+
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_subs(
+    const uint32_t* __restrict__ sub_count, const uint32_t* __restrict__ sub_list,
+    const Tile* __restrict__ tiles, const SigTileSums* __restrict__ sums,
+    const Fq2* __restrict__ tables, const uint32_t* __restrict__ inf,
+    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
+    int32_t* __restrict__ status, uint32_t* __restrict__ leaf_count,
+    uint32_t* __restrict__ leaves) {
+  const uint32_t n_units = *sub_count * 8u;
+  if (blockIdx.x * UNITS_PER_WAVE >= n_units) return;
+  const UnitLane ul = unit_lane();
+  const uint32_t u = blockIdx.x * UNITS_PER_WAVE + ul.unit;
+  bool active = ul.unit < UNITS_PER_WAVE && u < n_units;
+  uint32_t k = 0, lo = 0, hi = 0, g = 0;
+  bool inf2 = true;
+  G1J P;
+  jac_set_inf(P);
+  if (active) {
+    const uint32_t t = sub_list[u >> 3], sub = u & 7u;
+    const Tile tile = tiles[t];
+    k = tile.inst;
+    lo = tile.first + sub * 8u;
+    hi = min(tile.first + tile.count, lo + 8u);
+    active = lo < hi;
+    if (active) {
+      P = ul.side ? sums[t].PW[sub] : sums[t].P[sub];
+      g = 16u * (u >> 3) + 2u * sub + ul.side;  // k_plines mode 1 numbering
+      inf2 = inf[g] != 0;
+    }
+  }
+  const bool use1 = active && !jac_is_inf(P) && !h_aff[k].inf;
+  const bool use2 = active && !inf2;
+  Fq2 e, T, Tw;
+  sig_pair_value(e, P, use1, h_lines + (size_t)k * MILLER_STEPS, tables + (size_t)g * PLINES_FQ2,
+                 use2, ul.ps);
+  const bool pass = unit_values(T, Tw, e, ul);
+  const bool fail = active && !pass;
+  const int32_t loc = locate(T, Tw, hi - lo, 2, fail, ul);
+  if (!fail || ul.side != 0 || ul.ps.k != 0) return;
+  if (loc >= 0 && status[lo + loc] == HBTC_RLC_PENDING) {
+    status[lo + loc] = HBTC_REJECT;
+    return;
+  }
+  for (uint32_t i = lo; i < hi; ++i)
+    if (status[i] == HBTC_RLC_PENDING) {
+      const uint32_t pos = atomicAdd(leaf_count, 1u);
+      leaves[2 * pos] = i;
+      leaves[2 * pos + 1] = k;
+    }
+}
+
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_leaves(
+    uint32_t base, uint32_t chunk, const uint32_t* __restrict__ leaf_count,
+    const uint32_t* __restrict__ leaves,
+    const uint32_t* __restrict__ idx, const G1A* __restrict__ pk,
+    const Fq2* __restrict__ tables, const uint32_t* __restrict__ inf,
+    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
+    int32_t* __restrict__ status) {
+  // leaves [base, base + chunk) of the list; tables are numbered from the chunk start
+  const uint32_t c = *leaf_count;
+  const uint32_t n = c > base ? min(c - base, chunk) : 0u;
+  if (blockIdx.x * 2 * UNITS_PER_WAVE >= n) return;
+  const UnitLane ul = unit_lane();
+  const uint32_t g = (blockIdx.x * UNITS_PER_WAVE + ul.unit) * 2u + ul.side;
+  const bool active = ul.unit < UNITS_PER_WAVE && g < n;
+  uint32_t item = 0, k = 0;
+  bool inf2 = true;
+  G1J P;
+  jac_set_inf(P);
+  if (active) {
+    item = leaves[2 * (base + g)];
+    k = leaves[2 * (base + g) + 1];
+    P = g1j_of(pk[idx[item]]);
+    inf2 = inf[g] != 0;
+  }
+  const bool use1 = active && !jac_is_inf(P) && !h_aff[k].inf;
+  const bool use2 = active && !inf2;
+  Fq2 e;
+  sig_pair_value(e, P, use1, h_lines + (size_t)k * MILLER_STEPS,
+                 tables + (size_t)(active ? g : 0) * PLINES_FQ2, use2, ul.ps);
+  const bool ok = gt::is_one(e, ul.ps);
+  if (active && ul.ps.k == 0) status[item] = ok ? HBTC_ACCEPT : HBTC_REJECT;
+}
+
 // ------------------------------------------------------------------------------ launchers
 static inline uint32_t unit_blocks(uint64_t units) {
   return (uint32_t)((units + UNITS_PER_WAVE - 1) / UNITS_PER_WAVE);
@@ -268,6 +409,39 @@ hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t*
   if (max_leaves == 0) return hipSuccess;
   hipLaunchKernelGGL(k_chk_leaves, dim3(unit_blocks(((uint64_t)max_leaves + 1) / 2)), dim3(64), 0,
                      s, leaf_count, leaves, idx, dec, pk, h_aff, h_lines, w_aff, w_lines, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_sigchk_tiles(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                               const SigTileSums* sums, const Fq2* tables, const uint32_t* inf,
+                               const G2A* h_aff, const Line* h_lines, const int32_t* h_status,
+                               int32_t* status, uint32_t* sub_count, uint32_t* sub_list) {
+  if (n_tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sigchk_tiles, dim3(unit_blocks(n_tiles)), dim3(64), 0, s, n_tiles, tiles, sums,
+                     tables, inf, h_aff, h_lines, h_status, status, sub_count, sub_list);
+  return hipGetLastError();
+}
+
+hipError_t launch_sigchk_subs(hipStream_t s, uint32_t max_tiles, const uint32_t* sub_count,
+                              const uint32_t* sub_list, const Tile* tiles,
+                              const SigTileSums* sums, const Fq2* tables, const uint32_t* inf,
+                              const G2A* h_aff, const Line* h_lines, int32_t* status,
+                              uint32_t* leaf_count, uint32_t* leaves) {
+  if (max_tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sigchk_subs, dim3(unit_blocks((uint64_t)max_tiles * 8)), dim3(64), 0, s,
+                     sub_count, sub_list, tiles, sums, tables, inf, h_aff, h_lines, status,
+                     leaf_count, leaves);
+  return hipGetLastError();
+}
+
+hipError_t launch_sigchk_leaves(hipStream_t s, uint32_t base, uint32_t chunk,
+                                const uint32_t* leaf_count, const uint32_t* leaves,
+                                const uint32_t* idx, const G1A* pk, const Fq2* tables,
+                                const uint32_t* inf, const G2A* h_aff, const Line* h_lines,
+                                int32_t* status) {
+  if (chunk == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sigchk_leaves, dim3(unit_blocks(((uint64_t)chunk + 1) / 2)), dim3(64), 0, s,
+                     base, chunk, leaf_count, leaves, idx, pk, tables, inf, h_aff, h_lines, status);
   return hipGetLastError();
 }
 

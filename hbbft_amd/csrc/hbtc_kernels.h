@@ -30,6 +30,17 @@ struct TileSums {
   G1J PW[9];  // sum pos_i r_i pk_i
 };
 
+// Partial sums of one tile of SignatureShares (hbtc_sig.hip): S = sum r_i sigma_i in G2 and
+// P = sum r_i pk_i in G1, plain and position-weighted, [0..7] sub-tiles and [8] the tile.
+struct SigTileSums {
+  G2J S[9];
+  G2J SW[9];
+  G1J P[9];
+  G1J PW[9];
+};
+// Projective line table of a G2 point (pairing.h g2_proj_lines): 3 Fq2 per Miller step.
+constexpr uint32_t PLINES_FQ2 = 3 * MILLER_STEPS;
+
 // Fixed-base table of every public-key share (built once per key set, resident in HBM):
 // tab[(i * PK_TAB_WIN + w) * 256 + v] = v * 2^(8w) * pk_i (affine, v >= 1), so [a] pk_i for a
 // 32-bit a is PK_TAB_WIN = 4 mixed additions and no doublings.
@@ -61,6 +72,33 @@ hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t*
                              const uint32_t* leaves, const uint32_t* idx, const G1A* dec,
                              const G1A* pk, const G2A* h_aff, const Line* h_lines,
                              const G2A* w_aff, const Line* w_lines, int32_t* status);
+
+// ---- RLC batch verification of SignatureShares (hbtc_sig.hip, checks in hbtc_check.hip)
+hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
+                            const uint8_t* sigs, const G1A* pk, const int32_t* pk_status,
+                            const PtXY* pk_tab, uint32_t n_pk, RlcKey key, SigTileSums* sums,
+                            G2A* dec, int32_t* status);
+// Projective line tables of the G2 sums the next check level needs: mode 0 every tile
+// (2 per tile: plain, weighted), mode 1 the 8 sub-tiles of the listed tiles (16 per listed
+// tile), mode 2 the listed leaf shares (decoded sigma).  inf[g] = 1: the sum is infinity.
+// (mode 2 handles leaves [base, base + max_groups) of the list: chunks bound the tables)
+hipError_t launch_plines(hipStream_t s, int mode, uint32_t max_groups, uint32_t base,
+                         const uint32_t* count, const uint32_t* list, const Tile* tiles,
+                         const SigTileSums* sums, const G2A* dec, Fq2* tables, uint32_t* inf);
+hipError_t launch_sigchk_tiles(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                               const SigTileSums* sums, const Fq2* tables, const uint32_t* inf,
+                               const G2A* h_aff, const Line* h_lines, const int32_t* h_status,
+                               int32_t* status, uint32_t* sub_count, uint32_t* sub_list);
+hipError_t launch_sigchk_subs(hipStream_t s, uint32_t max_tiles, const uint32_t* sub_count,
+                              const uint32_t* sub_list, const Tile* tiles,
+                              const SigTileSums* sums, const Fq2* tables, const uint32_t* inf,
+                              const G2A* h_aff, const Line* h_lines, int32_t* status,
+                              uint32_t* leaf_count, uint32_t* leaves);
+hipError_t launch_sigchk_leaves(hipStream_t s, uint32_t base, uint32_t chunk,
+                                const uint32_t* leaf_count, const uint32_t* leaves,
+                                const uint32_t* idx, const G1A* pk, const Fq2* tables,
+                                const uint32_t* inf, const G2A* h_aff, const Line* h_lines,
+                                int32_t* status);
 
 hipError_t launch_g1_decode(hipStream_t s, const uint8_t* in, uint32_t n, G1A* out,
                             int32_t* status);
@@ -99,6 +137,8 @@ hipError_t launch_msm_digits(hipStream_t s, const MsmPlan& p, const uint32_t* sc
                              int16_t* digits, uint32_t* list, uint32_t* roff);
 hipError_t launch_msm_gather_g1(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_pos,
                                 const uint32_t* sel_cnt, const G1A* dec, G1A* pts);
+hipError_t launch_msm_gather_g2(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_pos,
+                                const uint32_t* sel_cnt, const G2A* dec, G2A* pts);
 hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
                                 const uint8_t* pts_c, const uint32_t* sel_pos,
                                 const uint32_t* sel_cnt, const int32_t* item_status,

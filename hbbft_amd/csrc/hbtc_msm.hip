@@ -361,16 +361,17 @@ __global__ void __launch_bounds__(64) k_msm_decode(uint32_t n_inst, uint32_t t, 
 
 #if HBTC_IN_PART(8)
 // The selected terms of a combine over VERIFIED items whose decoded form the verification kept
-// (k_rlc_items): a plain gather, no decode and no subgroup check.
+// (k_rlc_items / k_sig_items): a plain gather, no decode and no subgroup check.
+template <class A>
 __global__ void __launch_bounds__(256) k_msm_gather(uint32_t n_inst, uint32_t t,
                                                     const uint32_t* __restrict__ sel_pos,
                                                     const uint32_t* __restrict__ sel_cnt,
-                                                    const G1A* __restrict__ dec,
-                                                    G1A* __restrict__ out) {
+                                                    const A* __restrict__ dec,
+                                                    A* __restrict__ out) {
   const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (g >= (uint64_t)n_inst * t) return;
   const uint32_t k = (uint32_t)(g / t), i = (uint32_t)(g % t);
-  G1A p;
+  A p;
   if (i < sel_cnt[k]) {
     p = dec[sel_pos[g]];
   } else {
@@ -380,6 +381,10 @@ __global__ void __launch_bounds__(256) k_msm_gather(uint32_t n_inst, uint32_t t,
   }
   out[g] = p;
 }
+template __global__ void k_msm_gather<G1A>(uint32_t, uint32_t, const uint32_t*, const uint32_t*,
+                                           const G1A*, G1A*);
+template __global__ void k_msm_gather<G2A>(uint32_t, uint32_t, const uint32_t*, const uint32_t*,
+                                           const G2A*, G2A*);
 #endif  // part 8
 
 // Rank whose bucket holds sorted position p: the largest r < B with ro[r] <= p (ro[0] = 0 and
@@ -589,13 +594,23 @@ static hipError_t launch_msm_reduce(hipStream_t s, const MsmPlan& p, const Aff<F
 }
 
 #if HBTC_IN_PART(8)
-hipError_t launch_msm_gather_g1(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_pos,
-                                const uint32_t* sel_cnt, const G1A* dec, G1A* pts) {
+template <class A>
+static hipError_t launch_msm_gather(hipStream_t s, uint32_t n_inst, uint32_t t,
+                                    const uint32_t* sel_pos, const uint32_t* sel_cnt, const A* dec,
+                                    A* pts) {
   const uint64_t terms = (uint64_t)n_inst * t;
   if (terms == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_msm_gather, dim3(msm_blocks(terms, 256)), dim3(256), 0, s, n_inst, t, sel_pos,
-                     sel_cnt, dec, pts);
+  hipLaunchKernelGGL((k_msm_gather<A>), dim3(msm_blocks(terms, 256)), dim3(256), 0, s, n_inst, t,
+                     sel_pos, sel_cnt, dec, pts);
   return hipGetLastError();
+}
+hipError_t launch_msm_gather_g1(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_pos,
+                                const uint32_t* sel_cnt, const G1A* dec, G1A* pts) {
+  return launch_msm_gather(s, n_inst, t, sel_pos, sel_cnt, dec, pts);
+}
+hipError_t launch_msm_gather_g2(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_pos,
+                                const uint32_t* sel_cnt, const G2A* dec, G2A* pts) {
+  return launch_msm_gather(s, n_inst, t, sel_pos, sel_cnt, dec, pts);
 }
 hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
                                 const uint8_t* pts_c, const uint32_t* sel_pos,

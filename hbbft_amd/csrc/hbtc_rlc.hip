@@ -30,7 +30,7 @@
 // Work per share in the honest case: decode + r_i d_i (a joint 32-bit double-and-add through
 // the GLV endomorphism) + r_i pk_i (8 mixed additions from the key set's fixed-base table) + a
 // share of the wave's reduction tree; the pairing work is per group.
-#include "hbtc_kernels.h"
+#include "rlc_common.h"
 
 #ifndef HBTC_PART
 #define HBTC_PART 0
@@ -39,117 +39,8 @@
 
 namespace hbtc {
 
-__device__ __forceinline__ void rlc_load_words(uint32_t* w, const uint8_t* base, size_t item,
-                                               int nwords) {
-  const uint4* q = reinterpret_cast<const uint4*>(base + item * (size_t)(nwords * 4));
-  for (int i = 0; i < nwords / 4; ++i) {
-    const uint4 v = q[i];
-    w[4 * i] = v.x;
-    w[4 * i + 1] = v.y;
-    w[4 * i + 2] = v.z;
-    w[4 * i + 3] = v.w;
-  }
-}
-
-// ChaCha20 block (RFC 8439 layout: constants, 8 key words, counter, 3 nonce words) -> the
-// two 32-bit words [2j, 2j+1] of block `ctr`, combined into the 64-bit scalar r_i.
-__device__ __forceinline__ uint32_t rotl32(uint32_t x, int s) { return (x << s) | (x >> (32 - s)); }
-__device__ uint64_t rlc_scalar(const RlcKey& key, uint64_t item) {
-  uint32_t st[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
-                     key.k[0], key.k[1], key.k[2], key.k[3], key.k[4], key.k[5], key.k[6], key.k[7],
-                     (uint32_t)(item >> 3), (uint32_t)(item >> 35), 0x68626266u, 0x72726c63u};
-  uint32_t x[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) x[i] = st[i];
-#define QR(a, b, c, d)                 \
-  x[a] += x[b];                        \
-  x[d] = rotl32(x[d] ^ x[a], 16);      \
-  x[c] += x[d];                        \
-  x[b] = rotl32(x[b] ^ x[c], 12);      \
-  x[a] += x[b];                        \
-  x[d] = rotl32(x[d] ^ x[a], 8);       \
-  x[c] += x[d];                        \
-  x[b] = rotl32(x[b] ^ x[c], 7);
-#pragma unroll 1
-  for (int r = 0; r < 10; ++r) {
-    QR(0, 4, 8, 12) QR(1, 5, 9, 13) QR(2, 6, 10, 14) QR(3, 7, 11, 15)
-    QR(0, 5, 10, 15) QR(1, 6, 11, 12) QR(2, 7, 8, 13) QR(3, 4, 9, 14)
-  }
-#undef QR
-  const int j = (int)(item & 7);
-  uint32_t lo = 0, hi = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if (i == j) {
-      lo = x[2 * i] + st[2 * i];
-      hi = x[2 * i + 1] + st[2 * i + 1];
-    }
-  return ((uint64_t)hi << 32) | lo;
-}
-
 #if HBTC_IN_PART(6)
 // ------------------------------------------------------------------------------ per item
-// Tree reduction of the per-lane points q over the wave (lane = position in the tile): the sum
-// A and the position-weighted sum B of every aligned group of 8 (-> outA/outB[0..7]) and of the
-// tile (-> [8]).  Merging halves of size s:  A = A_l + A_r,  B = B_l + B_r + s A_r.
-__device__ void rlc_reduce(G1J* redA, G1J* redB, const G1J& q, uint32_t lane, G1J* outA,
-                           G1J* outB) {
-  G1J z;
-  jac_set_inf(z);
-  redA[lane] = q;
-  redB[lane] = z;
-  __syncthreads();
-  for (uint32_t s = 1; s < 64; s <<= 1) {
-    if ((lane & (2 * s - 1)) == 0) {
-      G1J a = redA[lane], ar = redA[lane + s];
-      G1J b = redB[lane], br = redB[lane + s];
-      jac_add(b, b, br);
-      G1J sa = ar;
-      for (uint32_t d = 1; d < s; d <<= 1) jac_dbl(sa, sa);
-      jac_add(b, b, sa);
-      jac_add(a, a, ar);
-      redA[lane] = a;
-      redB[lane] = b;
-    }
-    __syncthreads();
-    if (s == 4 && (lane & 7) == 0) {
-      outA[lane >> 3] = redA[lane];
-      outB[lane >> 3] = redB[lane];
-    }
-  }
-  if (lane == 0) {
-    outA[8] = redA[0];
-    outB[8] = redB[0];
-  }
-  __syncthreads();  // the arrays are reused by the next reduction
-}
-
-// [a] pk + [b] phi(pk) from the key set's fixed-base table (8 mixed additions, no doublings).
-__device__ void rlc_pk_mul(G1J& r, const PtXY* __restrict__ tab, uint32_t a, uint32_t b) {
-  jac_set_inf(r);
-#pragma unroll
-  for (int w = 0; w < PK_TAB_WIN; ++w) {
-    const uint32_t va = (a >> (8 * w)) & 0xffu, vb = (b >> (8 * w)) & 0xffu;
-    if (va) {
-      const PtXY e = tab[w * 256 + va];
-      G1A q;
-      q.x = e.x;
-      q.y = e.y;
-      q.inf = 0;
-      jac_add_aff(r, r, q);
-    }
-    if (vb) {
-      const PtXY e = tab[w * 256 + vb];
-      G1A q, pq;
-      q.x = e.x;
-      q.y = e.y;
-      q.inf = 0;
-      g1_phi(pq, q);
-      jac_add_aff(r, r, pq);
-    }
-  }
-}
-
 // One wave per tile: decode every share, draw r_i = a_i + b_i mu (a_i, b_i the two 32-bit
 // halves of a ChaCha20 word, mu the eigenvalue of the GLV endomorphism phi: 2^64 distinct
 // residues mod r), compute r_i d_i = [a] d + [b] phi(d) (joint 32-bit

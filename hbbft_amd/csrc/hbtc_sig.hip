@@ -1,0 +1,160 @@
+// Random-linear-combination batch verification of SignatureShares — the fast path behind
+// hbtc_verify_sig_shares (PublicKeyShare::verify, /root/reference/src/coin.rs:151, called once
+// per share by the reference; every share of a coin instance signs the same nonce, so
+// H = hash_g2(nonce) is one G2 point per instance: SURVEY.md §3.1's batching lever).
+//
+// Share i of instance k is valid iff E_i = e(pk_i, H) e(-G1, sigma_i) == 1.  For a group G:
+//     every share valid  =>  e(sum_G r_i pk_i, H) * e(-G1, sum_G r_i sigma_i) == prod E_i^r_i == 1
+// with r_i = a_i + b_i mu drawn as in hbtc_rlc.hip (mu = -x^2 mod r, the eigenvalue of phi on
+// G1 and of -psi^2 on G2, so r_i pk_i comes from the fixed-base table and r_i sigma_i =
+// [a] sigma + [b] (-psi^2(sigma)) is a joint 32-bit double-and-add in G2).  Location of a single
+// wrong share (position-weighted sums), the 64 -> 8 -> 1 split and the probability bounds are
+// those of the DecryptionShare path.
+//
+// The G2 argument of the second pair varies per group, so its Miller-loop lines are computed
+// per group (k_plines: one lane walks the 68 steps of the affine sum, projective (A, B, C) per
+// step) and evaluated at the fixed point -G1 by the cooperative check (gt6.h miller2_t<true>).
+#include "gt6.h"
+#include "rlc_common.h"
+
+namespace hbtc {
+
+// -psi^2(q) = [mu] q on G2 (psi has eigenvalue x, mu = -x^2)
+__device__ __forceinline__ void g2_mu(G2A& r, const G2A& q) {
+  G2A t;
+  g2_psi(t.x, t.y, q);
+  t.inf = q.inf;
+  g2_psi(r.x, r.y, t);
+  fq2_neg(r.y, r.y);
+  r.inf = q.inf;
+}
+
+#ifndef HBTC_SIG_ITEMS_WAVES
+#define HBTC_SIG_ITEMS_WAVES 2
+#endif
+// One wave per tile: decode every SignatureShare (zcash compressed G2 + subgroup check), r_i,
+// r_i sigma_i, r_i pk_i, then the plain and weighted tile / sub-tile sums in both groups.
+__global__ void __launch_bounds__(64, HBTC_SIG_ITEMS_WAVES) k_sig_items(
+    const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
+    const uint8_t* __restrict__ sigs, const G1A* __restrict__ pk,
+    const int32_t* __restrict__ pk_status, const PtXY* __restrict__ pk_tab, uint32_t n_pk,
+    RlcKey key, SigTileSums* __restrict__ sums, G2A* __restrict__ dec,
+    int32_t* __restrict__ status) {
+  __shared__ G2J red2[2][64];  // reused for the G1 reduction
+  G1J* red1 = reinterpret_cast<G1J*>(&red2[0][0]);
+  const Tile tile = tiles[blockIdx.x];
+  const uint32_t lane = threadIdx.x;
+  const size_t item = (size_t)tile.first + lane;
+  G2J S;
+  G1J P;
+  jac_set_inf(S);
+  jac_set_inf(P);
+  if (lane < tile.count) {
+    int32_t st = HBTC_RLC_PENDING;
+    const uint32_t id = idx[item];
+    if (id >= n_pk) {
+      st = HBTC_UNKNOWN_SENDER;
+    } else if (pk_status[id] != HBTC_ACCEPT) {
+      st = HBTC_DECODE_ERR;
+    } else {
+      uint32_t w[24];
+      rlc_load_words(w, sigs, item, 24);
+      G2A sg;
+      if (!g2_decompress(sg, w)) {
+        st = HBTC_DECODE_ERR;
+      } else {
+        dec[item] = sg;  // for the exact leaf checks and the combine (no second decode)
+        const uint64_t r = rlc_scalar(key, item);
+        const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
+        G2A ms;
+        g2_mu(ms, sg);
+        jac_mul2_u32(S, sg, ra, ms, rb);
+        if (!pk[id].inf) rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb);
+      }
+    }
+    status[item] = st;
+  }
+  SigTileSums* ts = sums + blockIdx.x;
+  rlc_reduce<Fq2>(red2[0], red2[1], S, lane, ts->S, ts->SW);
+  rlc_reduce<Fq>(red1, red1 + 64, P, lane, ts->P, ts->PW);
+}
+
+// Projective line table of one G2 sum: affine (one Fq2 inversion) then the 68 steps.
+__device__ __forceinline__ void g2j_plines(Fq2* out, uint32_t* inf, const G2J& S) {
+  if (jac_is_inf(S)) {
+    *inf = 1;
+    return;
+  }
+  *inf = 0;
+  Fq nrm, t, ni;
+  fq_sqr(nrm, S.z.c0);
+  fq_sqr(t, S.z.c1);
+  fq_add(nrm, nrm, t);
+  gt::fq_inv_binary(ni, nrm);
+  Fq2 zi, zi2, zi3;
+  fq_mul(zi.c0, S.z.c0, ni);
+  fq_mul(t, S.z.c1, ni);
+  fq_neg(zi.c1, t);
+  fq2_sqr(zi2, zi);
+  fq2_mul(zi3, zi2, zi);
+  G2A Q;
+  fq2_mul(Q.x, S.x, zi2);
+  fq2_mul(Q.y, S.y, zi3);
+  Q.inf = 0;
+  g2_proj_lines(out, Q);
+}
+
+__global__ void __launch_bounds__(64) k_plines(int mode, uint32_t max_groups, uint32_t base,
+                                               const uint32_t* __restrict__ count,
+                                               const uint32_t* __restrict__ list,
+                                               const Tile* __restrict__ tiles,
+                                               const SigTileSums* __restrict__ sums,
+                                               const G2A* __restrict__ dec,
+                                               Fq2* __restrict__ tables,
+                                               uint32_t* __restrict__ inf) {
+  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+  // mode 2: leaves [base, base + max_groups) of the list (chunks keep the tables bounded)
+  const uint32_t c = mode == 0 ? 0u : *count;
+  const uint32_t n = mode == 0 ? max_groups
+                   : mode == 1 ? c * 16u
+                               : (c > base ? min(c - base, max_groups) : 0u);
+  if (g >= n) return;
+  G2J S;
+  if (mode == 0) {
+    const uint32_t t = g >> 1;
+    S = (g & 1u) ? sums[t].SW[8] : sums[t].S[8];
+  } else if (mode == 1) {
+    const uint32_t t = list[g >> 4], sub = (g >> 1) & 7u;
+    const Tile tile = tiles[t];
+    if (sub * 8u >= tile.count)
+      jac_set_inf(S);
+    else
+      S = (g & 1u) ? sums[t].SW[sub] : sums[t].S[sub];
+  } else {
+    jac_from_aff(S, dec[list[2 * (base + g)]]);
+  }
+  g2j_plines(tables + (size_t)g * PLINES_FQ2, inf + g, S);
+}
+
+static inline uint32_t sig_blocks(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
+
+hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
+                            const uint8_t* sigs, const G1A* pk, const int32_t* pk_status,
+                            const PtXY* pk_tab, uint32_t n_pk, RlcKey key, SigTileSums* sums,
+                            G2A* dec, int32_t* status) {
+  if (n_tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sig_items, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk, pk_status,
+                     pk_tab, n_pk, key, sums, dec, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_plines(hipStream_t s, int mode, uint32_t max_groups, uint32_t base,
+                         const uint32_t* count, const uint32_t* list, const Tile* tiles,
+                         const SigTileSums* sums, const G2A* dec, Fq2* tables, uint32_t* inf) {
+  if (max_groups == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_plines, dim3(sig_blocks(max_groups, 64)), dim3(64), 0, s, mode, max_groups,
+                     base, count, list, tiles, sums, dec, tables, inf);
+  return hipGetLastError();
+}
+
+}  // namespace hbtc

@@ -78,6 +78,22 @@ HD void g2_add_step(G2J& T, const G2A& Q, Fq2& A, Fq2& B, Fq2& C) {
   jac_add_aff(T, T, Q);
 }
 
+// The 68 projective lines (A, B, C) of a G2 point Q (not infinity), 3 Fq2 per step: the line at
+// an affine G1 point (x, y) is A + B x v + C y v w (gt6.h miller2_t<true> evaluates them).
+HD void g2_proj_lines(Fq2* out, const G2A& Q) {
+  G2J T;
+  jac_from_aff(T, Q);
+  int j = 0;
+  for (int bit = 62; bit >= 0; --bit) {
+    g2_dbl_step(T, out[3 * j], out[3 * j + 1], out[3 * j + 2]);
+    ++j;
+    if ((BLS_X_ABS >> bit) & 1ull) {
+      g2_add_step(T, Q, out[3 * j], out[3 * j + 1], out[3 * j + 2]);
+      ++j;
+    }
+  }
+}
+
 // Precompute the 68 affine-normalised lines of a G2 point Q (not infinity): one pass of
 // projective steps, then Montgomery's batched inversion of the 68 C values.  `Cs` and `pre`
 // are MILLER_STEPS-entry workspaces (global memory on the device, so no per-lane private

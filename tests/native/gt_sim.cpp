@@ -246,7 +246,7 @@ int ht_gt_check(const uint8_t* p1, const uint8_t* q1, const uint8_t* p2, const u
   std::mutex mu;
   run_lanes(12, [&](uint32_t l) {
     const gt::Pos ps = gt::pos();
-    gt::MillerArg a{l1, J1, use1}, b{l2, J2, use2};
+    gt::MillerArg a{l1, nullptr, J1, use1}, b{l2, nullptr, J2, use2};
     Fq2 f, e;
     if (l < 6)
       gt::miller2(f, a, b, ps);
@@ -272,6 +272,52 @@ int ht_gt_check(const uint8_t* p1, const uint8_t* q1, const uint8_t* p2, const u
   fq12_store(out_f576, F);
   fq12_store(out_e576, E);
   return (same ? 1 : 0) | (one0 ? 2 : 0) | (one1 ? 4 : 0);
+}
+
+// Signature-share form of the check on 6 simulated lanes: e(P1, Q1) e(-G1, Q2) with Q1's
+// affine-normalised lines (P1 Jacobian-scaled by z1) and Q2's PROJECTIVE lines evaluated at
+// the fixed affine -G1 (gt6.h miller2_t<true>).  Outputs the final value (tower layout);
+// returns 1 if it is one, 0 if not, -1 on a decode error.
+int ht_gt_check_proj(const uint8_t* p1, const uint8_t* q1, const uint8_t* q2, const uint8_t* z1,
+                     uint8_t* out_e576) {
+  G1A P1;
+  G2A Q1, Q2;
+  if (!decode_g1(P1, p1) || !decode_g2(Q1, q1) || !decode_g2(Q2, q2)) return -1;
+  static Line l1[MILLER_STEPS];
+  static Fq2 pl[3 * MILLER_STEPS];
+  if (!Q1.inf) g2_precompute_lines(l1, Q1);
+  if (!Q2.inf) g2_proj_lines(pl, Q2);
+  G1J J1, NG;
+  jac_from_aff(J1, P1);
+  if (!P1.inf) {
+    Fq z, zz2, zz3;
+    fq_load_be(z, z1);
+    fq_sqr(zz2, z);
+    fq_mul(zz3, zz2, z);
+    fq_mul(J1.x, P1.x, zz2);
+    fq_mul(J1.y, P1.y, zz3);
+    J1.z = z;
+  }
+  fq_set(NG.x, G1_GEN_X);
+  fq_set(NG.y, G1_GEN_Y);
+  fq_neg(NG.y, NG.y);
+  fq_one(NG.z);
+  Fq12 E;
+  bool one = false;
+  std::mutex mu;
+  run_lanes(6, [&](uint32_t l) {
+    const gt::Pos ps = gt::pos();
+    gt::MillerArg a{l1, nullptr, J1, !P1.inf && !Q1.inf}, b{nullptr, pl, NG, !Q2.inf};
+    Fq2 f, e;
+    gt::miller2_t<true>(f, a, b, ps);
+    gt::final_exp(e, f, ps);
+    const bool o = gt::is_one(e, ps);
+    std::lock_guard<std::mutex> lk(mu);
+    *tower_slot(E, flat_to_tower(ps.k)) = e;
+    one = o;
+  });
+  fq12_store(out_e576, E);
+  return one ? 1 : 0;
 }
 
 // The serial reference: miller_loop_2 with the same line tables, then the final exponentiation.

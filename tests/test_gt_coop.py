@@ -121,3 +121,21 @@ def test_binary_gcd_inversion(ht):
     assert ht.ht_fq_inv_binary(len(vals), raw, out) == 0
     for i, v in enumerate(vals):
         assert int.from_bytes(out.raw[48 * i:48 * i + 48], "big") == pow(v, -1, B.P), hex(v)
+
+
+def test_gt_check_projective_second_pair(ht):
+    """SignatureShare form: e(pk, H) e(-G1, sigma) with sigma's lines projective (A, B, C) at
+    the fixed affine -G1 — equal to the serial check's final value, accept and reject."""
+    rng = random.Random(12)
+    sk, h = rng.randrange(1, B.R), rng.randrange(1, B.R)
+    pk = B.g1_compress(B.g1_mul(B.G1_GEN, sk))
+    H = B.g2_compress(B.g2_mul(B.G2_GEN, h))
+    sig = B.g2_compress(B.g2_mul(B.G2_GEN, sk * h % B.R))
+    bad = B.g2_compress(B.g2_mul(B.G2_GEN, (sk * h + 7) % B.R))
+    g1 = B.g1_compress(B.G1_GEN)
+    for s2, want in ((sig, 1), (bad, 0)):
+        e = ctypes.create_string_buffer(576)
+        rc = ht.ht_gt_check_proj(pk, H, s2, rng.randrange(1, B.P).to_bytes(48, "big"), e)
+        sf, se = ctypes.create_string_buffer(576), ctypes.create_string_buffer(576)
+        rs = ht.ht_serial_check(pk, H, g1, s2, sf, se)
+        assert rc == want and rs == want and e.raw == se.raw
