@@ -58,7 +58,11 @@ $(BUILD)/hbtc_api.o: $(CSRC)/hbtc_api.hip $(HDRS) | $(BUILD)
 $(BUILD)/hbtc_hash.o: $(CSRC)/hbtc_hash.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(KOBJS) $(BUILD)/hbtc_api.o $(BUILD)/hbtc_hash.o
+# host-only C++ over the public ABI (no device code)
+$(BUILD)/hbtc_node.o: $(CSRC)/hbtc_node.cpp include/hbtc.h | $(BUILD)
+	g++ -O2 -std=c++17 -fPIC -pthread -Wall -Iinclude -c $< -o $@
+
+$(LIB): $(KOBJS) $(BUILD)/hbtc_api.o $(BUILD)/hbtc_hash.o $(BUILD)/hbtc_node.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
 # per-kernel VGPR / scratch / occupancy report (one part at a time: make resources PART=2)

@@ -12,16 +12,25 @@ HBM when the timed region starts; decode + subgroup checks are inside it.  ~1% o
 corrupted (valid points, wrong share) and a few carry invalid encodings; decisions are checked
 against the construction after timing.
 
-Multi-GPU (weak scaling): one process per GPU (torch.distributed.run), each rank verifies its
-own epoch shard of 1000 ciphertexts (shards are independent, SURVEY.md §8e: no data-path
-collective); gloo carries the barrier and the max-over-ranks time only.
+Multi-GPU (strong scaling, the default for --gpus N > 1): one process per GPU
+(torch.distributed.run), the SAME C3 epoch split over the ranks by hbtc_shard_instances (whole
+ciphertexts, balanced by share count; hbbft_amd/shard.py): every rank verifies and combines its
+ciphertexts, then one RCCL all-gather over xGMI merges the verdicts and combined points into the
+whole epoch's arrays on every rank (the north star's only collective), ordered behind the
+library's streams with hbtc_stream_wait_ctx.  The merged epoch is checked against the
+construction after timing.  --scaling weak runs an independent 1000-ciphertext epoch per rank
+instead (no collective).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with "roofline" (the longest
 critical-path kernel of the default RLC mode; Fqm counted by tools/fqm_count.cpp ->
-bench/roofline_constants.json; HBM traffic from the committed PMC passes) and
-"cpu_baseline" (the oracle's threshold_crypto restatement timed on this host).
+bench/roofline_constants.json; HBM traffic from the committed PMC passes), "cpu_baseline" (the
+oracle's threshold_crypto restatement timed on this host), and at N = 1 two more measured
+lines: "adversarial" (f = 333 Byzantine senders send wrong shares on every ciphertext, BFT's
+worst case) and "host_buffers" (the same epoch through the host-buffer entry points: H2D of
+the compressed shares and D2H of the verdicts inside the timed region).
 """
 import argparse
+import ctypes
 import json
 import os
 import random
@@ -57,10 +66,17 @@ def scalars_bytes(vals):
 
 
 class Epoch:
-    """Synthetic C3 epoch for one rank, generated on the GPU with the library's batched scalar
-    multiplication (setup, outside the timed region)."""
+    """Synthetic C3 epoch, generated on the GPU with the library's batched scalar multiplication
+    (setup, outside the timed region).  Every ciphertext k's data derives from (seed, k) alone,
+    so a rank holding ciphertexts [a, b) of a sharded epoch has exactly the rows the one-GPU
+    epoch has there; the key set and the corruption pattern are global.
 
-    def __init__(self, ctx, n, n_ct, seed, corrupt_frac=0.01):
+    corrupt_mode "uniform": round(corrupt * n) wrong shares (valid points, wrong scalar) in every
+    ciphertext; "senders": the f Byzantine senders send wrong shares on every ciphertext.  Plus 8
+    shares of the whole epoch with an invalid encoding."""
+
+    def __init__(self, ctx, n, n_ct, seed, corrupt_frac=0.01, corrupt_mode="uniform", ct_range=None,
+                 out_alloc=None):
         rng = random.Random(seed)
         self.n, self.n_ct = n, n_ct
         self.f = (n - 1) // 3
@@ -73,84 +89,152 @@ class Epoch:
             for c in reversed(coeffs):
                 acc = (acc * (i + 1) + c) % R
             sks.append(acc)
+        liars = set(rng.sample(range(n), self.f)) if corrupt_mode == "senders" else set()
+        enc_bad = set(rng.sample(range(n * n_ct), 8))
+        a, b = ct_range or (0, n_ct)
+        self.a, self.b = a, b
         pk, st = ctx.g1_mul(G1_GEN, scalars_bytes(sks))
         assert not st.any()
         self.keyset, bad = ctx.keyset_load(pk)
         assert bad == 0
-        rs = [rng.randrange(1, R) for _ in range(n_ct)]
-        hs = [rng.randrange(1, R) for _ in range(n_ct)]
+        rs, hs = [], []
+        for k in range(a, b):
+            rk = random.Random(seed * 1000003 + k)
+            rs.append(rk.randrange(1, R))
+            hs.append(rk.randrange(1, R))
         self.rs = rs
         H, _ = ctx.g2_mul(G2_GEN, scalars_bytes(hs))
         w, _ = ctx.g2_mul(G2_GEN, scalars_bytes([r * h % R for r, h in zip(rs, hs)]))
         u, _ = ctx.g1_mul(G1_GEN, scalars_bytes(rs))
+        self.H, self.w = H, w
         self.pk_bytes = [bytes(pk[48 * i:48 * i + 48]) for i in range(n)]
-        self.u_bytes = [bytes(u[48 * k:48 * k + 48]) for k in range(n_ct)]
-        self.w_bytes = [bytes(w[96 * k:96 * k + 96]) for k in range(n_ct)]
-        total = n * n_ct
-        scal = [sks[i] * rs[k] % R for k in range(n_ct) for i in range(n)]
-        # corruption: wrong shares (valid points) and bad encodings anywhere; the combine takes
-        # the first t VERIFIED shares of every ciphertext, as hbbft does
+        self.u_bytes = [bytes(u[48 * k:48 * k + 48]) for k in range(b - a)]
+        self.w_bytes = [bytes(w[96 * k:96 * k + 96]) for k in range(b - a)]
+        m = b - a
+        total = n * m
+        scal = [sks[i] * r % R for r in rs for i in range(n)]
         self.expected = np.zeros(total, np.int32)
-        n_bad = int(total * corrupt_frac)
-        cand = rng.sample(range(total), min(total, n_bad + 8))
-        wrong, enc = cand[:n_bad], cand[n_bad:n_bad + 8]
-        for j in wrong:
-            scal[j] = (scal[j] + 1) % R
-            self.expected[j] = N.REJECT
+        n_wrong = int(round(n * corrupt_frac)) if corrupt_mode == "uniform" else 0
+        for kk in range(m):
+            k = a + kk
+            wrong = liars or random.Random(seed * 1000003 + k + 0x5EED).sample(range(n), n_wrong)
+            for i in wrong:
+                j = kk * n + i
+                scal[j] = (scal[j] + 1) % R
+                self.expected[j] = N.REJECT
         shares, st = ctx.g1_mul(G1_GEN, scalars_bytes(scal))
         assert not st.any()
         shares = shares.reshape(total, 48)
-        for j in enc:
-            shares[j, 0] &= 0x7F  # clear the compression flag: pairing 0.14 rejects it
-            self.expected[j] = N.DECODE_ERR
+        for g in enc_bad:
+            if a * n <= g < b * n:
+                shares[g - a * n, 0] &= 0x7F  # clear the compression flag: pairing 0.14 rejects it
+                self.expected[g - a * n] = N.DECODE_ERR
         self.offsets = np.arange(0, total + 1, n, dtype=np.uint32)
-        idx = np.tile(np.arange(n, dtype=np.uint32), n_ct)
+        self.idx = np.tile(np.arange(n, dtype=np.uint32), m)
         # resident device copies
         self.d = {}
-        for name, arr in (("H", H), ("w", w), ("idx", idx), ("shares", shares.reshape(-1))):
+        for name, arr in (("H", H), ("w", w), ("idx", self.idx), ("shares", shares.reshape(-1))):
             p = ctx.dev_alloc(arr.nbytes)
             ctx.dev_upload(p, arr)
             self.d[name] = p
         # two sets of outputs, alternated per step: epoch k+1's verification writes one status
-        # array while epoch k's combine still reads the other (hbtc.h ordering rules)
+        # array while epoch k's combine (and its gather) still reads the other (hbtc.h ordering)
+        alloc = out_alloc or (lambda nbytes, i32: (ctx.dev_alloc(nbytes), None))
+        self.out = []
         for j in range(2):
-            self.d["status%d" % j] = ctx.dev_alloc(4 * total)
-            self.d["g%d" % j] = ctx.dev_alloc(48 * n_ct)
-            self.d["cst%d" % j] = ctx.dev_alloc(4 * n_ct)
+            self.out.append({name: alloc(nb, i32) for name, nb, i32 in
+                             (("status", 4 * total, True), ("g", 48 * m, False), ("cst", 4 * m, True))})
         self.cur = 0
+        self.m = m
         self.total = total
         self.host_shares = shares
 
+    def ptr(self, j, name):
+        return self.out[j][name][0]
+
     def step(self, ctx):
-        """One epoch: the 10^6 share checks, then the 1000 combines of the first t VERIFIED
-        shares of every ciphertext (PublicKeySet::decrypt over ThresholdDecryption's verified
-        share map, td.rs:184).  The combines run on the library's combine stream behind this
-        epoch's verification, so they overlap the NEXT epoch's verification (pipelined epochs);
-        the timed region ends when the last combine is done."""
+        """One epoch: the share checks, then the combines of the first t VERIFIED shares of
+        every ciphertext (PublicKeySet::decrypt over ThresholdDecryption's verified share map,
+        td.rs:184).  The combines run on the library's combine stream behind this epoch's
+        verification, so they overlap the NEXT epoch's verification (pipelined epochs)."""
         lib, h, d = ctx.lib, ctx.h, self.d
         self.cur ^= 1
         j = self.cur
         off = N._ptr(self.offsets)
-        ctx._check(lib.hbtc_verify_dec_shares_dev(h, self.keyset, self.n_ct, d["H"], d["w"], off,
-                                                  d["idx"], d["shares"], d["status%d" % j]),
+        ctx._check(lib.hbtc_verify_dec_shares_dev(h, self.keyset, self.m, d["H"], d["w"], off,
+                                                  d["idx"], d["shares"], self.ptr(j, "status")),
                    "verify_dec_shares_dev")
-        ctx._check(lib.hbtc_combine_dec_verified_dev(h, self.n_ct, off, d["idx"], d["shares"],
-                                                     d["status%d" % j], self.t, d["g%d" % j],
-                                                     d["cst%d" % j]),
+        ctx._check(lib.hbtc_combine_dec_verified_dev(h, self.m, off, d["idx"], d["shares"],
+                                                     self.ptr(j, "status"), self.t, self.ptr(j, "g"),
+                                                     self.ptr(j, "cst")),
                    "combine_dec_verified_dev")
 
-    def check(self, ctx):
-        j = self.cur  # the last step's outputs
+    def results(self, ctx, j=None):
+        """(status, g, cst) of the last step (host arrays)."""
+        j = self.cur if j is None else j
         st = np.empty(self.total, np.int32)
-        ctx.dev_download(st, self.d["status%d" % j])
-        mism = int((st != self.expected).sum())
-        g = np.empty(48 * self.n_ct, np.uint8)
-        ctx.dev_download(g, self.d["g%d" % j])
-        cst = np.empty(self.n_ct, np.int32)
-        ctx.dev_download(cst, self.d["cst%d" % j])
+        g = np.empty(48 * self.m, np.uint8)
+        cst = np.empty(self.m, np.int32)
+        for arr, name in ((st, "status"), (g, "g"), (cst, "cst")):
+            ctx.dev_download(arr, self.ptr(j, name))
+        return st, g, cst
+
+    def want_g(self, ctx):
         want, _ = ctx.g1_mul(G1_GEN, scalars_bytes([self.master_sk * r % R for r in self.rs]))
-        comb_ok = bool((cst == 0).all() and bytes(g) == bytes(want))
+        return want
+
+    def check(self, ctx):
+        st, g, cst = self.results(ctx)
+        mism = int((st != self.expected).sum())
+        comb_ok = bool((cst == 0).all() and bytes(g) == bytes(self.want_g(ctx)))
         return mism, comb_ok, int((st == N.ACCEPT).sum())
+
+    def free(self, ctx):
+        for p in self.d.values():
+            ctx.dev_free(p)
+        for o in self.out:
+            for p, t in o.values():
+                if t is None:
+                    ctx.dev_free(p)
+        ctx.keyset_free(self.keyset)
+
+
+class StrongGather:
+    """The merge of a sharded epoch: after a rank's verification + combines, one all-gather of
+    the statuses, combined points and combine statuses (RCCL over xGMI; hbbft_amd/shard.py).
+    Gathers of output set j run on torch stream j, ordered after the library's streams
+    (hbtc_stream_wait_ctx); the library writes output set j again only after stream j's gather
+    has read it (hbtc_ctx_wait_stream)."""
+
+    def __init__(self, ep, dist, slices, torch):
+        self.ep, self.dist, self.torch = ep, dist, torch
+        self.len_items = [hi - lo for _, (lo, hi) in slices]
+        self.len_cts = [b - a for (a, b), _ in slices]
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.streams = [torch.cuda.Stream(dev) for _ in range(2)]
+        tot_items, tot_cts = sum(self.len_items), sum(self.len_cts)
+        self.all = [{"status": torch.empty(tot_items, dtype=torch.int32, device=dev),
+                     "g": torch.empty((tot_cts, 48), dtype=torch.uint8, device=dev),
+                     "cst": torch.empty(tot_cts, dtype=torch.int32, device=dev)} for _ in range(2)]
+
+    def before_step(self, ctx):
+        ctx.ctx_wait_stream(self.streams[self.ep.cur ^ 1].cuda_stream)
+
+    def after_step(self, ctx):
+        from hbbft_amd import shard
+        j = self.ep.cur
+        s = self.streams[j]
+        ctx.stream_wait_ctx(s.cuda_stream)
+        out = self.ep.out[j]
+        with self.torch.cuda.stream(s):
+            shard.gather_slices(self.dist, out["status"][1], self.len_items, out=self.all[j]["status"])
+            shard.gather_slices(self.dist, out["g"][1].view(-1, 48), self.len_cts, out=self.all[j]["g"])
+            shard.gather_slices(self.dist, out["cst"][1], self.len_cts, out=self.all[j]["cst"])
+
+    def merged(self):
+        self.torch.cuda.synchronize()
+        a = self.all[self.ep.cur]
+        return a["status"].cpu().numpy(), a["g"].cpu().numpy().reshape(-1), a["cst"].cpu().numpy()
 
 
 def cpu_baseline(ep, budget_s):
@@ -168,20 +252,78 @@ def cpu_baseline(ep, budget_s):
 
 
 def rank_seed(rank):
-    """Seed of a rank's epoch shard: ranks verify disjoint, independently generated epochs
-    (weak scaling, SURVEY.md §8e: no shared state besides the read-only key set)."""
+    """Seed of a rank's epoch under --scaling weak: ranks verify disjoint, independently
+    generated epochs (no shared state besides the read-only key set)."""
     return SEED + 7919 * rank
 
 
-def max_over_ranks(elapsed, dist):
-    """The job's time: barrier, then the MAX of the ranks' timed regions (gloo all-reduce)."""
+def max_over_ranks(elapsed, dist, device=None):
+    """The job's time: barrier, then the MAX of the ranks' timed regions (all-reduce on the
+    process group's backend: host tensor for gloo, device tensor for RCCL)."""
     if dist is None:
         return elapsed
     import torch
     dist.barrier()
-    tt = torch.tensor([elapsed], dtype=torch.float64)
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     return float(tt.item())
+
+
+FAMS = ["dec_verify", "rlc_items", "chk_tiles", "chk_subs", "chk_leaves", "rlc_finalize",
+        "lagrange", "comb_decode", "comb_digits", "combine", "prepare"]
+
+
+def timed(ctx, ep, steps, warmup, dist=None, gather=None, sync_all=None):
+    """W untimed steps, then exactly K steps bracketed by barrier + device syncs."""
+    def run():
+        if gather:
+            gather.before_step(ctx)
+        ep.step(ctx)
+        if gather:
+            gather.after_step(ctx)
+
+    def fence():
+        ctx.sync()
+        if sync_all:
+            sync_all()
+
+    ctx.timing_enable(True)
+    for _ in range(warmup):
+        run()
+    fence()
+    ctx.timing_reset()
+    if dist:
+        dist.barrier()
+    fence()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    fence()
+    return time.perf_counter() - t0
+
+
+def host_buffer_line(ctx, ep, steps):
+    """The epoch through the host-buffer entry points (what an FFI caller holding wire bytes
+    does): hbtc_verify_dec_shares (H2D of shares + idx, verification, D2H of the statuses), the
+    first t ACCEPTed shares of every ciphertext picked on the host, hbtc_combine_dec (H2D of
+    those shares, combine, D2H of the points)."""
+    sh = ep.host_shares.reshape(-1)
+    m, n = ep.m, ep.n
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        st = ctx.verify_dec_shares(ep.keyset, ep.H, ep.w, None, ep.idx, sh, offsets=ep.offsets)
+        acc = (st == N.ACCEPT).reshape(m, n)
+        sel = acc & (np.cumsum(acc, axis=1) <= ep.t)
+        counts = sel.sum(axis=1)
+        flat = sel.reshape(-1)
+        g, cst = ctx.combine_dec(counts, ep.idx[flat], ep.host_shares[flat].reshape(-1), ep.t)
+    elapsed = time.perf_counter() - t0
+    ok = bool((st == ep.expected).all() and (cst == 0).all()
+              and b"".join(g) == bytes(ep.want_g(ctx)))
+    return {"value": round(ep.total * steps / elapsed, 1), "unit": "shares/s",
+            "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "results_ok": ok,
+            "path": "hbtc_verify_dec_shares + hbtc_combine_dec (host buffers: H2D of compressed "
+                    "shares/idx and D2H of statuses/points inside the timed region)"}
 
 
 def main():
@@ -189,62 +331,89 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=1000, help="validators N (f = (N-1)/3)")
-    ap.add_argument("--cts", type=int, default=1000, help="ciphertexts per epoch per GPU")
+    ap.add_argument("--validators", dest="n", type=int, default=1000, help="validators N (f = (N-1)/3)")
+    ap.add_argument("--cts", type=int, default=1000,
+                    help="ciphertexts per epoch (strong: of the whole job; weak: per GPU)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the adversarial / host-buffer lines")
     ap.add_argument("--mode", choices=["rlc", "per_share"], default="rlc",
                     help="rlc: batched random-linear-combination checks with exact fallback "
                          "(default); per_share: one pairing check per share")
     ap.add_argument("--corrupt", type=float, default=0.01, help="fraction of wrong shares")
+    ap.add_argument("--corrupt-mode", choices=["uniform", "senders"], default="uniform")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend of the merge (nccl = RCCL over xGMI; gloo only to "
+                         "rehearse the sharded path with several ranks on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    strong = args.scaling == "strong" and world > 1
+    dist, torch, dev = None, None, None
     if world > 1:
+        import torch
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        local = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     ctx = N.Context(local)
     t0 = time.time()
     ctx.set_verify_mode(N.MODE_RLC if args.mode == "rlc" else N.MODE_PER_SHARE)
-    ep = Epoch(ctx, args.n, args.cts, rank_seed(rank), corrupt_frac=args.corrupt)
+    gather, slices = None, None
+    if strong:
+        from hbbft_amd import shard
+        offsets_all = np.arange(0, args.n * args.cts + 1, args.n, dtype=np.uint32)
+        slices = shard.instance_slices(world, offsets_all)
+
+        def out_alloc(nbytes, i32):
+            tns = torch.zeros(nbytes // 4 if i32 else nbytes, dtype=torch.int32 if i32 else torch.uint8,
+                              device=dev)
+            return ctypes.c_void_p(tns.data_ptr()), tns
+        ep = Epoch(ctx, args.n, args.cts, SEED, args.corrupt, args.corrupt_mode,
+                   ct_range=slices[rank][0], out_alloc=out_alloc)
+        gather = StrongGather(ep, dist, slices, torch)
+    else:
+        ep = Epoch(ctx, args.n, args.cts, SEED if world == 1 else rank_seed(rank), args.corrupt,
+                   args.corrupt_mode)
     log("rank %d: setup %.1fs (%d shares)" % (rank, time.time() - t0, ep.total))
 
-    ctx.timing_enable(True)
-    for _ in range(args.warmup):
-        ep.step(ctx)
-    ctx.sync()
-    ctx.timing_reset()
-    if dist:
-        dist.barrier()
-    ctx.sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ep.step(ctx)
-    ctx.sync()
-    elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(elapsed, dist)
-    fams = ["dec_verify", "rlc_items", "chk_tiles", "chk_subs", "chk_leaves", "rlc_finalize",
-            "lagrange", "comb_decode", "comb_digits", "combine", "prepare"]
-    breakdown = {f: ctx.timing_read(f) for f in fams}
+    elapsed = timed(ctx, ep, args.steps, args.warmup, dist, gather,
+                    torch.cuda.synchronize if torch else None)
+    elapsed = max_over_ranks(elapsed, dist, dev if args.backend == "nccl" else None)
+    breakdown = {f: ctx.timing_read(f) for f in FAMS}
     leaves = ctx.rlc_last_leaves() if args.mode == "rlc" else ep.total
-    mism, comb_ok, n_acc = ep.check(ctx)
+    if strong:
+        # the merged whole epoch on every rank, against the whole epoch's construction
+        st, g, cst = gather.merged()
+        expected = np.concatenate([np.asarray(x) for x in _all_expected(dist, ep, torch, dev, slices)])
+        want, _ = ctx.g1_mul(G1_GEN, scalars_bytes(_all_master_r(args, ep)))
+        mism = int((st != expected).sum())
+        comb_ok = bool((cst == 0).all() and bytes(g) == bytes(want))
+        n_acc = int((st == N.ACCEPT).sum())
+    else:
+        mism, comb_ok, n_acc = ep.check(ctx)
     log("rank %d: %.3fs for %d steps; kernel ms/step %s; leaves %d; mismatches %d, combine ok %s"
         % (rank, elapsed, args.steps,
-           {f: round(breakdown[f][0] / args.steps, 1) for f in fams if breakdown[f][1]}, leaves,
+           {f: round(breakdown[f][0] / args.steps, 1) for f in FAMS if breakdown[f][1]}, leaves,
            mism, comb_ok))
     if mism or not comb_ok:
         raise SystemExit("rank %d: results differ from the construction (%d mismatches, combine %s)"
                          % (rank, mism, comb_ok))
 
-    shares_total = ep.total * world * args.steps
-    value = shares_total / elapsed
-    combines = args.cts * world * args.steps / elapsed
+    job_shares = args.n * args.cts * (1 if args.scaling == "strong" else world)
+    job_cts = args.cts * (1 if args.scaling == "strong" else world)
+    value = job_shares * args.steps / elapsed
+    combines = job_cts * args.steps / elapsed
     consts = json.load(open(os.path.join(ROOT, "bench", "roofline_constants.json")))
-    n_tiles = sum((ep.n + 63) // 64 for _ in range(ep.n_ct))
+    n_tiles = ep.m * ((ep.n + 63) // 64)
     # algorithmic Fqm per launch of each kernel family (tools/fqm_count.cpp)
     fqm_per_launch = {
         "dec_verify": consts["dec_share"]["total"] * ep.total,
@@ -253,9 +422,9 @@ def main():
         # the cooperative kernel issues more lane-level work than this)
         "chk_tiles": consts["rlc_group_check"] * 2 * n_tiles,
         "chk_leaves": consts["dec_share"]["total"] * leaves,
-        "combine": consts.get("g1_msm_combine", 0) * ep.n_ct,
+        "combine": consts.get("g1_msm_combine", 0) * ep.m,
     }
-    per_step = {f: round(breakdown[f][0] / args.steps, 3) for f in fams if breakdown[f][1]}
+    per_step = {f: round(breakdown[f][0] / args.steps, 3) for f in FAMS if breakdown[f][1]}
     # The dominant kernel is chosen among the main-stream (critical-path) families: the
     # combine runs concurrently on its own stream, so its event span includes the time it
     # shares the CUs with the verify chain and is not a launch duration.
@@ -272,6 +441,12 @@ def main():
         pmc = json.load(open(pmc_path)).get("hbtc::" + KERNEL_NAME[dom], {})
         if "hbm_read_bytes" in pmc and "hbm_write_bytes" in pmc:
             traffic = pmc["hbm_read_bytes"] + pmc["hbm_write_bytes"]
+    if strong:
+        par = "strong: one epoch sharded by whole ciphertexts over %d GPU(s) (hbtc_shard_instances), RCCL all-gather of statuses + combined points" % world
+    elif world > 1:
+        par = "weak: an independent epoch per GPU (%d GPUs), no collective" % world
+    else:
+        par = "1 GPU"
     out = {
         "metric": "verified BLS12-381 shares/sec (whole node) at N=1000; combines/sec",
         "value": round(value, 1),
@@ -281,20 +456,21 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.scaling == "strong" else "weak",
         "vs_baseline": None,
         "dtype": "u32 (381-bit Montgomery limbs)",
-        "data": "synthetic (seeded key set, shares generated on device; %g%% wrong shares + 8 bad encodings)"
-                % (100 * args.corrupt),
-        "config": {"workload": "C3 HoneyBadger epoch: %d ciphertexts x %d DecryptionShares verified + %d G1 combines (t=%d) per GPU"
-                   % (args.cts, args.n, args.cts, ep.t),
-                   "N": args.n, "f": ep.f, "t": ep.t, "ciphertexts_per_gpu": args.cts,
-                   "shares_per_step": ep.total * world, "parallelism": "shard ciphertexts over %d GPU(s)" % world},
+        "data": "synthetic (seeded key set, shares generated on device; %s + 8 bad encodings)"
+                % ("%g%% wrong shares" % (100 * args.corrupt) if args.corrupt_mode == "uniform"
+                   else "f = %d Byzantine senders send wrong shares on every ciphertext" % ep.f),
+        "config": {"workload": "C3 HoneyBadger epoch: %d ciphertexts x %d DecryptionShares verified + %d G1 combines (t=%d)%s"
+                   % (job_cts, args.n, job_cts, ep.t, "" if args.scaling == "strong" else " per GPU"),
+                   "N": args.n, "f": ep.f, "t": ep.t, "ciphertexts": job_cts,
+                   "shares_per_step": job_shares, "parallelism": par},
         "combines_per_s": round(combines, 1),
-        "accepted_per_step_rank0": n_acc,
+        "accepted_per_step": n_acc,
         "mode": args.mode,
-        "exact_single_share_checks_per_step": leaves,
-        "kernel_ms_per_step": per_step,
+        "exact_single_share_checks_per_step_rank0": leaves,
+        "kernel_ms_per_step_rank0": per_step,
         "roofline": {
             "bound": "valu-int (v_mad_u64_u32)",
             "kernel": KERNEL_NAME[dom],
@@ -311,6 +487,10 @@ def main():
             "valu_insts_per_launch": pmc.get("counters_mean_per_dispatch", {}).get("SQ_INSTS_VALU"),
         },
     }
+    if world == 1 and not args.no_extra:
+        out["host_buffers"] = host_buffer_line(ctx, ep, max(1, min(args.steps, 2)))
+        if args.corrupt_mode == "uniform":
+            out["adversarial"] = adversarial_line(ctx, args, ep)
     if rank == 0 and not args.no_cpu:
         try:
             out["cpu_baseline"] = cpu_baseline(ep, args.cpu_budget)
@@ -320,6 +500,41 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def _all_expected(dist, ep, torch, dev, slices):
+    """Every rank's expected statuses (construction), gathered over the job (check only)."""
+    from hbbft_amd import shard
+    loc = torch.from_numpy(ep.expected).to(dev)
+    return [shard.gather_slices(dist, loc, [hi - lo for _, (lo, hi) in slices]).cpu().numpy()]
+
+
+def _all_master_r(args, ep):
+    """master_sk * r_k of every ciphertext of the whole epoch (r_k derives from (seed, k))."""
+    return [ep.master_sk * random.Random(SEED * 1000003 + k).randrange(1, R) % R
+            for k in range(args.cts)]
+
+
+def adversarial_line(ctx, args, base):
+    """The same configuration under BFT's worst case: f = 333 Byzantine senders send wrong
+    shares on every ciphertext (33 % of all shares, concentrated by sender)."""
+    base.free(ctx)
+    ep = Epoch(ctx, args.n, args.cts, SEED, 0.0, "senders")
+    steps = max(1, min(args.steps, 2))
+    elapsed = timed(ctx, ep, steps, 1)
+    per = {f: round(ctx.timing_read(f)[0] / steps, 3) for f in FAMS if ctx.timing_read(f)[1]}
+    leaves = ctx.rlc_last_leaves() if args.mode == "rlc" else ep.total
+    mism, comb_ok, n_acc = ep.check(ctx)
+    if mism or not comb_ok:
+        raise SystemExit("adversarial: results differ from the construction (%d mismatches, combine %s)"
+                         % (mism, comb_ok))
+    ep.free(ctx)
+    return {"value": round(ep.total * steps / elapsed, 1), "unit": "shares/s",
+            "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps,
+            "data": "f = %d Byzantine senders send wrong shares on every ciphertext (%d of %d shares) + 8 bad encodings"
+                    % (ep.f, ep.f * ep.m, ep.total),
+            "accepted_per_step": n_acc, "exact_single_share_checks_per_step": leaves,
+            "kernel_ms_per_step": per}
 
 
 if __name__ == "__main__":

@@ -86,6 +86,23 @@ SIGNATURES = {
     "hbtc_timing_read": (_I32, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(ctypes.c_uint64)]),
     "hbtc_timing_reset": (_I32, [_P]),
+    "hbtc_stream_wait_ctx": (_I32, [_P, _P]),
+    "hbtc_ctx_wait_stream": (_I32, [_P, _P]),
+    "hbtc_shard_items": (_I32, [_U32, _U32, _U32, _P, ctypes.POINTER(_U32), ctypes.POINTER(_U32),
+                                ctypes.POINTER(_U32), _P, _P]),
+    "hbtc_shard_instances": (_I32, [_U32, _U32, _P, _P]),
+    "hbtc_node_create": (_I32, [_I32, _P, ctypes.POINTER(_P)]),
+    "hbtc_node_destroy": (None, [_P]),
+    "hbtc_node_last_error": (ctypes.c_char_p, [_P]),
+    "hbtc_node_devices": (_I32, [_P]),
+    "hbtc_node_context": (_P, [_P, _I32]),
+    "hbtc_node_set_verify_mode": (_I32, [_P, _I32]),
+    "hbtc_node_keyset_load": (_I32, [_P, _P, _U32, ctypes.POINTER(_U32), ctypes.POINTER(_U32)]),
+    "hbtc_node_keyset_free": (_I32, [_P, _U32]),
+    "hbtc_node_verify_dec_shares": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P, _P]),
+    "hbtc_node_verify_sig_shares": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P]),
+    "hbtc_node_combine_dec": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P]),
+    "hbtc_node_combine_sigs": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P, _P]),
 }
 
 _lib = None
@@ -429,6 +446,17 @@ class Context:
     def sync(self):
         self._check(self.lib.hbtc_sync(self.h), "hbtc_sync")
 
+    def stream_wait_ctx(self, hip_stream):
+        """Work enqueued later on `hip_stream` (a raw HIP stream handle, e.g.
+        torch.cuda.Stream.cuda_stream) waits for everything already enqueued on this context."""
+        self._check(self.lib.hbtc_stream_wait_ctx(self.h, ctypes.c_void_p(hip_stream)),
+                    "hbtc_stream_wait_ctx")
+
+    def ctx_wait_stream(self, hip_stream):
+        """This context's later work waits for everything already enqueued on `hip_stream`."""
+        self._check(self.lib.hbtc_ctx_wait_stream(self.h, ctypes.c_void_p(hip_stream)),
+                    "hbtc_ctx_wait_stream")
+
     def set_verify_mode(self, mode):
         """MODE_RLC (default): batched random-linear-combination checks with exact fallback;
         MODE_PER_SHARE: one pairing check per share."""
@@ -450,3 +478,92 @@ class Context:
         self._check(self.lib.hbtc_timing_read(self.h, family.encode(), ctypes.byref(ms),
                                               ctypes.byref(n)), "hbtc_timing_read")
         return ms.value, n.value
+
+
+class Node:
+    """A multi-device node (include/hbtc.h hbtc_node_*): one epoch's batch split across the
+    devices (strong scaling), the same host-buffer interface and statuses as Context."""
+
+    def __init__(self, devices):
+        self.lib = load()
+        devs = np.ascontiguousarray(devices, dtype=np.int32)
+        h = ctypes.c_void_p()
+        rc = self.lib.hbtc_node_create(int(devs.size), _ptr(devs), ctypes.byref(h))
+        if rc != 0:
+            raise HbtcError("hbtc_node_create(%s) failed: %d" % (list(devices), rc))
+        self.h = h
+        self.devices = list(devices)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.hbtc_node_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.lib.hbtc_node_last_error(self.h)
+            raise HbtcError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+    def set_verify_mode(self, mode):
+        self._check(self.lib.hbtc_node_set_verify_mode(self.h, int(mode)), "hbtc_node_set_verify_mode")
+
+    def keyset_load(self, pk_shares):
+        pk = _join(pk_shares, 48)
+        kid, bad = _U32(), _U32()
+        self._check(self.lib.hbtc_node_keyset_load(self.h, _ptr(pk), pk.size // 48, ctypes.byref(kid),
+                                                   ctypes.byref(bad)), "hbtc_node_keyset_load")
+        return kid.value, bad.value
+
+    def keyset_free(self, kid):
+        self._check(self.lib.hbtc_node_keyset_free(self.h, kid), "hbtc_node_keyset_free")
+
+    def verify_dec_shares(self, keyset, H, w, counts, idx, shares, offsets=None):
+        off = _offsets(offsets if offsets is not None else counts, offsets is not None)
+        Hb, wb = _join(H, 96), _join(w, 96)
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        sh = _join(shares, 48)
+        st = np.zeros(max(int(off[-1]), 1), np.int32)
+        self._check(self.lib.hbtc_node_verify_dec_shares(self.h, keyset, off.size - 1, _ptr(Hb), _ptr(wb),
+                                                         _ptr(off), _ptr(ix), _ptr(sh), _ptr(st)),
+                    "hbtc_node_verify_dec_shares")
+        return st[:int(off[-1])]
+
+    def verify_sig_shares(self, keyset, H, counts, idx, sigs, offsets=None):
+        off = _offsets(offsets if offsets is not None else counts, offsets is not None)
+        Hb = _join(H, 96)
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        sg = _join(sigs, 96)
+        st = np.zeros(max(int(off[-1]), 1), np.int32)
+        self._check(self.lib.hbtc_node_verify_sig_shares(self.h, keyset, off.size - 1, _ptr(Hb), _ptr(off),
+                                                         _ptr(ix), _ptr(sg), _ptr(st)),
+                    "hbtc_node_verify_sig_shares")
+        return st[:int(off[-1])]
+
+    def combine_dec(self, counts, idx, shares, t, offsets=None):
+        off = _offsets(offsets if offsets is not None else counts, offsets is not None)
+        n = off.size - 1
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        sh = _join(shares, 48)
+        out = np.zeros(48 * max(n, 1), np.uint8)
+        st = np.zeros(max(n, 1), np.int32)
+        self._check(self.lib.hbtc_node_combine_dec(self.h, n, _ptr(off), _ptr(ix), _ptr(sh), t, _ptr(out),
+                                                   _ptr(st)), "hbtc_node_combine_dec")
+        return [bytes(out[48 * k:48 * k + 48]) for k in range(n)], st[:n]
+
+    def combine_sigs(self, counts, idx, sigs, t, offsets=None):
+        off = _offsets(offsets if offsets is not None else counts, offsets is not None)
+        n = off.size - 1
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        sg = _join(sigs, 96)
+        out = np.zeros(96 * max(n, 1), np.uint8)
+        par = np.zeros(max(n, 1), np.uint8)
+        st = np.zeros(max(n, 1), np.int32)
+        self._check(self.lib.hbtc_node_combine_sigs(self.h, n, _ptr(off), _ptr(ix), _ptr(sg), t, _ptr(out),
+                                                    _ptr(par), _ptr(st)), "hbtc_node_combine_sigs")
+        return [bytes(out[96 * k:96 * k + 96]) for k in range(n)], par[:n], st[:n]

@@ -64,6 +64,7 @@ struct hbtc_ctx {
   hipStream_t s_prep = nullptr;  // per-instance G2 preparation, overlapped with the item pass
   hipStream_t s_comb = nullptr;  // combines (Lagrange), overlapped with verification
   hipEvent_t ev_main = nullptr, ev_prep = nullptr, ev_comb = nullptr;
+  hipEvent_t ev_ext = nullptr, ev_ext2 = nullptr, ev_ext3 = nullptr;  // external-stream ordering
   std::map<std::string, Stage> stages;
   std::mutex mu;
   std::string err;
@@ -683,7 +684,10 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
       hipStreamCreateWithFlags(&c->s_comb, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_prep, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_ext2, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_ext3, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return HBTC_ERR_DEVICE;
   }
@@ -714,6 +718,9 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
   (void)hipEventDestroy(c->ev_main);
   (void)hipEventDestroy(c->ev_prep);
   (void)hipEventDestroy(c->ev_comb);
+  (void)hipEventDestroy(c->ev_ext);
+  (void)hipEventDestroy(c->ev_ext2);
+  (void)hipEventDestroy(c->ev_ext3);
   (void)hipStreamDestroy(c->s_prep);
   (void)hipStreamDestroy(c->s_comb);
   (void)hipStreamDestroy(c->stream);
@@ -937,6 +944,25 @@ int hbtc_sync(hbtc_ctx* c) {
   if (!c) return HBTC_ERR_ARG;
   Guard g(c);
   return sync(c);
+}
+
+int hbtc_stream_wait_ctx(hbtc_ctx* c, void* stream) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  hipStream_t ext = static_cast<hipStream_t>(stream);
+  HB_TRY(stream_after(c, ext, c->stream, c->ev_ext));
+  HB_TRY(stream_after(c, ext, c->s_prep, c->ev_ext2));
+  return stream_after(c, ext, c->s_comb, c->ev_ext3);
+}
+
+int hbtc_ctx_wait_stream(hbtc_ctx* c, void* stream) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  HB_CHECK(c, hipEventRecord(c->ev_ext, static_cast<hipStream_t>(stream)));
+  HB_CHECK(c, hipStreamWaitEvent(c->stream, c->ev_ext, 0));
+  HB_CHECK(c, hipStreamWaitEvent(c->s_prep, c->ev_ext, 0));
+  HB_CHECK(c, hipStreamWaitEvent(c->s_comb, c->ev_ext, 0));
+  return HBTC_OK;
 }
 
 int hbtc_verify_dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct,

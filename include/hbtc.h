@@ -162,6 +162,13 @@ int hbtc_dev_free(hbtc_ctx* ctx, void* d_ptr);
 int hbtc_dev_upload(hbtc_ctx* ctx, void* d_dst, const void* h_src, size_t bytes);
 int hbtc_dev_download(hbtc_ctx* ctx, void* h_dst, const void* d_src, size_t bytes);
 int hbtc_sync(hbtc_ctx* ctx);
+/* Ordering with a caller's HIP stream (e.g. the stream an RCCL all-gather runs on):
+ * hbtc_stream_wait_ctx  work enqueued on `stream` after this call waits for everything already
+ *                       enqueued on the context (verification, preparation, combines);
+ * hbtc_ctx_wait_stream  the context's later work waits for everything already on `stream`
+ *                       (before overwriting a buffer the caller's stream still reads). */
+int hbtc_stream_wait_ctx(hbtc_ctx* ctx, void* hip_stream);
+int hbtc_ctx_wait_stream(hbtc_ctx* ctx, void* hip_stream);
 /* Same semantics as the host entry points; every d_* argument is a device pointer from
  * hbtc_dev_alloc and `offsets` stays a HOST array (it shapes the launch).  Work is enqueued on
  * the context's stream; call hbtc_sync before reading results. */
@@ -229,6 +236,50 @@ int hbtc_skg_check_acks(hbtc_ctx* ctx, uint32_t n_parts, uint32_t t, uint32_t ou
                         const uint8_t* row_ok, uint32_t n_acks, const uint32_t* ack_part,
                         const uint32_t* ack_sender, const uint8_t* vals_le32,
                         int32_t* ack_status);
+
+/* ---- multi-device node ------------------------------------------------------------------- */
+/* One hbbft node (one process, /root/reference/src/messaging.rs:188) driving several GPUs: a
+ * context per device, each call's batch split across them (strong scaling of ONE epoch).
+ * Verification cuts the item range into equal contiguous slices (an instance crossing a cut is
+ * verified as one sub-instance per side with the same H / w: the RLC groups are tiles inside an
+ * instance, so no exchange is needed); combines take whole instances, balanced by share count.
+ * Host buffers, blocking, the same semantics and statuses as the single-context calls.
+ * devices == NULL means 0 .. n_devices-1; a device may repeat (several contexts on one GPU). */
+typedef struct hbtc_node hbtc_node;
+int hbtc_node_create(int n_devices, const int* devices, hbtc_node** out);
+void hbtc_node_destroy(hbtc_node* node);
+const char* hbtc_node_last_error(hbtc_node* node);
+int hbtc_node_devices(hbtc_node* node);
+hbtc_ctx* hbtc_node_context(hbtc_node* node, int device_slot);
+int hbtc_node_set_verify_mode(hbtc_node* node, int mode);
+int hbtc_node_keyset_load(hbtc_node* node, const uint8_t* pk_shares_c48, uint32_t n,
+                          uint32_t* keyset_id, uint32_t* n_bad);
+int hbtc_node_keyset_free(hbtc_node* node, uint32_t keyset_id);
+int hbtc_node_verify_dec_shares(hbtc_node* node, uint32_t keyset_id, uint32_t n_ct,
+                                const uint8_t* H_c96, const uint8_t* w_c96,
+                                const uint32_t* offsets, const uint32_t* idx,
+                                const uint8_t* share_c48, int32_t* status);
+int hbtc_node_verify_sig_shares(hbtc_node* node, uint32_t keyset_id, uint32_t n_inst,
+                                const uint8_t* H_c96, const uint32_t* offsets,
+                                const uint32_t* idx, const uint8_t* sig_c96, int32_t* status);
+int hbtc_node_combine_dec(hbtc_node* node, uint32_t n_ct, const uint32_t* offsets,
+                          const uint32_t* idx, const uint8_t* share_c48, uint32_t t,
+                          uint8_t* out_g_c48, int32_t* inst_status);
+int hbtc_node_combine_sigs(hbtc_node* node, uint32_t n_inst, const uint32_t* offsets,
+                           const uint32_t* idx, const uint8_t* sig_c96, uint32_t t,
+                           uint8_t* out_sig_c96, uint8_t* out_parity, int32_t* inst_status);
+
+/* The node's shard plans (host code, no GPU), for callers that run one process per GPU and
+ * merge with their own collective (bench.py: RCCL all-gather of statuses and combined points).
+ * hbtc_shard_items: device `dev`'s verification slice [*lo, *hi) of the item range and its
+ *   *n_sub sub-instances: parent[s] (capacity n_inst) is the instance of sub-instance s,
+ *   sub_offsets (capacity n_inst + 1) their item offsets relative to *lo.
+ * hbtc_shard_instances: the combine plan, device d takes instances [first[d], first[d+1])
+ *   (first has n_dev + 1 entries), balanced by share count. */
+int hbtc_shard_items(uint32_t n_dev, uint32_t dev, uint32_t n_inst, const uint32_t* offsets,
+                     uint32_t* lo, uint32_t* hi, uint32_t* n_sub, uint32_t* parent,
+                     uint32_t* sub_offsets);
+int hbtc_shard_instances(uint32_t n_dev, uint32_t n_inst, const uint32_t* offsets, uint32_t* first);
 
 /* ---- verification strategy ----------------------------------------------------------------- */
 /* HBTC_MODE_RLC (default): shares of one instance are checked together by a random linear
