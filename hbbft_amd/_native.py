@@ -86,6 +86,7 @@ SIGNATURES = {
     "hbtc_timing_read": (_I32, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(ctypes.c_uint64)]),
     "hbtc_timing_reset": (_I32, [_P]),
+    "hbtc_set_sender_tracking": (_I32, [_P, _I32]),
     "hbtc_stream_wait_ctx": (_I32, [_P, _P]),
     "hbtc_ctx_wait_stream": (_I32, [_P, _P]),
     "hbtc_shard_items": (_I32, [_U32, _U32, _U32, _P, ctypes.POINTER(_U32), ctypes.POINTER(_U32),
@@ -461,6 +462,11 @@ class Context:
         """MODE_RLC (default): batched random-linear-combination checks with exact fallback;
         MODE_PER_SHARE: one pairing check per share."""
         self._check(self.lib.hbtc_set_verify_mode(self.h, int(mode)), "hbtc_set_verify_mode")
+
+    def set_sender_tracking(self, on):
+        """Sender tracking (default on): recent liars' shares are checked one by one."""
+        self._check(self.lib.hbtc_set_sender_tracking(self.h, 1 if on else 0),
+                    "hbtc_set_sender_tracking")
 
     def rlc_last_leaves(self):
         n = _U32()

@@ -39,6 +39,9 @@ struct Keyset {
   G1A* pk = nullptr;
   int32_t* st = nullptr;
   PtXY* tab = nullptr;  // fixed-base tables (n * PK_TAB_WIN * 256 points, ~98 KB per share)
+  uint32_t* last_bad = nullptr;  // sender tracking: the call that last flagged each sender
+  uint32_t* rejects = nullptr;   // per-sender REJECT counts of the running call
+  uint32_t calls = 0;            // RLC verification calls on this key set
   uint32_t n = 0;
 };
 
@@ -72,6 +75,7 @@ struct hbtc_ctx {
   uint32_t next_keyset = 1;
   std::map<std::string, DevBuf> bufs;
   int verify_mode = HBTC_MODE_RLC;
+  bool track_senders = true;
   const uint32_t* last_leaf_count = nullptr;  // device counter of the last RLC call
   // Device ranges that combines enqueued on s_comb still read, each with the event recorded
   // after that combine: main-stream work that writes an overlapping range waits on it first
@@ -329,6 +333,22 @@ int prepare_g2(hbtc_ctx* c, const uint8_t* d0, const uint8_t* d1, uint32_t n, G2
   });
 }
 
+// Sender tracking view of one RLC call on key set ks (hbtc_kernels.h Suspects).
+Suspects suspects_of(hbtc_ctx* c, Keyset* ks, uint32_t* leaf_count, uint32_t* leaves) {
+  Suspects s{nullptr, 0, leaf_count, leaves};
+  if (c->track_senders) {
+    s.last_bad = ks->last_bad;
+    s.now = ++ks->calls;
+  }
+  return s;
+}
+
+// REJECTs that flag a sender in one call: 1/8 of the call's average shares per sender (>= 1).
+uint32_t track_threshold(const Keyset* ks, uint32_t n_items) {
+  const uint64_t t = (uint64_t)n_items / (8ull * ks->n);
+  return t ? (uint32_t)t : 1u;
+}
+
 // ---------------------------------------------------------------- device-pointer cores
 int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t* d_H,
                    const uint8_t* d_w, const uint32_t* offsets, const uint32_t* d_idx,
@@ -384,9 +404,10 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   uint32_t* leaf_count = counters;
   uint32_t* sub_count = counters + 1;
   HB_CHECK(c, hipMemsetAsync(counters, 0, 2 * sizeof(uint32_t), c->stream));
+  const Suspects sus = suspects_of(c, ks, leaf_count, leaves);
   HB_TRY(timed(c, "rlc_items", [&] {
     return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->tab,
-                            ks->n, key, sums, dec, d_status);
+                            ks->n, key, sus, sums, dec, d_status);
   }));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
   HB_TRY(timed(c, "chk_tiles", [&] {
@@ -403,7 +424,9 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   }));
   c->last_leaf_count = leaf_count;
   return timed(c, "rlc_finalize", [&] {
-    return launch_rlc_finalize(c->stream, n_tiles, tiles, h_st, w_st, d_status);
+    return launch_rlc_finalize(c->stream, n_tiles, tiles, h_st, w_st, d_status, d_idx, ks->n,
+                               ks->rejects, const_cast<uint32_t*>(sus.last_bad), sus.now,
+                               track_threshold(ks, n_items));
   });
 }
 
@@ -458,9 +481,10 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   uint32_t* leaf_count = counters;
   uint32_t* sub_count = counters + 1;
   HB_CHECK(c, hipMemsetAsync(counters, 0, 2 * sizeof(uint32_t), c->stream));
+  const Suspects sus = suspects_of(c, ks, leaf_count, leaves);
   HB_TRY(timed(c, "sig_items", [&] {
     return launch_sig_items(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->tab,
-                            ks->n, key, sums, dec, d_status);
+                            ks->n, key, sus, sums, dec, d_status);
   }));
   HB_TRY(timed(c, "sig_lines", [&] {
     return launch_plines(c->stream, 0, 2 * n_tiles, 0, nullptr, nullptr, tiles, sums, dec, tables,
@@ -493,7 +517,9 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   }
   c->last_leaf_count = leaf_count;
   return timed(c, "rlc_finalize", [&] {
-    return launch_rlc_finalize(c->stream, n_tiles, tiles, h_st, h_st, d_status);
+    return launch_rlc_finalize(c->stream, n_tiles, tiles, h_st, h_st, d_status, d_idx, ks->n,
+                               ks->rejects, const_cast<uint32_t*>(sus.last_bad), sus.now,
+                               track_threshold(ks, n_items));
   });
 }
 
@@ -705,6 +731,8 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
     (void)hipFree(kv.second.pk);
     (void)hipFree(kv.second.st);
     (void)hipFree(kv.second.tab);
+    (void)hipFree(kv.second.last_bad);
+    (void)hipFree(kv.second.rejects);
   }
   for (Span& sp : c->spans) {
     (void)hipEventDestroy(sp.a);
@@ -743,6 +771,10 @@ int hbtc_keyset_load(hbtc_ctx* c, const uint8_t* pk_c48, uint32_t n, uint32_t* k
     return launch_g1_decode(c->stream, (const uint8_t*)d_in, n, ks.pk, ks.st);
   }));
   HB_CHECK(c, hipMalloc(&ks.tab, sizeof(PtXY) * (size_t)n * PK_TAB_WIN * 256));
+  HB_CHECK(c, hipMalloc(&ks.last_bad, sizeof(uint32_t) * n));
+  HB_CHECK(c, hipMemsetAsync(ks.last_bad, 0, sizeof(uint32_t) * n, c->stream));
+  HB_CHECK(c, hipMalloc(&ks.rejects, sizeof(uint32_t) * n));
+  HB_CHECK(c, hipMemsetAsync(ks.rejects, 0, sizeof(uint32_t) * n, c->stream));
   Fq* tab_ws;
   HB_TRY(wst(c, "pktab.ws", (size_t)n * PK_TAB_WIN * 512, &tab_ws));
   HB_TRY(timed(c, "prepare", [&] {
@@ -769,6 +801,8 @@ int hbtc_keyset_free(hbtc_ctx* c, uint32_t keyset_id) {
   (void)hipFree(it->second.pk);
   (void)hipFree(it->second.st);
   (void)hipFree(it->second.tab);
+  (void)hipFree(it->second.last_bad);
+  (void)hipFree(it->second.rejects);
   c->keysets.erase(it);
   return HBTC_OK;
 }
@@ -1410,6 +1444,13 @@ int hbtc_g2_msm(hbtc_ctx* c, uint32_t n_msm, uint32_t n, const uint8_t* pts_c96,
   if (!c || (n_msm && (!pts_c96 || !scalars_le32 || !out_c96 || !status))) return HBTC_ERR_ARG;
   Guard g(c);
   return msm_host(c, 2, n_msm, n, pts_c96, scalars_le32, out_c96, status);
+}
+
+int hbtc_set_sender_tracking(hbtc_ctx* c, int enable) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  c->track_senders = enable != 0;
+  return HBTC_OK;
 }
 
 int hbtc_set_verify_mode(hbtc_ctx* c, int mode) {

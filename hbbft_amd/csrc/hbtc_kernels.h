@@ -17,6 +17,25 @@ constexpr uint32_t TILE_ITEMS = 64;
 
 // ---- RLC batch verification (hbtc_rlc.hip)
 constexpr int32_t HBTC_RLC_PENDING = -1;  // internal: decided by a group check or a leaf check
+constexpr int32_t HBTC_RLC_LEAF = -2;     // internal: a tracked sender's share, listed for a leaf check
+// Sender tracking (hbtc.h hbtc_set_sender_tracking): a sender with many shares REJECTed (>= 1/8
+// of the call's average shares per sender) in one of the last SUSPECT_WINDOW calls on a key set
+// is tracked; its shares skip the group sums and go
+// straight to the exact leaf checks, so f Byzantine senders who lie in every epoch no longer
+// make every tile and sub-tile of the honest shares fail.  Decisions are unchanged (every share
+// still gets an exact verdict); only the work differs.
+constexpr uint32_t SUSPECT_WINDOW = 16;
+struct Suspects {
+  const uint32_t* last_bad;  // per sender: the call number of its last REJECT (0 = none); null = off
+  uint32_t now;              // this call's number (>= 1)
+  uint32_t* leaf_count;      // the leaf list the item pass appends tracked shares to
+  uint32_t* leaves;
+};
+__device__ __forceinline__ bool is_suspect(const Suspects& s, uint32_t id) {
+  if (!s.last_bad) return false;
+  const uint32_t b = s.last_bad[id];
+  return b != 0 && s.now - b <= SUSPECT_WINDOW;
+}
 struct RlcKey {
   uint32_t k[8];  // ChaCha20 key, fresh from the host's random source for every call
 };
@@ -53,10 +72,14 @@ hipError_t launch_pk_table(hipStream_t s, const G1A* pk, const int32_t* pk_statu
                            PtXY* tab, Fq* ws);
 hipError_t launch_rlc_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* shares, const G1A* pk, const int32_t* pk_status,
-                            const PtXY* pk_tab, uint32_t n_pk, RlcKey key, TileSums* sums,
-                            G1A* dec, int32_t* status);
+                            const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,
+                            TileSums* sums, G1A* dec, int32_t* status);
+// Final decisions; with last_bad != null, counts every sender's REJECTs in `rejects` and stamps
+// last_bad[i] = now for the senders with >= thresh of them (clearing the counts).
 hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
-                               const int32_t* h_status, const int32_t* w_status, int32_t* status);
+                               const int32_t* h_status, const int32_t* w_status, int32_t* status,
+                               const uint32_t* idx, uint32_t n_pk, uint32_t* rejects,
+                               uint32_t* last_bad, uint32_t now, uint32_t thresh);
 // the pairing-product checks (hbtc_check.hip, cooperative GT arithmetic of gt6.h)
 hipError_t launch_chk_tiles(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
                             const TileSums* sums, const G2A* h_aff, const Line* h_lines,
@@ -76,8 +99,8 @@ hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t*
 // ---- RLC batch verification of SignatureShares (hbtc_sig.hip, checks in hbtc_check.hip)
 hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* sigs, const G1A* pk, const int32_t* pk_status,
-                            const PtXY* pk_tab, uint32_t n_pk, RlcKey key, SigTileSums* sums,
-                            G2A* dec, int32_t* status);
+                            const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,
+                            SigTileSums* sums, G2A* dec, int32_t* status);
 // Projective line tables of the G2 sums the next check level needs: mode 0 every tile
 // (2 per tile: plain, weighted), mode 1 the 8 sub-tiles of the listed tiles (16 per listed
 // tile), mode 2 the listed leaf shares (decoded sigma).  inf[g] = 1: the sum is infinity.

@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
     const uint8_t* __restrict__ shares, const G1A* __restrict__ pk,
     const int32_t* __restrict__ pk_status, const PtXY* __restrict__ pk_tab, uint32_t n_pk,
-    RlcKey key, TileSums* __restrict__ sums, G1A* __restrict__ dec,
+    RlcKey key, Suspects sus, TileSums* __restrict__ sums, G1A* __restrict__ dec,
     int32_t* __restrict__ status) {
   __shared__ G1J redA[64];
   __shared__ G1J redB[64];
@@ -66,6 +66,7 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
   G1J S, P;
   jac_set_inf(S);
   jac_set_inf(P);
+  bool leaf = false;
   if (lane < tile.count) {
     int32_t st = HBTC_RLC_PENDING;
     const uint32_t id = idx[item];
@@ -81,16 +82,22 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
         st = HBTC_DECODE_ERR;
       } else {
         dec[item] = d;  // for the exact leaf checks and the combine (no second decode)
-        const uint64_t r = rlc_scalar(key, item);
-        const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
-        G1A pd;
-        g1_phi(pd, d);
-        jac_mul2_u32(S, d, ra, pd, rb);
-        if (!pk[id].inf) rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb);
+        if (is_suspect(sus, id)) {
+          st = HBTC_RLC_LEAF;  // straight to an exact check, outside the group sums
+        } else {
+          const uint64_t r = rlc_scalar(key, item);
+          const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
+          G1A pd;
+          g1_phi(pd, d);
+          jac_mul2_u32(S, d, ra, pd, rb);
+          if (!pk[id].inf) rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb);
+        }
       }
     }
     status[item] = st;
+    leaf = st == HBTC_RLC_LEAF;
   }
+  rlc_list_leaf(sus, leaf, (uint32_t)item, tile.inst, lane);
   TileSums* ts = sums + blockIdx.x;
   rlc_reduce(redA, redB, S, lane, ts->S, ts->SW);
   rlc_reduce(redA, redB, P, lane, ts->P, ts->PW);
@@ -99,18 +106,42 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
 
 #if HBTC_IN_PART(6)
 // Every item still pending passed some group check: ACCEPT.  Items of a ciphertext whose own
-// H / w failed to decode: INSTANCE_ERR.
+// H / w failed to decode: INSTANCE_ERR.  With sender tracking on, the REJECTs of every sender
+// are counted (k_track_update turns the counts into tracking stamps).
 __global__ void __launch_bounds__(64) k_rlc_finalize(const Tile* __restrict__ tiles,
                                                      const int32_t* __restrict__ h_status,
                                                      const int32_t* __restrict__ w_status,
-                                                     int32_t* __restrict__ status) {
+                                                     int32_t* __restrict__ status,
+                                                     const uint32_t* __restrict__ idx, uint32_t n_pk,
+                                                     uint32_t* __restrict__ rejects) {
   const Tile tile = tiles[blockIdx.x];
   if (threadIdx.x >= tile.count) return;
   const uint32_t i = tile.first + threadIdx.x;
-  if (h_status[tile.inst] != HBTC_ACCEPT || w_status[tile.inst] != HBTC_ACCEPT)
+  if (h_status[tile.inst] != HBTC_ACCEPT || w_status[tile.inst] != HBTC_ACCEPT) {
     status[i] = HBTC_INSTANCE_ERR;
-  else if (status[i] == HBTC_RLC_PENDING)
-    status[i] = HBTC_ACCEPT;
+  } else {
+    const int32_t st = status[i];
+    if (st == HBTC_RLC_PENDING) {
+      status[i] = HBTC_ACCEPT;
+    } else if (st == HBTC_REJECT && rejects) {
+      const uint32_t id = idx[i];
+      if (id < n_pk) atomicAdd(rejects + id, 1u);
+    }
+  }
+}
+
+// A sender whose REJECTs in this call reach `thresh` (1/8 of the call's average shares per
+// sender: a liar, not a sender hit by a stray corrupted share) is stamped with the call number;
+// the counts are cleared for the next call.
+__global__ void __launch_bounds__(256) k_track_update(uint32_t n_pk, uint32_t* __restrict__ rejects,
+                                                      uint32_t* __restrict__ last_bad, uint32_t now,
+                                                      uint32_t thresh) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_pk) return;
+  const uint32_t r = rejects[i];
+  if (r == 0) return;
+  if (r >= thresh) last_bad[i] = now;
+  rejects[i] = 0;
 }
 #endif  // part 6
 
@@ -120,18 +151,23 @@ static inline uint32_t rlc_blocks(uint64_t n, uint32_t bs) { return (uint32_t)((
 #if HBTC_IN_PART(6)
 hipError_t launch_rlc_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* shares, const G1A* pk, const int32_t* pk_status,
-                            const PtXY* pk_tab, uint32_t n_pk, RlcKey key, TileSums* sums,
-                            G1A* dec, int32_t* status) {
+                            const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,
+                            TileSums* sums, G1A* dec, int32_t* status) {
   if (n_tiles == 0) return hipSuccess;
   hipLaunchKernelGGL(k_rlc_items, dim3(n_tiles), dim3(64), 0, s, tiles, idx, shares, pk, pk_status,
-                     pk_tab, n_pk, key, sums, dec, status);
+                     pk_tab, n_pk, key, sus, sums, dec, status);
   return hipGetLastError();
 }
 hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
-                               const int32_t* h_status, const int32_t* w_status, int32_t* status) {
+                               const int32_t* h_status, const int32_t* w_status, int32_t* status,
+                               const uint32_t* idx, uint32_t n_pk, uint32_t* rejects,
+                               uint32_t* last_bad, uint32_t now, uint32_t thresh) {
   if (n_tiles == 0) return hipSuccess;
   hipLaunchKernelGGL(k_rlc_finalize, dim3(n_tiles), dim3(64), 0, s, tiles, h_status, w_status,
-                     status);
+                     status, idx, n_pk, last_bad ? rejects : nullptr);
+  if (last_bad)
+    hipLaunchKernelGGL(k_track_update, dim3(rlc_blocks(n_pk, 256)), dim3(256), 0, s, n_pk, rejects,
+                       last_bad, now, thresh);
   return hipGetLastError();
 }
 #endif  // part 6

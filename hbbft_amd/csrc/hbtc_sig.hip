@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(64, HBTC_SIG_ITEMS_WAVES) k_sig_items(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
     const uint8_t* __restrict__ sigs, const G1A* __restrict__ pk,
     const int32_t* __restrict__ pk_status, const PtXY* __restrict__ pk_tab, uint32_t n_pk,
-    RlcKey key, SigTileSums* __restrict__ sums, G2A* __restrict__ dec,
+    RlcKey key, Suspects sus, SigTileSums* __restrict__ sums, G2A* __restrict__ dec,
     int32_t* __restrict__ status) {
   __shared__ G2J red2[2][64];  // reused for the G1 reduction
   G1J* red1 = reinterpret_cast<G1J*>(&red2[0][0]);
@@ -49,6 +49,7 @@ __global__ void __launch_bounds__(64, HBTC_SIG_ITEMS_WAVES) k_sig_items(
   G1J P;
   jac_set_inf(S);
   jac_set_inf(P);
+  bool leaf = false;
   if (lane < tile.count) {
     int32_t st = HBTC_RLC_PENDING;
     const uint32_t id = idx[item];
@@ -64,16 +65,22 @@ __global__ void __launch_bounds__(64, HBTC_SIG_ITEMS_WAVES) k_sig_items(
         st = HBTC_DECODE_ERR;
       } else {
         dec[item] = sg;  // for the exact leaf checks and the combine (no second decode)
-        const uint64_t r = rlc_scalar(key, item);
-        const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
-        G2A ms;
-        g2_mu(ms, sg);
-        jac_mul2_u32(S, sg, ra, ms, rb);
-        if (!pk[id].inf) rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb);
+        if (is_suspect(sus, id)) {
+          st = HBTC_RLC_LEAF;  // straight to an exact check, outside the group sums
+        } else {
+          const uint64_t r = rlc_scalar(key, item);
+          const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
+          G2A ms;
+          g2_mu(ms, sg);
+          jac_mul2_u32(S, sg, ra, ms, rb);
+          if (!pk[id].inf) rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb);
+        }
       }
     }
     status[item] = st;
+    leaf = st == HBTC_RLC_LEAF;
   }
+  rlc_list_leaf(sus, leaf, (uint32_t)item, tile.inst, lane);
   SigTileSums* ts = sums + blockIdx.x;
   rlc_reduce<Fq2>(red2[0], red2[1], S, lane, ts->S, ts->SW);
   rlc_reduce<Fq>(red1, red1 + 64, P, lane, ts->P, ts->PW);
@@ -140,11 +147,11 @@ static inline uint32_t sig_blocks(uint64_t n, uint32_t bs) { return (uint32_t)((
 
 hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* sigs, const G1A* pk, const int32_t* pk_status,
-                            const PtXY* pk_tab, uint32_t n_pk, RlcKey key, SigTileSums* sums,
-                            G2A* dec, int32_t* status) {
+                            const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,
+                            SigTileSums* sums, G2A* dec, int32_t* status) {
   if (n_tiles == 0) return hipSuccess;
   hipLaunchKernelGGL(k_sig_items, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk, pk_status,
-                     pk_tab, n_pk, key, sums, dec, status);
+                     pk_tab, n_pk, key, sus, sums, dec, status);
   return hipGetLastError();
 }
 

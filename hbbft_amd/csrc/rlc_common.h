@@ -54,6 +54,22 @@ static __device__ uint64_t rlc_scalar(const RlcKey& key, uint64_t item) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// Append the wave's tracked-sender items to the leaf list: one atomic per wave.  Called by all
+// 64 lanes (wave-uniform control flow).
+__device__ __forceinline__ void rlc_list_leaf(const Suspects& sus, bool leaf, uint32_t item,
+                                              uint32_t inst, uint32_t lane) {
+  const uint64_t m = __ballot(leaf);
+  if (!m) return;
+  uint32_t base = 0;
+  if (lane == 0) base = atomicAdd(sus.leaf_count, (uint32_t)__popcll(m));
+  base = __shfl(base, 0);
+  if (leaf) {
+    const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    sus.leaves[2 * pos] = item;
+    sus.leaves[2 * pos + 1] = inst;
+  }
+}
+
 // Tree reduction of the per-lane points q over the wave (lane = position in the tile): the sum
 // A and the position-weighted sum B of every aligned group of 8 (-> outA/outB[0..7]) and of the
 // tile (-> [8]).  Merging halves of size s:  A = A_l + A_r,  B = B_l + B_r + s A_r.

@@ -294,6 +294,12 @@ int hbtc_shard_instances(uint32_t n_dev, uint32_t n_inst, const uint32_t* offset
 #define HBTC_MODE_PER_SHARE 0
 #define HBTC_MODE_RLC 1
 int hbtc_set_verify_mode(hbtc_ctx* ctx, int mode);
+/* Sender tracking (default on, RLC mode): a sender with many shares REJECTed (at least 1/8 of
+ * the call's average shares per sender) by one of the last 16 RLC calls on a key set has its
+ * shares checked one by one, outside the group sums, so f Byzantine senders who lie in every
+ * epoch cannot make the honest shares' groups fail.  The
+ * decisions are exactly those of the per-share check either way; only the work differs. */
+int hbtc_set_sender_tracking(hbtc_ctx* ctx, int enable);
 /* Number of shares that needed the exact single-share check in the last RLC call (syncs). */
 int hbtc_rlc_last_leaves(hbtc_ctx* ctx, uint32_t* leaves);
 

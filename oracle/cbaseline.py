@@ -97,10 +97,52 @@ def bench_dec_shares(mode, threads, budget_s, shares, pk48, u48, v, w96):
     return int(done), wall.value, int(acc.value)
 
 
+def host_cpus():
+    """The host's CPUs as this process may use them: nproc (os.cpu_count), the affinity mask,
+    the cgroup CPU quota (cpu.max) and the CPU model.  `usable` = min(affinity, quota): every
+    core the scheduler will actually give the baseline's threads (on a shared GPU box the quota
+    is the box's CPU share, e.g. 16 of a 192-CPU machine)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = min(aff, quota) if quota else aff
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and quota is None and usable > int(env) > 0:
+        usable = int(env)  # the box's stated CPU share when no cgroup quota is visible
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota": quota, "model": model, "usable": usable}
+
+
 def run_dec_share_baseline(ep, budget_s, cores=None):
-    """bench.py cpu_baseline leg: the reference-faithful per-call path on all host cores (up to
-    the box's CPU share), on real decryption shares of the benchmark's ciphertext 0."""
-    cores = cores or min(16, os.cpu_count() or 1)
+    """bench.py cpu_baseline leg: the reference-faithful per-call path on every core this process
+    may use (host_cpus()['usable']), on real decryption shares of the benchmark's ciphertext 0."""
+    cpus = host_cpus()
+    cores = cores or cpus["usable"]
     rng = random.Random(3)
     k = 0
     shares = [bytes(ep.host_shares[k * ep.n + i]) for i in range(ep.n)]
@@ -115,6 +157,7 @@ def run_dec_share_baseline(ep, budget_s, cores=None):
         "value": round(done / wall, 2),
         "unit": "shares/s",
         "cores": cores,
+        "host_cpus": cpus,
         "kind": "port",
         "impl": "C restatement of threshold_crypto 0.1 / pairing 0.14 (oracle/c/tc_oracle.c), pthreads",
         "sample": "%d DecryptionShare checks of ciphertext 0 in %.1fs: per share serde decode ([r]P "
