@@ -87,6 +87,9 @@ SIGNATURES = {
                                 ctypes.POINTER(ctypes.c_uint64)]),
     "hbtc_timing_reset": (_I32, [_P]),
     "hbtc_set_sender_tracking": (_I32, [_P, _I32]),
+    "hbtc_hash_bytes": (_I32, [_P, _SZ, _P]),
+    "hbtc_xor_hash_bytes_batch": (_I32, [_U32, _P, _P, _P, _P]),
+    "hbtc_commitment_evaluate": (_I32, [_P, _U32, _P, _U32, _P, _P, _P]),
     "hbtc_stream_wait_ctx": (_I32, [_P, _P]),
     "hbtc_ctx_wait_stream": (_I32, [_P, _P]),
     "hbtc_shard_items": (_I32, [_U32, _U32, _U32, _P, ctypes.POINTER(_U32), ctypes.POINTER(_U32),
@@ -160,6 +163,30 @@ def hash_g1_g2(g1_c48, msg):
     if load().hbtc_hash_g1_g2(g, m, len(m), out) != 0:
         raise HbtcError("hbtc_hash_g1_g2 failed")
     return out.raw
+
+
+def hash_bytes(g1_c48, length):
+    """threshold_crypto's hash_bytes(g, len): the encrypt / decrypt XOR pad (host code)."""
+    g = bytes(g1_c48)
+    if len(g) != 48:
+        raise ValueError("g1 must be 48 compressed bytes")
+    out = ctypes.create_string_buffer(max(1, length))
+    if load().hbtc_hash_bytes(g, length, out) != 0:
+        raise HbtcError("hbtc_hash_bytes failed")
+    return out.raw[:length]
+
+
+def xor_hash_bytes_batch(gs, msgs):
+    """msgs[i] XOR hash_bytes(gs[i], |msgs[i]|) for every i, over the host's cores."""
+    buf, off = _msg_batch(msgs)
+    n = off.size - 1
+    g = _join(gs, 48)
+    if g.size != 48 * n:
+        raise ValueError("one 48-byte g per message")
+    out = np.zeros(max(1, int(off[-1])), np.uint8)
+    if load().hbtc_xor_hash_bytes_batch(n, _ptr(g), _ptr(buf), _ptr(off), _ptr(out)) != 0:
+        raise HbtcError("hbtc_xor_hash_bytes_batch failed")
+    return [bytes(out[off[i]:off[i + 1]]) for i in range(n)]
 
 
 def _msg_batch(msgs):
@@ -427,6 +454,17 @@ class Context:
                                                  _ptr(ok), ap.size, _ptr(ap), _ptr(sd), _ptr(vb),
                                                  _ptr(st)), "hbtc_skg_check_acks")
         return st
+
+    # ---- commitments
+    def commitment_evaluate(self, commit, xs):
+        """Commitment::evaluate(x) for every x in xs (compressed G1 coefficients)."""
+        cm = _join(commit, 48)
+        x = np.ascontiguousarray(xs, dtype=np.uint32)
+        out = np.zeros(48 * max(1, x.size), np.uint8)
+        st = np.zeros(max(1, x.size), np.int32)
+        self._check(self.lib.hbtc_commitment_evaluate(self.h, cm.size // 48, _ptr(cm), x.size, _ptr(x),
+                                                      _ptr(out), _ptr(st)), "hbtc_commitment_evaluate")
+        return [bytes(out[48 * k:48 * k + 48]) for k in range(x.size)], st[:x.size]
 
     # ---- device memory (benchmarks)
     def dev_alloc(self, nbytes):

@@ -1432,6 +1432,33 @@ int hbtc_skg_check_acks(hbtc_ctx* c, uint32_t n_parts, uint32_t t, uint32_t our_
   return HBTC_OK;
 }
 
+int hbtc_commitment_evaluate(hbtc_ctx* c, uint32_t n_coeff, const uint8_t* commit_c48,
+                             uint32_t n_x, const uint32_t* xs, uint8_t* out_c48, int32_t* status) {
+  if (!c || (n_x && (!commit_c48 || !xs || !out_c48 || !status)) || (n_x && n_coeff == 0))
+    return HBTC_ERR_ARG;
+  Guard g(c);
+  if (n_x == 0) return HBTC_OK;
+  // one MSM per point x: sum_j x^j C_j (the coefficients repeated per MSM)
+  const uint32_t chunk = std::max<uint32_t>(1, std::min<uint32_t>(n_x, (uint32_t)((64ull << 20) / (48ull * n_coeff + 32ull * n_coeff))));
+  std::vector<uint8_t> pts((size_t)chunk * n_coeff * 48), sc((size_t)chunk * n_coeff * 32);
+  for (uint32_t x0 = 0; x0 < n_x; x0 += chunk) {
+    const uint32_t m = std::min(chunk, n_x - x0);
+    for (uint32_t k = 0; k < m; ++k) {
+      memcpy(&pts[(size_t)k * n_coeff * 48], commit_c48, (size_t)n_coeff * 48);
+      Fr x, p, cn;
+      fr_from_u64(x, xs[x0 + k]);
+      fr_from_u64(p, 1);
+      for (uint32_t j = 0; j < n_coeff; ++j) {
+        fr_from_mont(cn, p);
+        memcpy(&sc[((size_t)k * n_coeff + j) * 32], cn.v, 32);
+        fr_mul(p, p, x);
+      }
+    }
+    HB_TRY(msm_host(c, 1, m, n_coeff, pts.data(), sc.data(), out_c48 + (size_t)x0 * 48, status + x0));
+  }
+  return HBTC_OK;
+}
+
 int hbtc_g1_msm(hbtc_ctx* c, uint32_t n_msm, uint32_t n, const uint8_t* pts_c48,
                 const uint8_t* scalars_le32, uint8_t* out_c48, int32_t* status) {
   if (!c || (n_msm && (!pts_c48 || !scalars_le32 || !out_c48 || !status))) return HBTC_ERR_ARG;

@@ -211,6 +211,15 @@ void hash_g1_g2_c96(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8
   hash_g2_c96(m.data(), m.size(), out96);
 }
 
+// threshold_crypto's hash_bytes(g, len): ChaChaRng seeded with sha3_256(compressed g), one
+// byte per draw (rand 0.4's u8: the low byte of next_u32).
+void hash_bytes(const uint8_t* g1_c48, size_t len, uint8_t* out) {
+  uint32_t seed[8];
+  seed_of(g1_c48, 48, seed);
+  ChaCha04 rng(seed);
+  for (size_t i = 0; i < len; ++i) out[i] = (uint8_t)rng.next_u32();
+}
+
 // The first on-curve candidate of hash_g2(msg) (before [h2]); the GPU clears the cofactor.
 void hash_g2_candidate(const uint8_t* msg, size_t len, G2A& p) {
   uint32_t seed[8];
@@ -295,6 +304,27 @@ int hbtc_hash_g2(const uint8_t* msg, size_t len, uint8_t* out_c96) {
 int hbtc_hash_g1_g2(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8_t* out_c96) {
   if (!g1_c48 || (!msg && len) || !out_c96) return HBTC_ERR_ARG;
   hbtc::hash_g1_g2_c96(g1_c48, msg, len, out_c96);
+  return HBTC_OK;
+}
+
+int hbtc_hash_bytes(const uint8_t* g1_c48, size_t len, uint8_t* out) {
+  if (!g1_c48 || (!out && len)) return HBTC_ERR_ARG;
+  hbtc::hash_bytes(g1_c48, len, out);
+  return HBTC_OK;
+}
+
+int hbtc_xor_hash_bytes_batch(uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
+                              const uint32_t* offsets, uint8_t* out) {
+  if (n == 0) return HBTC_OK;
+  if (!g1_c48 || !offsets || (!msgs && offsets[n]) || (!out && offsets[n]) ||
+      !hbtc::hash_offsets_ok(n, offsets))
+    return HBTC_ERR_ARG;
+  hbtc::parallel_items(n, [&](uint32_t i) {
+    const size_t len = offsets[i + 1] - offsets[i];
+    uint8_t* o = out + offsets[i];
+    hbtc::hash_bytes(g1_c48 + 48 * (size_t)i, len, o);
+    for (size_t j = 0; j < len; ++j) o[j] ^= msgs[offsets[i] + j];
+  });
   return HBTC_OK;
 }
 

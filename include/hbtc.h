@@ -135,6 +135,14 @@ int hbtc_verify_ciphertexts(hbtc_ctx* ctx, uint32_t n, const uint8_t* u_c48,
 int hbtc_sha3_256(const uint8_t* msg, size_t len, uint8_t* out32);
 int hbtc_hash_g2(const uint8_t* msg, size_t len, uint8_t* out_c96);
 int hbtc_hash_g1_g2(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8_t* out_c96);
+/* threshold_crypto's hash_bytes(g, len) (crate-internal): the XOR pad of PublicKey::encrypt and
+ * SecretKey::decrypt (v = msg XOR hash_bytes(r * pk, |msg|); src/sync_key_gen.rs:321,358,377,483).
+ * rand 0.4 ChaChaRng seeded with sha3_256(compressed g), the low byte of one next_u32 per byte.
+ * The batch form XORs item i's pad into msgs[offsets[i] .. offsets[i+1]) -> out (same layout),
+ * i.e. it encrypts or decrypts n messages given g_i, over the host's cores. */
+int hbtc_hash_bytes(const uint8_t* g1_c48, size_t len, uint8_t* out);
+int hbtc_xor_hash_bytes_batch(uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
+                              const uint32_t* offsets, uint8_t* out);
 /* Batches over the host's cores: message i = msgs[offsets[i] .. offsets[i+1]) (offsets[0] == 0,
  * non-decreasing); ciphertext i's u is g1_c48[48 i ..]. */
 int hbtc_hash_g2_batch(uint32_t n, const uint8_t* msgs, const uint32_t* offsets,
@@ -200,6 +208,15 @@ int hbtc_combine_sigs_verified_dev(hbtc_ctx* ctx, uint32_t n_inst, const uint32_
                                    const uint32_t* d_idx, const uint8_t* d_sig_c96,
                                    const int32_t* d_status, uint32_t t, uint8_t* d_out_sig_c96,
                                    uint8_t* d_out_parity, int32_t* d_inst_status);
+
+/* ---- commitments ------------------------------------------------------------------------ */
+/* Commitment::evaluate(x) for n_x points at once: out_k = sum_j xs[k]^j C_j over the n_coeff
+ * compressed G1 coefficients (Poly::commitment order, constant term first).  This is the
+ * per-era public-key-share table: NetworkInfo::new evaluates public_key_share(i) =
+ * commitment.evaluate(i + 1) for every node (src/messaging.rs:253-256, PublicKeySet from
+ * SyncKeyGen::generate, src/sync_key_gen.rs:428-447).  status[k] = ACCEPT or DECODE_ERR. */
+int hbtc_commitment_evaluate(hbtc_ctx* ctx, uint32_t n_coeff, const uint8_t* commit_c48,
+                             uint32_t n_x, const uint32_t* xs, uint8_t* out_c48, int32_t* status);
 
 /* ---- batched multi-scalar multiplication (Pippenger) -------------------------------------- */
 /* n_msm independent MSMs of n terms: out_m = sum_i k_{m,i} P_{m,i} (points item-major

@@ -153,3 +153,120 @@ class ThresholdDecryption:
         for ev in events:
             out.append(self.set_ciphertext(ev[1]) if ev[0] == "ct" else self.handle_message(ev[1], ev[2]))
         return out
+
+
+# ------------------------------------------------------------------------------ SyncKeyGen
+def _fr_from_wire(b, pos=0):
+    """bincode FieldWrap<Fr>: u64 LE length 32 + 32-byte big-endian value < r (restated)."""
+    R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    if len(b) < pos + 40 or int.from_bytes(b[pos:pos + 8], "little") != 32:
+        raise ValueError("FieldWrap")
+    v = int.from_bytes(b[pos + 8:pos + 40], "big")
+    if v >= R:
+        raise ValueError("FieldWrap >= r")
+    return v, pos + 40
+
+
+def _poly_from_wire(b):
+    if len(b) < 8:
+        raise ValueError("Poly")
+    n = int.from_bytes(b[:8], "little")
+    if 8 + 40 * n != len(b):
+        raise ValueError("Poly length")
+    out, pos = [], 8
+    for _ in range(n):
+        v, pos = _fr_from_wire(b, pos)
+        out.append(v)
+    return out
+
+
+class SyncKeyGen:
+    """sync_key_gen.rs:272-509 — one node, every message handled the moment it arrives.
+    Injected: decrypt(ct) -> bytes or None (SecretKey::decrypt), row_matches(commit, row) ->
+    bool (row.commitment() == commit.row(our_idx + 1)), value_matches(commit, sender_idx, val)
+    -> bool (commit.evaluate(our_idx + 1, sender_idx + 1) == val * G1)."""
+
+    def __init__(self, node_ids, our_id, threshold, decrypt, row_matches, value_matches):
+        self.ids = sorted(node_ids)
+        self.index = {n: i for i, n in enumerate(self.ids)}
+        self.our_idx = self.index.get(our_id)
+        self.t = threshold
+        self.decrypt = decrypt
+        self.row_matches = row_matches
+        self.value_matches = value_matches
+        self.parts = {}  # sender_idx -> {"commit", "values", "acks"}
+
+    def handle_part(self, sender, part):  # :338-381; part = (commit, rows)
+        if sender not in self.index:
+            return None
+        s_idx = self.index[sender]
+        commit, rows = part
+        if s_idx in self.parts:
+            return None
+        self.parts[s_idx] = {"commit": commit, "values": {}, "acks": set()}
+        if self.our_idx is None:
+            return None
+        if self.our_idx >= len(rows):
+            return None
+        ser_row = self.decrypt(rows[self.our_idx])
+        if ser_row is None:
+            return None
+        try:
+            row = _poly_from_wire(ser_row)
+        except ValueError:
+            return ("invalid", [(sender, "InvalidPartMessage")])
+        if len(row) != self.t + 1 or not self.row_matches(commit, row):
+            return ("invalid", [(sender, "InvalidPartMessage")])
+        return ("valid", row)
+
+    def handle_ack(self, sender, ack):  # :387-396 -> :462-498; ack = (proposer, values)
+        if sender not in self.index:
+            return []
+        s_idx = self.index[sender]
+        proposer, values = ack
+        fault = lambda k: [(sender, ("AckMessage", k))]  # noqa: E731
+        if len(values) != len(self.ids):
+            return fault("NodeCount")
+        part = self.parts.get(proposer)
+        if part is None:
+            return fault("SenderExist")
+        if s_idx in part["acks"]:
+            return fault("DuplicateAck")
+        part["acks"].add(s_idx)
+        if self.our_idx is None:
+            return []
+        ser_val = self.decrypt(values[self.our_idx])
+        if ser_val is None:
+            return fault("ValueDecryption")
+        try:
+            val, end = _fr_from_wire(ser_val)
+            if end != len(ser_val):
+                raise ValueError("trailing")
+        except ValueError:
+            return fault("ValueDeserialization")
+        if not self.value_matches(part["commit"], s_idx, val):
+            return fault("ValueInvalid")
+        part["values"][s_idx + 1] = val
+        return []
+
+    def complete(self):
+        return [p for p in sorted(self.parts) if len(self.parts[p]["acks"]) > 2 * self.t]
+
+    def is_ready(self):
+        return len(self.complete()) > self.t
+
+    def secret_share(self):  # :428-447, the Fr half of generate()
+        R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+        if self.our_idx is None:
+            return None
+        sk = 0
+        for p in self.complete():
+            items = sorted(self.parts[p]["values"].items())[:self.t + 1]
+            for x, y in items:
+                num = den = 1
+                for x0, _ in items:
+                    if x0 != x:
+                        num = num * x0 % R
+                        den = den * (x0 - x) % R
+                sk = (sk + y * num * pow(den, R - 2, R)) % R
+        return sk

@@ -50,3 +50,21 @@ def test_batches_match_single_calls():
     us = [B.g1_compress(B.g1_mul(B.G1_GEN, rng.randrange(1, B.R))) for _ in msgs]
     assert N.hash_g1_g2_batch(us, msgs) == [N.hash_g1_g2(u, m) for u, m in zip(us, msgs)]
     assert N.hash_g2_batch([]) == []
+
+
+@pytest.mark.parametrize("length", [0, 1, 40, 64, 4097])
+def test_hash_bytes_matches_oracle(length):
+    rng = random.Random(length + 5)
+    g = B.g1_mul(B.G1_GEN, rng.randrange(1, B.R))
+    assert N.hash_bytes(B.g1_compress(g), length) == TC.hash_bytes(g, length)
+
+
+def test_xor_hash_bytes_batch_roundtrip():
+    """The encrypt / decrypt pad: msg XOR pad XOR pad == msg, and each pad is hash_bytes(g)."""
+    rng = random.Random(77)
+    gs = [B.g1_compress(B.g1_mul(B.G1_GEN, rng.randrange(1, B.R))) for _ in range(9)]
+    msgs = [bytes(rng.randrange(256) for _ in range(rng.randrange(0, 300))) for _ in gs]
+    enc = N.xor_hash_bytes_batch(gs, msgs)
+    for g, m, e in zip(gs, msgs, enc):
+        assert bytes(a ^ b for a, b in zip(e, m)) == N.hash_bytes(g, len(m))
+    assert N.xor_hash_bytes_batch(gs, enc) == msgs
