@@ -32,9 +32,10 @@ $(BUILD):
 $(BUILD)/hbtc_kernels.p%.o: $(CSRC)/hbtc_kernels.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
 
-# part 6 (per-item G1 work) is built with every helper inlined: no calls, no scratch
+# part 6 (per-item G1 work) is built with every helper and the Fq product inlined: no calls
+# (each call saves / restores live registers through scratch; 72.6 -> 67.9 ms per C3 launch)
 $(BUILD)/hbtc_rlc.p6.o: $(CSRC)/hbtc_rlc.hip $(HDRS) | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=6 -DHBTC_INLINE_ALL -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=6 -DHBTC_INLINE_ALL -DHBTC_FQMUL_INLINE -c $< -o $@
 
 $(BUILD)/hbtc_rlc.p%.o: $(CSRC)/hbtc_rlc.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@

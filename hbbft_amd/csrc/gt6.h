@@ -122,7 +122,9 @@ HD void mul2_fq(Fq2& r, const Fq2& a, const Fq& y) {
 // call these a few dozen times per check, so one copy each keeps the kernels inside the
 // instruction cache; their by-reference operands cost ~100 dwords of stack traffic per call
 // against ~10^4 instructions of work.
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(HBTC_GT_INLINE)
+#define GTN __device__ __forceinline__
+#elif defined(__HIP_DEVICE_COMPILE__)
 #define GTN __device__ __attribute__((noinline))
 #else
 #define GTN static inline

@@ -106,6 +106,66 @@ __device__ void rlc_reduce(Jac<F>* redA, Jac<F>* redB, const Jac<F>& q, uint32_t
   __syncthreads();  // the arrays are reused by the next reduction
 }
 
+// The two G1 sums of a DecryptionShare tile (S = sum r_i d_i, P = sum r_i pk_i), each with its
+// position-weighted sum, in ONE tree with every level's S and P merges on different lanes.
+// Level 1 pairs lanes (2m, 2m+1) in registers: the even lane forms the S pair, the odd lane the
+// P pair (A = left + right, B = right).  From then on LDS entry 2m holds an S group and entry
+// 2m+1 a P group; at level s the lanes with lane mod 2s in {0, 1} merge entry `lane` with entry
+// `lane + s` (A = A_l + A_r, B = B_l + B_r + s A_r).  Outputs as rlc_reduce: [0..7] the aligned
+// groups of 8, [8] the tile.  Half the sequential merge chain of two separate reductions.
+__device__ __forceinline__ void rlc_reduce_sp(G1J* redA, G1J* redB, const G1J& S, const G1J& P,
+                                              uint32_t lane, G1J* outS, G1J* outSW, G1J* outP,
+                                              G1J* outPW) {
+  const bool odd = (lane & 1u) != 0;
+  G1J x = odd ? S : P, y;  // the value the neighbour lane needs
+  {
+    const uint32_t* xs = reinterpret_cast<const uint32_t*>(&x);
+    uint32_t* ys = reinterpret_cast<uint32_t*>(&y);
+    const int addr = (int)((lane ^ 1u) << 2);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(G1J) / 4); ++i)
+      ys[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)xs[i]);
+  }
+  G1J a;
+  const G1J& l = odd ? y : S;
+  const G1J& r = odd ? P : y;
+  jac_add(a, l, r);
+  redA[lane] = a;
+  redB[lane] = r;
+  __syncthreads();
+  for (uint32_t s = 2; s < 64; s <<= 1) {
+    if ((lane & (2 * s - 1)) < 2) {
+      G1J al = redA[lane], ar = redA[lane + s];
+      G1J bl = redB[lane], br = redB[lane + s];
+      jac_add(bl, bl, br);
+      G1J sa = ar;
+      for (uint32_t d = 1; d < s; d <<= 1) jac_dbl(sa, sa);
+      jac_add(bl, bl, sa);
+      jac_add(al, al, ar);
+      redA[lane] = al;
+      redB[lane] = bl;
+    }
+    __syncthreads();
+    if (s == 4 && (lane & 7u) < 2) {
+      if ((lane & 7u) == 0) {
+        outS[lane >> 3] = redA[lane];
+        outSW[lane >> 3] = redB[lane];
+      } else {
+        outP[lane >> 3] = redA[lane];
+        outPW[lane >> 3] = redB[lane];
+      }
+    }
+  }
+  if (lane == 0) {
+    outS[8] = redA[0];
+    outSW[8] = redB[0];
+  } else if (lane == 1) {
+    outP[8] = redA[1];
+    outPW[8] = redB[1];
+  }
+  __syncthreads();
+}
+
 // [a] pk + [b] phi(pk) from the key set's fixed-base table (8 mixed additions, no doublings).
 static __device__ void rlc_pk_mul(G1J& r, const PtXY* __restrict__ tab, uint32_t a, uint32_t b) {
   jac_set_inf(r);

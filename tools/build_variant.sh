@@ -1,21 +1,34 @@
 #!/bin/bash
-# Build a variant of libhbtc.so whose RLC kernels (hbtc_rlc.hip parts 6 and 7) use extra
-# compile flags, for occupancy / register-allocation experiments:
-#   tools/build_variant.sh NAME "P6 FLAGS" "P7 FLAGS"
+# Build a variant of libhbtc.so with extra compile flags on chosen objects, for occupancy /
+# register-allocation / inlining experiments:
+#   tools/build_variant.sh NAME OBJ "FLAGS" [OBJ "FLAGS" ...]
+#   OBJ is a build/ object stem: hbtc_check, hbtc_sig, hbtc_rlc.p6, hbtc_msm.p8, ...
 #   -> hbbft_amd/libhbtc_NAME.so   (select it with HBTC_LIB_PATH=... python bench.py)
-# The other objects come from the regular build (make lib must have run).
+# Every other object comes from the regular build (make lib must have run).
 set -euo pipefail
 cd "$(dirname "$0")/.."
-name=$1
-p6flags=${2:-}
-p7flags=${3:-}
+name=$1; shift
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Ihbbft_amd/csrc"
 out=build/var_$name
 mkdir -p "$out"
-$HIPCC $FLAGS -DHBTC_PART=6 -DHBTC_INLINE_ALL $p6flags -c hbbft_amd/csrc/hbtc_rlc.hip -o "$out/p6.o" &
-$HIPCC $FLAGS -DHBTC_PART=7 $p7flags -c hbbft_amd/csrc/hbtc_rlc.hip -o "$out/p7.o" &
+declare -A extra
+while [ $# -ge 2 ]; do extra[$1]=$2; shift 2; done
+objs=()
+for o in build/*.o; do
+  stem=$(basename "$o" .o)
+  if [ -n "${extra[$stem]+x}" ]; then
+    src=${stem%%.p*}
+    part=""
+    if [[ $stem == *.p* ]]; then part="-DHBTC_PART=${stem##*.p}"; fi
+    base=""
+    case $stem in hbtc_rlc.p6) base="-DHBTC_INLINE_ALL -DHBTC_FQMUL_INLINE";; hbtc_sig) base="-DHBTC_INLINE_ALL";; esac
+    $HIPCC $FLAGS $part $base ${extra[$stem]} -c "hbbft_amd/csrc/$src.hip" -o "$out/$stem.o" &
+    objs+=("$out/$stem.o")
+  else
+    objs+=("$o")
+  fi
+done
 wait
-$HIPCC --offload-arch=gfx950 -shared -fPIC build/hbtc_kernels.p{1,2,3,4,5}.o "$out/p6.o" "$out/p7.o" \
-  build/hbtc_api.o -o "hbbft_amd/libhbtc_$name.so"
+$HIPCC --offload-arch=gfx950 -shared -fPIC "${objs[@]}" -o "hbbft_amd/libhbtc_$name.so"
 echo "built hbbft_amd/libhbtc_$name.so"
