@@ -276,6 +276,43 @@ HDN void jac_mul2_u32(Jac<F>& r, const Aff<F>& p, uint32_t a, const Aff<F>& q, u
   r = acc;
 }
 
+// [a] p + [b] q in G1 (32-bit a, b) with ONE mixed addition per bit from the table {p, q, p + q}
+// (p + q made affine by one binary-GCD inversion): every lane of a wave runs the same 32
+// doublings and 32 additions.  The two-branch form (jac_mul2_u32) diverges on random scalars,
+// so a wave pays both additions on nearly every bit (32 doublings + 64 additions).
+HD void g1_mul2_u32_uniform(G1J& r, const G1A& p, uint32_t a, const G1A& q, uint32_t b) {
+  G1J s;
+  jac_from_aff(s, p);
+  jac_add_aff(s, s, q);
+  G1A pq;
+  pq.inf = jac_is_inf(s) ? 1u : 0u;
+  {
+    Fq zi, zi2, zi3;
+    fq_inv_binary(zi, s.z);  // s.z = 0 (infinity): garbage, unused (pq.inf)
+    fq_sqr(zi2, zi);
+    fq_mul(zi3, zi2, zi);
+    fq_mul(pq.x, s.x, zi2);
+    fq_mul(pq.y, s.y, zi3);
+  }
+  G1J acc;
+  jac_set_inf(acc);
+  for (int bit = 31; bit >= 0; --bit) {
+    jac_dbl(acc, acc);
+    const bool ba = ((a >> bit) & 1u) != 0, bb = ((b >> bit) & 1u) != 0;
+    G1A t;
+    fq_sel(t.x, bb, ba ? pq.x : q.x, p.x);
+    fq_sel(t.y, bb, ba ? pq.y : q.y, p.y);
+    t.inf = bb ? (ba ? pq.inf : q.inf) : p.inf;
+    G1J n;
+    jac_add_aff(n, acc, t);
+    const bool take = ba || bb;
+    fq_sel(acc.x, take, n.x, acc.x);
+    fq_sel(acc.y, take, n.y, acc.y);
+    fq_sel(acc.z, take, n.z, acc.z);
+  }
+  r = acc;
+}
+
 // GLV endomorphism of G1: phi(x, y) = (beta x, y) = [-x^2] (x, y) on the r-order subgroup
 HD void g1_phi(G1A& r, const G1A& p) {
   Fq beta;

@@ -67,10 +67,6 @@ HD Pos pos() {
 }
 HD uint32_t src(const Pos& ps, uint32_t k) { return ps.base + k; }
 
-HD void fq_sel(Fq& r, bool c, const Fq& a, const Fq& b) {  // r = c ? a : b
-#pragma unroll
-  for (int i = 0; i < 12; ++i) r.v[i] = c ? a.v[i] : b.v[i];
-}
 HD void fq2_sel(Fq2& r, bool c, const Fq2& a, const Fq2& b) {
   fq_sel(r.c0, c, a.c0, b.c0);
   fq_sel(r.c1, c, a.c1, b.c1);
@@ -354,90 +350,7 @@ GTN void exp_by_x(Fq2& r, const Fq2& y, const Pos& ps) {
   r = acc;
 }
 
-// Inversion in Fq by the binary extended Euclidean algorithm (variable time: every input is
-// public), about a quarter of the instruction count of the Fermat power a^(p-2).
-// Invariants x1 A = u, x2 A = v (mod p) with A the canonical input, u, v odd after the first
-// step; each iteration subtracts the smaller of u, v from the larger and strips the difference's
-// factors of two (up to 31 per iteration: x <- x / 2^k mod p as (x + m p) / 2^k with
-// m = -x p^-1 mod 2^k, the Montgomery digit).  The loop is wave-uniform: lanes that finished
-// keep their state until every lane has.  Montgomery in, Montgomery out: for the input aR the
-// loop finds x = (aR)^-1 and the result is x R^3 R^-1 = a^-1 R.
-HD void half_k(Fq& x, uint32_t k) {  // x / 2^k mod p for x < p, 0 <= k <= 31  (result < p)
-  const uint32_t mask = k ? (0xffffffffu >> (32 - k)) : 0u;
-  const uint32_t m = (x.v[0] * FQ_NP) & mask;
-  uint32_t t[13];
-  uint64_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    c += (uint64_t)m * FQ_P[i] + x.v[i];
-    t[i] = (uint32_t)c;
-    c >>= 32;
-  }
-  t[12] = (uint32_t)c;
-#pragma unroll
-  for (int i = 0; i < 12; ++i)
-    x.v[i] = k ? ((t[i] >> k) | (t[i + 1] << (32 - k))) : t[i];
-  fq_canon(x, x);  // (x + m p) / 2^k < 2p
-}
-HD uint32_t ctz31(const Fq& a) {
-  const uint32_t w = a.v[0];
-  return w ? (uint32_t)__builtin_ctz(w) : 31u;
-}
-HD void shr_k(Fq& a, uint32_t k) {
-#pragma unroll
-  for (int i = 0; i < 11; ++i) a.v[i] = k ? ((a.v[i] >> k) | (a.v[i + 1] << (32 - k))) : a.v[i];
-  a.v[11] = a.v[11] >> k;
-}
-HD void fq_inv_binary(Fq& r, const Fq& a_mont) {
-  Fq u, v, x1, x2, one;
-  fq_canon(u, a_mont);
-  limbs_set_const<12>(v, FQ_P);
-  limbs_zero<12>(x1);
-  x1.v[0] = 1;
-  limbs_zero<12>(x2);
-  limbs_zero<12>(one);
-  one.v[0] = 1;
-  bool zero = limbs_is_zero<12>(u);
-  {  // make u odd
-    uint32_t k = ctz31(u);
-#pragma unroll 1
-    for (int rep = 0; rep < 13 && k && !zero; ++rep) {
-      shr_k(u, k);
-      half_k(x1, k);
-      k = ctz31(u);
-    }
-  }
-  bool done = zero || limbs_eq<12>(u, one);
-#pragma unroll 1
-  for (int it = 0; it < 2 * 384; ++it) {
-    if (!wave_any(!done)) break;
-    Fq duv, dvu, d, xd, t;
-    const bool ge = limbs_sub<12>(duv, u, v) == 0;  // u >= v
-    limbs_sub<12>(dvu, v, u);
-    fq_sel(d, ge, duv, dvu);
-    // xd = ge ? x1 - x2 : x2 - x1 (mod p, canonical)
-    Fq xa, xb;
-    fq_sel(xa, ge, x1, x2);
-    fq_sel(xb, ge, x2, x1);
-    const uint32_t bw = limbs_sub<12>(xd, xa, xb);
-    limbs_add_const<12>(t, xd, FQ_P);
-    fq_sel(xd, bw != 0, t, xd);
-    uint32_t k = ctz31(d);
-    shr_k(d, k);
-    half_k(xd, k);
-    if (!done) {
-      fq_sel(u, ge, d, u);
-      fq_sel(x1, ge, xd, x1);
-      fq_sel(v, ge, v, d);
-      fq_sel(x2, ge, x2, xd);
-    }
-    done = done || limbs_eq<12>(u, one) || limbs_eq<12>(v, one);
-  }
-  Fq x, r3;
-  fq_sel(x, limbs_eq<12>(u, one), x1, x2);
-  limbs_set_const<12>(r3, FQ_R3);
-  fq_mul(r, x, r3);
-}
+// fq_inv_binary: field.h (binary extended Euclid, also used by the item passes).
 
 // f^(p^6 - 1) = conj(f)^2 / N with N = f conj(f) in Fq6 (coefficients 0, 2, 4 = its
 // v-basis digits n0, n1, n2); N^-1 = (t0 + t1 v + t2 v^2) / d with

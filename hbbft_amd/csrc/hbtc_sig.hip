@@ -97,7 +97,7 @@ __device__ __forceinline__ void g2j_plines(Fq2* out, uint32_t* inf, const G2J& S
   fq_sqr(nrm, S.z.c0);
   fq_sqr(t, S.z.c1);
   fq_add(nrm, nrm, t);
-  gt::fq_inv_binary(ni, nrm);
+  fq_inv_binary(ni, nrm);
   Fq2 zi, zi2, zi3;
   fq_mul(zi.c0, S.z.c0, ni);
   fq_mul(t, S.z.c1, ni);
