@@ -276,39 +276,62 @@ HDN void jac_mul2_u32(Jac<F>& r, const Aff<F>& p, uint32_t a, const Aff<F>& q, u
   r = acc;
 }
 
-// [a] p + [b] q in G1 (32-bit a, b) with ONE mixed addition per bit from the table {p, q, p + q}
+// 1/a by one binary-GCD inversion in Fq (Fq2: through the norm, conj(a) / (a0^2 + a1^2))
+HD void finv_fast(Fq& r, const Fq& a) { fq_inv_binary(r, a); }
+HD void finv_fast(Fq2& r, const Fq2& a) {
+  Fq n, t, ni;
+  fq_sqr(n, a.c0);
+  fq_sqr(t, a.c1);
+  fq_add(n, n, t);
+  fq_inv_binary(ni, n);
+  fq_mul(r.c0, a.c0, ni);
+  fq_mul(t, a.c1, ni);
+  fq_neg(r.c1, t);
+}
+template <class F>
+HD void fsel(F& r, bool c, const F& a, const F& b);
+template <>
+HD void fsel<Fq>(Fq& r, bool c, const Fq& a, const Fq& b) { fq_sel(r, c, a, b); }
+template <>
+HD void fsel<Fq2>(Fq2& r, bool c, const Fq2& a, const Fq2& b) {
+  fq_sel(r.c0, c, a.c0, b.c0);
+  fq_sel(r.c1, c, a.c1, b.c1);
+}
+
+// [a] p + [b] q (32-bit a, b) with ONE mixed addition per bit from the table {p, q, p + q}
 // (p + q made affine by one binary-GCD inversion): every lane of a wave runs the same 32
 // doublings and 32 additions.  The two-branch form (jac_mul2_u32) diverges on random scalars,
 // so a wave pays both additions on nearly every bit (32 doublings + 64 additions).
-HD void g1_mul2_u32_uniform(G1J& r, const G1A& p, uint32_t a, const G1A& q, uint32_t b) {
-  G1J s;
+template <class F>
+HD void jac_mul2_u32_uniform(Jac<F>& r, const Aff<F>& p, uint32_t a, const Aff<F>& q, uint32_t b) {
+  Jac<F> s;
   jac_from_aff(s, p);
   jac_add_aff(s, s, q);
-  G1A pq;
+  Aff<F> pq;
   pq.inf = jac_is_inf(s) ? 1u : 0u;
   {
-    Fq zi, zi2, zi3;
-    fq_inv_binary(zi, s.z);  // s.z = 0 (infinity): garbage, unused (pq.inf)
-    fq_sqr(zi2, zi);
-    fq_mul(zi3, zi2, zi);
-    fq_mul(pq.x, s.x, zi2);
-    fq_mul(pq.y, s.y, zi3);
+    F zi, zi2, zi3;
+    finv_fast(zi, s.z);  // s.z = 0 (infinity): garbage, unused (pq.inf)
+    fsqr(zi2, zi);
+    fmul(zi3, zi2, zi);
+    fmul(pq.x, s.x, zi2);
+    fmul(pq.y, s.y, zi3);
   }
-  G1J acc;
+  Jac<F> acc;
   jac_set_inf(acc);
   for (int bit = 31; bit >= 0; --bit) {
     jac_dbl(acc, acc);
     const bool ba = ((a >> bit) & 1u) != 0, bb = ((b >> bit) & 1u) != 0;
-    G1A t;
-    fq_sel(t.x, bb, ba ? pq.x : q.x, p.x);
-    fq_sel(t.y, bb, ba ? pq.y : q.y, p.y);
+    Aff<F> t;
+    fsel(t.x, bb, ba ? pq.x : q.x, p.x);
+    fsel(t.y, bb, ba ? pq.y : q.y, p.y);
     t.inf = bb ? (ba ? pq.inf : q.inf) : p.inf;
-    G1J n;
+    Jac<F> n;
     jac_add_aff(n, acc, t);
     const bool take = ba || bb;
-    fq_sel(acc.x, take, n.x, acc.x);
-    fq_sel(acc.y, take, n.y, acc.y);
-    fq_sel(acc.z, take, n.z, acc.z);
+    fsel(acc.x, take, n.x, acc.x);
+    fsel(acc.y, take, n.y, acc.y);
+    fsel(acc.z, take, n.z, acc.z);
   }
   r = acc;
 }

@@ -89,7 +89,7 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
           const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
           G1A pd;
           g1_phi(pd, d);
-          g1_mul2_u32_uniform(S, d, ra, pd, rb);
+          jac_mul2_u32_uniform(S, d, ra, pd, rb);
           if (!pk[id].inf) rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb);
         }
       }

@@ -72,7 +72,7 @@ __global__ void __launch_bounds__(64, HBTC_SIG_ITEMS_WAVES) k_sig_items(
           const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
           G2A ms;
           g2_mu(ms, sg);
-          jac_mul2_u32(S, sg, ra, ms, rb);
+          jac_mul2_u32_uniform(S, sg, ra, ms, rb);
           if (!pk[id].inf) rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb);
         }
       }
