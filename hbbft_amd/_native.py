@@ -90,6 +90,7 @@ SIGNATURES = {
     "hbtc_hash_bytes": (_I32, [_P, _SZ, _P]),
     "hbtc_xor_hash_bytes_batch": (_I32, [_U32, _P, _P, _P, _P]),
     "hbtc_commitment_evaluate": (_I32, [_P, _U32, _P, _U32, _P, _P, _P]),
+    "hbtc_decrypt": (_I32, [_P, _U32, _P, _P, _P, _P, _P, _P, _P]),
     "hbtc_stream_wait_ctx": (_I32, [_P, _P]),
     "hbtc_ctx_wait_stream": (_I32, [_P, _P]),
     "hbtc_shard_items": (_I32, [_U32, _U32, _U32, _P, ctypes.POINTER(_U32), ctypes.POINTER(_U32),
@@ -454,6 +455,21 @@ class Context:
                                                  _ptr(ok), ap.size, _ptr(ap), _ptr(sd), _ptr(vb),
                                                  _ptr(st)), "hbtc_skg_check_acks")
         return st
+
+    # ---- SecretKey::decrypt
+    def decrypt(self, sk, us, ws, vs):
+        """[plaintext or None] and status for ciphertexts (u_i, v_i, w_i) under secret key sk."""
+        buf, off = _msg_batch(vs)
+        n = off.size - 1
+        if n == 0:
+            return [], np.zeros(0, np.int32)
+        u, w = _join(us, 48), _join(ws, 96)
+        out = np.zeros(max(1, int(off[-1])), np.uint8)
+        st = np.zeros(n, np.int32)
+        k = np.frombuffer(int(sk).to_bytes(32, "little"), np.uint8).copy()
+        self._check(self.lib.hbtc_decrypt(self.h, n, _ptr(k), _ptr(u), _ptr(w), _ptr(buf), _ptr(off),
+                                          _ptr(out), _ptr(st)), "hbtc_decrypt")
+        return [bytes(out[off[i]:off[i + 1]]) if st[i] == ACCEPT else None for i in range(n)], st
 
     # ---- commitments
     def commitment_evaluate(self, commit, xs):

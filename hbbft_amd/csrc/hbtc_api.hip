@@ -22,6 +22,10 @@ namespace hbtc {
 void hash_g2_c96(const uint8_t* msg, size_t len, uint8_t* out96);
 void g1_g2_message(const uint8_t* g1_c48, const uint8_t* msg, size_t len, std::vector<uint8_t>& m);
 void hash_g2_candidate(const uint8_t* msg, size_t len, G2A& p);
+void hash_g1_g2_c96(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8_t* out96);
+hipError_t launch_hash_cand(hipStream_t s, uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
+                            const uint32_t* offsets, G2A* cand);
+void hash_bytes(const uint8_t* g1_c48, size_t len, uint8_t* out);
 void parallel_items(uint32_t n, const std::function<void(uint32_t)>& f);
 bool hash_offsets_ok(uint32_t n, const uint32_t* offsets);
 hipError_t launch_g2_clear_cofactor(hipStream_t s, uint32_t n, const G2A* in, uint8_t* out_c96,
@@ -671,7 +675,7 @@ int point_mul_host(hbtc_ctx* c, int group, uint32_t n, const uint8_t* base,
   HB_TRY(ws(c, "out1", (size_t)4 * n, &d_st));
   HB_TRY(timed(c, "mul", [&] {
     return launch_point_mul(c->stream, group, n, (const uint8_t*)d_base, base_stride,
-                            (const uint8_t*)d_k, (uint8_t*)d_out, (int32_t*)d_st);
+                            (const uint8_t*)d_k, 1, (uint8_t*)d_out, (int32_t*)d_st);
   }));
   HB_TRY(download(c, out, d_out, pb * n));
   HB_TRY(download(c, status, d_st, (size_t)4 * n));
@@ -1522,24 +1526,40 @@ int hbtc_timing_reset(hbtc_ctx* c) {
 }
 
 // ---- hashes with the cofactor clearing on the GPU (the host draws the candidates)
-static int hash_batch_gpu(hbtc_ctx* c, uint32_t n, const std::vector<std::vector<uint8_t>>& msgs,
-                          uint8_t* out_c96) {
-  std::vector<G2A> cand(n);
-  parallel_items(n, [&](uint32_t i) { hash_g2_candidate(msgs[i].data(), msgs[i].size(), cand[i]); });
+// hash_g2(msg_i) (g1 == null) or hash_g1_g2(g1_i, msg_i) for a batch, entirely on the GPU: the
+// candidate draw (k_hash_cand: sha3, rand 0.4 ChaCha, G2::rand's loop) and [h2] P; a candidate
+// whose [h2] P is O (probability ~2^-250) continues G2::rand's loop on the host (exact).
+static int hash_batch_gpu(hbtc_ctx* c, uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
+                          const uint32_t* offsets, uint8_t* out_c96, uint8_t** d_out_keep = nullptr) {
   HB_TRY(sync(c));
-  void* d_cand;
+  void *d_msgs, *d_off, *d_g1 = nullptr;
+  G2A* d_cand;
   uint8_t* d_out;
   int32_t* d_st;
-  HB_TRY(stage_upload(c, "hash.cand", cand.data(), (size_t)n * sizeof(G2A), c->stream, &d_cand));
+  HB_TRY(upload(c, "hash.msgs", msgs, offsets[n] ? offsets[n] : 1, &d_msgs));
+  HB_TRY(upload(c, "hash.off", offsets, (size_t)4 * (n + 1), &d_off));
+  if (g1_c48) HB_TRY(upload(c, "hash.g1", g1_c48, (size_t)48 * n, &d_g1));
+  HB_TRY(wst(c, "hash.cand", n, &d_cand));
   HB_TRY(wst(c, "hash.out", (size_t)n * 96, &d_out));
   HB_TRY(wst(c, "hash.st", n, &d_st));
-  HB_CHECK(c, launch_g2_clear_cofactor(c->stream, n, (const G2A*)d_cand, d_out, d_st));
+  HB_TRY(timed(c, "hash", [&] {
+    return launch_hash_cand(c->stream, n, (const uint8_t*)d_g1, (const uint8_t*)d_msgs,
+                            (const uint32_t*)d_off, d_cand);
+  }));
+  HB_TRY(timed(c, "hash", [&] { return launch_g2_clear_cofactor(c->stream, n, d_cand, d_out, d_st); }));
   std::vector<int32_t> st(n);
   HB_CHECK(c, hipMemcpyAsync(out_c96, d_out, (size_t)n * 96, hipMemcpyDeviceToHost, c->stream));
   HB_CHECK(c, hipMemcpyAsync(st.data(), d_st, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
   HB_TRY(sync(c));
   for (uint32_t i = 0; i < n; ++i)  // [h2] P = O: G2::rand draws again (host, exact)
-    if (st[i]) hash_g2_c96(msgs[i].data(), msgs[i].size(), out_c96 + 96 * (size_t)i);
+    if (st[i]) {
+      if (g1_c48)
+        hash_g1_g2_c96(g1_c48 + 48 * (size_t)i, msgs + offsets[i], offsets[i + 1] - offsets[i],
+                       out_c96 + 96 * (size_t)i);
+      else
+        hash_g2_c96(msgs + offsets[i], offsets[i + 1] - offsets[i], out_c96 + 96 * (size_t)i);
+    }
+  if (d_out_keep) *d_out_keep = d_out;
   return HBTC_OK;
 }
 
@@ -1550,9 +1570,7 @@ int hbtc_hash_g2_batch_gpu(hbtc_ctx* c, uint32_t n, const uint8_t* msgs, const u
   if (!offsets || !out_c96 || (!msgs && offsets[n]) || !hash_offsets_ok(n, offsets))
     return HBTC_ERR_ARG;
   Guard g(c);
-  std::vector<std::vector<uint8_t>> m(n);
-  for (uint32_t i = 0; i < n; ++i) m[i].assign(msgs + offsets[i], msgs + offsets[i + 1]);
-  return hash_batch_gpu(c, n, m, out_c96);
+  return hash_batch_gpu(c, n, nullptr, msgs, offsets, out_c96);
 }
 
 int hbtc_hash_g1_g2_batch_gpu(hbtc_ctx* c, uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
@@ -1562,11 +1580,59 @@ int hbtc_hash_g1_g2_batch_gpu(hbtc_ctx* c, uint32_t n, const uint8_t* g1_c48, co
   if (!g1_c48 || !offsets || !out_c96 || (!msgs && offsets[n]) || !hash_offsets_ok(n, offsets))
     return HBTC_ERR_ARG;
   Guard g(c);
-  std::vector<std::vector<uint8_t>> m(n);
+  return hash_batch_gpu(c, n, g1_c48, msgs, offsets, out_c96);
+}
+
+int hbtc_decrypt(hbtc_ctx* c, uint32_t n, const uint8_t* sk_le32, const uint8_t* u_c48,
+                 const uint8_t* w_c96, const uint8_t* msgs, const uint32_t* offsets, uint8_t* out,
+                 int32_t* status) {
+  if (!c) return HBTC_ERR_ARG;
+  if (n == 0) return HBTC_OK;
+  if (!sk_le32 || !u_c48 || !w_c96 || !offsets || !status || (offsets[n] && (!msgs || !out)) ||
+      !hash_offsets_ok(n, offsets))
+    return HBTC_ERR_ARG;
+  Guard g(c);
+  // 1. H_i = hash_g1_g2(u_i, v_i) on the GPU
+  std::vector<uint8_t> H((size_t)n * 96);
+  HB_TRY(hash_batch_gpu(c, n, u_c48, msgs, offsets, H.data()));
+  // 2. Ciphertext::verify: e(G1, w) == e(u, H);  3. g = sk * u
+  Fr k;
+  scalar_mod_r(k.v, sk_le32);
+  void *d_u, *d_H, *d_w, *d_st, *d_k, *d_g, *d_gst;
+  HB_TRY(upload(c, "in0", u_c48, (size_t)48 * n, &d_u));
+  HB_TRY(upload(c, "in1", H.data(), (size_t)96 * n, &d_H));
+  HB_TRY(upload(c, "in2", w_c96, (size_t)96 * n, &d_w));
+  HB_TRY(upload(c, "in3", k.v, 32, &d_k));
+  HB_TRY(ws(c, "out0", (size_t)4 * n, &d_st));
+  HB_TRY(ws(c, "out1", (size_t)48 * n, &d_g));
+  HB_TRY(ws(c, "out2", (size_t)4 * n, &d_gst));
+  HB_TRY(timed(c, "pair_verify", [&] {
+    return launch_pair_verify(c->stream, n, nullptr, (const uint8_t*)d_w, (const uint8_t*)d_u,
+                              (const uint8_t*)d_H, (int32_t*)d_st);
+  }));
+  HB_TRY(timed(c, "mul", [&] {
+    return launch_point_mul(c->stream, 1, n, (const uint8_t*)d_u, 1, (const uint8_t*)d_k, 0,
+                            (uint8_t*)d_g, (int32_t*)d_gst);
+  }));
+  std::vector<uint8_t> gb((size_t)n * 48);
+  std::vector<int32_t> gst(n);
+  HB_TRY(download(c, status, d_st, (size_t)4 * n));
+  HB_TRY(download(c, gb.data(), d_g, (size_t)48 * n));
+  HB_TRY(download(c, gst.data(), d_gst, (size_t)4 * n));
+  HB_TRY(sync(c));
+  // 4. plaintext = v XOR hash_bytes(g, |v|) for the ciphertexts that verify
   parallel_items(n, [&](uint32_t i) {
-    g1_g2_message(g1_c48 + 48 * (size_t)i, msgs + offsets[i], offsets[i + 1] - offsets[i], m[i]);
+    if (status[i] == HBTC_ACCEPT && gst[i] != HBTC_ACCEPT) status[i] = HBTC_DECODE_ERR;
+    const size_t len = offsets[i + 1] - offsets[i];
+    uint8_t* o = out + offsets[i];
+    if (status[i] != HBTC_ACCEPT) {
+      if (len) memset(o, 0, len);
+      return;
+    }
+    hash_bytes(gb.data() + 48 * (size_t)i, len, o);
+    for (size_t j2 = 0; j2 < len; ++j2) o[j2] ^= msgs[offsets[i] + j2];
   });
-  return hash_batch_gpu(c, n, m, out_c96);
+  return HBTC_OK;
 }
 
 }  // extern "C"

@@ -28,19 +28,24 @@ namespace hbtc {
 namespace {
 
 // ------------------------------------------------------------------ SHA3-256 (FIPS 202)
-const uint64_t KECCAK_RC[24] = {
-    0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808aull, 0x8000000080008000ull,
-    0x000000000000808bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
-    0x000000000000008aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000aull,
-    0x000000008000808bull, 0x800000000000008bull, 0x8000000000008089ull, 0x8000000000008003ull,
-    0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800aull, 0x800000008000000aull,
-    0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
-const int KECCAK_ROT[25] = {0,  1,  62, 28, 27, 36, 44, 6,  55, 20, 3,  10, 43,
-                            25, 39, 41, 45, 15, 21, 8,  18, 2,  61, 56, 14};
+// Host + device: the GPU candidate kernel (k_hash_cand) runs the same code as the host path.
+#define HASH_HD __host__ __device__ inline
+HASH_HD uint64_t keccak_rc(int i) {
+  const uint64_t RC[24] = {
+      0x0000000000000001ull, 0x0000000000008082ull, 0x800000000000808aull, 0x8000000080008000ull,
+      0x000000000000808bull, 0x0000000080000001ull, 0x8000000080008081ull, 0x8000000000008009ull,
+      0x000000000000008aull, 0x0000000000000088ull, 0x0000000080008009ull, 0x000000008000000aull,
+      0x000000008000808bull, 0x800000000000008bull, 0x8000000000008089ull, 0x8000000000008003ull,
+      0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800aull, 0x800000008000000aull,
+      0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
+  return RC[i];
+}
 
-inline uint64_t rotl64(uint64_t v, int c) { return c ? (v << c) | (v >> (64 - c)) : v; }
+HASH_HD uint64_t rotl64(uint64_t v, int c) { return c ? (v << c) | (v >> (64 - c)) : v; }
 
-void keccak_f(uint64_t a[25]) {
+HASH_HD void keccak_f(uint64_t a[25]) {
+  const int ROT[25] = {0,  1,  62, 28, 27, 36, 44, 6,  55, 20, 3,  10, 43,
+                       25, 39, 41, 45, 15, 21, 8,  18, 2,  61, 56, 14};
   for (int round = 0; round < 24; ++round) {
     uint64_t c[5], b[25];
     for (int x = 0; x < 5; ++x) c[x] = a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20];
@@ -50,51 +55,65 @@ void keccak_f(uint64_t a[25]) {
     }
     // rho + pi: b[y, 2x + 3y] = rot(a[x, y])
     for (int x = 0; x < 5; ++x)
-      for (int y = 0; y < 5; ++y) b[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(a[x + 5 * y], KECCAK_ROT[x + 5 * y]);
+      for (int y = 0; y < 5; ++y) b[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(a[x + 5 * y], ROT[x + 5 * y]);
     for (int y = 0; y < 25; y += 5)
       for (int x = 0; x < 5; ++x) a[y + x] = b[y + x] ^ (~b[y + (x + 1) % 5] & b[y + (x + 2) % 5]);
-    a[0] ^= KECCAK_RC[round];
+    a[0] ^= keccak_rc(round);
   }
 }
 
-void sha3_256(const uint8_t* msg, size_t len, uint8_t out[32]) {
-  const size_t rate = 136;
-  uint64_t a[25] = {0};
-  std::vector<uint8_t> buf(msg, msg + len);
-  buf.push_back(0x06);
-  while (buf.size() % rate) buf.push_back(0);
-  buf.back() |= 0x80;
-  for (size_t off = 0; off < buf.size(); off += rate) {
-    for (size_t i = 0; i < rate / 8; ++i) {
-      uint64_t v = 0;
-      for (int j = 7; j >= 0; --j) v = (v << 8) | buf[off + 8 * i + j];
-      a[i] ^= v;
-    }
-    keccak_f(a);
+// SHA3-256 of the concatenation p1 || p2, absorbed byte by byte (no buffer).
+struct Sha3 {
+  uint64_t a[25];
+  int pos;
+  HASH_HD Sha3() : pos(0) {
+    for (int i = 0; i < 25; ++i) a[i] = 0;
   }
-  for (int i = 0; i < 32; ++i) out[i] = (uint8_t)(a[i / 8] >> (8 * (i % 8)));
+  HASH_HD void absorb(const uint8_t* p, size_t len) {
+    for (size_t i = 0; i < len; ++i) {
+      a[pos >> 3] ^= (uint64_t)p[i] << (8 * (pos & 7));
+      if (++pos == 136) {
+        keccak_f(a);
+        pos = 0;
+      }
+    }
+  }
+  HASH_HD void finish(uint8_t out[32]) {
+    a[pos >> 3] ^= (uint64_t)0x06 << (8 * (pos & 7));
+    a[135 >> 3] ^= (uint64_t)0x80 << (8 * (135 & 7));
+    keccak_f(a);
+    for (int i = 0; i < 32; ++i) out[i] = (uint8_t)(a[i / 8] >> (8 * (i % 8)));
+  }
+};
+
+HASH_HD void sha3_256(const uint8_t* msg, size_t len, uint8_t out[32]) {
+  Sha3 h;
+  h.absorb(msg, len);
+  h.finish(out);
 }
 
 // ------------------------------------------------------------------ rand 0.4 ChaChaRng
 struct ChaCha04 {
   uint32_t state[16], buf[16];
   int index = 16;
-  explicit ChaCha04(const uint32_t seed[8]) {
-    const uint32_t k[4] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
-    for (int i = 0; i < 4; ++i) state[i] = k[i];
+  HASH_HD explicit ChaCha04(const uint32_t seed[8]) {
+    state[0] = 0x61707865u;
+    state[1] = 0x3320646eu;
+    state[2] = 0x79622d32u;
+    state[3] = 0x6b206574u;
     for (int i = 0; i < 8; ++i) state[4 + i] = seed[i];
     for (int i = 12; i < 16; ++i) state[i] = 0;
   }
-  static inline uint32_t rotl(uint32_t v, int c) { return (v << c) | (v >> (32 - c)); }
-  static inline void qr(uint32_t* s, int a, int b, int c, int d) {
+  static HASH_HD uint32_t rotl(uint32_t v, int c) { return (v << c) | (v >> (32 - c)); }
+  static HASH_HD void qr(uint32_t* s, int a, int b, int c, int d) {
     s[a] += s[b]; s[d] = rotl(s[d] ^ s[a], 16);
     s[c] += s[d]; s[b] = rotl(s[b] ^ s[c], 12);
     s[a] += s[b]; s[d] = rotl(s[d] ^ s[a], 8);
     s[c] += s[d]; s[b] = rotl(s[b] ^ s[c], 7);
   }
-  void refill() {
+  HASH_HD void refill() {
     uint32_t s[16];
-    memcpy(s, state, sizeof(s));
+    for (int i = 0; i < 16; ++i) s[i] = state[i];
     for (int i = 0; i < 10; ++i) {
       qr(s, 0, 4, 8, 12); qr(s, 1, 5, 9, 13); qr(s, 2, 6, 10, 14); qr(s, 3, 7, 11, 15);
       qr(s, 0, 5, 10, 15); qr(s, 1, 6, 11, 12); qr(s, 2, 7, 8, 13); qr(s, 3, 4, 9, 14);
@@ -104,18 +123,18 @@ struct ChaCha04 {
     for (int i = 12; i < 16; ++i)  // 128-bit block counter
       if (++state[i] != 0) break;
   }
-  uint32_t next_u32() {
+  HASH_HD uint32_t next_u32() {
     if (index == 16) refill();
     return buf[index++];
   }
-  uint64_t next_u64() {  // rand 0.4's default: the first word is the high half
+  HASH_HD uint64_t next_u64() {  // rand 0.4's default: the first word is the high half
     const uint64_t hi = next_u32();
     return (hi << 32) | next_u32();
   }
 };
 
 // ff_derive Rand for Fq: the drawn limbs are the Montgomery representation
-void fq_rand(Fq& r, ChaCha04& rng) {
+HASH_HD void fq_rand(Fq& r, ChaCha04& rng) {
   for (;;) {
     uint64_t l[6];
     for (int i = 0; i < 6; ++i) l[i] = rng.next_u64();
@@ -135,7 +154,7 @@ const Limbs<16> G2_COFACTOR = {{0x1c7238e5u, 0xcf1c38e3u, 0x786f0c70u, 0x1616ec6
 
 // One draw of G2::rand's loop: x, greatest, get_point_from_x.  False if x^3 + b is not a square
 // (the loop draws again).
-bool g2_rand_candidate(G2A& p, ChaCha04& rng) {
+HASH_HD bool g2_rand_candidate(G2A& p, ChaCha04& rng) {
   Fq2 x;
   fq_rand(x.c0, rng);
   fq_rand(x.c1, rng);
@@ -173,12 +192,16 @@ void store_le_words(uint8_t* b, const uint32_t* w, int nwords) {
     for (int j = 0; j < 4; ++j) b[4 * i + j] = (uint8_t)(w[i] >> (8 * j));
 }
 
-void seed_of(const uint8_t* msg, size_t len, uint32_t seed[8]) {
-  uint8_t d[32];
-  sha3_256(msg, len, d);
+HASH_HD void seed_of_digest(const uint8_t d[32], uint32_t seed[8]) {
   for (int i = 0; i < 8; ++i)
     seed[i] = ((uint32_t)d[4 * i] << 24) | ((uint32_t)d[4 * i + 1] << 16) |
               ((uint32_t)d[4 * i + 2] << 8) | d[4 * i + 3];
+}
+
+void seed_of(const uint8_t* msg, size_t len, uint32_t seed[8]) {
+  uint8_t d[32];
+  sha3_256(msg, len, d);
+  seed_of_digest(d, seed);
 }
 
 }  // namespace
@@ -252,6 +275,44 @@ bool hash_offsets_ok(uint32_t n, const uint32_t* offsets) {
   for (uint32_t i = 0; i < n; ++i)
     if (offsets[i + 1] < offsets[i]) return false;
   return true;
+}
+
+// GPU candidates of hash_g2 / hash_g1_g2 (one lane per message): the seed, the ChaCha stream
+// and G2::rand's draw loop before [h2] — the host path's code (k_g2_clear_cofactor finishes).
+// g1_c48 != null: hash_g1_g2(u_i, v_i), the seed message (|v| > 64 ? sha3(v) : v) || u_i.
+__global__ void __launch_bounds__(64) k_hash_cand(uint32_t n, const uint8_t* __restrict__ g1_c48,
+                                                  const uint8_t* __restrict__ msgs,
+                                                  const uint32_t* __restrict__ offsets,
+                                                  G2A* __restrict__ cand) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* v = msgs + offsets[i];
+  const size_t len = offsets[i + 1] - offsets[i];
+  uint8_t d[32];
+  Sha3 h;
+  if (g1_c48 && len > 64) {
+    uint8_t inner[32];
+    sha3_256(v, len, inner);
+    h.absorb(inner, 32);
+  } else {
+    h.absorb(v, len);
+  }
+  if (g1_c48) h.absorb(g1_c48 + 48 * (size_t)i, 48);
+  h.finish(d);
+  uint32_t seed[8];
+  seed_of_digest(d, seed);
+  ChaCha04 rng(seed);
+  G2A p;
+  while (!g2_rand_candidate(p, rng)) {
+  }
+  cand[i] = p;
+}
+
+hipError_t launch_hash_cand(hipStream_t s, uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
+                            const uint32_t* offsets, G2A* cand) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hash_cand, dim3((n + 63) / 64), dim3(64), 0, s, n, g1_c48, msgs, offsets, cand);
+  return hipGetLastError();
 }
 
 // [h2] P for candidates P (one lane each) -> compressed G2 words; st = 1 if [h2] P = O (the

@@ -140,9 +140,10 @@ hipError_t launch_sig_verify(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
                              const int32_t* h_status, const Line* h_lines, int32_t* status);
 hipError_t launch_pair_verify(hipStream_t s, uint32_t n, const uint8_t* a1, const uint8_t* a2,
                               const uint8_t* b1, const uint8_t* b2, int32_t* status);
+// k_i P_i; base_stride / scalar_stride 0 = one base / scalar for every item
 hipError_t launch_point_mul(hipStream_t s, int group, uint32_t n, const uint8_t* base,
-                            uint32_t base_stride, const uint8_t* scalars, uint8_t* out,
-                            int32_t* status);
+                            uint32_t base_stride, const uint8_t* scalars, uint32_t scalar_stride,
+                            uint8_t* out, int32_t* status);
 
 // ---- batched Pippenger MSM + Lagrange combine (hbtc_msm.hip)
 // n_msm MSMs of n terms each; signed c-bit digits over W = ceil(256 / c) windows, 2^(c-1)

@@ -342,6 +342,7 @@ template <class F, int NW>
 __global__ void __launch_bounds__(64) k_point_mul(uint32_t n, const uint8_t* __restrict__ base,
                                                   uint32_t base_stride,
                                                   const uint8_t* __restrict__ scalars,
+                                                  uint32_t scalar_stride,
                                                   uint8_t* __restrict__ out,
                                                   int32_t* __restrict__ status) {
   const uint32_t i = blockIdx.x * 64 + threadIdx.x;
@@ -356,7 +357,7 @@ __global__ void __launch_bounds__(64) k_point_mul(uint32_t n, const uint8_t* __r
     return;
   }
   Fr k;
-  load_words(k.v, scalars, i, 8);
+  load_words(k.v, scalars, (size_t)i * scalar_stride, 8);
   Jac<F> r;
   jac_mul_fr(r, p, k);
   Aff<F> a;
@@ -367,9 +368,9 @@ __global__ void __launch_bounds__(64) k_point_mul(uint32_t n, const uint8_t* __r
 }
 
 template __global__ void k_point_mul<Fq, 12>(uint32_t, const uint8_t*, uint32_t, const uint8_t*,
-                                             uint8_t*, int32_t*);
+                                             uint32_t, uint8_t*, int32_t*);
 template __global__ void k_point_mul<Fq2, 24>(uint32_t, const uint8_t*, uint32_t,
-                                              const uint8_t*, uint8_t*, int32_t*);
+                                              const uint8_t*, uint32_t, uint8_t*, int32_t*);
 
 #endif  // part 1
 
@@ -448,15 +449,15 @@ hipError_t launch_pair_verify(hipStream_t s, uint32_t n, const uint8_t* a1, cons
 
 #if HBTC_IN_PART(1)
 hipError_t launch_point_mul(hipStream_t s, int group, uint32_t n, const uint8_t* base,
-                            uint32_t base_stride, const uint8_t* scalars, uint8_t* out,
-                            int32_t* status) {
+                            uint32_t base_stride, const uint8_t* scalars, uint32_t scalar_stride,
+                            uint8_t* out, int32_t* status) {
   if (n == 0) return hipSuccess;
   if (group == 1)
     hipLaunchKernelGGL((k_point_mul<Fq, 12>), dim3(blocks_for(n, 64)), dim3(64), 0, s, n, base,
-                       base_stride, scalars, out, status);
+                       base_stride, scalars, scalar_stride, out, status);
   else
     hipLaunchKernelGGL((k_point_mul<Fq2, 24>), dim3(blocks_for(n, 64)), dim3(64), 0, s, n, base,
-                       base_stride, scalars, out, status);
+                       base_stride, scalars, scalar_stride, out, status);
   return hipGetLastError();
 }
 

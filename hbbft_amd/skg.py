@@ -6,8 +6,7 @@ it, check it against the proposer's bivariate commitment — one BivarCommitment
 BivarCommitment::evaluate (Ack) per message, G1-MSM heavy.  Here messages queue in arrival order;
 ``flush`` then
   1. decrypts every queued ciphertext addressed to us in one batch (SecretKey::decrypt:
-     Ciphertext::verify + r*u + the hash_bytes pad; hbtc_verify_ciphertexts, hbtc_g1_mul,
-     hbtc_xor_hash_bytes_batch),
+     Ciphertext::verify + sk u + the hash_bytes pad; hbtc_decrypt),
   2. checks every decoded row in one hbtc_skg_check_parts call and every decoded value in one
      hbtc_skg_check_acks call (the value check of an Ack uses the commitment of the FIRST Part
      received from its proposer, the only one the reference ever stores, :346-354),
@@ -77,22 +76,13 @@ def encrypt_batch(ctx, pks, msgs, rs=None):
 
 
 def decrypt_batch(ctx, sk, cts):
-    """SecretKey::decrypt for n ciphertexts under one key: None where Ciphertext::verify fails
-    (or u / w does not decode), else v XOR hash_bytes(sk u)."""
-    n = len(cts)
-    if n == 0:
+    """SecretKey::decrypt for n ciphertexts under one key (hbtc_decrypt): None where
+    Ciphertext::verify fails (or u / w does not decode), else v XOR hash_bytes(sk u)."""
+    if not cts:
         return []
-    us = [bytes(c.u) for c in cts]
-    H = ctx.hash_g1_g2_batch(us, [bytes(c.v) for c in cts])
-    ok = ctx.verify_ciphertexts(us, H, [bytes(c.w) for c in cts]) == N.ACCEPT
-    g, st = ctx.g1_mul(us, _fr_le([sk] * n))
-    good = [i for i in range(n) if ok[i] and st[i] == N.ACCEPT]
-    pts = N.xor_hash_bytes_batch([bytes(g[48 * i:48 * i + 48]) for i in good],
-                                 [bytes(cts[i].v) for i in good])
-    out = [None] * n
-    for i, p in zip(good, pts):
-        out[i] = p
-    return out
+    pts, _ = ctx.decrypt(sk, [bytes(c.u) for c in cts], [bytes(c.w) for c in cts],
+                         [bytes(c.v) for c in cts])
+    return pts
 
 
 # ------------------------------------------------------------------------------ SyncKeyGen

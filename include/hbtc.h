@@ -121,6 +121,16 @@ int hbtc_combine_dec(hbtc_ctx* ctx, uint32_t n_ct, const uint32_t* offsets, cons
                      const uint8_t* share_c48, uint32_t t, uint8_t* out_g_c48,
                      int32_t* inst_status);
 
+/* SecretKey::decrypt for n ciphertexts (u_i, v_i, w_i) under ONE secret key (32-byte LE scalar):
+ * the row / value a node decrypts from every SyncKeyGen Part and Ack (src/sync_key_gen.rs:358,
+ * 481-484; 10^6 Acks per era at N = 1000).  Per item: H = hash_g1_g2(u, v) (host candidates, GPU
+ * cofactor clearing), Ciphertext::verify e(G1, w) == e(u, H) and g = sk u on the GPU, then
+ * out = v XOR hash_bytes(g, |v|) on the host's cores.  v_i = msgs[offsets[i] .. offsets[i+1]),
+ * out has the same layout.  status[i] = ACCEPT (decrypted), REJECT (Ciphertext::verify failed:
+ * decrypt returns None, Fault::ValueDecryption), DECODE_ERR (u or w does not decode). */
+int hbtc_decrypt(hbtc_ctx* ctx, uint32_t n, const uint8_t* sk_le32, const uint8_t* u_c48,
+                 const uint8_t* w_c96, const uint8_t* msgs, const uint32_t* offsets, uint8_t* out,
+                 int32_t* status);
 /* Ciphertext::verify: e(G1, w_i) == e(u_i, H_i) with H_i = hash_g1_g2(u_i, v_i). */
 int hbtc_verify_ciphertexts(hbtc_ctx* ctx, uint32_t n, const uint8_t* u_c48,
                             const uint8_t* H_c96, const uint8_t* w_c96, int32_t* status);

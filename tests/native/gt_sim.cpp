@@ -181,7 +181,7 @@ int ht_gt_op(int op, const uint8_t* a576, const uint8_t* b576, uint8_t* out576) 
 int ht_fq_inv_binary(uint32_t n, const uint8_t* in48, uint8_t* out48) {
   std::vector<Fq> a(n), r(n);
   for (uint32_t i = 0; i < n; ++i) fq_load_be(a[i], in48 + 48 * i);
-  run_lanes(n, [&](uint32_t l) { gt::fq_inv_binary(r[l], a[l]); });
+  run_lanes(n, [&](uint32_t l) { fq_inv_binary(r[l], a[l]); });
   for (uint32_t i = 0; i < n; ++i) fq_store_be(out48 + 48 * i, r[i]);
   return 0;
 }

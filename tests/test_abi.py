@@ -28,3 +28,12 @@ def test_no_device_is_reported_cleanly_without_gpu():
     n = N.device_count()
     assert n >= 0
     assert b"gfx950" in N.load().hbtc_version()
+
+
+def test_rust_ffi_matches_header():
+    """rust/hbtc-sys/src/ffi.rs is generated from include/hbtc.h (tools/gen_rust_ffi.py)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rc = subprocess.call([sys.executable, os.path.join(root, "tools", "gen_rust_ffi.py"), "--check"])
+    assert rc == 0, "run tools/gen_rust_ffi.py after changing include/hbtc.h"

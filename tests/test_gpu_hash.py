@@ -25,6 +25,7 @@ def test_gpu_hash_g2_matches_oracle_and_host(ctx):
     rng = random.Random(3)
     msgs = [b"", b"hbbft"] + [bytes(rng.randrange(256) for _ in range(rng.randrange(1, 120)))
                               for _ in range(70)]
+    msgs += [bytes(rng.randrange(256) for _ in range(L)) for L in (135, 136, 137, 271, 272, 500)]
     got = ctx.hash_g2_batch(msgs)
     assert got == N.hash_g2_batch(msgs)
     for m in msgs[:3]:

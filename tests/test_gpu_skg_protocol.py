@@ -244,3 +244,27 @@ def test_commitment_evaluate_matches_oracle(ctx):
     assert not st.any()
     for x, g in zip(xs, got):
         assert g == B.g1_compress(TC.commitment_evaluate([B.g1_decompress(c) for c in commit], x))
+
+
+def test_decrypt_batch_matches_oracle(ctx):
+    """hbtc_decrypt (SecretKey::decrypt over a batch): plaintexts of valid ciphertexts (short and
+    > 64-byte messages: hash_g1_g2 hashes long v first), None for a ciphertext whose w does not
+    match (Ciphertext::verify fails) and for an undecodable u."""
+    rng = random.Random(44)
+    sk = rng.randrange(1, R)
+    pk, _ = ctx.g1_mul(G1, [sk])
+    msgs = [bytes(rng.randrange(256) for _ in range(L)) for L in (0, 1, 40, 64, 65, 300)]
+    cts = skg.encrypt_batch(ctx, [bytes(pk)] * len(msgs), msgs)
+    # oracle: the same ciphertexts decrypt to the same messages with the Python restatement
+    for m, c in zip(msgs[:3], cts[:3]):
+        u = B.g1_decompress(c.u)
+        g = B.g1_mul(u, sk)
+        assert bytes(a ^ b for a, b in zip(TC.hash_bytes(g, len(c.v)), c.v)) == m
+        assert TC.ciphertext_verify((u, c.v, B.g2_decompress(c.w)))
+    bad_w = skg.Ciphertext(cts[2].u, cts[2].v, cts[3].w)
+    bad_u = skg.Ciphertext(bytes([cts[1].u[0] & 0x7F]) + cts[1].u[1:], cts[1].v, cts[1].w)
+    out, st = ctx.decrypt(sk, [c.u for c in cts + [bad_w, bad_u]], [c.w for c in cts + [bad_w, bad_u]],
+                          [c.v for c in cts + [bad_w, bad_u]])
+    assert out[:len(msgs)] == msgs
+    assert out[-2] is None and st[-2] == N.REJECT
+    assert out[-1] is None and st[-1] == N.DECODE_ERR
