@@ -11,11 +11,15 @@ checked against the construction after timing:
       shares (combine_signatures + parity, src/coin.rs:185-191,173).  Inputs resident in HBM.
   c4  N=10,000: I coin instances x 10^4 SignatureShares + I G2 Pippenger combines (t=3334).
       SURVEY §8 shards the I=64 instances over 8 GPUs; this 1-GPU line runs --inst of them.
-  c5  SyncKeyGen N=1000, one node's view: 1000 Parts (row.commitment() == commit.row(x),
-      src/sync_key_gen.rs:366) then 10^6 Acks (commit.evaluate(x, y) == val*G1, :493).  The
-      SKG entry points take host buffers, so this line is PCIe-inclusive (2.7 GB of commitments
-      per Part batch); the Parts reuse --distinct bivariate polynomials (laid out per Part in
-      HBM as 1000 separate copies, so the device work and traffic are those of 1000 Parts).
+  c5  SyncKeyGen N=1000, one node's view of an era: 1000 Parts (row.commitment() ==
+      commit.row(x), src/sync_key_gen.rs:366), then the 10^6 Acks: each Ack value addressed to
+      us decrypted (SecretKey::decrypt = hash_g1_g2 + Ciphertext::verify + sk u + pad,
+      :481-484; hbtc_decrypt) and checked (commit.evaluate(x, y) == val*G1, :493).  The SKG
+      entry points take host buffers, so this line is PCIe-inclusive (2.7 GB of commitments per
+      Part batch); the Parts reuse --distinct bivariate polynomials (laid out per Part in HBM as
+      1000 separate copies, so the device work and traffic are those of 1000 Parts), and the
+      Ack ciphertexts repeat per distinct (polynomial, sender) value (every Ack is still
+      hashed, verified, multiplied and padded on its own).
 
 Usage: python bench_configs.py [--configs c2,c4,c5] [--steps K] [--warmup W]
 """
@@ -223,47 +227,79 @@ def bench_skg(ctx, n, n_parts, n_distinct, steps, warmup):
         vals[a] = np.frombuffer(v.to_bytes(32, "little"), np.uint8)
         ack_expect[a] = N.REJECT
     vals = vals.reshape(-1)
-    log("c5: setup %.1fs (%d Parts x %d commitment points, %d Acks)"
-        % (time.time() - t0, n_parts, m, n_acks))
+    # the Ack values addressed to us, encrypted to our key (one ciphertext per distinct value)
+    from hbbft_amd import skg, wire
+    our_sk = rng.randrange(1, R)
+    our_pk, _ = ctx.g1_mul(G1_GEN, fr_bytes([our_sk]))
+    vmat = vals.reshape(n_acks, 32)
+    keyof = {}
+    for a in range(n_acks):
+        keyof.setdefault(vmat[a].tobytes(), len(keyof))
+    distinct = [None] * len(keyof)
+    for k, j in keyof.items():
+        distinct[j] = wire.fr_to_wire(int.from_bytes(k, "little"))
+    pool = skg.encrypt_batch(ctx, [bytes(our_pk)] * len(distinct), distinct)
+    which = np.array([keyof[vmat[a].tobytes()] for a in range(n_acks)], np.int64)
+    pu = np.frombuffer(b"".join(c.u for c in pool), np.uint8).reshape(-1, 48)
+    pw = np.frombuffer(b"".join(c.w for c in pool), np.uint8).reshape(-1, 96)
+    pv = np.frombuffer(b"".join(c.v for c in pool), np.uint8).reshape(-1, 40)
+    ack_u, ack_w, ack_v = (np.ascontiguousarray(x[which]).reshape(-1) for x in (pu, pw, pv))
+    ack_off = np.arange(0, 40 * n_acks + 1, 40, dtype=np.uint32)
+    ack_plain = np.empty(40 * n_acks, np.uint8)
+    ack_dst = np.empty(n_acks, np.int32)
+    sk_b = fr_bytes([our_sk])
+    log("c5: setup %.1fs (%d Parts x %d commitment points, %d Acks, %d distinct Ack ciphertexts)"
+        % (time.time() - t0, n_parts, m, n_acks, len(pool)))
     lib, h = ctx.lib, ctx.h
     pst = np.empty(n_parts, np.int32)
     ast = np.empty(n_acks, np.int32)
     row_ok = np.empty(n_parts, np.uint8)
     t_parts = [0.0]
+    t_dec = [0.0]
+    dec_vals = np.empty(32 * n_acks, np.uint8)
 
     def step():
         a0 = time.perf_counter()
         ctx._check(lib.hbtc_skg_check_parts(h, n_parts, t, our, N._ptr(commits), N._ptr(rows_b),
                                             N._ptr(pst)), "skg_check_parts")
-        t_parts[0] += time.perf_counter() - a0
+        a1 = time.perf_counter()
+        t_parts[0] += a1 - a0
         row_ok[:] = (pst == N.ACCEPT)
+        # our value of every Ack: SecretKey::decrypt, then the FieldWrap<Fr> framing (32-byte BE)
+        ctx._check(lib.hbtc_decrypt(h, n_acks, N._ptr(sk_b), N._ptr(ack_u), N._ptr(ack_w),
+                                    N._ptr(ack_v), N._ptr(ack_off), N._ptr(ack_plain),
+                                    N._ptr(ack_dst)), "decrypt")
+        dec_vals.reshape(n_acks, 32)[:] = ack_plain.reshape(n_acks, 40)[:, 8:][:, ::-1]
+        t_dec[0] += time.perf_counter() - a1
         ctx._check(lib.hbtc_skg_check_acks(h, n_parts, t, our, N._ptr(commits), N._ptr(rows_b),
                                            N._ptr(row_ok), n_acks, N._ptr(ack_part),
-                                           N._ptr(ack_sender), N._ptr(vals), N._ptr(ast)),
+                                           N._ptr(ack_sender), N._ptr(dec_vals), N._ptr(ast)),
                    "skg_check_acks")
 
     for _ in range(warmup):
         step()
-    t_parts[0] = 0.0
+    t_parts[0] = t_dec[0] = 0.0
     elapsed = timed_steps(ctx, step, steps, 0)
     per = breakdown(ctx, steps, ["skg_scalars", "skg_ack_rows", "comb_decode", "comb_digits",
-                                 "combine", "mul"])
+                                 "combine", "mul", "hash", "pair_verify"])
     pm = int((pst != part_expect).sum())
-    am = int((ast != ack_expect).sum())
+    am = int((ast != ack_expect).sum()) + int((ack_dst != N.ACCEPT).sum())
     if pm or am:
         raise SystemExit("c5: results differ from the construction (%d Part, %d Ack mismatches)" % (pm, am))
     tp = t_parts[0] / steps
+    td = t_dec[0] / steps
     ta = elapsed / steps - tp
     return {
         "metric": "SyncKeyGen checks/sec: Parts/s and Acks/s (one node's view)",
         "value": round(n_acks * steps / elapsed, 1), "unit": "acks/s (Parts + Acks of the era in the timed region)",
         "n_gpus": 1, "steps": steps, "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 3),
         "higher_is_better": True, "dtype": "u32 (381-bit Montgomery limbs)",
-        "data": "synthetic (%d distinct bivariate polynomials reused over %d Parts; 1 Part with a tampered row, 100 tampered Ack values); host buffers (PCIe-inclusive)"
-                % (n_distinct, n_parts),
-        "config": {"workload": "c5: SyncKeyGen N=%d: %d Parts (%d-point BivarCommitments) + %d Acks"
+        "data": "synthetic (%d distinct bivariate polynomials reused over %d Parts; 1 Part with a tampered row, 100 tampered Ack values; %d distinct Ack ciphertexts); host buffers (PCIe-inclusive)"
+                % (n_distinct, n_parts, len(pool)),
+        "config": {"workload": "c5: SyncKeyGen N=%d: %d Parts (%d-point BivarCommitments) + %d Acks (decrypt + value check)"
                    % (n, n_parts, m, n_acks), "N": n, "t": t, "parts": n_parts, "acks": n_acks},
         "parts_ms": round(tp * 1e3, 3), "acks_ms": round(ta * 1e3, 3),
+        "acks_decrypt_ms": round(td * 1e3, 3),
         "parts_per_s": round(n_parts / tp, 1), "acks_per_s": round(n_acks / ta, 1),
         "kernel_ms_per_step": per, "mismatches": pm + am,
     }
