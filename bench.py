@@ -54,7 +54,9 @@ SEED = 0x6862626674
 MAD_U64_PEAK = 29.51e12
 # timing family -> kernel (hbtc_api.hip timed() families, rocprofv3 names)
 KERNEL_NAME = {"dec_verify": "k_dec_verify", "rlc_items": "k_rlc_items",
-               "chk_tiles": "k_chk_tiles", "chk_subs": "k_chk_subs", "chk_leaves": "k_chk_leaves"}
+               "chk_tiles": "k_chk_plain<0>", "chk_tiles_w": "k_chk_weighted<0>",
+               "chk_subs": "k_chk_plain<1>", "chk_subs_w": "k_chk_weighted<1>",
+               "chk_leaves": "k_chk_leaves"}
 
 
 def log(*a):
@@ -269,8 +271,8 @@ def max_over_ranks(elapsed, dist, device=None):
     return float(tt.item())
 
 
-FAMS = ["dec_verify", "rlc_items", "chk_tiles", "chk_subs", "chk_leaves", "rlc_finalize",
-        "lagrange", "comb_decode", "comb_digits", "combine", "prepare"]
+FAMS = ["dec_verify", "rlc_items", "chk_tiles", "chk_tiles_w", "chk_subs", "chk_subs_w",
+        "chk_leaves", "rlc_finalize", "lagrange", "comb_decode", "comb_digits", "combine", "prepare"]
 
 
 def timed(ctx, ep, steps, warmup, dist=None, gather=None, sync_all=None):
@@ -418,9 +420,9 @@ def main():
     fqm_per_launch = {
         "dec_verify": consts["dec_share"]["total"] * ep.total,
         "rlc_items": consts["rlc_item"] * ep.total,
-        # a tile unit = the plain and the weighted 2-pair check (serial Fqm count of one check;
-        # the cooperative kernel issues more lane-level work than this)
-        "chk_tiles": consts["rlc_group_check"] * 2 * n_tiles,
+        # the plain 2-pair check of every tile (serial Fqm count of one check; the cooperative
+        # kernel issues more lane-level work than this)
+        "chk_tiles": consts["rlc_group_check"] * n_tiles,
         "chk_leaves": consts["dec_share"]["total"] * leaves,
         "combine": consts.get("g1_msm_combine", 0) * ep.m,
     }
@@ -438,7 +440,8 @@ def main():
     traffic, pmc = None, {}
     pmc_path = os.path.join(ROOT, "profiles", "r02_pmc_summary.json")
     if os.path.exists(pmc_path):
-        pmc = json.load(open(pmc_path)).get("hbtc::" + KERNEL_NAME[dom], {})
+        summ = json.load(open(pmc_path))
+        pmc = summ.get("hbtc::" + KERNEL_NAME[dom]) or summ.get("void hbtc::" + KERNEL_NAME[dom], {})
         if "hbm_read_bytes" in pmc and "hbm_write_bytes" in pmc:
             traffic = pmc["hbm_read_bytes"] + pmc["hbm_write_bytes"]
     if strong:

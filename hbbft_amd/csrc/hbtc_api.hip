@@ -394,7 +394,8 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   for (int i = 0; i < 8; ++i) key.k[i] = c->rd();
   TileSums* sums;
   G1A* dec;
-  uint32_t *counters, *sub_list, *leaves;
+  uint32_t *counters, *sub_list, *leaves, *tw_list, *sw_list;
+  Fq2 *t_tiles, *t_subs;
   HB_TRY(wst(c, "rlc.sums", n_tiles, &sums));
   // two alternating buffers: a combine of the previous call may still read the other one
   c->dec_flip ^= 1;
@@ -402,12 +403,19 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
   HB_TRY(guard_write(c, dec, (size_t)n_items * sizeof(G1A)));
   c->last_dec = {d_status, d_share, n_items, dec, nullptr};
-  HB_TRY(wst(c, "rlc.counters", 2, &counters));  // [0] leaves, [1] sub-tile list
+  // counters: [0] leaves, [1] listed tiles (sub-tile pass), [2] failing tiles, [3] failing subs
+  HB_TRY(wst(c, "rlc.counters", 4, &counters));
   HB_TRY(wst(c, "rlc.sub_list", n_tiles, &sub_list));
+  HB_TRY(wst(c, "rlc.tw_list", n_tiles, &tw_list));
+  HB_TRY(wst(c, "rlc.sw_list", (size_t)8 * n_tiles, &sw_list));
+  HB_TRY(wst(c, "rlc.t_tiles", (size_t)6 * n_tiles, &t_tiles));
+  HB_TRY(wst(c, "rlc.t_subs", (size_t)48 * n_tiles, &t_subs));
   HB_TRY(wst(c, "rlc.leaves", (size_t)2 * n_items, &leaves));
   uint32_t* leaf_count = counters;
   uint32_t* sub_count = counters + 1;
-  HB_CHECK(c, hipMemsetAsync(counters, 0, 2 * sizeof(uint32_t), c->stream));
+  uint32_t* tw_count = counters + 2;
+  uint32_t* sw_count = counters + 3;
+  HB_CHECK(c, hipMemsetAsync(counters, 0, 4 * sizeof(uint32_t), c->stream));
   const Suspects sus = suspects_of(c, ks, leaf_count, leaves);
   HB_TRY(timed(c, "rlc_items", [&] {
     return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->tab,
@@ -415,12 +423,22 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   }));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
   HB_TRY(timed(c, "chk_tiles", [&] {
-    return launch_chk_tiles(c->stream, n_tiles, tiles, sums, h_aff, h_lines, w_aff, w_lines, h_st,
-                            w_st, d_status, sub_count, sub_list);
+    return launch_chk_plain(c->stream, 0, n_tiles, n_tiles, nullptr, nullptr, tiles, sums, h_aff,
+                            h_lines, w_aff, w_lines, h_st, w_st, t_tiles, tw_count, tw_list);
+  }));
+  HB_TRY(timed(c, "chk_tiles_w", [&] {
+    return launch_chk_weighted(c->stream, 0, n_tiles, tw_count, tw_list, nullptr, tiles, sums,
+                               h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_tiles, d_status,
+                               sub_count, sub_list);
   }));
   HB_TRY(timed(c, "chk_subs", [&] {
-    return launch_chk_subs(c->stream, n_tiles, sub_count, sub_list, tiles, sums, h_aff, h_lines,
-                           w_aff, w_lines, d_status, leaf_count, leaves);
+    return launch_chk_plain(c->stream, 1, 8 * n_tiles, 0, sub_count, sub_list, tiles, sums, h_aff,
+                            h_lines, w_aff, w_lines, h_st, w_st, t_subs, sw_count, sw_list);
+  }));
+  HB_TRY(timed(c, "chk_subs_w", [&] {
+    return launch_chk_weighted(c->stream, 1, 8 * n_tiles, sw_count, sw_list, sub_list, tiles, sums,
+                               h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_subs, d_status,
+                               leaf_count, leaves);
   }));
   HB_TRY(timed(c, "chk_leaves", [&] {
     return launch_chk_leaves(c->stream, n_items, leaf_count, leaves, d_idx, dec, ks->pk, h_aff,

@@ -107,97 +107,182 @@ __device__ __forceinline__ bool unit_values(Fq2& T, Fq2& Tw, const Fq2& e, const
 
 }  // namespace
 
-// ------------------------------------------------------------------------------ level 1: tiles
-__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_tiles(
-    uint32_t n_tiles, const Tile* __restrict__ tiles, const TileSums* __restrict__ sums,
-    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
-    const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
-    const int32_t* __restrict__ h_status, const int32_t* __restrict__ w_status,
-    int32_t* __restrict__ status, uint32_t* __restrict__ sub_count,
-    uint32_t* __restrict__ sub_list) {
-  const UnitLane ul = unit_lane();
-  const uint32_t t = blockIdx.x * UNITS_PER_WAVE + ul.unit;
-  const bool active = ul.unit < UNITS_PER_WAVE && t < n_tiles;
-  uint32_t k = 0, first = 0, count = 0;
-  bool inst_ok = false;
-  G1J S, P;
-  jac_set_inf(S);
-  jac_set_inf(P);
-  if (active) {
-    const Tile tile = tiles[t];
-    k = tile.inst;
-    first = tile.first;
-    count = tile.count;
-    inst_ok = h_status[k] == HBTC_ACCEPT && w_status[k] == HBTC_ACCEPT;
-    S = ul.side ? sums[t].SW[8] : sums[t].S[8];
-    P = ul.side ? sums[t].PW[8] : sums[t].P[8];
+// ------------------------------------------------------------------------------ group levels
+// Plain first: a group's weighted check (needed only to locate a wrong share) runs only when
+// its plain check failed.  Every group of a level is one 6-lane check; a unit carries two
+// groups.  Level 0 = the 64-share tiles (group g = tile g), level 1 = the 8-share sub-tiles of
+// the listed tiles (group g = sub-tile g & 7 of tile sub_list[g >> 3]).
+namespace {
+
+struct GroupRef {
+  uint32_t inst, t, sub, lo, hi;
+  bool active, inst_ok;
+};
+
+template <int LEVEL>
+__device__ __forceinline__ GroupRef group_ref(uint32_t g, uint32_t n, const Tile* tiles,
+                                              const uint32_t* sub_list, const int32_t* h_status,
+                                              const int32_t* w_status) {
+  GroupRef r{0, 0, 8, 0, 0, false, false};
+  if (g >= n) return r;
+  const uint32_t t = LEVEL == 0 ? g : sub_list[g >> 3];
+  const Tile tile = tiles[t];
+  r.t = t;
+  r.inst = tile.inst;
+  if (LEVEL == 0) {
+    r.lo = tile.first;
+    r.hi = tile.first + tile.count;
+    r.inst_ok = h_status[tile.inst] == HBTC_ACCEPT && w_status[tile.inst] == HBTC_ACCEPT;
+  } else {
+    r.sub = g & 7u;
+    r.lo = tile.first + r.sub * 8u;
+    r.hi = min(tile.first + tile.count, r.lo + 8u);
+    r.inst_ok = true;  // listed tiles belong to instances whose H and w decoded
   }
-  const bool use1 = inst_ok && !jac_is_inf(S) && !h_aff[k].inf;
-  const bool use2 = inst_ok && !jac_is_inf(P) && !w_aff[k].inf;
-  Fq2 e, T, Tw;
-  pair_value(e, S, use1, h_lines + (size_t)k * MILLER_STEPS, P, use2,
-             w_lines + (size_t)k * MILLER_STEPS, ul.ps);
-  const bool pass = unit_values(T, Tw, e, ul);
-  const bool fail = active && inst_ok && !pass;
-  const int32_t loc = locate(T, Tw, count, 5, fail, ul);
-  if (!fail || ul.side != 0 || ul.ps.k != 0) return;
-  // undecodable H / w or a passing tile: k_rlc_finalize decides the pending items
-  if (loc >= 0 && status[first + loc] == HBTC_RLC_PENDING) {
-    status[first + loc] = HBTC_REJECT;
-    return;
-  }
-  sub_list[atomicAdd(sub_count, 1u)] = t;
+  r.active = r.lo < r.hi;
+  return r;
 }
 
-// ------------------------------------------------------------------------------ level 2: sub-tiles
-__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_subs(
-    const uint32_t* __restrict__ sub_count, const uint32_t* __restrict__ sub_list,
+// 64-bit fingerprint of a GT value (canonical low words of coefficients 0 and 3), group-wide.
+__device__ __forceinline__ void gt_fingerprint(uint32_t& a, uint32_t& b, const Fq2& x, const Pos& ps) {
+  Fq c;
+  fq_canon(c, x.c0);
+  a = gt::shfl(c.v[0], gt::src(ps, 0));
+  b = gt::shfl(c.v[0], gt::src(ps, 3));
+}
+
+// Single-error location inside one group: the p < count with Tw == T^p, or -1.  Baby-step
+// giant-step over p = 8 a + b: fingerprints of T^b (b < 8), then Tw T^(-8 a) (T^-8 = conj(T^8):
+// T is cyclotomic) for a < 8 — at most 16 products instead of 64 — and the match is confirmed
+// exactly (T^p recomputed by square-and-multiply and compared in full).
+__device__ __forceinline__ int32_t locate_group(const Fq2& T, const Fq2& Tw, uint32_t count,
+                                                bool need, const Pos& ps) {
+  uint32_t fa[8], fb[8];
+  Fq2 acc;
+  gt::set_one(acc, ps);
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    gt_fingerprint(fa[b], fb[b], acc, ps);
+    gt::mul(acc, acc, T, ps);  // ends as T^8
+  }
+  Fq2 step = acc;
+  gt::conj(step, ps);  // T^-8
+  Fq2 g = Tw;
+  int32_t found = -1;
+#pragma unroll 1
+  for (uint32_t a = 0; a < 8u; ++a) {
+    const bool live = need && found < 0 && 8u * a < count;
+    if (!gt::wave_any(live)) break;
+    uint32_t ga, gb;
+    gt_fingerprint(ga, gb, g, ps);
+#pragma unroll
+    for (int b = 0; b < 8; ++b)
+      if (live && found < 0 && ga == fa[b] && gb == fb[b] && 8u * a + (uint32_t)b < count)
+        found = (int32_t)(8u * a + (uint32_t)b);
+    gt::mul(g, g, step, ps);
+  }
+  // confirm: T^found == Tw (a fingerprint match is only a candidate)
+  const uint32_t pe = found >= 0 ? (uint32_t)found : 0u;
+  Fq2 tp;
+  gt::set_one(tp, ps);
+#pragma unroll 1
+  for (int bit = 5; bit >= 0; --bit) {
+    gt::cyc_sqr(tp, ps);
+    Fq2 m;
+    gt::mul(m, tp, T, ps);
+    gt::fq2_sel(tp, ((pe >> bit) & 1u) != 0, m, tp);
+  }
+  const bool ok = gt::equal(tp, Tw, ps);
+  return found >= 0 && ok ? found : -1;
+}
+
+}  // namespace
+
+// Plain check of every group of the level; a failing group stores its value T (6 lanes, one
+// Fq2 each) and joins the list of the weighted pass.
+template <int LEVEL>
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_plain(
+    uint32_t n_direct, const uint32_t* __restrict__ n_listed, const uint32_t* __restrict__ sub_list,
     const Tile* __restrict__ tiles, const TileSums* __restrict__ sums,
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
     const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
-    int32_t* __restrict__ status, uint32_t* __restrict__ leaf_count,
-    uint32_t* __restrict__ leaves) {
-  const uint32_t n_units = *sub_count * 8u;
-  if (blockIdx.x * UNITS_PER_WAVE >= n_units) return;  // wave-uniform: the grid is sized for the worst case
+    const int32_t* __restrict__ h_status, const int32_t* __restrict__ w_status,
+    Fq2* __restrict__ Tbuf, uint32_t* __restrict__ fail_count, uint32_t* __restrict__ fail_list) {
+  const uint32_t n = LEVEL == 0 ? n_direct : *n_listed * 8u;
+  if (blockIdx.x * 2u * UNITS_PER_WAVE >= n) return;  // wave-uniform: grids are sized for the worst case
   const UnitLane ul = unit_lane();
-  const uint32_t u = blockIdx.x * UNITS_PER_WAVE + ul.unit;
-  bool active = ul.unit < UNITS_PER_WAVE && u < n_units;
-  uint32_t k = 0, lo = 0, hi = 0;
+  const uint32_t g = (blockIdx.x * UNITS_PER_WAVE + ul.unit) * 2u + ul.side;
+  const GroupRef r = group_ref<LEVEL>(ul.unit < UNITS_PER_WAVE ? g : n, n, tiles, sub_list,
+                                      h_status, w_status);
   G1J S, P;
   jac_set_inf(S);
   jac_set_inf(P);
-  if (active) {
-    const uint32_t t = sub_list[u >> 3], sub = u & 7u;
-    const Tile tile = tiles[t];
-    k = tile.inst;
-    lo = tile.first + sub * 8u;
-    hi = min(tile.first + tile.count, lo + 8u);
-    active = lo < hi;
-    if (active) {
-      S = ul.side ? sums[t].SW[sub] : sums[t].S[sub];
-      P = ul.side ? sums[t].PW[sub] : sums[t].P[sub];
-    }
+  if (r.active) {
+    S = sums[r.t].S[r.sub];
+    P = sums[r.t].P[r.sub];
   }
-  // listed tiles belong to ciphertexts whose H and w decoded (k_chk_tiles)
-  const bool use1 = active && !jac_is_inf(S) && !h_aff[k].inf;
-  const bool use2 = active && !jac_is_inf(P) && !w_aff[k].inf;
-  Fq2 e, T, Tw;
-  pair_value(e, S, use1, h_lines + (size_t)k * MILLER_STEPS, P, use2,
-             w_lines + (size_t)k * MILLER_STEPS, ul.ps);
-  const bool pass = unit_values(T, Tw, e, ul);
-  const bool fail = active && !pass;
-  const int32_t loc = locate(T, Tw, hi - lo, 2, fail, ul);
-  if (!fail || ul.side != 0 || ul.ps.k != 0) return;
-  if (loc >= 0 && status[lo + loc] == HBTC_RLC_PENDING) {
-    status[lo + loc] = HBTC_REJECT;
+  const bool use1 = r.active && r.inst_ok && !jac_is_inf(S) && !h_aff[r.inst].inf;
+  const bool use2 = r.active && r.inst_ok && !jac_is_inf(P) && !w_aff[r.inst].inf;
+  Fq2 e;
+  pair_value(e, S, use1, h_lines + (size_t)r.inst * MILLER_STEPS, P, use2,
+             w_lines + (size_t)r.inst * MILLER_STEPS, ul.ps);
+  const bool pass = gt::is_one(e, ul.ps);
+  // undecodable H / w: k_rlc_finalize decides the group's items
+  if (!r.active || !r.inst_ok || pass) return;
+  Tbuf[(size_t)g * 6u + ul.ps.k] = e;
+  if (ul.ps.k == 0) fail_list[atomicAdd(fail_count, 1u)] = g;
+}
+
+// Weighted check of every listed group: locate its single wrong share (REJECT it), else pass
+// the group down (level 0: its tile to the sub-tile list; level 1: its pending shares to the
+// exact leaf checks).
+template <int LEVEL>
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_weighted(
+    const uint32_t* __restrict__ fail_count, const uint32_t* __restrict__ fail_list,
+    const uint32_t* __restrict__ sub_list_in, const Tile* __restrict__ tiles,
+    const TileSums* __restrict__ sums, const G2A* __restrict__ h_aff,
+    const Line* __restrict__ h_lines, const G2A* __restrict__ w_aff,
+    const Line* __restrict__ w_lines, const int32_t* __restrict__ h_status,
+    const int32_t* __restrict__ w_status, const Fq2* __restrict__ Tbuf,
+    int32_t* __restrict__ status, uint32_t* __restrict__ out_count, uint32_t* __restrict__ out_list) {
+  const uint32_t n = *fail_count;
+  if (blockIdx.x * 2u * UNITS_PER_WAVE >= n) return;
+  const UnitLane ul = unit_lane();
+  const uint32_t j = (blockIdx.x * UNITS_PER_WAVE + ul.unit) * 2u + ul.side;
+  const bool listed = ul.unit < UNITS_PER_WAVE && j < n;
+  const uint32_t g = listed ? fail_list[j] : 0u;
+  const GroupRef r = group_ref<LEVEL>(listed ? g : ~0u, ~0u, tiles, sub_list_in, h_status, w_status);
+  G1J S, P;
+  jac_set_inf(S);
+  jac_set_inf(P);
+  Fq2 T;
+  gt::set_one(T, ul.ps);
+  if (r.active) {
+    S = sums[r.t].SW[r.sub];
+    P = sums[r.t].PW[r.sub];
+    T = Tbuf[(size_t)g * 6u + ul.ps.k];
+  }
+  const bool use1 = r.active && !jac_is_inf(S) && !h_aff[r.inst].inf;
+  const bool use2 = r.active && !jac_is_inf(P) && !w_aff[r.inst].inf;
+  Fq2 Tw;
+  pair_value(Tw, S, use1, h_lines + (size_t)r.inst * MILLER_STEPS, P, use2,
+             w_lines + (size_t)r.inst * MILLER_STEPS, ul.ps);
+  const int32_t loc = locate_group(T, Tw, r.hi - r.lo, r.active, ul.ps);
+  if (!r.active || ul.ps.k != 0) return;
+  if (loc >= 0 && status[r.lo + loc] == HBTC_RLC_PENDING) {
+    status[r.lo + loc] = HBTC_REJECT;
     return;
   }
-  for (uint32_t i = lo; i < hi; ++i)
-    if (status[i] == HBTC_RLC_PENDING) {
-      const uint32_t pos = atomicAdd(leaf_count, 1u);
-      leaves[2 * pos] = i;
-      leaves[2 * pos + 1] = k;
-    }
+  if (LEVEL == 0) {
+    out_list[atomicAdd(out_count, 1u)] = r.t;
+  } else {
+    for (uint32_t i = r.lo; i < r.hi; ++i)
+      if (status[i] == HBTC_RLC_PENDING) {
+        const uint32_t pos = atomicAdd(out_count, 1u);
+        out_list[2 * pos] = i;
+        out_list[2 * pos + 1] = r.inst;
+      }
+  }
 }
 
 // ------------------------------------------------------------------------------ level 3: leaves
@@ -378,27 +463,40 @@ static inline uint32_t unit_blocks(uint64_t units) {
   return (uint32_t)((units + UNITS_PER_WAVE - 1) / UNITS_PER_WAVE);
 }
 
-hipError_t launch_chk_tiles(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+hipError_t launch_chk_plain(hipStream_t s, int level, uint32_t max_groups, uint32_t n_direct,
+                            const uint32_t* n_listed, const uint32_t* sub_list, const Tile* tiles,
                             const TileSums* sums, const G2A* h_aff, const Line* h_lines,
                             const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
-                            const int32_t* w_status, int32_t* status, uint32_t* sub_count,
-                            uint32_t* sub_list) {
-  if (n_tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_chk_tiles, dim3(unit_blocks(n_tiles)), dim3(64), 0, s, n_tiles, tiles, sums,
-                     h_aff, h_lines, w_aff, w_lines, h_status, w_status, status, sub_count,
-                     sub_list);
+                            const int32_t* w_status, Fq2* Tbuf, uint32_t* fail_count,
+                            uint32_t* fail_list) {
+  if (max_groups == 0) return hipSuccess;
+  const dim3 grid(unit_blocks(((uint64_t)max_groups + 1) / 2));
+  if (level == 0)
+    hipLaunchKernelGGL(k_chk_plain<0>, grid, dim3(64), 0, s, n_direct, n_listed, sub_list, tiles, sums,
+                       h_aff, h_lines, w_aff, w_lines, h_status, w_status, Tbuf, fail_count, fail_list);
+  else
+    hipLaunchKernelGGL(k_chk_plain<1>, grid, dim3(64), 0, s, n_direct, n_listed, sub_list, tiles, sums,
+                       h_aff, h_lines, w_aff, w_lines, h_status, w_status, Tbuf, fail_count, fail_list);
   return hipGetLastError();
 }
 
-hipError_t launch_chk_subs(hipStream_t s, uint32_t max_tiles, const uint32_t* sub_count,
-                           const uint32_t* sub_list, const Tile* tiles, const TileSums* sums,
-                           const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
-                           const Line* w_lines, int32_t* status, uint32_t* leaf_count,
-                           uint32_t* leaves) {
-  if (max_tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_chk_subs, dim3(unit_blocks((uint64_t)max_tiles * 8)), dim3(64), 0, s,
-                     sub_count, sub_list, tiles, sums, h_aff, h_lines, w_aff, w_lines, status,
-                     leaf_count, leaves);
+hipError_t launch_chk_weighted(hipStream_t s, int level, uint32_t max_groups,
+                               const uint32_t* fail_count, const uint32_t* fail_list,
+                               const uint32_t* sub_list, const Tile* tiles, const TileSums* sums,
+                               const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
+                               const Line* w_lines, const int32_t* h_status,
+                               const int32_t* w_status, const Fq2* Tbuf, int32_t* status,
+                               uint32_t* out_count, uint32_t* out_list) {
+  if (max_groups == 0) return hipSuccess;
+  const dim3 grid(unit_blocks(((uint64_t)max_groups + 1) / 2));
+  if (level == 0)
+    hipLaunchKernelGGL(k_chk_weighted<0>, grid, dim3(64), 0, s, fail_count, fail_list, sub_list, tiles,
+                       sums, h_aff, h_lines, w_aff, w_lines, h_status, w_status, Tbuf, status,
+                       out_count, out_list);
+  else
+    hipLaunchKernelGGL(k_chk_weighted<1>, grid, dim3(64), 0, s, fail_count, fail_list, sub_list, tiles,
+                       sums, h_aff, h_lines, w_aff, w_lines, h_status, w_status, Tbuf, status,
+                       out_count, out_list);
   return hipGetLastError();
 }
 

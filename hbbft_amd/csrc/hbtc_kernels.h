@@ -81,16 +81,24 @@ hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n_tiles, const Tile* tile
                                const uint32_t* idx, uint32_t n_pk, uint32_t* rejects,
                                uint32_t* last_bad, uint32_t now, uint32_t thresh);
 // the pairing-product checks (hbtc_check.hip, cooperative GT arithmetic of gt6.h)
-hipError_t launch_chk_tiles(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+// Group checks, plain first (hbtc_check.hip): level 0 = tiles (n_direct groups), level 1 =
+// the 8 sub-tiles of the *n_listed tiles of sub_list.  The plain pass stores a failing group's
+// T (6 Fq2 at Tbuf[6 g]) and lists g; the weighted pass locates a single wrong share, else
+// lists the tile (level 0, out_list = sub_list) or the group's pending shares (level 1,
+// out_list = leaves as (item, instance) pairs).
+hipError_t launch_chk_plain(hipStream_t s, int level, uint32_t max_groups, uint32_t n_direct,
+                            const uint32_t* n_listed, const uint32_t* sub_list, const Tile* tiles,
                             const TileSums* sums, const G2A* h_aff, const Line* h_lines,
                             const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
-                            const int32_t* w_status, int32_t* status, uint32_t* sub_count,
-                            uint32_t* sub_list);
-hipError_t launch_chk_subs(hipStream_t s, uint32_t max_tiles, const uint32_t* sub_count,
-                           const uint32_t* sub_list, const Tile* tiles, const TileSums* sums,
-                           const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
-                           const Line* w_lines, int32_t* status, uint32_t* leaf_count,
-                           uint32_t* leaves);
+                            const int32_t* w_status, Fq2* Tbuf, uint32_t* fail_count,
+                            uint32_t* fail_list);
+hipError_t launch_chk_weighted(hipStream_t s, int level, uint32_t max_groups,
+                               const uint32_t* fail_count, const uint32_t* fail_list,
+                               const uint32_t* sub_list, const Tile* tiles, const TileSums* sums,
+                               const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
+                               const Line* w_lines, const int32_t* h_status,
+                               const int32_t* w_status, const Fq2* Tbuf, int32_t* status,
+                               uint32_t* out_count, uint32_t* out_list);
 hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t* leaf_count,
                              const uint32_t* leaves, const uint32_t* idx, const G1A* dec,
                              const G1A* pk, const G2A* h_aff, const Line* h_lines,
