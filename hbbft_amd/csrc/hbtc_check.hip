@@ -29,6 +29,12 @@ using gt::Pos;
 #ifndef HBTC_GT_WAVES
 #define HBTC_GT_WAVES 2  // minimum waves per SIMD the check kernels' register budget must allow
 #endif
+// The weighted passes run few groups (the failing ones: fewer waves than SIMDs): one wave per
+// SIMD, the full register file, no spills (C3: 13.9 -> 11.5 ms; the plain passes, whose grids
+// fill the chip, lose 17.4 -> 21.7 ms at one wave, so they keep two).
+#ifndef HBTC_GT_WAVES_SMALL
+#define HBTC_GT_WAVES_SMALL 1
+#endif
 
 namespace {
 
@@ -237,7 +243,7 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_plain(
 // the group down (level 0: its tile to the sub-tile list; level 1: its pending shares to the
 // exact leaf checks).
 template <int LEVEL>
-__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_weighted(
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_weighted(
     const uint32_t* __restrict__ fail_count, const uint32_t* __restrict__ fail_list,
     const uint32_t* __restrict__ sub_list_in, const Tile* __restrict__ tiles,
     const TileSums* __restrict__ sums, const G2A* __restrict__ h_aff,
