@@ -18,7 +18,7 @@ MSM_PARTS := 8 9
 SKG_PARTS := 10
 KOBJS := $(foreach p,$(PARTS),$(BUILD)/hbtc_kernels.p$(p).o) $(foreach p,$(RLC_PARTS),$(BUILD)/hbtc_rlc.p$(p).o) \
          $(foreach p,$(MSM_PARTS),$(BUILD)/hbtc_msm.p$(p).o) $(foreach p,$(SKG_PARTS),$(BUILD)/hbtc_skg.p$(p).o) \
-         $(BUILD)/hbtc_check.o $(BUILD)/hbtc_sig.o
+         $(BUILD)/hbtc_check.c1.o $(BUILD)/hbtc_check.c2.o $(BUILD)/hbtc_sig.o
 LIB := hbbft_amd/libhbtc.so
 
 .PHONY: all lib hosttest oracle clean resources roofline-constants
@@ -46,8 +46,10 @@ $(BUILD)/hbtc_msm.p%.o: $(CSRC)/hbtc_msm.hip $(HDRS) | $(BUILD)
 $(BUILD)/hbtc_skg.p%.o: $(CSRC)/hbtc_skg.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
 
-$(BUILD)/hbtc_check.o: $(CSRC)/hbtc_check.hip $(HDRS) | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+# the group checks in two translation units: the one-wave weighted passes (part 2) must not share
+# the out-of-line GT helpers with the two-wave kernels (part 1)
+$(BUILD)/hbtc_check.c%.o: $(CSRC)/hbtc_check.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DHBTC_CHECK_PART=$* -c $< -o $@
 
 # the G2 item pass, all helpers inlined (no calls; the product itself stays out of line)
 $(BUILD)/hbtc_sig.o: $(CSRC)/hbtc_sig.hip $(HDRS) | $(BUILD)

@@ -35,6 +35,13 @@ using gt::Pos;
 #ifndef HBTC_GT_WAVES_SMALL
 #define HBTC_GT_WAVES_SMALL 1
 #endif
+// The file is compiled twice (Makefile): part 1 = every kernel but the weighted passes, part 2 =
+// the weighted passes.  The out-of-line GT helpers take the register budget of their most
+// generous caller, so one-wave and two-wave kernels must not share a translation unit.
+#ifndef HBTC_CHECK_PART
+#define HBTC_CHECK_PART 0
+#endif
+#define HBTC_CHECK_IN(n) (HBTC_CHECK_PART == 0 || HBTC_CHECK_PART == (n))
 
 namespace {
 
@@ -204,6 +211,7 @@ __device__ __forceinline__ int32_t locate_group(const Fq2& T, const Fq2& Tw, uin
 
 }  // namespace
 
+#if HBTC_CHECK_IN(1)
 // Plain check of every group of the level; a failing group stores its value T (6 lanes, one
 // Fq2 each) and joins the list of the weighted pass.
 template <int LEVEL>
@@ -239,6 +247,9 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_plain(
   if (ul.ps.k == 0) fail_list[atomicAdd(fail_count, 1u)] = g;
 }
 
+#endif  // part 1
+
+#if HBTC_CHECK_IN(2)
 // Weighted check of every listed group: locate its single wrong share (REJECT it), else pass
 // the group down (level 0: its tile to the sub-tile list; level 1: its pending shares to the
 // exact leaf checks).
@@ -291,6 +302,9 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_weighted(
   }
 }
 
+#endif  // part 2
+
+#if HBTC_CHECK_IN(1)
 // ------------------------------------------------------------------------------ level 3: leaves
 // e(d_i, H_k) e(-pk_i, w_k) == 1 for two listed shares per unit.
 __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_leaves(
@@ -464,11 +478,14 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_leaves(
   if (active && ul.ps.k == 0) status[item] = ok ? HBTC_ACCEPT : HBTC_REJECT;
 }
 
+#endif  // part 1 (leaves, SignatureShare kernels)
+
 // ------------------------------------------------------------------------------ launchers
 static inline uint32_t unit_blocks(uint64_t units) {
   return (uint32_t)((units + UNITS_PER_WAVE - 1) / UNITS_PER_WAVE);
 }
 
+#if HBTC_CHECK_IN(1)
 hipError_t launch_chk_plain(hipStream_t s, int level, uint32_t max_groups, uint32_t n_direct,
                             const uint32_t* n_listed, const uint32_t* sub_list, const Tile* tiles,
                             const TileSums* sums, const G2A* h_aff, const Line* h_lines,
@@ -486,6 +503,9 @@ hipError_t launch_chk_plain(hipStream_t s, int level, uint32_t max_groups, uint3
   return hipGetLastError();
 }
 
+#endif
+
+#if HBTC_CHECK_IN(2)
 hipError_t launch_chk_weighted(hipStream_t s, int level, uint32_t max_groups,
                                const uint32_t* fail_count, const uint32_t* fail_list,
                                const uint32_t* sub_list, const Tile* tiles, const TileSums* sums,
@@ -506,6 +526,9 @@ hipError_t launch_chk_weighted(hipStream_t s, int level, uint32_t max_groups,
   return hipGetLastError();
 }
 
+#endif
+
+#if HBTC_CHECK_IN(1)
 hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t* leaf_count,
                              const uint32_t* leaves, const uint32_t* idx, const G1A* dec,
                              const G1A* pk, const G2A* h_aff, const Line* h_lines,
@@ -548,5 +571,7 @@ hipError_t launch_sigchk_leaves(hipStream_t s, uint32_t base, uint32_t chunk,
                      base, chunk, leaf_count, leaves, idx, pk, tables, inf, h_aff, h_lines, status);
   return hipGetLastError();
 }
+
+#endif
 
 }  // namespace hbtc

@@ -18,9 +18,10 @@ objs=()
 for o in build/*.o; do
   stem=$(basename "$o" .o)
   if [ -n "${extra[$stem]+x}" ]; then
-    src=${stem%%.p*}
+    src=${stem%%.*}
     part=""
     if [[ $stem == *.p* ]]; then part="-DHBTC_PART=${stem##*.p}"; fi
+    if [[ $stem == hbtc_check.c* ]]; then src=hbtc_check; part="-DHBTC_CHECK_PART=${stem##*.c}"; fi
     base=""
     case $stem in hbtc_rlc.p6) base="-DHBTC_INLINE_ALL -DHBTC_FQMUL_INLINE";; hbtc_sig) base="-DHBTC_INLINE_ALL";; esac
     $HIPCC $FLAGS $part $base ${extra[$stem]} -c "hbbft_amd/csrc/$src.hip" -o "$out/$stem.o" &
