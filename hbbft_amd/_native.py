@@ -91,6 +91,7 @@ SIGNATURES = {
     "hbtc_xor_hash_bytes_batch": (_I32, [_U32, _P, _P, _P, _P]),
     "hbtc_commitment_evaluate": (_I32, [_P, _U32, _P, _U32, _P, _P, _P]),
     "hbtc_decrypt": (_I32, [_P, _U32, _P, _P, _P, _P, _P, _P, _P]),
+    "hbtc_unframe_points_dev": (_I32, [_P, _U32, _U32, _P, _P]),
     "hbtc_stream_wait_ctx": (_I32, [_P, _P]),
     "hbtc_ctx_wait_stream": (_I32, [_P, _P]),
     "hbtc_shard_items": (_I32, [_U32, _U32, _U32, _P, ctypes.POINTER(_U32), ctypes.POINTER(_U32),

@@ -25,6 +25,7 @@ void hash_g2_candidate(const uint8_t* msg, size_t len, G2A& p);
 void hash_g1_g2_c96(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8_t* out96);
 hipError_t launch_hash_cand(hipStream_t s, uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
                             const uint32_t* offsets, G2A* cand);
+hipError_t launch_unframe(hipStream_t s, uint32_t n, uint32_t size, const uint8_t* framed, uint8_t* items);
 void hash_bytes(const uint8_t* g1_c48, size_t len, uint8_t* out);
 void parallel_items(uint32_t n, const std::function<void(uint32_t)>& f);
 bool hash_offsets_ok(uint32_t n, const uint32_t* offsets);
@@ -1019,6 +1020,16 @@ int hbtc_ctx_wait_stream(hbtc_ctx* c, void* stream) {
   HB_CHECK(c, hipStreamWaitEvent(c->s_prep, c->ev_ext, 0));
   HB_CHECK(c, hipStreamWaitEvent(c->s_comb, c->ev_ext, 0));
   return HBTC_OK;
+}
+
+int hbtc_unframe_points_dev(hbtc_ctx* c, uint32_t n, uint32_t point_size, const uint8_t* d_framed,
+                            uint8_t* d_items) {
+  if (!c || (point_size != 48 && point_size != 96) || (n && (!d_framed || !d_items))) return HBTC_ERR_ARG;
+  Guard g(c);
+  if ((reinterpret_cast<uintptr_t>(d_framed) & 3u) || !aligned16(d_items))
+    return fail(c, HBTC_ERR_ARG, "framed input must be 4-byte, items 16-byte aligned");
+  HB_TRY(guard_write(c, d_items, (size_t)n * point_size));
+  return timed(c, "unframe", [&] { return launch_unframe(c->stream, n, point_size, d_framed, d_items); });
 }
 
 int hbtc_verify_dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct,

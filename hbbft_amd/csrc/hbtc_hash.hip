@@ -315,6 +315,32 @@ hipError_t launch_hash_cand(hipStream_t s, uint32_t n, const uint8_t* g1_c48, co
   return hipGetLastError();
 }
 
+// bincode framing of wire points: item i = u64 LE length || `size` bytes.  Copies
+// the point to the 16-aligned item array the verifiers read; a frame whose length is not
+// `size` gets a zero compression flag, so the decoder reports HBTC_DECODE_ERR for it (serde
+// refused the message).
+__global__ void __launch_bounds__(64) k_unframe(uint32_t n, uint32_t size, const uint32_t* __restrict__ framed,
+                                                uint32_t* __restrict__ items) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t words = size / 4, stride = words + 2;
+  const uint32_t* f = framed + (size_t)i * stride;
+  const bool ok = f[0] == size && f[1] == 0u;
+  uint32_t* o = items + (size_t)i * words;
+  for (uint32_t w = 0; w < words; ++w) {
+    uint32_t v = f[2 + w];
+    if (w == 0 && !ok) v &= ~0x80u;  // first byte's compression flag
+    o[w] = v;
+  }
+}
+
+hipError_t launch_unframe(hipStream_t s, uint32_t n, uint32_t size, const uint8_t* framed, uint8_t* items) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_unframe, dim3((n + 63) / 64), dim3(64), 0, s, n, size,
+                     reinterpret_cast<const uint32_t*>(framed), reinterpret_cast<uint32_t*>(items));
+  return hipGetLastError();
+}
+
 // [h2] P for candidates P (one lane each) -> compressed G2 words; st = 1 if [h2] P = O (the
 // host then continues G2::rand's loop itself).
 __global__ void __launch_bounds__(64) k_g2_clear_cofactor(uint32_t n, const G2A* __restrict__ in,

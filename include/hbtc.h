@@ -187,6 +187,12 @@ int hbtc_sync(hbtc_ctx* ctx);
  *                       (before overwriting a buffer the caller's stream still reads). */
 int hbtc_stream_wait_ctx(hbtc_ctx* ctx, void* hip_stream);
 int hbtc_ctx_wait_stream(hbtc_ctx* ctx, void* hip_stream);
+/* bincode-framed wire points (a SignatureShare / DecryptionShare as serialized: u64 LE length
+ * || 96 / 48 compressed bytes, back to back) -> the 16-aligned item array the *_dev verifiers
+ * read, on the context's main stream.  A frame whose length is not point_size yields an item
+ * that decodes to HBTC_DECODE_ERR (the message serde would refuse). */
+int hbtc_unframe_points_dev(hbtc_ctx* ctx, uint32_t n, uint32_t point_size, const uint8_t* d_framed,
+                            uint8_t* d_items);
 /* Same semantics as the host entry points; every d_* argument is a device pointer from
  * hbtc_dev_alloc and `offsets` stays a HOST array (it shapes the launch).  Work is enqueued on
  * the context's stream; call hbtc_sync before reading results. */
