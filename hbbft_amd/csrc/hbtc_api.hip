@@ -66,8 +66,24 @@ struct Stage {
 
 }  // namespace
 
+// One verification lane: its main and preparation streams, their events, and the device ranges
+// its last verification read and wrote (the hazards a call on the other lane checks).
+struct Lane {
+  hipStream_t stream = nullptr, s_prep = nullptr;
+  hipEvent_t ev_main = nullptr, ev_prep = nullptr, done = nullptr;
+  std::vector<std::pair<uintptr_t, uintptr_t>> rd, wr;
+  bool busy = false;
+};
+
 struct hbtc_ctx {
   int device = 0;
+  // Verification calls alternate between two lanes, so epoch k+1's item pass fills the SIMDs
+  // that epoch k's small check levels leave idle; `stream` / `s_prep` / `ev_*` / `ws_suffix`
+  // are the lane of the most recent verification (what the combine and the guards order on).
+  Lane lanes[2];
+  int lane = 0;
+  bool pin_lane = false;  // host entry points: stay on the lane their uploads went to
+  std::string ws_suffix;
   hipStream_t stream = nullptr;  // main: items, checks, leaves
   hipStream_t s_prep = nullptr;  // per-instance G2 preparation, overlapped with the item pass
   hipStream_t s_comb = nullptr;  // combines (Lagrange), overlapped with verification
@@ -130,7 +146,7 @@ int fail(hbtc_ctx* c, int code, const std::string& msg) {
 
 // Grow-only named device workspace.
 int ws(hbtc_ctx* c, const char* name, size_t bytes, void** out) {
-  DevBuf& b = c->bufs[name];
+  DevBuf& b = c->bufs[c->ws_suffix.empty() ? std::string(name) : std::string(name) + c->ws_suffix];
   if (bytes == 0) bytes = 16;
   if (b.cap < bytes) {
     if (b.p) HB_CHECK(c, hipFree(b.p));
@@ -165,10 +181,63 @@ int download(hbtc_ctx* c, void* dst, const void* src, size_t bytes) {
 }
 
 int sync(hbtc_ctx* c) {
-  HB_CHECK(c, hipStreamSynchronize(c->stream));
-  HB_CHECK(c, hipStreamSynchronize(c->s_prep));
+  for (Lane& l : c->lanes) {
+    HB_CHECK(c, hipStreamSynchronize(l.stream));
+    HB_CHECK(c, hipStreamSynchronize(l.s_prep));
+  }
   HB_CHECK(c, hipStreamSynchronize(c->s_comb));
   return HBTC_OK;
+}
+
+void select_lane(hbtc_ctx* c, int l) {
+  c->lane = l;
+  c->stream = c->lanes[l].stream;
+  c->s_prep = c->lanes[l].s_prep;
+  c->ev_main = c->lanes[l].ev_main;
+  c->ev_prep = c->lanes[l].ev_prep;
+  c->ws_suffix = l ? "#1" : "";
+}
+
+bool ranges_overlap(const std::vector<std::pair<uintptr_t, uintptr_t>>& a,
+                    const std::vector<std::pair<uintptr_t, uintptr_t>>& b) {
+  for (const auto& x : a)
+    for (const auto& y : b)
+      if (x.first < y.second && y.first < x.second) return true;
+  return false;
+}
+
+// Start a verification on the next lane: it waits for the other lane's last verification only
+// when their device ranges conflict (write/write, read/write either way).
+int begin_verify(hbtc_ctx* c, std::vector<std::pair<uintptr_t, uintptr_t>> rd,
+                 std::vector<std::pair<uintptr_t, uintptr_t>> wr) {
+  const int l = c->pin_lane ? c->lane : (c->lane ^ 1), o = l ^ 1;
+  select_lane(c, l);
+  Lane& me = c->lanes[l];
+  const Lane& other = c->lanes[o];
+  if (other.busy && (ranges_overlap(wr, other.wr) || ranges_overlap(rd, other.wr) ||
+                     ranges_overlap(wr, other.rd)))
+    HB_CHECK(c, hipStreamWaitEvent(me.stream, other.done, 0));
+  me.rd = std::move(rd);
+  me.wr = std::move(wr);
+  return HBTC_OK;
+}
+
+int end_verify(hbtc_ctx* c) {
+  Lane& me = c->lanes[c->lane];
+  HB_CHECK(c, hipEventRecord(me.done, me.stream));
+  me.busy = true;
+  return HBTC_OK;
+}
+
+struct PinLane {
+  hbtc_ctx* c;
+  explicit PinLane(hbtc_ctx* cc) : c(cc) { c->pin_lane = true; }
+  ~PinLane() { c->pin_lane = false; }
+};
+
+std::pair<uintptr_t, uintptr_t> rng(const void* p, size_t bytes) {
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
+  return {lo, lo + bytes};
 }
 
 // `waiter` runs everything enqueued after this behind all work already on `on`.
@@ -243,7 +312,7 @@ int timed(hbtc_ctx* c, const char* family, F&& launch) {
 // Host table -> device workspace `name` through its pinned stage, ordered on `st`.
 int stage_upload(hbtc_ctx* c, const char* name, const void* src, size_t bytes, hipStream_t st,
                  void** d_out) {
-  Stage& sg = c->stages[name];
+  Stage& sg = c->stages[c->ws_suffix.empty() ? std::string(name) : std::string(name) + c->ws_suffix];
   if (sg.used) HB_CHECK(c, hipEventSynchronize(sg.ev));  // the previous copy out of it is done
   if (sg.cap < bytes || !sg.h) {
     if (sg.h) HB_CHECK(c, hipHostFree(sg.h));
@@ -365,6 +434,9 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   if (n_items == 0) return HBTC_OK;
   if (!aligned16(d_H) || !aligned16(d_w) || !aligned16(d_share))
     return fail(c, HBTC_ERR_ARG, "item arrays must be 16-byte aligned");
+  HB_TRY(begin_verify(c, {rng(d_H, 96 * (size_t)n_ct), rng(d_w, 96 * (size_t)n_ct),
+                          rng(d_idx, 4 * (size_t)n_items), rng(d_share, 48 * (size_t)n_items)},
+                      {rng(d_status, 4 * (size_t)n_items)}));
   G2A *h_aff, *w_aff;
   int32_t *h_st, *w_st;
   Line *h_lines, *w_lines;
@@ -378,10 +450,11 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
     w_st = h_st + n_ct;
     w_lines = h_lines + (size_t)n_ct * MILLER_STEPS;
     HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles));
-    return timed(c, "dec_verify", [&] {
+    HB_TRY(timed(c, "dec_verify", [&] {
       return launch_dec_verify(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n,
                                h_aff, h_st, h_lines, w_aff, w_st, w_lines, d_status);
-    });
+    }));
+    return end_verify(c);
   }
   // RLC batch verification with hierarchical fallback (hbtc_rlc.hip).  The per-ciphertext G2
   // preparation runs on s_prep concurrently with the item pass; the checks wait for both.
@@ -446,11 +519,13 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
                              h_lines, w_aff, w_lines, d_status);
   }));
   c->last_leaf_count = leaf_count;
-  return timed(c, "rlc_finalize", [&] {
+  HB_TRY(timed(c, "rlc_finalize", [&] {
     return launch_rlc_finalize(c->stream, n_tiles, tiles, h_st, w_st, d_status, d_idx, ks->n,
-                               ks->rejects, const_cast<uint32_t*>(sus.last_bad), sus.now,
+                               ks->rejects + (size_t)c->lane * ks->n,
+                               const_cast<uint32_t*>(sus.last_bad), sus.now,
                                track_threshold(ks, n_items));
-  });
+  }));
+  return end_verify(c);
 }
 
 int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8_t* d_H,
@@ -463,6 +538,9 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   if (n_items == 0) return HBTC_OK;
   if (!aligned16(d_H) || !aligned16(d_sig))
     return fail(c, HBTC_ERR_ARG, "item arrays must be 16-byte aligned");
+  HB_TRY(begin_verify(c, {rng(d_H, 96 * (size_t)n_inst), rng(d_idx, 4 * (size_t)n_items),
+                          rng(d_sig, 96 * (size_t)n_items)},
+                      {rng(d_status, 4 * (size_t)n_items)}));
   HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
   if (c->last_dec.status == d_status) c->last_dec = {};
   G2A* h_aff;
@@ -473,10 +551,11 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   if (c->verify_mode == HBTC_MODE_PER_SHARE) {
     HB_TRY(prepare_g2(c, d_H, nullptr, n_inst, &h_aff, &h_st, &h_lines));
     HB_TRY(make_tiles(c, n_inst, offsets, &tiles, &n_tiles));
-    return timed(c, "sig_verify", [&] {
+    HB_TRY(timed(c, "sig_verify", [&] {
       return launch_sig_verify(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->n,
                                h_aff, h_st, h_lines, d_status);
-    });
+    }));
+    return end_verify(c);
   }
   // RLC batch verification (hbtc_sig.hip): H's line tables on s_prep beside the item pass; the
   // G2 sums' projective line tables before each check level.
@@ -539,11 +618,13 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
     }));
   }
   c->last_leaf_count = leaf_count;
-  return timed(c, "rlc_finalize", [&] {
+  HB_TRY(timed(c, "rlc_finalize", [&] {
     return launch_rlc_finalize(c->stream, n_tiles, tiles, h_st, h_st, d_status, d_idx, ks->n,
-                               ks->rejects, const_cast<uint32_t*>(sus.last_bad), sus.now,
+                               ks->rejects + (size_t)c->lane * ks->n,
+                               const_cast<uint32_t*>(sus.last_bad), sus.now,
                                track_threshold(ks, n_items));
-  });
+  }));
+  return end_verify(c);
 }
 
 // Window width of a batch of n-term MSMs: minimise ceil(256/c) * (mixed adds + bucket adds) in
@@ -617,7 +698,8 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
   if (!aligned16(d_pts) || !aligned16(d_out))
     return fail(c, HBTC_ERR_ARG, "point arrays must be 16-byte aligned");
   hipStream_t sc = c->s_comb;
-  HB_TRY(stream_after(c, sc, c->stream, c->ev_main));
+  for (Lane& l : c->lanes)  // behind every verification issued so far (its inputs)
+    HB_TRY(stream_after(c, sc, l.stream, l.ev_main));
   void* p;
   HB_TRY(stage_upload(c, "comb.offsets", offsets, ((size_t)n_inst + 1) * 4, sc, &p));
   uint32_t* d_off = static_cast<uint32_t*>(p);
@@ -728,11 +810,17 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return HBTC_ERR_DEVICE;
   hbtc_ctx* c = new hbtc_ctx();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->s_prep, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->s_comb, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_main, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_prep, hipEventDisableTiming) != hipSuccess ||
+  for (Lane& l : c->lanes)
+    if (hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&l.s_prep, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&l.ev_main, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&l.ev_prep, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&l.done, hipEventDisableTiming) != hipSuccess) {
+      delete c;
+      return HBTC_ERR_DEVICE;
+    }
+  select_lane(c, 0);
+  if (hipStreamCreateWithFlags(&c->s_comb, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_ext2, hipEventDisableTiming) != hipSuccess ||
@@ -766,15 +854,18 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
     if (kv.second.h) (void)hipHostFree(kv.second.h);
     if (kv.second.ev) (void)hipEventDestroy(kv.second.ev);
   }
-  (void)hipEventDestroy(c->ev_main);
-  (void)hipEventDestroy(c->ev_prep);
+  for (Lane& l : c->lanes) {
+    (void)hipEventDestroy(l.ev_main);
+    (void)hipEventDestroy(l.ev_prep);
+    (void)hipEventDestroy(l.done);
+    (void)hipStreamDestroy(l.s_prep);
+    (void)hipStreamDestroy(l.stream);
+  }
   (void)hipEventDestroy(c->ev_comb);
   (void)hipEventDestroy(c->ev_ext);
   (void)hipEventDestroy(c->ev_ext2);
   (void)hipEventDestroy(c->ev_ext3);
-  (void)hipStreamDestroy(c->s_prep);
   (void)hipStreamDestroy(c->s_comb);
-  (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
@@ -796,8 +887,8 @@ int hbtc_keyset_load(hbtc_ctx* c, const uint8_t* pk_c48, uint32_t n, uint32_t* k
   HB_CHECK(c, hipMalloc(&ks.tab, sizeof(PtXY) * (size_t)n * PK_TAB_WIN * 256));
   HB_CHECK(c, hipMalloc(&ks.last_bad, sizeof(uint32_t) * n));
   HB_CHECK(c, hipMemsetAsync(ks.last_bad, 0, sizeof(uint32_t) * n, c->stream));
-  HB_CHECK(c, hipMalloc(&ks.rejects, sizeof(uint32_t) * n));
-  HB_CHECK(c, hipMemsetAsync(ks.rejects, 0, sizeof(uint32_t) * n, c->stream));
+  HB_CHECK(c, hipMalloc(&ks.rejects, 2 * sizeof(uint32_t) * n));  // one count array per lane
+  HB_CHECK(c, hipMemsetAsync(ks.rejects, 0, 2 * sizeof(uint32_t) * n, c->stream));
   Fq* tab_ws;
   HB_TRY(wst(c, "pktab.ws", (size_t)n * PK_TAB_WIN * 512, &tab_ws));
   HB_TRY(timed(c, "prepare", [&] {
@@ -843,6 +934,7 @@ int hbtc_verify_sig_shares(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, con
   HB_TRY(upload(c, "in1", idx, (size_t)4 * n, &d_idx));
   HB_TRY(upload(c, "in2", sig, (size_t)96 * n, &d_sig));
   HB_TRY(ws(c, "out0", (size_t)4 * n, &d_st));
+  PinLane pin(c);  // the uploads above went to the current lane
   HB_TRY(sig_shares_dev(c, keyset_id, n_inst, (const uint8_t*)d_H, offsets,
                         (const uint32_t*)d_idx, (const uint8_t*)d_sig, (int32_t*)d_st));
   HB_TRY(download(c, status, d_st, (size_t)4 * n));
@@ -924,6 +1016,7 @@ int hbtc_verify_dec_shares(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const
   HB_TRY(upload(c, "in2", idx, (size_t)4 * n, &d_idx));
   HB_TRY(upload(c, "in3", share, (size_t)48 * n, &d_sh));
   HB_TRY(ws(c, "out0", (size_t)4 * n, &d_st));
+  PinLane pin(c);  // the uploads above went to the current lane
   HB_TRY(dec_shares_dev(c, keyset_id, n_ct, (const uint8_t*)d_H, (const uint8_t*)d_w, offsets,
                         (const uint32_t*)d_idx, (const uint8_t*)d_sh, (int32_t*)d_st));
   HB_TRY(download(c, status, d_st, (size_t)4 * n));
@@ -984,6 +1077,8 @@ int hbtc_dev_upload(hbtc_ctx* c, void* d_dst, const void* h_src, size_t bytes) {
   if (!c) return HBTC_ERR_ARG;
   Guard g(c);
   HB_TRY(guard_write(c, d_dst, bytes));  // a combine still reading the old contents
+  Lane& other = c->lanes[c->lane ^ 1];  // or a verification on the other lane
+  if (other.busy) HB_CHECK(c, hipStreamWaitEvent(c->stream, other.done, 0));
   HB_CHECK(c, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, c->stream));
   HB_CHECK(c, hipStreamSynchronize(c->stream));
   return HBTC_OK;
@@ -1007,8 +1102,10 @@ int hbtc_stream_wait_ctx(hbtc_ctx* c, void* stream) {
   if (!c) return HBTC_ERR_ARG;
   Guard g(c);
   hipStream_t ext = static_cast<hipStream_t>(stream);
-  HB_TRY(stream_after(c, ext, c->stream, c->ev_ext));
-  HB_TRY(stream_after(c, ext, c->s_prep, c->ev_ext2));
+  for (Lane& l : c->lanes) {  // the lane events are re-recorded: waits capture them at once
+    HB_TRY(stream_after(c, ext, l.stream, c->ev_ext));
+    HB_TRY(stream_after(c, ext, l.s_prep, c->ev_ext2));
+  }
   return stream_after(c, ext, c->s_comb, c->ev_ext3);
 }
 
@@ -1016,8 +1113,10 @@ int hbtc_ctx_wait_stream(hbtc_ctx* c, void* stream) {
   if (!c) return HBTC_ERR_ARG;
   Guard g(c);
   HB_CHECK(c, hipEventRecord(c->ev_ext, static_cast<hipStream_t>(stream)));
-  HB_CHECK(c, hipStreamWaitEvent(c->stream, c->ev_ext, 0));
-  HB_CHECK(c, hipStreamWaitEvent(c->s_prep, c->ev_ext, 0));
+  for (Lane& l : c->lanes) {
+    HB_CHECK(c, hipStreamWaitEvent(l.stream, c->ev_ext, 0));
+    HB_CHECK(c, hipStreamWaitEvent(l.s_prep, c->ev_ext, 0));
+  }
   HB_CHECK(c, hipStreamWaitEvent(c->s_comb, c->ev_ext, 0));
   return HBTC_OK;
 }
