@@ -139,11 +139,12 @@ class Epoch:
             p = ctx.dev_alloc(arr.nbytes)
             ctx.dev_upload(p, arr)
             self.d[name] = p
-        # two sets of outputs, alternated per step: epoch k+1's verification writes one status
-        # array while epoch k's combine (and its gather) still reads the other (hbtc.h ordering)
+        # four sets of outputs, rotated per step: the library runs two verifications at once
+        # (its two lanes) while the combines of the two epochs before them still read their
+        # statuses, so epoch k writes the set epoch k-4's combine (and gather) has finished with
         alloc = out_alloc or (lambda nbytes, i32: (ctx.dev_alloc(nbytes), None))
         self.out = []
-        for j in range(2):
+        for j in range(N_OUT):
             self.out.append({name: alloc(nb, i32) for name, nb, i32 in
                              (("status", 4 * total, True), ("g", 48 * m, False), ("cst", 4 * m, True))})
         self.cur = 0
@@ -160,7 +161,7 @@ class Epoch:
         td.rs:184).  The combines run on the library's combine stream behind this epoch's
         verification, so they overlap the NEXT epoch's verification (pipelined epochs)."""
         lib, h, d = ctx.lib, ctx.h, self.d
-        self.cur ^= 1
+        self.cur = (self.cur + 1) % N_OUT
         j = self.cur
         off = N._ptr(self.offsets)
         ctx._check(lib.hbtc_verify_dec_shares_dev(h, self.keyset, self.m, d["H"], d["w"], off,
@@ -213,14 +214,14 @@ class StrongGather:
         self.len_items = [hi - lo for _, (lo, hi) in slices]
         self.len_cts = [b - a for (a, b), _ in slices]
         dev = torch.device("cuda", torch.cuda.current_device())
-        self.streams = [torch.cuda.Stream(dev) for _ in range(2)]
+        self.streams = [torch.cuda.Stream(dev) for _ in range(N_OUT)]
         tot_items, tot_cts = sum(self.len_items), sum(self.len_cts)
         self.all = [{"status": torch.empty(tot_items, dtype=torch.int32, device=dev),
                      "g": torch.empty((tot_cts, 48), dtype=torch.uint8, device=dev),
-                     "cst": torch.empty(tot_cts, dtype=torch.int32, device=dev)} for _ in range(2)]
+                     "cst": torch.empty(tot_cts, dtype=torch.int32, device=dev)} for _ in range(N_OUT)]
 
     def before_step(self, ctx):
-        ctx.ctx_wait_stream(self.streams[self.ep.cur ^ 1].cuda_stream)
+        ctx.ctx_wait_stream(self.streams[(self.ep.cur + 1) % N_OUT].cuda_stream)
 
     def after_step(self, ctx):
         from hbbft_amd import shard
@@ -270,6 +271,8 @@ def max_over_ranks(elapsed, dist, device=None):
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     return float(tt.item())
 
+
+N_OUT = 4  # output sets rotated per step (Epoch.step)
 
 FAMS = ["dec_verify", "rlc_items", "chk_tiles", "chk_tiles_w", "chk_subs", "chk_subs_w",
         "chk_leaves", "rlc_finalize", "lagrange", "comb_decode", "comb_digits", "combine", "prepare"]

@@ -38,6 +38,18 @@
 #define HDN __host__ __device__ inline __attribute__((noinline))
 #endif
 #define HBTC_CONST static constexpr
+// Latency-bound kernels (the group-check levels and the per-instance G2 preparation: a few
+// waves per SIMD, each a long dependent chain) raise their wave priority, so when the next
+// epoch's item pass shares the SIMDs with them the arbiter issues their instructions first and
+// the item waves fill the remaining slots.  HBTC_LATENCY_PRIO_LEVEL=0 turns it off.
+#ifndef HBTC_LATENCY_PRIO_LEVEL
+#define HBTC_LATENCY_PRIO_LEVEL 2
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HBTC_LATENCY_PRIO() __builtin_amdgcn_s_setprio(HBTC_LATENCY_PRIO_LEVEL)
+#else
+#define HBTC_LATENCY_PRIO() ((void)0)
+#endif
 #else
 #define HD static inline
 #define HDN static inline __attribute__((noinline))

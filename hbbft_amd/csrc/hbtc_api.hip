@@ -26,6 +26,8 @@ void hash_g1_g2_c96(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8
 hipError_t launch_hash_cand(hipStream_t s, uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
                             const uint32_t* offsets, G2A* cand);
 hipError_t launch_unframe(hipStream_t s, uint32_t n, uint32_t size, const uint8_t* framed, uint8_t* items);
+hipError_t launch_stage_copy(hipStream_t s, const void* src, void* dst, size_t bytes);
+hipError_t launch_zero_u32(hipStream_t s, uint32_t* p, size_t n);
 void hash_bytes(const uint8_t* g1_c48, size_t len, uint8_t* out);
 void parallel_items(uint32_t n, const std::function<void(uint32_t)>& f);
 bool hash_offsets_ok(uint32_t n, const uint32_t* offsets);
@@ -57,6 +59,8 @@ struct Span {
 
 // Pinned host staging buffer for small host-shaped tables (tiles, offsets); `ev` marks the
 // completion of the last copy out of it, so it is reused without synchronising a stream.
+constexpr unsigned STAGE_SLOTS = 4;
+
 struct Stage {
   void* h = nullptr;
   size_t cap = 0;
@@ -71,6 +75,7 @@ struct Stage {
 struct Lane {
   hipStream_t stream = nullptr, s_prep = nullptr;
   hipEvent_t ev_main = nullptr, ev_prep = nullptr, done = nullptr;
+  int dec_flip = 0;  // alternates the lane's decoded-item buffers (a combine may still read one)
   std::vector<std::pair<uintptr_t, uintptr_t>> rd, wr;
   bool busy = false;
 };
@@ -90,6 +95,7 @@ struct hbtc_ctx {
   hipEvent_t ev_main = nullptr, ev_prep = nullptr, ev_comb = nullptr;
   hipEvent_t ev_ext = nullptr, ev_ext2 = nullptr, ev_ext3 = nullptr;  // external-stream ordering
   std::map<std::string, Stage> stages;
+  std::map<std::string, unsigned> stage_next;
   std::mutex mu;
   std::string err;
   std::map<uint32_t, Keyset> keysets;
@@ -115,7 +121,6 @@ struct hbtc_ctx {
     const G1A* dec = nullptr;   // DecryptionShares (G1)
     const G2A* dec2 = nullptr;  // SignatureShares (G2)
   } last_dec;
-  int dec_flip = 0;
   std::random_device rd;
   bool timing = false;
   std::vector<Span> spans;
@@ -222,6 +227,22 @@ int begin_verify(hbtc_ctx* c, std::vector<std::pair<uintptr_t, uintptr_t>> rd,
   return HBTC_OK;
 }
 
+// Another asynchronous operation on the current lane (e.g. unframing): it waits for the other
+// lane on conflicting ranges, and its ranges join the lane's, so the next verification (on the
+// other lane) orders itself after it when it reads what this writes.
+int lane_async(hbtc_ctx* c, std::initializer_list<std::pair<uintptr_t, uintptr_t>> rd,
+               std::initializer_list<std::pair<uintptr_t, uintptr_t>> wr) {
+  Lane& me = c->lanes[c->lane];
+  const Lane& other = c->lanes[c->lane ^ 1];
+  const std::vector<std::pair<uintptr_t, uintptr_t>> r(rd), w(wr);
+  if (other.busy && (ranges_overlap(w, other.wr) || ranges_overlap(r, other.wr) ||
+                     ranges_overlap(w, other.rd)))
+    HB_CHECK(c, hipStreamWaitEvent(me.stream, other.done, 0));
+  me.rd.insert(me.rd.end(), r.begin(), r.end());
+  me.wr.insert(me.wr.end(), w.begin(), w.end());
+  return HBTC_OK;
+}
+
 int end_verify(hbtc_ctx* c) {
   Lane& me = c->lanes[c->lane];
   HB_CHECK(c, hipEventRecord(me.done, me.stream));
@@ -312,19 +333,28 @@ int timed(hbtc_ctx* c, const char* family, F&& launch) {
 // Host table -> device workspace `name` through its pinned stage, ordered on `st`.
 int stage_upload(hbtc_ctx* c, const char* name, const void* src, size_t bytes, hipStream_t st,
                  void** d_out) {
-  Stage& sg = c->stages[c->ws_suffix.empty() ? std::string(name) : std::string(name) + c->ws_suffix];
-  if (sg.used) HB_CHECK(c, hipEventSynchronize(sg.ev));  // the previous copy out of it is done
+  // a ring of pinned host buffers per name: the host waits only for the copy out of the slot
+  // it reuses, STAGE_SLOTS calls back, not for the previous call's (which may sit behind a
+  // whole verification on its stream) -- the host stays ahead of the device
+  const std::string base = c->ws_suffix.empty() ? std::string(name) : std::string(name) + c->ws_suffix;
+  const unsigned slot = c->stage_next[base]++ % STAGE_SLOTS;
+  Stage& sg = c->stages[base + "@" + std::to_string(slot)];
+  if (sg.used) HB_CHECK(c, hipEventSynchronize(sg.ev));  // the copy out of this slot is done
   if (sg.cap < bytes || !sg.h) {
     if (sg.h) HB_CHECK(c, hipHostFree(sg.h));
     sg.h = nullptr;
     const size_t want = bytes + bytes / 4 + 256;
-    HB_CHECK(c, hipHostMalloc(&sg.h, want));
+    HB_CHECK(c, hipHostMalloc(&sg.h, want, hipHostMallocMapped | hipHostMallocPortable));
     sg.cap = want;
   }
   if (!sg.ev) HB_CHECK(c, hipEventCreateWithFlags(&sg.ev, hipEventDisableTiming));
   if (bytes) memcpy(sg.h, src, bytes);
   HB_TRY(ws(c, name, bytes, d_out));
-  if (bytes) HB_CHECK(c, hipMemcpyAsync(*d_out, sg.h, bytes, hipMemcpyHostToDevice, st));
+  if (bytes) {
+    void* src = nullptr;
+    HB_CHECK(c, hipHostGetDevicePointer(&src, sg.h, 0));
+    HB_CHECK(c, launch_stage_copy(st, src, *d_out, bytes));
+  }
   HB_CHECK(c, hipEventRecord(sg.ev, st));
   sg.used = true;
   return HBTC_OK;
@@ -472,8 +502,8 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   Fq2 *t_tiles, *t_subs;
   HB_TRY(wst(c, "rlc.sums", n_tiles, &sums));
   // two alternating buffers: a combine of the previous call may still read the other one
-  c->dec_flip ^= 1;
-  HB_TRY(wst(c, c->dec_flip ? "rlc.dec1" : "rlc.dec0", n_items, &dec));
+  c->lanes[c->lane].dec_flip ^= 1;
+  HB_TRY(wst(c, c->lanes[c->lane].dec_flip ? "rlc.dec1" : "rlc.dec0", n_items, &dec));
   HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
   HB_TRY(guard_write(c, dec, (size_t)n_items * sizeof(G1A)));
   c->last_dec = {d_status, d_share, n_items, dec, nullptr};
@@ -489,7 +519,7 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   uint32_t* sub_count = counters + 1;
   uint32_t* tw_count = counters + 2;
   uint32_t* sw_count = counters + 3;
-  HB_CHECK(c, hipMemsetAsync(counters, 0, 4 * sizeof(uint32_t), c->stream));
+  HB_CHECK(c, launch_zero_u32(c->stream, counters, 4));
   const Suspects sus = suspects_of(c, ks, leaf_count, leaves);
   HB_TRY(timed(c, "rlc_items", [&] {
     return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->tab,
@@ -571,8 +601,8 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   Fq2* tables;
   uint32_t *inf, *counters, *sub_list, *leaves;
   HB_TRY(wst(c, "sig.sums", n_tiles, &sums));
-  c->dec_flip ^= 1;
-  HB_TRY(wst(c, c->dec_flip ? "sig.dec1" : "sig.dec0", n_items, &dec));
+  c->lanes[c->lane].dec_flip ^= 1;
+  HB_TRY(wst(c, c->lanes[c->lane].dec_flip ? "sig.dec1" : "sig.dec0", n_items, &dec));
   HB_TRY(guard_write(c, dec, (size_t)n_items * sizeof(G2A)));
   c->last_dec = {d_status, d_sig, n_items, nullptr, dec};
   HB_TRY(wst(c, "sig.tables", n_tables * PLINES_FQ2, &tables));
@@ -582,7 +612,7 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   HB_TRY(wst(c, "sig.leaves", (size_t)2 * n_items, &leaves));
   uint32_t* leaf_count = counters;
   uint32_t* sub_count = counters + 1;
-  HB_CHECK(c, hipMemsetAsync(counters, 0, 2 * sizeof(uint32_t), c->stream));
+  HB_CHECK(c, launch_zero_u32(c->stream, counters, 2));
   const Suspects sus = suspects_of(c, ks, leaf_count, leaves);
   HB_TRY(timed(c, "sig_items", [&] {
     return launch_sig_items(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->tab,
@@ -698,8 +728,16 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
   if (!aligned16(d_pts) || !aligned16(d_out))
     return fail(c, HBTC_ERR_ARG, "point arrays must be 16-byte aligned");
   hipStream_t sc = c->s_comb;
-  for (Lane& l : c->lanes)  // behind every verification issued so far (its inputs)
-    HB_TRY(stream_after(c, sc, l.stream, l.ev_main));
+  {  // behind the current lane (the verification that produced the statuses, or whatever wrote
+     // the inputs) and behind the other lane when it writes any of them
+    const std::vector<std::pair<uintptr_t, uintptr_t>> reads = {
+        rng(d_idx, (size_t)n_items * 4), rng(d_pts, (size_t)n_items * (group == 1 ? 48 : 96)),
+        rng(d_item_status, d_item_status ? (size_t)n_items * 4 : 0)};
+    HB_TRY(stream_after(c, sc, c->stream, c->ev_main));
+    Lane& other = c->lanes[c->lane ^ 1];
+    if (other.busy && ranges_overlap(reads, other.wr))
+      HB_TRY(stream_after(c, sc, other.stream, other.ev_main));
+  }
   void* p;
   HB_TRY(stage_upload(c, "comb.offsets", offsets, ((size_t)n_inst + 1) * 4, sc, &p));
   uint32_t* d_off = static_cast<uint32_t*>(p);
@@ -713,8 +751,8 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
   HB_TRY(wst(c, "comb.dup", n_inst, &d_dup));
   HB_TRY(wst(c, "comb.bad", n_inst, &d_bad));
   HB_TRY(wst(c, "comb.lambda", terms, &d_lambda));
-  HB_CHECK(c, hipMemsetAsync(d_dup, 0, (size_t)n_inst * 4, sc));
-  HB_CHECK(c, hipMemsetAsync(d_bad, 0, (size_t)n_inst * 4, sc));
+  HB_CHECK(c, launch_zero_u32(sc, d_dup, n_inst));
+  HB_CHECK(c, launch_zero_u32(sc, d_bad, n_inst));
   HB_TRY(timed_on(c, sc, "lagrange", [&] {
     hipError_t e = launch_select(sc, n_inst, d_off, t, d_item_status, d_idx, d_sel_pos, d_sel_idx,
                                  d_sel_cnt);
@@ -810,15 +848,26 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return HBTC_ERR_DEVICE;
   hbtc_ctx* c = new hbtc_ctx();
   c->device = device;
+  // four streams, so each gets a hardware queue of its own (GPU_MAX_HW_QUEUES = 4): a stream
+  // sharing a queue would also stall behind the other stream's event waits.  The G2
+  // preparation stream is shared by the lanes (its work is short and ordered anyway).
   for (Lane& l : c->lanes)
     if (hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&l.s_prep, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&l.ev_main, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&l.ev_prep, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&l.done, hipEventDisableTiming) != hipSuccess) {
       delete c;
       return HBTC_ERR_DEVICE;
     }
+  // the preparation is a short latency-bound chain (few waves) that the checks wait for: its
+  // stream has the highest priority, so its workgroups are dispatched ahead of the item pass's
+  int prio_least = 0, prio_greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
+  if (hipStreamCreateWithPriority(&c->lanes[0].s_prep, hipStreamNonBlocking, prio_greatest) != hipSuccess) {
+    delete c;
+    return HBTC_ERR_DEVICE;
+  }
+  c->lanes[1].s_prep = c->lanes[0].s_prep;
   select_lane(c, 0);
   if (hipStreamCreateWithFlags(&c->s_comb, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming) != hipSuccess ||
@@ -858,9 +907,9 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
     (void)hipEventDestroy(l.ev_main);
     (void)hipEventDestroy(l.ev_prep);
     (void)hipEventDestroy(l.done);
-    (void)hipStreamDestroy(l.s_prep);
     (void)hipStreamDestroy(l.stream);
   }
+  (void)hipStreamDestroy(c->lanes[0].s_prep);
   (void)hipEventDestroy(c->ev_comb);
   (void)hipEventDestroy(c->ev_ext);
   (void)hipEventDestroy(c->ev_ext2);
@@ -886,9 +935,9 @@ int hbtc_keyset_load(hbtc_ctx* c, const uint8_t* pk_c48, uint32_t n, uint32_t* k
   }));
   HB_CHECK(c, hipMalloc(&ks.tab, sizeof(PtXY) * (size_t)n * PK_TAB_WIN * 256));
   HB_CHECK(c, hipMalloc(&ks.last_bad, sizeof(uint32_t) * n));
-  HB_CHECK(c, hipMemsetAsync(ks.last_bad, 0, sizeof(uint32_t) * n, c->stream));
+  HB_CHECK(c, launch_zero_u32(c->stream, ks.last_bad, n));
   HB_CHECK(c, hipMalloc(&ks.rejects, 2 * sizeof(uint32_t) * n));  // one count array per lane
-  HB_CHECK(c, hipMemsetAsync(ks.rejects, 0, 2 * sizeof(uint32_t) * n, c->stream));
+  HB_CHECK(c, launch_zero_u32(c->stream, ks.rejects, 2 * (size_t)n));
   Fq* tab_ws;
   HB_TRY(wst(c, "pktab.ws", (size_t)n * PK_TAB_WIN * 512, &tab_ws));
   HB_TRY(timed(c, "prepare", [&] {
@@ -1128,7 +1177,9 @@ int hbtc_unframe_points_dev(hbtc_ctx* c, uint32_t n, uint32_t point_size, const 
   if ((reinterpret_cast<uintptr_t>(d_framed) & 3u) || !aligned16(d_items))
     return fail(c, HBTC_ERR_ARG, "framed input must be 4-byte, items 16-byte aligned");
   HB_TRY(guard_write(c, d_items, (size_t)n * point_size));
-  return timed(c, "unframe", [&] { return launch_unframe(c->stream, n, point_size, d_framed, d_items); });
+  HB_TRY(lane_async(c, {rng(d_framed, (size_t)n * (point_size + 8))}, {rng(d_items, (size_t)n * point_size)}));
+  HB_TRY(timed(c, "unframe", [&] { return launch_unframe(c->stream, n, point_size, d_framed, d_items); }));
+  return end_verify(c);
 }
 
 int hbtc_verify_dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct,
@@ -1221,7 +1272,7 @@ int msm_dev(hbtc_ctx* c, int group, uint32_t n_msm, uint32_t n, uint32_t stride,
   HB_TRY(stage_upload(c, "msm.cnt", cnt.data(), (size_t)n_msm * 4, sc, &d_cnt));
   uint32_t* d_bad;
   HB_TRY(wst(c, "msm.bad", n_msm, &d_bad));
-  HB_CHECK(c, hipMemsetAsync(d_bad, 0, (size_t)n_msm * 4, sc));
+  HB_CHECK(c, launch_zero_u32(sc, d_bad, n_msm));
   const MsmPlan p = msm_plan(n_msm, n);
   if (group == 1) {
     G1A* d_aff;

@@ -222,6 +222,7 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_plain(
     const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
     const int32_t* __restrict__ h_status, const int32_t* __restrict__ w_status,
     Fq2* __restrict__ Tbuf, uint32_t* __restrict__ fail_count, uint32_t* __restrict__ fail_list) {
+  HBTC_LATENCY_PRIO();
   const uint32_t n = LEVEL == 0 ? n_direct : *n_listed * 8u;
   if (blockIdx.x * 2u * UNITS_PER_WAVE >= n) return;  // wave-uniform: grids are sized for the worst case
   const UnitLane ul = unit_lane();
@@ -262,6 +263,7 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_weighted(
     const Line* __restrict__ w_lines, const int32_t* __restrict__ h_status,
     const int32_t* __restrict__ w_status, const Fq2* __restrict__ Tbuf,
     int32_t* __restrict__ status, uint32_t* __restrict__ out_count, uint32_t* __restrict__ out_list) {
+  HBTC_LATENCY_PRIO();
   const uint32_t n = *fail_count;
   if (blockIdx.x * 2u * UNITS_PER_WAVE >= n) return;
   const UnitLane ul = unit_lane();
@@ -313,6 +315,7 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_leaves(
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
     const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
     int32_t* __restrict__ status) {
+  HBTC_LATENCY_PRIO();
   const uint32_t n = *leaf_count;
   if (blockIdx.x * 2 * UNITS_PER_WAVE >= n) return;
   const UnitLane ul = unit_lane();
@@ -362,6 +365,7 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_tiles(
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
     const int32_t* __restrict__ h_status, int32_t* __restrict__ status,
     uint32_t* __restrict__ sub_count, uint32_t* __restrict__ sub_list) {
+  HBTC_LATENCY_PRIO();
   const UnitLane ul = unit_lane();
   const uint32_t t = blockIdx.x * UNITS_PER_WAVE + ul.unit;
   const bool active = ul.unit < UNITS_PER_WAVE && t < n_tiles;
@@ -402,6 +406,7 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_subs(
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
     int32_t* __restrict__ status, uint32_t* __restrict__ leaf_count,
     uint32_t* __restrict__ leaves) {
+  HBTC_LATENCY_PRIO();
   const uint32_t n_units = *sub_count * 8u;
   if (blockIdx.x * UNITS_PER_WAVE >= n_units) return;
   const UnitLane ul = unit_lane();
@@ -452,6 +457,7 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_leaves(
     const Fq2* __restrict__ tables, const uint32_t* __restrict__ inf,
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
     int32_t* __restrict__ status) {
+  HBTC_LATENCY_PRIO();
   // leaves [base, base + chunk) of the list; tables are numbered from the chunk start
   const uint32_t c = *leaf_count;
   const uint32_t n = c > base ? min(c - base, chunk) : 0u;

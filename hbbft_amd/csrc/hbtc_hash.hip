@@ -341,6 +341,40 @@ hipError_t launch_unframe(hipStream_t s, uint32_t n, uint32_t size, const uint8_
   return hipGetLastError();
 }
 
+// Host stage -> device workspace copy as a kernel on the caller's stream (the pinned stage is
+// device-visible): a DMA-engine copy would queue behind copies of other streams that are still
+// waiting on their own dependencies, stalling this stream with them.
+__global__ void __launch_bounds__(256) k_stage_copy(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                    size_t n16, const uint8_t* __restrict__ src_b,
+                                                    uint8_t* __restrict__ dst_b, size_t n) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n16) dst[i] = src[i];
+  const size_t tail = n - 16 * n16;
+  if (i < tail) dst_b[16 * n16 + i] = src_b[16 * n16 + i];
+}
+
+hipError_t launch_stage_copy(hipStream_t s, const void* src, void* dst, size_t bytes) {
+  if (bytes == 0) return hipSuccess;
+  const size_t n16 = bytes / 16, work = n16 > 16 ? n16 : 16;
+  hipLaunchKernelGGL(k_stage_copy, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s,
+                     static_cast<const uint4*>(src), static_cast<uint4*>(dst), n16,
+                     static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), bytes);
+  return hipGetLastError();
+}
+
+// Zero n words on the caller's stream (the runtime's fill runs as a blit that can wait on other
+// streams' work; this is an ordinary kernel of ours).
+__global__ void __launch_bounds__(256) k_zero_u32(uint32_t* __restrict__ p, size_t n) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) p[i] = 0u;
+}
+
+hipError_t launch_zero_u32(hipStream_t s, uint32_t* p, size_t n) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_zero_u32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, n);
+  return hipGetLastError();
+}
+
 // [h2] P for candidates P (one lane each) -> compressed G2 words; st = 1 if [h2] P = O (the
 // host then continues G2::rand's loop itself).
 __global__ void __launch_bounds__(64) k_g2_clear_cofactor(uint32_t n, const G2A* __restrict__ in,

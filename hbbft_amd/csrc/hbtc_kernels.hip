@@ -93,6 +93,7 @@ __global__ void __launch_bounds__(64) k_g2_steps(const uint8_t* __restrict__ in0
                                                  const uint8_t* __restrict__ in1, uint32_t n1,
                                                  G2A* __restrict__ aff, Fq2* __restrict__ ws,
                                                  int32_t* __restrict__ status) {
+  HBTC_LATENCY_PRIO();
   const uint32_t g = blockIdx.x * 64 + threadIdx.x;
   if (g >= n0 + n1) return;
   uint32_t w[24];
@@ -128,6 +129,7 @@ __global__ void __launch_bounds__(64) k_g2_norm(uint32_t n, const G2A* __restric
                                                 const int32_t* __restrict__ status,
                                                 const Fq2* __restrict__ ws,
                                                 Line* __restrict__ lines) {
+  HBTC_LATENCY_PRIO();
   const uint32_t g = blockIdx.x * 64 + threadIdx.x;
   if (g >= n * MILLER_STEPS) return;
   const uint32_t a = g / MILLER_STEPS;
