@@ -23,6 +23,7 @@ NOT_ENOUGH_SHARES = 5
 DUPLICATE_ENTRY = 6
 MODE_PER_SHARE = 0
 MODE_RLC = 1
+CHECK_AUTO, CHECK_PLAIN_FIRST, CHECK_PAIR_SUBS, CHECK_PAIR_LEAVES = -1, 0, 1, 2
 STATUS_NAMES = {ACCEPT: "ACCEPT", REJECT: "REJECT", DECODE_ERR: "DECODE_ERR",
                 UNKNOWN_SENDER: "UNKNOWN_SENDER", INSTANCE_ERR: "INSTANCE_ERR",
                 NOT_ENOUGH_SHARES: "NOT_ENOUGH_SHARES", DUPLICATE_ENTRY: "DUPLICATE_ENTRY"}
@@ -87,6 +88,7 @@ SIGNATURES = {
                                 ctypes.POINTER(ctypes.c_uint64)]),
     "hbtc_timing_reset": (_I32, [_P]),
     "hbtc_set_sender_tracking": (_I32, [_P, _I32]),
+    "hbtc_set_check_schedule": (_I32, [_P, _I32]),
     "hbtc_hash_bytes": (_I32, [_P, _SZ, _P]),
     "hbtc_xor_hash_bytes_batch": (_I32, [_U32, _P, _P, _P, _P]),
     "hbtc_commitment_evaluate": (_I32, [_P, _U32, _P, _U32, _P, _P, _P]),
@@ -517,6 +519,10 @@ class Context:
         """MODE_RLC (default): batched random-linear-combination checks with exact fallback;
         MODE_PER_SHARE: one pairing check per share."""
         self._check(self.lib.hbtc_set_verify_mode(self.h, int(mode)), "hbtc_set_verify_mode")
+
+    def set_check_schedule(self, schedule):
+        """HBTC_CHECK_* (include/hbtc.h): -1 auto, 0 plain-first, 1 paired + sub-tiles, 2 paired -> leaves."""
+        self._check(self.lib.hbtc_set_check_schedule(self.h, int(schedule)), "hbtc_set_check_schedule")
 
     def set_sender_tracking(self, on):
         """Sender tracking (default on): recent liars' shares are checked one by one."""

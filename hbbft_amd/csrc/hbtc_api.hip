@@ -75,6 +75,8 @@ struct Stage {
 struct Lane {
   hipStream_t stream = nullptr, s_prep = nullptr;
   hipEvent_t ev_main = nullptr, ev_prep = nullptr, done = nullptr;
+  hipEvent_t items_done = nullptr;  // recorded after the lane's last item pass
+  bool items_rec = false;
   int dec_flip = 0;  // alternates the lane's decoded-item buffers (a combine may still read one)
   std::vector<std::pair<uintptr_t, uintptr_t>> rd, wr;
   bool busy = false;
@@ -88,6 +90,12 @@ struct hbtc_ctx {
   Lane lanes[2];
   int lane = 0;
   bool pin_lane = false;  // host entry points: stay on the lane their uploads went to
+  // item passes of the two lanes run one after the other (HBTC_ITEMS_SERIAL, default on): epoch
+  // k+1's item pass then overlaps epoch k's check levels instead of sharing the chip with epoch
+  // k's item pass
+  bool items_serial = true;
+  int n_cu = 256;               // compute units of the device (check schedule, check_mode)
+  int check_mode_forced = -1;  // HBTC_CHECK_MODE
   std::string ws_suffix;
   hipStream_t stream = nullptr;  // main: items, checks, leaves
   hipStream_t s_prep = nullptr;  // per-instance G2 preparation, overlapped with the item pass
@@ -247,6 +255,19 @@ int end_verify(hbtc_ctx* c) {
   Lane& me = c->lanes[c->lane];
   HB_CHECK(c, hipEventRecord(me.done, me.stream));
   me.busy = true;
+  return HBTC_OK;
+}
+
+// An item pass about to start on the current lane waits for the other lane's last item pass.
+int items_gate(hbtc_ctx* c) {
+  const Lane& other = c->lanes[c->lane ^ 1];
+  if (c->items_serial && other.items_rec) HB_CHECK(c, hipStreamWaitEvent(c->stream, other.items_done, 0));
+  return HBTC_OK;
+}
+int items_mark(hbtc_ctx* c) {
+  Lane& me = c->lanes[c->lane];
+  HB_CHECK(c, hipEventRecord(me.items_done, me.stream));
+  me.items_rec = true;
   return HBTC_OK;
 }
 
@@ -453,6 +474,24 @@ uint32_t track_threshold(const Keyset* ks, uint32_t n_items) {
   return t ? (uint32_t)t : 1u;
 }
 
+// Group-check schedule of one RLC call.  The plain-first form (5 levels: plain and weighted
+// checks of tiles, then of sub-tiles, then leaves) does the least work and is right when the
+// call fills the chip; a call with few tiles (a rank's slice under strong scaling, a small
+// epoch) is bound by the chain of check latencies instead, so it pairs the plain and weighted
+// checks of a group in one launch: tiles -> sub-tiles -> leaves (3 levels; C3 slices of 125
+// ciphertexts: 25.8 ms per epoch against 32.4 plain-first), or tiles -> leaves (2 levels) for
+// calls so small that their ~8.6 leaf checks per tile (1 % wrong shares) cost less than a level.  hbtc_set_check_schedule (or the environment's
+// HBTC_CHECK_MODE = plain | pair3 | pair2) forces one.
+enum { CHK_PLAIN_FIRST = HBTC_CHECK_PLAIN_FIRST, CHK_PAIR_SUBS = HBTC_CHECK_PAIR_SUBS,
+       CHK_PAIR_LEAVES = HBTC_CHECK_PAIR_LEAVES };
+int check_mode(hbtc_ctx* c, uint32_t n_tiles) {
+  if (c->check_mode_forced >= 0) return c->check_mode_forced;
+  const uint32_t simds = 4u * (uint32_t)c->n_cu;
+  if (n_tiles <= simds / 2u) return CHK_PAIR_LEAVES;
+  if (n_tiles <= 2u * simds) return CHK_PAIR_SUBS;
+  return CHK_PLAIN_FIRST;
+}
+
 // ---------------------------------------------------------------- device-pointer cores
 int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t* d_H,
                    const uint8_t* d_w, const uint32_t* offsets, const uint32_t* d_idx,
@@ -521,29 +560,48 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   uint32_t* sw_count = counters + 3;
   HB_CHECK(c, launch_zero_u32(c->stream, counters, 4));
   const Suspects sus = suspects_of(c, ks, leaf_count, leaves);
+  HB_TRY(items_gate(c));
   HB_TRY(timed(c, "rlc_items", [&] {
     return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->tab,
                             ks->n, key, sus, sums, dec, d_status);
   }));
+  HB_TRY(items_mark(c));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
-  HB_TRY(timed(c, "chk_tiles", [&] {
-    return launch_chk_plain(c->stream, 0, n_tiles, n_tiles, nullptr, nullptr, tiles, sums, h_aff,
-                            h_lines, w_aff, w_lines, h_st, w_st, t_tiles, tw_count, tw_list);
-  }));
-  HB_TRY(timed(c, "chk_tiles_w", [&] {
-    return launch_chk_weighted(c->stream, 0, n_tiles, tw_count, tw_list, nullptr, tiles, sums,
-                               h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_tiles, d_status,
-                               sub_count, sub_list);
-  }));
-  HB_TRY(timed(c, "chk_subs", [&] {
-    return launch_chk_plain(c->stream, 1, 8 * n_tiles, 0, sub_count, sub_list, tiles, sums, h_aff,
-                            h_lines, w_aff, w_lines, h_st, w_st, t_subs, sw_count, sw_list);
-  }));
-  HB_TRY(timed(c, "chk_subs_w", [&] {
-    return launch_chk_weighted(c->stream, 1, 8 * n_tiles, sw_count, sw_list, sub_list, tiles, sums,
-                               h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_subs, d_status,
-                               leaf_count, leaves);
-  }));
+  const int chk_mode = check_mode(c, n_tiles);
+  if (chk_mode != CHK_PLAIN_FIRST) {
+    // latency form: paired levels (hbtc_check.hip k_chk_pair)
+    const bool two = chk_mode == CHK_PAIR_LEAVES;
+    HB_TRY(timed(c, "chk_tiles", [&] {
+      return launch_chk_pair(c->stream, 0, two, n_tiles, n_tiles, nullptr, nullptr, tiles, sums,
+                             h_aff, h_lines, w_aff, w_lines, h_st, w_st, d_status,
+                             two ? leaf_count : sub_count, two ? leaves : sub_list);
+    }));
+    if (!two)
+      HB_TRY(timed(c, "chk_subs", [&] {
+        return launch_chk_pair(c->stream, 1, true, 8 * n_tiles, 0, sub_count, sub_list, tiles, sums,
+                               h_aff, h_lines, w_aff, w_lines, h_st, w_st, d_status, leaf_count,
+                               leaves);
+      }));
+  } else {  // throughput form: plain first (k_chk_plain / k_chk_weighted)
+    HB_TRY(timed(c, "chk_tiles", [&] {
+      return launch_chk_plain(c->stream, 0, n_tiles, n_tiles, nullptr, nullptr, tiles, sums, h_aff,
+                              h_lines, w_aff, w_lines, h_st, w_st, t_tiles, tw_count, tw_list);
+    }));
+    HB_TRY(timed(c, "chk_tiles_w", [&] {
+      return launch_chk_weighted(c->stream, 0, n_tiles, tw_count, tw_list, nullptr, tiles, sums,
+                                 h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_tiles, d_status,
+                                 sub_count, sub_list);
+    }));
+    HB_TRY(timed(c, "chk_subs", [&] {
+      return launch_chk_plain(c->stream, 1, 8 * n_tiles, 0, sub_count, sub_list, tiles, sums, h_aff,
+                              h_lines, w_aff, w_lines, h_st, w_st, t_subs, sw_count, sw_list);
+    }));
+    HB_TRY(timed(c, "chk_subs_w", [&] {
+      return launch_chk_weighted(c->stream, 1, 8 * n_tiles, sw_count, sw_list, sub_list, tiles, sums,
+                                 h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_subs, d_status,
+                                 leaf_count, leaves);
+    }));
+  }
   HB_TRY(timed(c, "chk_leaves", [&] {
     return launch_chk_leaves(c->stream, n_items, leaf_count, leaves, d_idx, dec, ks->pk, h_aff,
                              h_lines, w_aff, w_lines, d_status);
@@ -614,10 +672,12 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   uint32_t* sub_count = counters + 1;
   HB_CHECK(c, launch_zero_u32(c->stream, counters, 2));
   const Suspects sus = suspects_of(c, ks, leaf_count, leaves);
+  HB_TRY(items_gate(c));
   HB_TRY(timed(c, "sig_items", [&] {
     return launch_sig_items(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->tab,
                             ks->n, key, sus, sums, dec, d_status);
   }));
+  HB_TRY(items_mark(c));
   HB_TRY(timed(c, "sig_lines", [&] {
     return launch_plines(c->stream, 0, 2 * n_tiles, 0, nullptr, nullptr, tiles, sums, dec, tables,
                          inf);
@@ -848,6 +908,16 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return HBTC_ERR_DEVICE;
   hbtc_ctx* c = new hbtc_ctx();
   c->device = device;
+  if (const char* e = getenv("HBTC_ITEMS_SERIAL")) c->items_serial = atoi(e) != 0;
+  if (const char* e = getenv("HBTC_CHECK_MODE")) {
+    const std::string m(e);
+    c->check_mode_forced = m == "plain" ? 0 : m == "pair3" ? 1 : m == "pair2" ? 2 : -1;
+  }
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+      c->n_cu = prop.multiProcessorCount;
+  }
   // four streams, so each gets a hardware queue of its own (GPU_MAX_HW_QUEUES = 4): a stream
   // sharing a queue would also stall behind the other stream's event waits.  The G2
   // preparation stream is shared by the lanes (its work is short and ordered anyway).
@@ -855,7 +925,8 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
     if (hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&l.ev_main, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&l.ev_prep, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&l.done, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&l.done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&l.items_done, hipEventDisableTiming) != hipSuccess) {
       delete c;
       return HBTC_ERR_DEVICE;
     }
@@ -869,7 +940,11 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   }
   c->lanes[1].s_prep = c->lanes[0].s_prep;
   select_lane(c, 0);
-  if (hipStreamCreateWithFlags(&c->s_comb, hipStreamNonBlocking) != hipSuccess ||
+  // the combine stream's chain of small kernels also gets the highest priority (HBTC_COMB_PRIO=0:
+  // the lowest; C3 105.4 vs 108.7 ms per epoch)
+  const char* cp = getenv("HBTC_COMB_PRIO");
+  const int comb_prio = cp && !atoi(cp) ? prio_least : prio_greatest;
+  if (hipStreamCreateWithPriority(&c->s_comb, hipStreamNonBlocking, comb_prio) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_ext2, hipEventDisableTiming) != hipSuccess ||
@@ -907,6 +982,7 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
     (void)hipEventDestroy(l.ev_main);
     (void)hipEventDestroy(l.ev_prep);
     (void)hipEventDestroy(l.done);
+    (void)hipEventDestroy(l.items_done);
     (void)hipStreamDestroy(l.stream);
   }
   (void)hipStreamDestroy(c->lanes[0].s_prep);
@@ -1654,6 +1730,13 @@ int hbtc_g2_msm(hbtc_ctx* c, uint32_t n_msm, uint32_t n, const uint8_t* pts_c96,
   if (!c || (n_msm && (!pts_c96 || !scalars_le32 || !out_c96 || !status))) return HBTC_ERR_ARG;
   Guard g(c);
   return msm_host(c, 2, n_msm, n, pts_c96, scalars_le32, out_c96, status);
+}
+
+int hbtc_set_check_schedule(hbtc_ctx* c, int schedule) {
+  if (!c || schedule < HBTC_CHECK_AUTO || schedule > HBTC_CHECK_PAIR_LEAVES) return HBTC_ERR_ARG;
+  Guard g(c);
+  c->check_mode_forced = schedule;
+  return HBTC_OK;
 }
 
 int hbtc_set_sender_tracking(hbtc_ctx* c, int enable) {

@@ -304,6 +304,63 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_weighted(
   }
 }
 
+// Paired check (the latency form, for calls too small to fill the chip): a unit carries ONE
+// group, its plain value T on side 0 and its weighted value T_w on side 1, so a failing group's
+// single wrong share is located in the same launch.  An unlocated group either joins the
+// sub-tile list (LEVEL 0, !TO_LEAVES) or sends its pending shares to the exact leaf checks.
+// Levels per call: tiles -> leaves (2 check latencies) or tiles -> sub-tiles -> leaves (3),
+// instead of the plain-first form's 5 (hbtc_api.hip picks by the call's tile count).
+template <int LEVEL, bool TO_LEAVES>
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_pair(
+    uint32_t n_direct, const uint32_t* __restrict__ n_listed, const uint32_t* __restrict__ sub_list,
+    const Tile* __restrict__ tiles, const TileSums* __restrict__ sums,
+    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
+    const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
+    const int32_t* __restrict__ h_status, const int32_t* __restrict__ w_status,
+    int32_t* __restrict__ status, uint32_t* __restrict__ out_count, uint32_t* __restrict__ out_list) {
+  HBTC_LATENCY_PRIO();
+  const uint32_t n = LEVEL == 0 ? n_direct : *n_listed * 8u;
+  if (blockIdx.x * UNITS_PER_WAVE >= n) return;  // wave-uniform: grids are sized for the worst case
+  const UnitLane ul = unit_lane();
+  const uint32_t g = blockIdx.x * UNITS_PER_WAVE + ul.unit;
+  const GroupRef r = group_ref<LEVEL>(ul.unit < UNITS_PER_WAVE ? g : n, n, tiles, sub_list,
+                                      h_status, w_status);
+  G1J S, P;
+  jac_set_inf(S);
+  jac_set_inf(P);
+  if (r.active) {
+    S = ul.side ? sums[r.t].SW[r.sub] : sums[r.t].S[r.sub];
+    P = ul.side ? sums[r.t].PW[r.sub] : sums[r.t].P[r.sub];
+  }
+  const bool use1 = r.active && r.inst_ok && !jac_is_inf(S) && !h_aff[r.inst].inf;
+  const bool use2 = r.active && r.inst_ok && !jac_is_inf(P) && !w_aff[r.inst].inf;
+  Fq2 e, T, Tw;
+  pair_value(e, S, use1, h_lines + (size_t)r.inst * MILLER_STEPS, P, use2,
+             w_lines + (size_t)r.inst * MILLER_STEPS, ul.ps);
+  const bool pass = unit_values(T, Tw, e, ul);
+  // undecodable H / w: k_rlc_finalize decides the group's items
+  const bool fail = r.active && r.inst_ok && !pass;
+  const int32_t loc = locate(T, Tw, r.hi - r.lo, LEVEL == 0 ? 5 : 2, fail, ul);
+  if (!fail || ul.side != 0 || ul.ps.k != 0) return;
+  if (loc >= 0 && status[r.lo + loc] == HBTC_RLC_PENDING) {
+    status[r.lo + loc] = HBTC_REJECT;
+    return;
+  }
+  if (LEVEL == 0 && !TO_LEAVES) {
+    out_list[atomicAdd(out_count, 1u)] = r.t;
+  } else {
+    uint32_t m = 0;
+    for (uint32_t i = r.lo; i < r.hi; ++i) m += status[i] == HBTC_RLC_PENDING;
+    uint32_t pos = atomicAdd(out_count, m);
+    for (uint32_t i = r.lo; i < r.hi; ++i)
+      if (status[i] == HBTC_RLC_PENDING) {
+        out_list[2 * pos] = i;
+        out_list[2 * pos + 1] = r.inst;
+        ++pos;
+      }
+  }
+}
+
 #endif  // part 2
 
 #if HBTC_CHECK_IN(1)
@@ -529,6 +586,27 @@ hipError_t launch_chk_weighted(hipStream_t s, int level, uint32_t max_groups,
     hipLaunchKernelGGL(k_chk_weighted<1>, grid, dim3(64), 0, s, fail_count, fail_list, sub_list, tiles,
                        sums, h_aff, h_lines, w_aff, w_lines, h_status, w_status, Tbuf, status,
                        out_count, out_list);
+  return hipGetLastError();
+}
+
+hipError_t launch_chk_pair(hipStream_t s, int level, bool to_leaves, uint32_t max_groups,
+                           uint32_t n_direct, const uint32_t* n_listed, const uint32_t* sub_list,
+                           const Tile* tiles, const TileSums* sums, const G2A* h_aff,
+                           const Line* h_lines, const G2A* w_aff, const Line* w_lines,
+                           const int32_t* h_status, const int32_t* w_status, int32_t* status,
+                           uint32_t* out_count, uint32_t* out_list) {
+  if (max_groups == 0) return hipSuccess;
+  const dim3 grid(unit_blocks(max_groups));
+#define HBTC_PAIR_ARGS                                                                       \
+  grid, dim3(64), 0, s, n_direct, n_listed, sub_list, tiles, sums, h_aff, h_lines, w_aff, w_lines, \
+      h_status, w_status, status, out_count, out_list
+  if (level == 0 && to_leaves)
+    hipLaunchKernelGGL((k_chk_pair<0, true>), HBTC_PAIR_ARGS);
+  else if (level == 0)
+    hipLaunchKernelGGL((k_chk_pair<0, false>), HBTC_PAIR_ARGS);
+  else
+    hipLaunchKernelGGL((k_chk_pair<1, true>), HBTC_PAIR_ARGS);
+#undef HBTC_PAIR_ARGS
   return hipGetLastError();
 }
 

@@ -99,6 +99,12 @@ hipError_t launch_chk_weighted(hipStream_t s, int level, uint32_t max_groups,
                                const Line* w_lines, const int32_t* h_status,
                                const int32_t* w_status, const Fq2* Tbuf, int32_t* status,
                                uint32_t* out_count, uint32_t* out_list);
+hipError_t launch_chk_pair(hipStream_t s, int level, bool to_leaves, uint32_t max_groups,
+                           uint32_t n_direct, const uint32_t* n_listed, const uint32_t* sub_list,
+                           const Tile* tiles, const TileSums* sums, const G2A* h_aff,
+                           const Line* h_lines, const G2A* w_aff, const Line* w_lines,
+                           const int32_t* h_status, const int32_t* w_status, int32_t* status,
+                           uint32_t* out_count, uint32_t* out_list);
 hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t* leaf_count,
                              const uint32_t* leaves, const uint32_t* idx, const G1A* dec,
                              const G1A* pk, const G2A* h_aff, const Line* h_lines,

@@ -333,6 +333,18 @@ int hbtc_set_verify_mode(hbtc_ctx* ctx, int mode);
  * epoch cannot make the honest shares' groups fail.  The
  * decisions are exactly those of the per-share check either way; only the work differs. */
 int hbtc_set_sender_tracking(hbtc_ctx* ctx, int enable);
+/* Group-check schedule of RLC calls (DecryptionShares).  HBTC_CHECK_AUTO (default) picks by the
+ * call's tile count against the device's SIMDs: the plain-first schedule (plain checks of every
+ * group, weighted checks only of failing ones: tiles, tiles_w, sub-tiles, sub-tiles_w, leaves =
+ * 5 dependent check levels, the least work) for calls that fill the chip, the paired schedules
+ * (plain and weighted value of a group in one check launch: tiles -> sub-tiles -> leaves, or
+ * tiles -> leaves) for small calls, which are bound by the chain of check latencies (a rank's
+ * slice of an epoch under strong scaling).  Decisions are identical under every schedule. */
+#define HBTC_CHECK_AUTO (-1)
+#define HBTC_CHECK_PLAIN_FIRST 0
+#define HBTC_CHECK_PAIR_SUBS 1
+#define HBTC_CHECK_PAIR_LEAVES 2
+int hbtc_set_check_schedule(hbtc_ctx* ctx, int schedule);
 /* Number of shares that needed the exact single-share check in the last RLC call (syncs). */
 int hbtc_rlc_last_leaves(hbtc_ctx* ctx, uint32_t* leaves);
 

@@ -55,6 +55,24 @@ def test_c3_full_epoch_against_construction(ctx):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("cts", [125, 250])
+def test_c3_rank_slice_every_check_schedule(ctx, cts):
+    """One rank's slice of a C3 epoch under strong scaling (1000 / 8 and 1000 / 4 ciphertexts
+    of 1000 shares, 1 % wrong): the auto schedule (paired levels at this size), plain-first and
+    both paired schedules all match the construction."""
+    ep = bench.Epoch(ctx, 1000, cts, bench.SEED + cts, 0.01)
+    try:
+        for sched in (N.CHECK_AUTO, N.CHECK_PLAIN_FIRST, N.CHECK_PAIR_SUBS, N.CHECK_PAIR_LEAVES):
+            ctx.set_check_schedule(sched)
+            ep.step(ctx)
+            mism, comb_ok, _ = ep.check(ctx)
+            assert mism == 0 and comb_ok, sched
+    finally:
+        ctx.set_check_schedule(N.CHECK_AUTO)
+    ep.free(ctx)
+
+
+@pytest.mark.timeout(300)
 def test_c3_sender_concentrated_33_percent(ctx):
     """f = 333 senders lie on every ciphertext: the first epoch finds them through failing
     groups, the second runs them as tracked senders; both match the construction."""
