@@ -18,7 +18,7 @@ MSM_PARTS := 8 9
 SKG_PARTS := 10
 KOBJS := $(foreach p,$(PARTS),$(BUILD)/hbtc_kernels.p$(p).o) $(foreach p,$(RLC_PARTS),$(BUILD)/hbtc_rlc.p$(p).o) \
          $(foreach p,$(MSM_PARTS),$(BUILD)/hbtc_msm.p$(p).o) $(foreach p,$(SKG_PARTS),$(BUILD)/hbtc_skg.p$(p).o) \
-         $(BUILD)/hbtc_check.c1.o $(BUILD)/hbtc_check.c2.o $(BUILD)/hbtc_sig.o
+         $(BUILD)/hbtc_check.c1.o $(BUILD)/hbtc_check.c2.o $(BUILD)/hbtc_sig.o $(BUILD)/hbtc_bcast.o
 LIB := hbbft_amd/libhbtc.so
 
 .PHONY: all lib hosttest oracle clean resources roofline-constants
@@ -54,6 +54,10 @@ $(BUILD)/hbtc_check.c%.o: $(CSRC)/hbtc_check.hip $(HDRS) | $(BUILD)
 # the G2 item pass, all helpers inlined (no calls; the product itself stays out of line)
 $(BUILD)/hbtc_sig.o: $(CSRC)/hbtc_sig.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_INLINE_ALL -c $< -o $@
+
+# Reliable Broadcast: Reed-Solomon over GF(2^8), SHA3 Merkle trees and proofs
+$(BUILD)/hbtc_bcast.o: $(CSRC)/hbtc_bcast.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(BUILD)/hbtc_api.o: $(CSRC)/hbtc_api.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

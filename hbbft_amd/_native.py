@@ -89,6 +89,15 @@ SIGNATURES = {
     "hbtc_timing_reset": (_I32, [_P]),
     "hbtc_set_sender_tracking": (_I32, [_P, _I32]),
     "hbtc_set_check_schedule": (_I32, [_P, _I32]),
+    "hbtc_rs_encode": (_I32, [_P, _U32, _U32, _U32, _U32, _P]),
+    "hbtc_rs_reconstruct": (_I32, [_P, _U32, _U32, _U32, _U32, _P, _P, _P]),
+    "hbtc_merkle_digest_count": (_U32, [_U32]),
+    "hbtc_merkle_trees": (_I32, [_P, _U32, _U32, _U32, _P, _P]),
+    "hbtc_merkle_validate": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P, _P, _P]),
+    "hbtc_rs_encode_dev": (_I32, [_P, _U32, _U32, _U32, _U32, _P]),
+    "hbtc_rs_reconstruct_dev": (_I32, [_P, _U32, _U32, _U32, _U32, _P, _P, _P]),
+    "hbtc_merkle_trees_dev": (_I32, [_P, _U32, _U32, _U32, _P, _P]),
+    "hbtc_merkle_validate_dev": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P, _P, _P]),
     "hbtc_hash_bytes": (_I32, [_P, _SZ, _P]),
     "hbtc_xor_hash_bytes_batch": (_I32, [_U32, _P, _P, _P, _P]),
     "hbtc_commitment_evaluate": (_I32, [_P, _U32, _P, _U32, _P, _P, _P]),
@@ -414,6 +423,63 @@ class Context:
         st = np.empty(n_msm, np.int32)
         self._check(fn(self.h, n_msm, n, _ptr(pts), _ptr(sc), _ptr(out), _ptr(st)), "msm")
         return [bytes(out[size * m:size * m + size]) for m in range(n_msm)], st
+
+    # ---- Reliable Broadcast coding (include/hbtc.h, src/broadcast/)
+    def rs_encode(self, k, p, shard_len, shards):
+        """ReedSolomon::encode of every instance, in place on the uint8 array `shards`
+        (n_inst * (k + p) * shard_len bytes, parity rows overwritten); returns it."""
+        a = np.ascontiguousarray(shards, dtype=np.uint8).reshape(-1)
+        per = (k + p) * shard_len
+        if per == 0 or a.size % per:
+            raise ValueError("shards: a multiple of (k + p) * shard_len bytes")
+        self._check(self.lib.hbtc_rs_encode(self.h, k, p, shard_len, a.size // per, _ptr(a)), "rs_encode")
+        return a
+
+    def rs_reconstruct(self, k, p, shard_len, shards, present):
+        """ReedSolomon::reconstruct_shards per instance (present: n_inst * (k + p) flags); fills
+        the missing shards in place; returns the per-instance status."""
+        a = np.ascontiguousarray(shards, dtype=np.uint8).reshape(-1)
+        pr = np.ascontiguousarray(present, dtype=np.uint8).reshape(-1)
+        per = (k + p) * shard_len
+        if per == 0 or a.size % per or pr.size != (a.size // per) * (k + p):
+            raise ValueError("shards / present sizes")
+        n_inst = a.size // per
+        st = np.empty(n_inst, np.int32)
+        self._check(self.lib.hbtc_rs_reconstruct(self.h, k, p, shard_len, n_inst, _ptr(a), _ptr(pr),
+                                                 _ptr(st)), "rs_reconstruct")
+        return a, st
+
+    def merkle_trees(self, n_leaves, leaf_len, leaves):
+        """MerkleTree::from_vec of every instance: uint8[n_inst, digest_count, 32] (level 0
+        first, the root last)."""
+        a = np.ascontiguousarray(leaves, dtype=np.uint8).reshape(-1)
+        per = n_leaves * leaf_len
+        if per == 0 or a.size % per:
+            raise ValueError("leaves: a multiple of n_leaves * leaf_len bytes")
+        n_inst = a.size // per
+        nd = self.lib.hbtc_merkle_digest_count(n_leaves)
+        out = np.zeros(n_inst * nd * 32, np.uint8)
+        self._check(self.lib.hbtc_merkle_trees(self.h, n_leaves, leaf_len, n_inst, _ptr(a), _ptr(out)),
+                    "merkle_trees")
+        return out.reshape(n_inst, nd, 32)
+
+    def merkle_validate(self, n_nodes, values, index, digests, roots):
+        """Proof::validate(n_nodes) of each (values[i], index[i], digests[i] (list of 32-byte
+        digests), roots[i]); returns the status array (ACCEPT = valid)."""
+        n = len(values)
+        voff = np.zeros(n + 1, np.uint64)
+        voff[1:] = np.cumsum([len(v) for v in values]) if n else []
+        vals = np.frombuffer(b"".join(bytes(v) for v in values) or b"\0", np.uint8).copy()
+        doff = np.zeros(n + 1, np.uint32)
+        doff[1:] = np.cumsum([len(d) for d in digests]) if n else []
+        dig = np.frombuffer(b"".join(bytes(x) for d in digests for x in d) or bytes(32), np.uint8).copy()
+        rts = np.frombuffer(b"".join(bytes(r) for r in roots) or bytes(32), np.uint8).copy()
+        ix = np.ascontiguousarray(index, dtype=np.uint32)
+        st = np.empty(max(n, 1), np.int32)
+        self._check(self.lib.hbtc_merkle_validate(self.h, n, n_nodes, _ptr(voff), _ptr(vals), _ptr(ix),
+                                                  _ptr(doff), _ptr(dig), _ptr(rts), _ptr(st)),
+                    "merkle_validate")
+        return st[:n]
 
     def g1_msm(self, n_msm, n, points, scalars):
         """n_msm MSMs of n terms (points/scalars item-major [m][i]); returns ([48 B], status)."""

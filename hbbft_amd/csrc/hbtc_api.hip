@@ -129,6 +129,12 @@ struct hbtc_ctx {
     const G1A* dec = nullptr;   // DecryptionShares (G1)
     const G2A* dec2 = nullptr;  // SignatureShares (G2)
   } last_dec;
+  // Reed-Solomon plans (hbtc_rs_*): device row lists and nibble tables per (k, p, pattern)
+  struct GfPlan {
+    uint32_t *out_rows = nullptr, *in_rows = nullptr, *tabs = nullptr;
+    uint32_t n_out = 0, n_in = 0;
+  };
+  std::map<std::string, GfPlan> gf_plans;
   std::random_device rd;
   bool timing = false;
   std::vector<Span> spans;
@@ -974,6 +980,11 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
     (void)hipEventDestroy(sp.b);
   }
   for (auto& r : c->comb_reads) (void)hipEventDestroy(r.ev);
+  for (auto& kv : c->gf_plans) {
+    (void)hipFree(kv.second.out_rows);
+    (void)hipFree(kv.second.in_rows);
+    (void)hipFree(kv.second.tabs);
+  }
   for (auto& kv : c->stages) {
     if (kv.second.h) (void)hipHostFree(kv.second.h);
     if (kv.second.ev) (void)hipEventDestroy(kv.second.ev);
@@ -1895,6 +1906,391 @@ int hbtc_decrypt(hbtc_ctx* c, uint32_t n, const uint8_t* sk_le32, const uint8_t*
     for (size_t j2 = 0; j2 < len; ++j2) o[j2] ^= msgs[offsets[i] + j2];
   });
   return HBTC_OK;
+}
+
+}  // extern "C"
+
+// ============================================================================ Reliable Broadcast
+// reed-solomon-erasure 3.1 (hbbft's Coding, /root/reference/src/broadcast/broadcast.rs:395-459):
+// GF(2^8) mod x^8 + x^4 + x^3 + x^2 + 1 (0x11D), generator 2; build_matrix(k, n) =
+// vandermonde(n, k) * inverse(top k x k) (systematic); encode = the parity rows times the data;
+// reconstruct_shards = the inverse of the rows of the first k present shards for the missing
+// data, then the parity rows for the missing parity.  The matrices are built and inverted here
+// (once per shape / presence pattern, cached); the byte work runs in k_gf_apply.
+namespace {
+struct Gf {
+  uint8_t exp[512], log[256];
+  Gf() {
+    unsigned x = 1;
+    for (int i = 0; i < 255; ++i) {
+      exp[i] = exp[i + 255] = (uint8_t)x;
+      log[x] = (uint8_t)i;
+      x <<= 1;
+      if (x & 0x100) x ^= 0x11D;
+    }
+    exp[510] = exp[511] = exp[0];
+    log[0] = 0;
+  }
+  uint8_t mul(uint8_t a, uint8_t b) const { return a && b ? exp[log[a] + log[b]] : 0; }
+  uint8_t inv(uint8_t a) const { return exp[(255 - log[a]) % 255]; }
+  uint8_t pow(uint8_t a, unsigned n) const {  // galois_8::exp
+    if (n == 0) return 1;
+    if (a == 0) return 0;
+    return exp[(log[a] * (size_t)n) % 255];
+  }
+};
+const Gf& gf() {
+  static const Gf g;
+  return g;
+}
+typedef std::vector<std::vector<uint8_t>> GfMat;
+
+bool gf_invert(GfMat m, GfMat& inv) {
+  const size_t n = m.size();
+  const Gf& g = gf();
+  inv.assign(n, std::vector<uint8_t>(n, 0));
+  for (size_t i = 0; i < n; ++i) inv[i][i] = 1;
+  for (size_t c = 0; c < n; ++c) {
+    size_t p = c;
+    while (p < n && !m[p][c]) ++p;
+    if (p == n) return false;
+    std::swap(m[c], m[p]);
+    std::swap(inv[c], inv[p]);
+    const uint8_t f = g.inv(m[c][c]);
+    for (size_t j = 0; j < n; ++j) {
+      m[c][j] = g.mul(f, m[c][j]);
+      inv[c][j] = g.mul(f, inv[c][j]);
+    }
+    for (size_t r = 0; r < n; ++r) {
+      const uint8_t e = m[r][c];
+      if (r == c || !e) continue;
+      for (size_t j = 0; j < n; ++j) {
+        m[r][j] ^= g.mul(e, m[c][j]);
+        inv[r][j] ^= g.mul(e, inv[c][j]);
+      }
+    }
+  }
+  return true;
+}
+
+// build_matrix(k, k + p), rows [0, k + p)
+const GfMat& rs_matrix(uint32_t k, uint32_t p) {
+  static std::mutex mu;
+  static std::map<std::pair<uint32_t, uint32_t>, GfMat> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find({k, p});
+  if (it != cache.end()) return it->second;
+  const Gf& g = gf();
+  const uint32_t n = k + p;
+  GfMat v(n, std::vector<uint8_t>(k));
+  for (uint32_t r = 0; r < n; ++r)
+    for (uint32_t c = 0; c < k; ++c) v[r][c] = g.pow((uint8_t)r, c);
+  GfMat top(v.begin(), v.begin() + k), ti;
+  gf_invert(top, ti);  // a Vandermonde matrix of distinct points: always invertible
+  GfMat m(n, std::vector<uint8_t>(k, 0));
+  for (uint32_t r = 0; r < n; ++r)
+    for (uint32_t j = 0; j < k; ++j) {
+      uint8_t acc = 0;
+      for (uint32_t q = 0; q < k; ++q) acc ^= g.mul(v[r][q], ti[q][j]);
+      m[r][j] = acc;
+    }
+  return cache.emplace(std::make_pair(k, p), std::move(m)).first->second;
+}
+
+// nibble tables of coefficient c (k_gf_apply): c * x and c * 16x for x < 16, 4 bytes per dword
+void nib_tables(uint8_t c, uint32_t* t) {
+  const Gf& g = gf();
+  for (int w = 0; w < 8; ++w) {
+    uint32_t v = 0;
+    for (int b = 0; b < 4; ++b) {
+      const unsigned x = (unsigned)(4 * (w & 3) + b);
+      v |= (uint32_t)g.mul(c, (uint8_t)(w < 4 ? x : x << 4)) << (8 * b);
+    }
+    t[w] = v;
+  }
+}
+
+int gf_plan(hbtc_ctx* c, const std::string& key, const std::vector<uint32_t>& out_rows,
+            const std::vector<uint32_t>& in_rows, const GfMat& coef, const hbtc_ctx::GfPlan** out) {
+  auto it = c->gf_plans.find(key);
+  if (it == c->gf_plans.end()) {
+    if (c->gf_plans.size() >= 256) {  // presence patterns are few per era; bound the cache anyway
+      HB_CHECK(c, hipStreamSynchronize(c->stream));
+      for (auto& kv : c->gf_plans) {
+        (void)hipFree(kv.second.out_rows);
+        (void)hipFree(kv.second.in_rows);
+        (void)hipFree(kv.second.tabs);
+      }
+      c->gf_plans.clear();
+    }
+    hbtc_ctx::GfPlan pl;
+    pl.n_out = (uint32_t)out_rows.size();
+    pl.n_in = (uint32_t)in_rows.size();
+    std::vector<uint32_t> tabs((size_t)pl.n_out * pl.n_in * 8);
+    for (uint32_t r = 0; r < pl.n_out; ++r)
+      for (uint32_t j = 0; j < pl.n_in; ++j) nib_tables(coef[r][j], &tabs[((size_t)r * pl.n_in + j) * 8]);
+    HB_CHECK(c, hipMalloc(&pl.out_rows, 4 * std::max<size_t>(1, pl.n_out)));
+    HB_CHECK(c, hipMalloc(&pl.in_rows, 4 * std::max<size_t>(1, pl.n_in)));
+    HB_CHECK(c, hipMalloc(&pl.tabs, 4 * std::max<size_t>(1, tabs.size())));
+    HB_CHECK(c, hipMemcpy(pl.out_rows, out_rows.data(), 4 * out_rows.size(), hipMemcpyHostToDevice));
+    HB_CHECK(c, hipMemcpy(pl.in_rows, in_rows.data(), 4 * in_rows.size(), hipMemcpyHostToDevice));
+    HB_CHECK(c, hipMemcpy(pl.tabs, tabs.data(), 4 * tabs.size(), hipMemcpyHostToDevice));
+    it = c->gf_plans.emplace(key, pl).first;
+  }
+  *out = &it->second;
+  return HBTC_OK;
+}
+
+int rs_check(hbtc_ctx* c, uint32_t k, uint32_t p, uint32_t len) {
+  // ReedSolomon::new: TooFewDataShards / TooFewParityShards / TooManyShards (> 256)
+  if (k == 0 || p == 0 || k + p > 256) return fail(c, HBTC_ERR_ARG, "shard counts (ReedSolomon::new)");
+  if (len == 0) return fail(c, HBTC_ERR_ARG, "empty shards");
+  return HBTC_OK;
+}
+
+int rs_encode_dev(hbtc_ctx* c, uint32_t k, uint32_t p, uint32_t len, uint32_t n_inst, uint8_t* d) {
+  HB_TRY(rs_check(c, k, p, len));
+  if (n_inst == 0) return HBTC_OK;
+  const size_t bytes = (size_t)n_inst * (k + p) * len;
+  HB_TRY(begin_verify(c, {rng(d, bytes)}, {rng(d, bytes)}));
+  const std::string key = "enc/" + std::to_string(k) + "/" + std::to_string(p);
+  const hbtc_ctx::GfPlan* pl;
+  if (!c->gf_plans.count(key)) {
+    const GfMat& m = rs_matrix(k, p);
+    std::vector<uint32_t> outs(p), ins(k);
+    for (uint32_t i = 0; i < p; ++i) outs[i] = k + i;
+    for (uint32_t i = 0; i < k; ++i) ins[i] = i;
+    HB_TRY(gf_plan(c, key, outs, ins, GfMat(m.begin() + k, m.end()), &pl));
+  } else {
+    pl = &c->gf_plans[key];
+  }
+  HB_TRY(timed(c, "rs", [&] {
+    return launch_gf_apply(c->stream, n_inst, nullptr, d, (uint64_t)(k + p) * len, len, pl->n_out,
+                           pl->out_rows, pl->n_in, pl->in_rows, pl->tabs);
+  }));
+  return end_verify(c);
+}
+
+int rs_reconstruct_dev(hbtc_ctx* c, uint32_t k, uint32_t p, uint32_t len, uint32_t n_inst, uint8_t* d,
+                       const uint8_t* present, int32_t* status) {
+  HB_TRY(rs_check(c, k, p, len));
+  if (n_inst == 0) return HBTC_OK;
+  if (!present || !status) return fail(c, HBTC_ERR_ARG, "present / status");
+  const uint32_t n = k + p;
+  const size_t bytes = (size_t)n_inst * n * len;
+  HB_TRY(begin_verify(c, {rng(d, bytes)}, {rng(d, bytes)}));
+  // group the instances by presence pattern
+  std::map<std::string, std::vector<uint32_t>> groups;
+  for (uint32_t i = 0; i < n_inst; ++i) {
+    std::string pat(n, '0');
+    uint32_t cnt = 0;
+    for (uint32_t j = 0; j < n; ++j)
+      if (present[(size_t)i * n + j]) {
+        pat[j] = '1';
+        ++cnt;
+      }
+    if (cnt < k) {
+      status[i] = HBTC_NOT_ENOUGH_SHARES;  // TooFewShardsPresent
+      continue;
+    }
+    status[i] = HBTC_ACCEPT;
+    if (cnt < n) groups[pat].push_back(i);
+  }
+  const GfMat& m = rs_matrix(k, p);
+  for (auto& kv : groups) {
+    const std::string& pat = kv.first;
+    std::vector<uint32_t> use, miss_d, miss_p, all_d(k);
+    for (uint32_t j = 0; j < n; ++j) {
+      if (pat[j] == '1' && use.size() < k) use.push_back(j);
+      if (pat[j] == '0') (j < k ? miss_d : miss_p).push_back(j);
+    }
+    for (uint32_t j = 0; j < k; ++j) all_d[j] = j;
+    uint32_t* d_jobs;
+    HB_TRY(stage_upload(c, "rs.jobs", kv.second.data(), 4 * kv.second.size(), c->stream,
+                        reinterpret_cast<void**>(&d_jobs)));
+    const uint64_t stride = (uint64_t)n * len;
+    const uint32_t nj = (uint32_t)kv.second.size();
+    if (!miss_d.empty()) {
+      const std::string key = "dec/" + std::to_string(k) + "/" + pat;
+      const hbtc_ctx::GfPlan* pl;
+      if (!c->gf_plans.count(key)) {
+        GfMat sub, inv;
+        for (uint32_t j : use) sub.push_back(m[j]);
+        if (!gf_invert(sub, inv)) return fail(c, HBTC_ERR_DEVICE, "singular decode matrix");
+        GfMat rows;
+        for (uint32_t j : miss_d) rows.push_back(inv[j]);
+        HB_TRY(gf_plan(c, key, miss_d, use, rows, &pl));
+      } else {
+        pl = &c->gf_plans[key];
+      }
+      HB_TRY(timed(c, "rs", [&] {
+        return launch_gf_apply(c->stream, nj, d_jobs, d, stride, len, pl->n_out, pl->out_rows,
+                               pl->n_in, pl->in_rows, pl->tabs);
+      }));
+    }
+    if (!miss_p.empty()) {
+      std::string mp(p, '0');
+      for (uint32_t j : miss_p) mp[j - k] = '1';
+      const std::string key = "par/" + std::to_string(k) + "/" + mp;
+      const hbtc_ctx::GfPlan* pl;
+      if (!c->gf_plans.count(key)) {
+        GfMat rows;
+        for (uint32_t j : miss_p) rows.push_back(m[j]);
+        HB_TRY(gf_plan(c, key, miss_p, all_d, rows, &pl));
+      } else {
+        pl = &c->gf_plans[key];
+      }
+      HB_TRY(timed(c, "rs", [&] {
+        return launch_gf_apply(c->stream, nj, d_jobs, d, stride, len, pl->n_out, pl->out_rows,
+                               pl->n_in, pl->in_rows, pl->tabs);
+      }));
+    }
+  }
+  return end_verify(c);
+}
+
+uint32_t merkle_digests(uint32_t n) {
+  uint32_t t = n;
+  while (n > 1) {
+    n = (n + 1) / 2;
+    t += n;
+  }
+  return t;
+}
+
+int merkle_trees_dev(hbtc_ctx* c, uint32_t n, uint32_t len, uint32_t n_inst, const uint8_t* d_leaves,
+                     uint8_t* d_out) {
+  if (n_inst == 0 || n == 0) return HBTC_OK;
+  if (reinterpret_cast<uintptr_t>(d_out) & 7u) return fail(c, HBTC_ERR_ARG, "digests must be 8-byte aligned");
+  const uint32_t nd = merkle_digests(n);
+  HB_TRY(begin_verify(c, {rng(d_leaves, (size_t)n_inst * n * len)}, {rng(d_out, (size_t)n_inst * nd * 32)}));
+  HB_TRY(timed(c, "merkle", [&] {
+    return launch_merkle_tree(c->stream, n_inst, n, len, d_leaves, (uint64_t)n * len, nd, d_out);
+  }));
+  return end_verify(c);
+}
+
+int merkle_validate_dev(hbtc_ctx* c, uint32_t n, uint32_t n_nodes, const uint64_t* d_voff,
+                        const uint8_t* d_values, const uint32_t* d_idx, const uint32_t* d_doff,
+                        const uint8_t* d_dig, const uint8_t* d_roots, int32_t* d_status) {
+  if (n == 0) return HBTC_OK;
+  if ((reinterpret_cast<uintptr_t>(d_dig) & 7u) || (reinterpret_cast<uintptr_t>(d_roots) & 7u))
+    return fail(c, HBTC_ERR_ARG, "digests / roots must be 8-byte aligned");
+  HB_TRY(begin_verify(c, {rng(d_voff, 8 * ((size_t)n + 1)), rng(d_idx, 4 * (size_t)n),
+                          rng(d_doff, 4 * ((size_t)n + 1)), rng(d_roots, 32 * (size_t)n)},
+                      {rng(d_status, 4 * (size_t)n)}));
+  HB_TRY(timed(c, "merkle_validate", [&] {
+    return launch_merkle_validate(c->stream, n, n_nodes, d_voff, d_values, d_idx, d_doff, d_dig, d_roots,
+                                  d_status);
+  }));
+  return end_verify(c);
+}
+}  // namespace
+
+extern "C" {
+
+uint32_t hbtc_merkle_digest_count(uint32_t n_leaves) { return n_leaves ? merkle_digests(n_leaves) : 0; }
+
+int hbtc_rs_encode_dev(hbtc_ctx* c, uint32_t k, uint32_t p, uint32_t shard_len, uint32_t n_inst,
+                       uint8_t* d_shards) {
+  if (!c || (n_inst && !d_shards)) return HBTC_ERR_ARG;
+  Guard g(c);
+  return rs_encode_dev(c, k, p, shard_len, n_inst, d_shards);
+}
+
+int hbtc_rs_reconstruct_dev(hbtc_ctx* c, uint32_t k, uint32_t p, uint32_t shard_len, uint32_t n_inst,
+                            uint8_t* d_shards, const uint8_t* present, int32_t* status) {
+  if (!c || (n_inst && !d_shards)) return HBTC_ERR_ARG;
+  Guard g(c);
+  return rs_reconstruct_dev(c, k, p, shard_len, n_inst, d_shards, present, status);
+}
+
+int hbtc_merkle_trees_dev(hbtc_ctx* c, uint32_t n_leaves, uint32_t leaf_len, uint32_t n_inst,
+                          const uint8_t* d_leaves, uint8_t* d_digests) {
+  if (!c || (n_inst && n_leaves && (!d_leaves || !d_digests))) return HBTC_ERR_ARG;
+  Guard g(c);
+  return merkle_trees_dev(c, n_leaves, leaf_len, n_inst, d_leaves, d_digests);
+}
+
+int hbtc_merkle_validate_dev(hbtc_ctx* c, uint32_t n, uint32_t n_nodes, const uint64_t* d_value_off,
+                             const uint8_t* d_values, const uint32_t* d_index,
+                             const uint32_t* d_digest_off, const uint8_t* d_digests,
+                             const uint8_t* d_roots, int32_t* d_status) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  return merkle_validate_dev(c, n, n_nodes, d_value_off, d_values, d_index, d_digest_off, d_digests,
+                             d_roots, d_status);
+}
+
+// host-buffer forms: upload, the device core, download, wait
+int hbtc_rs_encode(hbtc_ctx* c, uint32_t k, uint32_t p, uint32_t shard_len, uint32_t n_inst,
+                   uint8_t* shards) {
+  if (!c || (n_inst && !shards)) return HBTC_ERR_ARG;
+  Guard g(c);
+  HB_TRY(rs_check(c, k, p, shard_len));
+  const size_t bytes = (size_t)n_inst * (k + p) * shard_len;
+  if (!bytes) return HBTC_OK;
+  HB_TRY(sync(c));
+  PinLane pin(c);  // the uploads below and the core run on one lane
+  void* d;
+  HB_TRY(upload(c, "rs.host", shards, bytes, &d));
+  HB_TRY(rs_encode_dev(c, k, p, shard_len, n_inst, (uint8_t*)d));
+  HB_TRY(download(c, shards, d, bytes));
+  return sync(c);
+}
+
+int hbtc_rs_reconstruct(hbtc_ctx* c, uint32_t k, uint32_t p, uint32_t shard_len, uint32_t n_inst,
+                        uint8_t* shards, const uint8_t* present, int32_t* status) {
+  if (!c || (n_inst && (!shards || !present || !status))) return HBTC_ERR_ARG;
+  Guard g(c);
+  HB_TRY(rs_check(c, k, p, shard_len));
+  const size_t bytes = (size_t)n_inst * (k + p) * shard_len;
+  if (!bytes) return HBTC_OK;
+  HB_TRY(sync(c));
+  PinLane pin(c);  // the uploads below and the core run on one lane
+  void* d;
+  HB_TRY(upload(c, "rs.host", shards, bytes, &d));
+  HB_TRY(rs_reconstruct_dev(c, k, p, shard_len, n_inst, (uint8_t*)d, present, status));
+  HB_TRY(download(c, shards, d, bytes));
+  return sync(c);
+}
+
+int hbtc_merkle_trees(hbtc_ctx* c, uint32_t n_leaves, uint32_t leaf_len, uint32_t n_inst,
+                      const uint8_t* leaves, uint8_t* digests) {
+  if (!c || (n_inst && n_leaves && (!leaves || !digests))) return HBTC_ERR_ARG;
+  Guard g(c);
+  if (!n_inst || !n_leaves) return HBTC_OK;
+  HB_TRY(sync(c));
+  PinLane pin(c);  // the uploads below and the core run on one lane
+  void *dl, *dd;
+  const size_t out_bytes = (size_t)n_inst * merkle_digests(n_leaves) * 32;
+  HB_TRY(upload(c, "mk.leaves", leaves, (size_t)n_inst * n_leaves * leaf_len, &dl));
+  HB_TRY(ws(c, "mk.out", out_bytes, &dd));
+  HB_TRY(merkle_trees_dev(c, n_leaves, leaf_len, n_inst, (const uint8_t*)dl, (uint8_t*)dd));
+  HB_TRY(download(c, digests, dd, out_bytes));
+  return sync(c);
+}
+
+int hbtc_merkle_validate(hbtc_ctx* c, uint32_t n, uint32_t n_nodes, const uint64_t* value_off,
+                         const uint8_t* values, const uint32_t* index, const uint32_t* digest_off,
+                         const uint8_t* digests, const uint8_t* roots, int32_t* status) {
+  if (!c || (n && (!value_off || !index || !digest_off || !roots || !status))) return HBTC_ERR_ARG;
+  Guard g(c);
+  if (!n) return HBTC_OK;
+  HB_TRY(sync(c));
+  PinLane pin(c);  // the uploads below and the core run on one lane
+  void *dv, *dvo, *di, *ddo, *dd, *dr, *ds;
+  HB_TRY(upload(c, "mv.values", values, value_off[n], &dv));
+  HB_TRY(upload(c, "mv.voff", value_off, 8 * ((size_t)n + 1), &dvo));
+  HB_TRY(upload(c, "mv.idx", index, 4 * (size_t)n, &di));
+  HB_TRY(upload(c, "mv.doff", digest_off, 4 * ((size_t)n + 1), &ddo));
+  HB_TRY(upload(c, "mv.dig", digests, 32 * (size_t)digest_off[n], &dd));
+  HB_TRY(upload(c, "mv.roots", roots, 32 * (size_t)n, &dr));
+  HB_TRY(ws(c, "mv.status", 4 * (size_t)n, &ds));
+  HB_TRY(merkle_validate_dev(c, n, n_nodes, (const uint64_t*)dvo, (const uint8_t*)dv, (const uint32_t*)di,
+                             (const uint32_t*)ddo, (const uint8_t*)dd, (const uint8_t*)dr, (int32_t*)ds));
+  HB_TRY(download(c, status, ds, 4 * (size_t)n));
+  return sync(c);
 }
 
 }  // extern "C"

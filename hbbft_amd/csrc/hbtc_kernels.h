@@ -203,4 +203,15 @@ hipError_t launch_skg_ack_rows(hipStream_t s, uint32_t n_acks, uint32_t t1, cons
                                const uint32_t* ack_part, const uint32_t* ack_sender,
                                const Fr* vals, int32_t* status);
 
+
+// ---- Reliable Broadcast (hbtc_bcast.hip)
+hipError_t launch_gf_apply(hipStream_t s, uint32_t n_jobs, const uint32_t* jobs, uint8_t* shards,
+                           uint64_t stride, uint32_t len, uint32_t n_out, const uint32_t* out_rows,
+                           uint32_t n_in, const uint32_t* in_rows, const uint32_t* tabs);
+hipError_t launch_merkle_tree(hipStream_t s, uint32_t n_inst, uint32_t n, uint32_t leaf_len,
+                              const uint8_t* leaves, uint64_t stride, uint32_t n_dig, uint8_t* out);
+hipError_t launch_merkle_validate(hipStream_t s, uint32_t n, uint32_t n_nodes, const uint64_t* voff,
+                                  const uint8_t* values, const uint32_t* idx, const uint32_t* doff,
+                                  const uint8_t* digests, const uint8_t* roots, int32_t* status);
+
 }  // namespace hbtc

@@ -116,15 +116,6 @@ __device__ void rlc_reduce(Jac<F>* redA, Jac<F>* redB, const Jac<F>& q, uint32_t
 __device__ __forceinline__ void rlc_reduce_sp(G1J* redA, G1J* redB, const G1J& S, const G1J& P,
                                               uint32_t lane, G1J* outS, G1J* outSW, G1J* outP,
                                               G1J* outPW) {
-#ifdef HBTC_EXP_NO_TREE  // timing experiment only: the sums are wrong
-  if (lane < 9) {
-    outS[lane] = S;
-    outSW[lane] = S;
-    outP[lane] = P;
-    outPW[lane] = P;
-  }
-  return;
-#endif
   const bool odd = (lane & 1u) != 0;
   G1J x = odd ? S : P, y;  // the value the neighbour lane needs
   {

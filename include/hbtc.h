@@ -348,10 +348,57 @@ int hbtc_set_check_schedule(hbtc_ctx* ctx, int schedule);
 /* Number of shares that needed the exact single-share check in the last RLC call (syncs). */
 int hbtc_rlc_last_leaves(hbtc_ctx* ctx, uint32_t* leaves);
 
+/* ---- Reliable Broadcast coding (hbbft src/broadcast/) ------------------------------------- */
+/* Reed-Solomon erasure code of reed-solomon-erasure 3.1 over GF(2^8) (0x11D), as hbbft's
+ * Coding wraps it (broadcast.rs:395-459): k data + p parity shards, k + p <= 256 (ReedSolomon::new
+ * refuses more: HBTC_ERR_ARG), every shard shard_len bytes.  Shards of one instance are
+ * contiguous ((k + p) * shard_len bytes, shard i at i * shard_len: hbbft's padded value buffer,
+ * broadcast.rs:171-178), instances back to back.
+ * hbtc_rs_encode: ReedSolomon::encode — the p parity shards of every instance (in place).
+ * hbtc_rs_reconstruct: ReedSolomon::reconstruct_shards — present[i * (k + p) + j] != 0 marks
+ *   shard j of instance i present; the missing ones are computed from the first k present
+ *   (in index order) and written in place; status[i] = HBTC_ACCEPT, or HBTC_NOT_ENOUGH_SHARES
+ *   (TooFewShardsPresent: fewer than k present; the instance's bytes are left unchanged). */
+int hbtc_rs_encode(hbtc_ctx* ctx, uint32_t data_shards, uint32_t parity_shards, uint32_t shard_len,
+                   uint32_t n_inst, uint8_t* shards);
+int hbtc_rs_reconstruct(hbtc_ctx* ctx, uint32_t data_shards, uint32_t parity_shards,
+                        uint32_t shard_len, uint32_t n_inst, uint8_t* shards, const uint8_t* present,
+                        int32_t* status);
+/* Merkle trees of merkle.rs (MerkleTree::from_vec, merkle.rs:19-32): SHA3-256 leaves, pair
+ * digests, an odd last digest carried up.  Per instance hbtc_merkle_digest_count(n_leaves)
+ * digests of 32 bytes: level 0 (the n_leaves leaf digests), level 1, ..., the root last (the
+ * levels MerkleTree::proof reads).  leaves: n_inst * n_leaves * leaf_len bytes. */
+uint32_t hbtc_merkle_digest_count(uint32_t n_leaves);
+int hbtc_merkle_trees(hbtc_ctx* ctx, uint32_t n_leaves, uint32_t leaf_len, uint32_t n_inst,
+                      const uint8_t* leaves, uint8_t* digests);
+/* Proof::validate(n_nodes) (merkle.rs:82-102) of n proofs: proof i has the value bytes
+ * values[value_off[i] .. value_off[i + 1]), index[i], the digests
+ * digests[32 * digest_off[i] .. 32 * digest_off[i + 1]) and root roots[32 * i ..].  status[i] =
+ * HBTC_ACCEPT (valid) or HBTC_REJECT.  (The caller's index == sender check,
+ * broadcast.rs:366, stays with the caller.) */
+int hbtc_merkle_validate(hbtc_ctx* ctx, uint32_t n, uint32_t n_nodes, const uint64_t* value_off,
+                         const uint8_t* values, const uint32_t* index, const uint32_t* digest_off,
+                         const uint8_t* digests, const uint8_t* roots, int32_t* status);
+/* Device-pointer forms (ordered on the context's streams like the other *_dev calls; present,
+ * status of hbtc_rs_reconstruct_dev and the offsets' last entries stay host-side where noted:
+ * present / status are HOST arrays, everything else device memory, digests 8-byte aligned). */
+int hbtc_rs_encode_dev(hbtc_ctx* ctx, uint32_t data_shards, uint32_t parity_shards,
+                       uint32_t shard_len, uint32_t n_inst, uint8_t* d_shards);
+int hbtc_rs_reconstruct_dev(hbtc_ctx* ctx, uint32_t data_shards, uint32_t parity_shards,
+                            uint32_t shard_len, uint32_t n_inst, uint8_t* d_shards,
+                            const uint8_t* present, int32_t* status);
+int hbtc_merkle_trees_dev(hbtc_ctx* ctx, uint32_t n_leaves, uint32_t leaf_len, uint32_t n_inst,
+                          const uint8_t* d_leaves, uint8_t* d_digests);
+int hbtc_merkle_validate_dev(hbtc_ctx* ctx, uint32_t n, uint32_t n_nodes, const uint64_t* d_value_off,
+                             const uint8_t* d_values, const uint32_t* d_index,
+                             const uint32_t* d_digest_off, const uint8_t* d_digests,
+                             const uint8_t* d_roots, int32_t* d_status);
+
 /* ---- kernel timing (HIP events on the context's stream) ---------------------------------- */
 /* Families: "prepare", "dec_verify", "sig_verify", "pair_verify", "lagrange" (selection +
  * Lagrange coefficients), "comb_decode", "comb_digits", "combine" (MSM bucket reduction), "skg_scalars", "skg_ack_rows",
- * "mul", "rlc_items", "chk_tiles", "chk_subs", "chk_leaves", "rlc_finalize".  Reading
+ * "mul", "rlc_items", "chk_tiles", "chk_subs", "chk_leaves", "rlc_finalize", "rs", "merkle",
+ * "merkle_validate".  Reading
  * synchronises the stream. */
 int hbtc_timing_enable(hbtc_ctx* ctx, int enable);
 int hbtc_timing_read(hbtc_ctx* ctx, const char* family, double* total_ms, uint64_t* launches);
