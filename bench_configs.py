@@ -21,7 +21,16 @@ checked against the construction after timing:
       Ack ciphertexts repeat per distinct (polynomial, sender) value (every Ack is still
       hashed, verified, multiplied and padded on its own).
 
-Usage: python bench_configs.py [--configs c2,c4,c5] [--steps K] [--warmup W]
+  bc  Reliable Broadcast of one HoneyBadger epoch at N = 256 (the largest network hbbft's
+      reed-solomon-erasure coding accepts: k + p <= 256), one node's view: the N^2 = 65,536 Echo
+      proofs it receives validated (Proof::validate, src/broadcast/merkle.rs:82-102, via
+      validate_proof, broadcast.rs:255), then the N values decoded (decode_from_shards,
+      broadcast.rs:461-493: reconstruct_shards of the f silent nodes' shards, the Merkle tree
+      of every instance, the root comparison).  Each proposer's value is --bc-value bytes
+      (shard_len = ceil((value + 4) / (N - 2f))).  Inputs resident in HBM; the outputs are
+      compared with the proposals after timing.
+
+Usage: python bench_configs.py [--configs c2,c4,c5,bc] [--steps K] [--warmup W]
 """
 import argparse
 import ctypes
@@ -305,6 +314,117 @@ def bench_skg(ctx, n, n_parts, n_distinct, steps, warmup):
     }
 
 
+def bench_broadcast(ctx, n, value_bytes, steps, warmup):
+    """bc: one node's Reliable Broadcast work for an epoch of n proposers (see the docstring)."""
+    from hbbft_amd import broadcast as G
+    lib, h = ctx.lib, ctx.h
+    rng = np.random.default_rng(SEED + n)
+    f = (n - 1) // 3
+    k, p = G.shard_counts(n, f)
+    t0 = time.time()
+    values = [rng.integers(0, 256, value_bytes, dtype=np.uint8).tobytes() for _ in range(n)]
+    shards = G.encode_batch(ctx, values, n, f)               # [n_inst, n, L] (setup)
+    L = shards.shape[2]
+    nd = lib.hbtc_merkle_digest_count(n)
+    dig = ctx.merkle_trees(n, L, shards.reshape(-1))        # [n_inst, nd, 32]
+    roots = dig[:, -1, :].copy()
+    # the Echo proofs this node receives: node j's proof of instance kk, for every (kk, j)
+    lvl_off, m, off = [], n, 0
+    while m > 1:
+        lvl_off.append((off, m))
+        off += m
+        m = (m + 1) // 2
+    per = []
+    for j in range(n):
+        pos, i = [], j
+        for o, size in lvl_off:
+            if (i ^ 1) < size:
+                pos.append(o + (i ^ 1))
+            i //= 2
+        per.append(pos)
+    depth = np.array([len(x) for x in per], np.uint32)
+    n_pr = n * n
+    doff = np.zeros(n_pr + 1, np.uint32)
+    doff[1:] = np.cumsum(np.tile(depth, n))
+    digs = np.concatenate([dig[kk][per[j]] for kk in range(n) for j in range(n)]).reshape(-1)
+    voff = (np.arange(n_pr + 1, dtype=np.uint64) * L).astype(np.uint64)
+    idx = np.tile(np.arange(n, dtype=np.uint32), n)
+    proot = np.repeat(roots, n, axis=0).reshape(-1)
+    # this node's view for decoding: the f silent nodes' shards are missing in every instance
+    silent = rng.choice(n, f, replace=False)
+    present = np.ones((n, n), np.uint8)
+    present[:, silent] = 0
+    recv = shards.copy()
+    recv[:, silent, :] = 0
+    d = {}
+    for name, arr in (("values", shards.reshape(-1)), ("voff", voff), ("idx", idx), ("doff", doff),
+                      ("digs", digs), ("roots", proot), ("recv", recv.reshape(-1))):
+        d[name] = ctx.dev_alloc(arr.nbytes)
+        ctx.dev_upload(d[name], arr)
+    d["status"] = ctx.dev_alloc(4 * n_pr)
+    d["out"] = ctx.dev_alloc(n * nd * 32)
+    rstatus = np.empty(n, np.int32)
+    log("bc: setup %.1fs (%d proofs, %d instances, shard_len %d)" % (time.time() - t0, n_pr, n, L))
+
+    def step():
+        ctx._check(lib.hbtc_merkle_validate_dev(h, n_pr, n, d["voff"], d["values"], d["idx"], d["doff"],
+                                                d["digs"], d["roots"], d["status"]), "validate")
+        ctx._check(lib.hbtc_rs_reconstruct_dev(h, k, p, L, n, d["recv"], N._ptr(present.reshape(-1)),
+                                               N._ptr(rstatus)), "reconstruct")
+        ctx._check(lib.hbtc_merkle_trees_dev(h, n, L, n, d["recv"], d["out"]), "trees")
+
+    dt = timed_steps(ctx, step, steps, warmup)
+    per_step = breakdown(ctx, steps, ["merkle_validate", "rs", "merkle"])
+    st = np.empty(n_pr, np.int32)
+    ctx.dev_download(st, d["status"])
+    out = np.empty(n * nd * 32, np.uint8)
+    ctx.dev_download(out, d["out"])
+    rec = np.empty(recv.size, np.uint8)
+    ctx.dev_download(rec, d["recv"])
+    ctx.sync()
+    ok = bool((st == N.ACCEPT).all()) and bool((rstatus == N.ACCEPT).all())
+    ok = ok and bool((out.reshape(n, nd, 32)[:, -1, :] == roots).all())
+    rec = rec.reshape(n, n, L)
+    ok = ok and all(G.glue_shards([bytes(rec[kk, j]) for j in range(k)], k) == values[kk] for kk in range(n))
+    for v in d.values():
+        ctx.dev_free(v)
+    # CPU baseline: the restatement (oracle/broadcast.py: hashlib SHA3, numpy GF(2^8)) on one
+    # core over a bounded sample of the same work: 2048 proofs and 2 decodes
+    from oracle import broadcast as B
+    t1 = time.perf_counter()
+    n_cpu = 2048
+    for q in range(n_cpu):
+        kk, j = divmod(q, n)
+        dg = [bytes(dig[kk][x]) for x in per[j]]
+        assert B.proof_validate((bytes(shards[kk, j]), j, dg, bytes(roots[kk])), n)
+    t_val = (time.perf_counter() - t1) / n_cpu
+    t1 = time.perf_counter()
+    for kk in range(2):
+        lv = [None if j in set(silent.tolist()) else bytes(shards[kk, j]) for j in range(n)]
+        assert B.decode_from_shards(lv, f, bytes(roots[kk])) == values[kk]
+    t_dec = (time.perf_counter() - t1) / 2
+    cpu_step = t_val * n_pr + t_dec * n
+    ms = dt / steps * 1e3
+    return {
+        "metric": "Reliable Broadcast Echo proofs validated/sec (one node, N=256); values decoded/sec",
+        "value": round(n_pr / (dt / steps), 1), "unit": "proofs/s", "n_gpus": 1, "steps": steps,
+        "warmup": warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "dtype": "u8 / u64 (GF(2^8), Keccak-f[1600])",
+        "data": "synthetic (seeded random proposals, f silent nodes)",
+        "config": {"workload": "bc: %d Echo proofs validated + %d values decoded (reconstruct %d missing "
+                               "shards of %d, Merkle tree, root check)" % (n_pr, n, f, n),
+                   "N": n, "f": f, "data_shards": k, "parity_shards": p, "value_bytes": value_bytes,
+                   "shard_len": L},
+        "values_decoded_per_s": round(n / (dt / steps), 1),
+        "input_bytes_per_step": int(n_pr * L + digs.size + n * (n - f) * L),
+        "kernel_ms_per_step": per_step, "results_ok": ok,
+        "cpu_baseline": {"value": round(n_pr / cpu_step, 1), "unit": "proofs/s (with the epoch's decodes)",
+                         "cores": 1, "kind": "port",
+                         "sample": "2048 Proof::validate + 2 decode_from_shards (first call builds the "
+                                   "decode matrix) by oracle/broadcast.py, scaled to the epoch: "
+                                   "%.1f us/proof, %.1f ms/decode" % (t_val * 1e6, t_dec * 1e3)},
+    }
+
+
 ctx_mode = [None]
 
 
@@ -316,6 +436,7 @@ def main():
     ap.add_argument("--inst", type=int, default=64, help="c4 coin instances on this GPU")
     ap.add_argument("--parts", type=int, default=1000, help="c5 Parts")
     ap.add_argument("--distinct", type=int, default=4, help="c5 distinct bivariate polynomials")
+    ap.add_argument("--bc-value", type=int, default=65536, help="bc: bytes per proposed value")
     ap.add_argument("--mode", choices=["rlc", "per_share"], default="rlc")
     ap.add_argument("--corrupt", type=float, default=0.01)
     ap.add_argument("--corrupt-mode", choices=["uniform", "senders"], default="uniform")
@@ -331,6 +452,8 @@ def main():
             elif c == "c4":
                 out = bench_coins(ctx, "c4", 10000, args.inst, args.steps, args.warmup, args.corrupt,
                                   args.corrupt_mode)
+            elif c == "bc":
+                out = bench_broadcast(ctx, 256, args.bc_value, args.steps, args.warmup)
             elif c == "c5":
                 out = bench_skg(ctx, 1000, args.parts, args.distinct, args.steps, args.warmup)
             else:
