@@ -99,17 +99,21 @@ __global__ void __launch_bounds__(64) k_g2_steps(const uint8_t* __restrict__ in0
   uint32_t w[24];
   load_words(w, g < n0 ? in0 : in1, g < n0 ? g : g - n0, 24);
   G2A q;
-  const bool ok = g2_decompress(q, w);
+  // the subgroup test (psi(Q) == -[|x|] Q, curve.h g2_in_subgroup) reuses the Miller loop's own
+  // double-and-add: after the 68 steps T = [|x|] Q
+  bool ok = g2_decompress(q, w, false);
   aff[g] = q;
-  status[g] = ok ? HBTC_ACCEPT : HBTC_DECODE_ERR;
-  if (!ok || q.inf) return;
+  if (!ok || q.inf) {
+    status[g] = ok ? HBTC_ACCEPT : HBTC_DECODE_ERR;
+    return;
+  }
   Fq2* out = ws + (size_t)g * 3 * MILLER_STEPS;
   G2J T;
   jac_from_aff(T, q);
   int j = 0;
   for (int bit = 62; bit >= 0; --bit) {
     Fq2 A, B, C;
-    g2_dbl_step(T, A, B, C);
+    g2_dbl_line(T, A, B, C);
     out[3 * j] = A;
     out[3 * j + 1] = B;
     out[3 * j + 2] = C;
@@ -122,6 +126,11 @@ __global__ void __launch_bounds__(64) k_g2_steps(const uint8_t* __restrict__ in0
       ++j;
     }
   }
+  Fq2 px, py, npy;
+  g2_psi(px, py, q);
+  fq2_neg(npy, py);
+  ok = !jac_is_inf(T) && jac_eq_aff(T, px, npy);
+  status[g] = ok ? HBTC_ACCEPT : HBTC_DECODE_ERR;
 }
 
 // One lane per (argument, step): the affine-normalised line (A / C, B / C) (pairing.h Line).
@@ -135,8 +144,18 @@ __global__ void __launch_bounds__(64) k_g2_norm(uint32_t n, const G2A* __restric
   const uint32_t a = g / MILLER_STEPS;
   if (status[a] != HBTC_ACCEPT || aff[a].inf) return;  // never read: the pair is unused
   const Fq2* in = ws + (size_t)g * 3;
+  // 1 / C = conj(C) / (c0^2 + c1^2), the Fq inversion by binary extended Euclid (field.h)
   Fq2 ci;
-  fq2_inv(ci, in[2]);
+  {
+    Fq n0, n1, ni;
+    fq_sqr(n0, in[2].c0);
+    fq_sqr(n1, in[2].c1);
+    fq_add(n0, n0, n1);
+    fq_inv_binary(ni, n0);
+    fq_mul(ci.c0, in[2].c0, ni);
+    fq_mul(n1, in[2].c1, ni);
+    fq_neg(ci.c1, n1);
+  }
   Line l;
   fq2_mul(l.a, in[0], ci);
   fq2_mul(l.b, in[1], ci);

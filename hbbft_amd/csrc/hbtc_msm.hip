@@ -94,6 +94,7 @@ __global__ void __launch_bounds__(64) k_select(const uint32_t* __restrict__ offs
                                                uint32_t* __restrict__ sel_pos,
                                                uint32_t* __restrict__ sel_idx,
                                                uint32_t* __restrict__ sel_cnt) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
   const uint32_t k = blockIdx.x, lane = threadIdx.x;
   const uint32_t a = offsets[k], b = offsets[k + 1];
   const size_t o = (size_t)k * t;
@@ -127,6 +128,7 @@ __global__ void __launch_bounds__(64) k_select(const uint32_t* __restrict__ offs
 // Fermat inversion per coefficient).
 __global__ void __launch_bounds__(256) k_lagrange_x(uint64_t n, const uint32_t* __restrict__ sel_idx,
                                                     Fr* __restrict__ x) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
   const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (g >= n) return;
   Fr v;
@@ -138,6 +140,7 @@ __global__ void __launch_bounds__(256) k_lagrange_den(uint32_t n_inst, uint32_t 
                                                       const Fr* __restrict__ x,
                                                       Fr* __restrict__ q,
                                                       uint32_t* __restrict__ dup) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
   const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (g >= (uint64_t)n_inst * t) return;
   const uint32_t k = (uint32_t)(g / t), i = (uint32_t)(g % t);
@@ -163,6 +166,7 @@ __global__ void __launch_bounds__(256) k_lagrange_den(uint32_t n_inst, uint32_t 
 constexpr uint32_t LG_BS = 256;
 __global__ void __launch_bounds__(LG_BS) k_lagrange_inv(uint32_t t, Fr* __restrict__ x,
                                                         Fr* __restrict__ q_lambda) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
   __shared__ Fr C[LG_BS];   // product of q over chunk u
   __shared__ Fr E[LG_BS];   // product of q over the chunks before u
   __shared__ Fr IE[LG_BS];  // (E[u] * C[u])^-1
@@ -220,6 +224,7 @@ __global__ void __launch_bounds__(LG_BS) k_lagrange_inv(uint32_t t, Fr* __restri
 __global__ void __launch_bounds__(256) k_msm_recode(uint64_t n_terms, uint32_t n, uint32_t c,
                                                     uint32_t W, const uint32_t* __restrict__ sc,
                                                     int16_t* __restrict__ digits) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
   const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (g >= n_terms) return;
   const uint64_t m = g / n, i = g % n;
@@ -257,6 +262,7 @@ __global__ void __launch_bounds__(MSM_SORT_BS) k_msm_sort(uint32_t n, uint32_t c
                                                           const int16_t* __restrict__ digits,
                                                           uint32_t* __restrict__ list,
                                                           uint32_t* __restrict__ roff) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
   extern __shared__ uint32_t cnt[];  // B counters, then MSM_SORT_BS chunk sums
   uint32_t* part = cnt + (1u << (c - 1));
   const uint32_t B = 1u << (c - 1), tid = threadIdx.x;
@@ -331,6 +337,7 @@ __global__ void __launch_bounds__(64) k_msm_decode(uint32_t n_inst, uint32_t t, 
                                                    const Aff<F>* __restrict__ dec,
                                                    Aff<F>* __restrict__ out,
                                                    uint32_t* __restrict__ bad) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
   const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
   if (g >= (uint64_t)n_inst * t) return;
   const uint32_t k = (uint32_t)(g / t), i = (uint32_t)(g % t);
@@ -368,6 +375,7 @@ __global__ void __launch_bounds__(256) k_msm_gather(uint32_t n_inst, uint32_t t,
                                                     const uint32_t* __restrict__ sel_cnt,
                                                     const A* __restrict__ dec,
                                                     A* __restrict__ out) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
   const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (g >= (uint64_t)n_inst * t) return;
   const uint32_t k = (uint32_t)(g / t), i = (uint32_t)(g % t);
@@ -412,6 +420,7 @@ __global__ void __launch_bounds__(64) k_msm_buckets(uint64_t n_lanes, uint32_t n
                                                     const uint32_t* __restrict__ roff,
                                                     const uint32_t* __restrict__ pts_map,
                                                     Jac<F>* __restrict__ part) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
   const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
   if (g >= n_lanes) return;
   const uint32_t B = 1u << (c - 1), S = B / 8;
@@ -455,6 +464,7 @@ template <class F>
 __global__ void __launch_bounds__(64) k_msm_wsum(uint64_t n_mw, uint32_t S,
                                                  const Jac<F>* __restrict__ part,
                                                  Jac<F>* __restrict__ wsum) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
   const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
   if (g >= n_mw) return;
   const Jac<F>* p = part + g * S;
@@ -475,6 +485,7 @@ __global__ void __launch_bounds__(64) k_msm_final(uint32_t n_msm, uint32_t c, ui
                                                   int32_t* __restrict__ status,
                                                   uint8_t* __restrict__ out,
                                                   uint8_t* __restrict__ parity) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
   const uint32_t m = blockIdx.x * 64 + threadIdx.x;
   if (m >= n_msm) return;
   const Jac<F>* ws = wsum + (size_t)m * W;

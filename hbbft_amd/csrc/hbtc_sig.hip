@@ -119,6 +119,7 @@ __global__ void __launch_bounds__(64) k_plines(int mode, uint32_t max_groups, ui
                                                const G2A* __restrict__ dec,
                                                Fq2* __restrict__ tables,
                                                uint32_t* __restrict__ inf) {
+  HBTC_LATENCY_PRIO();
   const uint32_t g = blockIdx.x * 64 + threadIdx.x;
   // mode 2: leaves [base, base + max_groups) of the list (chunks keep the tables bounded)
   const uint32_t c = mode == 0 ? 0u : *count;

@@ -60,6 +60,48 @@ HD void g2_dbl_step(G2J& T, Fq2& A, Fq2& B, Fq2& C) {
   jac_dbl(T, T);
 }
 
+// The doubling step with the line fused into the point doubling (the same line as g2_dbl_step up
+// to nothing: A = 3X^3 - 2Y^2 = X E - 2 YY, B = -E Z^2, C = Z3 Z^2 with E = 3 X^2, Z3 = 2 Y Z):
+// 6 squarings + 5 multiplications in Fq2 instead of 8 + 6.
+HD void g2_dbl_line(G2J& T, Fq2& A, Fq2& B, Fq2& C) {
+  Fq2 XX, YY, YYYY, ZZ, D, E, F, t;
+  fq2_sqr(XX, T.x);
+  fq2_sqr(YY, T.y);
+  fq2_sqr(YYYY, YY);
+  fq2_sqr(ZZ, T.z);
+  fq2_add(t, T.x, YY);
+  fq2_sqr(t, t);
+  fq2_sub(t, t, XX);
+  fq2_sub(t, t, YYYY);
+  fq2_dbl(D, t);
+  fq2_dbl(E, XX);
+  fq2_add(E, E, XX);
+  // line
+  fq2_mul(A, T.x, E);
+  fq2_dbl(t, YY);
+  fq2_sub(A, A, t);
+  fq2_mul(B, E, ZZ);
+  fq2_neg(B, B);
+  Fq2 z3;
+  fq2_mul(z3, T.y, T.z);
+  fq2_dbl(z3, z3);
+  fq2_mul(C, z3, ZZ);
+  // point
+  fq2_sqr(F, E);
+  Fq2 x3, y3;
+  fq2_dbl(t, D);
+  fq2_sub(x3, F, t);
+  fq2_sub(t, D, x3);
+  fq2_mul(y3, E, t);
+  fq2_dbl(YYYY, YYYY);
+  fq2_dbl(YYYY, YYYY);
+  fq2_dbl(YYYY, YYYY);
+  fq2_sub(y3, y3, YYYY);
+  T.x = x3;
+  T.y = y3;
+  T.z = z3;
+}
+
 // Addition step T <- T + Q (Q affine):  r = yQ Z^3 - Y, H = xQ Z^2 - X,
 //   A = r xQ - yQ Z H,  B = -r,  C = Z H
 HD void g2_add_step(G2J& T, const G2A& Q, Fq2& A, Fq2& B, Fq2& C) {
