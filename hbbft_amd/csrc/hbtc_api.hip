@@ -689,18 +689,24 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
                          inf);
   }));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
+  // paired checks either way (plain and weighted value of a group per unit); a small call goes
+  // from the tiles straight to the leaves (check_mode)
+  const bool to_leaves = check_mode(c, n_tiles) == CHK_PAIR_LEAVES;
   HB_TRY(timed(c, "chk_tiles", [&] {
     return launch_sigchk_tiles(c->stream, n_tiles, tiles, sums, tables, inf, h_aff, h_lines, h_st,
-                               d_status, sub_count, sub_list);
+                               d_status, to_leaves ? leaf_count : sub_count,
+                               to_leaves ? leaves : sub_list, to_leaves);
   }));
-  HB_TRY(timed(c, "sig_lines", [&] {
-    return launch_plines(c->stream, 1, 16 * n_tiles, 0, sub_count, sub_list, tiles, sums, dec,
-                         tables, inf);
-  }));
-  HB_TRY(timed(c, "chk_subs", [&] {
-    return launch_sigchk_subs(c->stream, n_tiles, sub_count, sub_list, tiles, sums, tables, inf,
-                              h_aff, h_lines, d_status, leaf_count, leaves);
-  }));
+  if (!to_leaves) {
+    HB_TRY(timed(c, "sig_lines", [&] {
+      return launch_plines(c->stream, 1, 16 * n_tiles, 0, sub_count, sub_list, tiles, sums, dec,
+                           tables, inf);
+    }));
+    HB_TRY(timed(c, "chk_subs", [&] {
+      return launch_sigchk_subs(c->stream, n_tiles, sub_count, sub_list, tiles, sums, tables, inf,
+                                h_aff, h_lines, d_status, leaf_count, leaves);
+    }));
+  }
   // leaves in chunks: launches past the device-side count exit at once
   for (uint32_t base = 0; base < n_items; base += LEAF_CHUNK) {
     const uint32_t chunk = std::min(LEAF_CHUNK, n_items - base);

@@ -421,7 +421,7 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_tiles(
     const Fq2* __restrict__ tables, const uint32_t* __restrict__ inf,
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
     const int32_t* __restrict__ h_status, int32_t* __restrict__ status,
-    uint32_t* __restrict__ sub_count, uint32_t* __restrict__ sub_list) {
+    uint32_t* __restrict__ sub_count, uint32_t* __restrict__ sub_list, bool to_leaves) {
   HBTC_LATENCY_PRIO();
   const UnitLane ul = unit_lane();
   const uint32_t t = blockIdx.x * UNITS_PER_WAVE + ul.unit;
@@ -453,7 +453,21 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_tiles(
     status[first + loc] = HBTC_REJECT;
     return;
   }
-  sub_list[atomicAdd(sub_count, 1u)] = t;
+  if (!to_leaves) {
+    sub_list[atomicAdd(sub_count, 1u)] = t;
+    return;
+  }
+  // the paired tiles -> leaves schedule: every pending share of the tile to the exact checks
+  // (sub_count / sub_list are then the leaf counter and list)
+  uint32_t m = 0;
+  for (uint32_t i = first; i < first + count; ++i) m += status[i] == HBTC_RLC_PENDING;
+  uint32_t pos = atomicAdd(sub_count, m);
+  for (uint32_t i = first; i < first + count; ++i)
+    if (status[i] == HBTC_RLC_PENDING) {
+      sub_list[2 * pos] = i;
+      sub_list[2 * pos + 1] = k;
+      ++pos;
+    }
 }
 
 __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_subs(
@@ -626,10 +640,11 @@ hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t*
 hipError_t launch_sigchk_tiles(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
                                const SigTileSums* sums, const Fq2* tables, const uint32_t* inf,
                                const G2A* h_aff, const Line* h_lines, const int32_t* h_status,
-                               int32_t* status, uint32_t* sub_count, uint32_t* sub_list) {
+                               int32_t* status, uint32_t* sub_count, uint32_t* sub_list,
+                               bool to_leaves) {
   if (n_tiles == 0) return hipSuccess;
   hipLaunchKernelGGL(k_sigchk_tiles, dim3(unit_blocks(n_tiles)), dim3(64), 0, s, n_tiles, tiles, sums,
-                     tables, inf, h_aff, h_lines, h_status, status, sub_count, sub_list);
+                     tables, inf, h_aff, h_lines, h_status, status, sub_count, sub_list, to_leaves);
   return hipGetLastError();
 }
 

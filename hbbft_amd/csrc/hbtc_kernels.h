@@ -125,7 +125,8 @@ hipError_t launch_plines(hipStream_t s, int mode, uint32_t max_groups, uint32_t 
 hipError_t launch_sigchk_tiles(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
                                const SigTileSums* sums, const Fq2* tables, const uint32_t* inf,
                                const G2A* h_aff, const Line* h_lines, const int32_t* h_status,
-                               int32_t* status, uint32_t* sub_count, uint32_t* sub_list);
+                               int32_t* status, uint32_t* sub_count, uint32_t* sub_list,
+                               bool to_leaves);
 hipError_t launch_sigchk_subs(hipStream_t s, uint32_t max_tiles, const uint32_t* sub_count,
                               const uint32_t* sub_list, const Tile* tiles,
                               const SigTileSums* sums, const Fq2* tables, const uint32_t* inf,

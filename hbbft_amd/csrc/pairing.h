@@ -127,7 +127,7 @@ HD void g2_proj_lines(Fq2* out, const G2A& Q) {
   jac_from_aff(T, Q);
   int j = 0;
   for (int bit = 62; bit >= 0; --bit) {
-    g2_dbl_step(T, out[3 * j], out[3 * j + 1], out[3 * j + 2]);
+    g2_dbl_line(T, out[3 * j], out[3 * j + 1], out[3 * j + 2]);
     ++j;
     if ((BLS_X_ABS >> bit) & 1ull) {
       g2_add_step(T, Q, out[3 * j], out[3 * j + 1], out[3 * j + 2]);
