@@ -70,8 +70,9 @@ struct Stage {
 
 }  // namespace
 
-// One verification lane: its main and preparation streams, their events, and the device ranges
-// its last verification read and wrote (the hazards a call on the other lane checks).
+// One verification lane: its stream (item pass, checks, then the combine of the same epoch), the
+// shared preparation stream, their events, and the device ranges its last verification read and
+// wrote (the hazards a call on another lane checks).
 struct Lane {
   hipStream_t stream = nullptr, s_prep = nullptr;
   hipEvent_t ev_main = nullptr, ev_prep = nullptr, done = nullptr;
@@ -84,13 +85,18 @@ struct Lane {
 
 struct hbtc_ctx {
   int device = 0;
-  // Verification calls alternate between two lanes, so epoch k+1's item pass fills the SIMDs
-  // that epoch k's small check levels leave idle; `stream` / `s_prep` / `ev_*` / `ws_suffix`
-  // are the lane of the most recent verification (what the combine and the guards order on).
-  Lane lanes[2];
+  // Verification calls rotate over NL lanes (hbbft keeps up to 3 epochs in flight,
+  // src/honey_badger/builder.rs:37), so epoch k+1's item pass fills the SIMDs that epoch k's
+  // check levels and combine leave idle, and a small epoch's chain of check latencies overlaps
+  // two others; `stream` / `s_prep` / `s_comb` / `ev_*` / `ws_suffix` are the lane of the most
+  // recent verification (its combine runs on the same stream, after it).  NL lane streams plus
+  // the preparation stream = 4 streams = GPU_MAX_HW_QUEUES: each has a hardware queue of its own.
+  static constexpr int NL = 3;
+  Lane lanes[NL];
   int lane = 0;
+  int last_items_lane = -1;  // the lane of the most recent item pass (items_gate)
   bool pin_lane = false;  // host entry points: stay on the lane their uploads went to
-  // item passes of the two lanes run one after the other (HBTC_ITEMS_SERIAL, default on): epoch
+  // item passes of the lanes run one after the other (HBTC_ITEMS_SERIAL, default on): epoch
   // k+1's item pass then overlaps epoch k's check levels instead of sharing the chip with epoch
   // k's item pass
   bool items_serial = true;
@@ -99,7 +105,7 @@ struct hbtc_ctx {
   std::string ws_suffix;
   hipStream_t stream = nullptr;  // main: items, checks, leaves
   hipStream_t s_prep = nullptr;  // per-instance G2 preparation, overlapped with the item pass
-  hipStream_t s_comb = nullptr;  // combines (Lagrange), overlapped with verification
+  hipStream_t s_comb = nullptr;  // combines: the current lane's stream (after its verification)
   hipEvent_t ev_main = nullptr, ev_prep = nullptr, ev_comb = nullptr;
   hipEvent_t ev_ext = nullptr, ev_ext2 = nullptr, ev_ext3 = nullptr;  // external-stream ordering
   std::map<std::string, Stage> stages;
@@ -112,9 +118,9 @@ struct hbtc_ctx {
   int verify_mode = HBTC_MODE_RLC;
   bool track_senders = true;
   const uint32_t* last_leaf_count = nullptr;  // device counter of the last RLC call
-  // Device ranges that combines enqueued on s_comb still read, each with the event recorded
-  // after that combine: main-stream work that writes an overlapping range waits on it first
-  // (combines run concurrently with the NEXT verification; hbtc.h: *_dev calls are ordered).
+  // Device ranges that combines still read, each with the event recorded after that combine:
+  // work on another lane that writes an overlapping range waits on it first (combines run
+  // concurrently with the NEXT verifications; hbtc.h: *_dev calls are ordered).
   struct PendingRead {
     uintptr_t lo, hi;
     hipEvent_t ev;
@@ -204,7 +210,6 @@ int sync(hbtc_ctx* c) {
     HB_CHECK(c, hipStreamSynchronize(l.stream));
     HB_CHECK(c, hipStreamSynchronize(l.s_prep));
   }
-  HB_CHECK(c, hipStreamSynchronize(c->s_comb));
   return HBTC_OK;
 }
 
@@ -214,7 +219,8 @@ void select_lane(hbtc_ctx* c, int l) {
   c->s_prep = c->lanes[l].s_prep;
   c->ev_main = c->lanes[l].ev_main;
   c->ev_prep = c->lanes[l].ev_prep;
-  c->ws_suffix = l ? "#1" : "";
+  c->s_comb = c->lanes[l].stream;
+  c->ws_suffix = l ? "#" + std::to_string(l) : "";
 }
 
 bool ranges_overlap(const std::vector<std::pair<uintptr_t, uintptr_t>>& a,
@@ -225,33 +231,40 @@ bool ranges_overlap(const std::vector<std::pair<uintptr_t, uintptr_t>>& a,
   return false;
 }
 
-// Start a verification on the next lane: it waits for the other lane's last verification only
-// when their device ranges conflict (write/write, read/write either way).
+// Wait on `me` for every other lane's last verification whose device ranges conflict with
+// (rd, wr) (write/write, read/write either way).
+int wait_conflicts(hbtc_ctx* c, int me_l, const std::vector<std::pair<uintptr_t, uintptr_t>>& rd,
+                   const std::vector<std::pair<uintptr_t, uintptr_t>>& wr) {
+  for (int o = 0; o < hbtc_ctx::NL; ++o) {
+    const Lane& other = c->lanes[o];
+    if (o == me_l || !other.busy) continue;
+    if (ranges_overlap(wr, other.wr) || ranges_overlap(rd, other.wr) || ranges_overlap(wr, other.rd))
+      HB_CHECK(c, hipStreamWaitEvent(c->lanes[me_l].stream, other.done, 0));
+  }
+  return HBTC_OK;
+}
+
+// Start a verification on the next lane: it waits for another lane's last verification only
+// when their device ranges conflict.
 int begin_verify(hbtc_ctx* c, std::vector<std::pair<uintptr_t, uintptr_t>> rd,
                  std::vector<std::pair<uintptr_t, uintptr_t>> wr) {
-  const int l = c->pin_lane ? c->lane : (c->lane ^ 1), o = l ^ 1;
+  const int l = c->pin_lane ? c->lane : (c->lane + 1) % hbtc_ctx::NL;
   select_lane(c, l);
   Lane& me = c->lanes[l];
-  const Lane& other = c->lanes[o];
-  if (other.busy && (ranges_overlap(wr, other.wr) || ranges_overlap(rd, other.wr) ||
-                     ranges_overlap(wr, other.rd)))
-    HB_CHECK(c, hipStreamWaitEvent(me.stream, other.done, 0));
+  HB_TRY(wait_conflicts(c, l, rd, wr));
   me.rd = std::move(rd);
   me.wr = std::move(wr);
   return HBTC_OK;
 }
 
-// Another asynchronous operation on the current lane (e.g. unframing): it waits for the other
-// lane on conflicting ranges, and its ranges join the lane's, so the next verification (on the
-// other lane) orders itself after it when it reads what this writes.
+// Another asynchronous operation on the current lane (e.g. unframing): it waits for other lanes
+// on conflicting ranges, and its ranges join the lane's, so a later verification on another lane
+// orders itself after it when it reads what this writes.
 int lane_async(hbtc_ctx* c, std::initializer_list<std::pair<uintptr_t, uintptr_t>> rd,
                std::initializer_list<std::pair<uintptr_t, uintptr_t>> wr) {
   Lane& me = c->lanes[c->lane];
-  const Lane& other = c->lanes[c->lane ^ 1];
   const std::vector<std::pair<uintptr_t, uintptr_t>> r(rd), w(wr);
-  if (other.busy && (ranges_overlap(w, other.wr) || ranges_overlap(r, other.wr) ||
-                     ranges_overlap(w, other.rd)))
-    HB_CHECK(c, hipStreamWaitEvent(me.stream, other.done, 0));
+  HB_TRY(wait_conflicts(c, c->lane, r, w));
   me.rd.insert(me.rd.end(), r.begin(), r.end());
   me.wr.insert(me.wr.end(), w.begin(), w.end());
   return HBTC_OK;
@@ -264,16 +277,19 @@ int end_verify(hbtc_ctx* c) {
   return HBTC_OK;
 }
 
-// An item pass about to start on the current lane waits for the other lane's last item pass.
+// An item pass about to start on the current lane waits for the most recent item pass (on
+// another lane): item passes form one chain.
 int items_gate(hbtc_ctx* c) {
-  const Lane& other = c->lanes[c->lane ^ 1];
-  if (c->items_serial && other.items_rec) HB_CHECK(c, hipStreamWaitEvent(c->stream, other.items_done, 0));
+  const int o = c->last_items_lane;
+  if (c->items_serial && o >= 0 && o != c->lane)
+    HB_CHECK(c, hipStreamWaitEvent(c->stream, c->lanes[o].items_done, 0));
   return HBTC_OK;
 }
 int items_mark(hbtc_ctx* c) {
   Lane& me = c->lanes[c->lane];
   HB_CHECK(c, hipEventRecord(me.items_done, me.stream));
   me.items_rec = true;
+  c->last_items_lane = c->lane;
   return HBTC_OK;
 }
 
@@ -800,15 +816,16 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
   if (!aligned16(d_pts) || !aligned16(d_out))
     return fail(c, HBTC_ERR_ARG, "point arrays must be 16-byte aligned");
   hipStream_t sc = c->s_comb;
-  {  // behind the current lane (the verification that produced the statuses, or whatever wrote
-     // the inputs) and behind the other lane when it writes any of them
+  {  // on the current lane, after the verification that produced the statuses (or whatever
+     // wrote the inputs), and behind any other lane that writes one of them
     const std::vector<std::pair<uintptr_t, uintptr_t>> reads = {
         rng(d_idx, (size_t)n_items * 4), rng(d_pts, (size_t)n_items * (group == 1 ? 48 : 96)),
         rng(d_item_status, d_item_status ? (size_t)n_items * 4 : 0)};
-    HB_TRY(stream_after(c, sc, c->stream, c->ev_main));
-    Lane& other = c->lanes[c->lane ^ 1];
-    if (other.busy && ranges_overlap(reads, other.wr))
-      HB_TRY(stream_after(c, sc, other.stream, other.ev_main));
+    for (int o = 0; o < hbtc_ctx::NL; ++o) {
+      Lane& other = c->lanes[o];
+      if (o != c->lane && other.busy && ranges_overlap(reads, other.wr))
+        HB_TRY(stream_after(c, sc, other.stream, other.ev_main));
+    }
   }
   void* p;
   HB_TRY(stage_upload(c, "comb.offsets", offsets, ((size_t)n_inst + 1) * 4, sc, &p));
@@ -930,9 +947,10 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
       c->n_cu = prop.multiProcessorCount;
   }
-  // four streams, so each gets a hardware queue of its own (GPU_MAX_HW_QUEUES = 4): a stream
-  // sharing a queue would also stall behind the other stream's event waits.  The G2
-  // preparation stream is shared by the lanes (its work is short and ordered anyway).
+  // four streams (the NL lanes and the preparation), so each gets a hardware queue of its own
+  // (GPU_MAX_HW_QUEUES = 4): a stream sharing a queue would also stall behind the other stream's
+  // event waits.  The G2 preparation stream is shared by the lanes (its work is short and
+  // ordered anyway); a lane's combines run on the lane's own stream.
   for (Lane& l : c->lanes)
     if (hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&l.ev_main, hipEventDisableTiming) != hipSuccess ||
@@ -950,14 +968,9 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
     delete c;
     return HBTC_ERR_DEVICE;
   }
-  c->lanes[1].s_prep = c->lanes[0].s_prep;
+  for (Lane& l : c->lanes) l.s_prep = c->lanes[0].s_prep;
   select_lane(c, 0);
-  // the combine stream's chain of small kernels also gets the highest priority (HBTC_COMB_PRIO=0:
-  // the lowest; C3 105.4 vs 108.7 ms per epoch)
-  const char* cp = getenv("HBTC_COMB_PRIO");
-  const int comb_prio = cp && !atoi(cp) ? prio_least : prio_greatest;
-  if (hipStreamCreateWithPriority(&c->s_comb, hipStreamNonBlocking, comb_prio) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming) != hipSuccess ||
+  if (hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_ext2, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_ext3, hipEventDisableTiming) != hipSuccess) {
@@ -1007,7 +1020,6 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
   (void)hipEventDestroy(c->ev_ext);
   (void)hipEventDestroy(c->ev_ext2);
   (void)hipEventDestroy(c->ev_ext3);
-  (void)hipStreamDestroy(c->s_comb);
   delete c;
 }
 
@@ -1029,8 +1041,8 @@ int hbtc_keyset_load(hbtc_ctx* c, const uint8_t* pk_c48, uint32_t n, uint32_t* k
   HB_CHECK(c, hipMalloc(&ks.tab, sizeof(PtXY) * (size_t)n * PK_TAB_WIN * 256));
   HB_CHECK(c, hipMalloc(&ks.last_bad, sizeof(uint32_t) * n));
   HB_CHECK(c, launch_zero_u32(c->stream, ks.last_bad, n));
-  HB_CHECK(c, hipMalloc(&ks.rejects, 2 * sizeof(uint32_t) * n));  // one count array per lane
-  HB_CHECK(c, launch_zero_u32(c->stream, ks.rejects, 2 * (size_t)n));
+  HB_CHECK(c, hipMalloc(&ks.rejects, hbtc_ctx::NL * sizeof(uint32_t) * n));  // one count array per lane
+  HB_CHECK(c, launch_zero_u32(c->stream, ks.rejects, hbtc_ctx::NL * (size_t)n));
   Fq* tab_ws;
   HB_TRY(wst(c, "pktab.ws", (size_t)n * PK_TAB_WIN * 512, &tab_ws));
   HB_TRY(timed(c, "prepare", [&] {
@@ -1219,8 +1231,8 @@ int hbtc_dev_upload(hbtc_ctx* c, void* d_dst, const void* h_src, size_t bytes) {
   if (!c) return HBTC_ERR_ARG;
   Guard g(c);
   HB_TRY(guard_write(c, d_dst, bytes));  // a combine still reading the old contents
-  Lane& other = c->lanes[c->lane ^ 1];  // or a verification on the other lane
-  if (other.busy) HB_CHECK(c, hipStreamWaitEvent(c->stream, other.done, 0));
+  for (int o = 0; o < hbtc_ctx::NL; ++o)  // or a verification on another lane
+    if (o != c->lane && c->lanes[o].busy) HB_CHECK(c, hipStreamWaitEvent(c->stream, c->lanes[o].done, 0));
   HB_CHECK(c, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, c->stream));
   HB_CHECK(c, hipStreamSynchronize(c->stream));
   return HBTC_OK;
@@ -1248,7 +1260,7 @@ int hbtc_stream_wait_ctx(hbtc_ctx* c, void* stream) {
     HB_TRY(stream_after(c, ext, l.stream, c->ev_ext));
     HB_TRY(stream_after(c, ext, l.s_prep, c->ev_ext2));
   }
-  return stream_after(c, ext, c->s_comb, c->ev_ext3);
+  return HBTC_OK;
 }
 
 int hbtc_ctx_wait_stream(hbtc_ctx* c, void* stream) {
@@ -1259,7 +1271,6 @@ int hbtc_ctx_wait_stream(hbtc_ctx* c, void* stream) {
     HB_CHECK(c, hipStreamWaitEvent(l.stream, c->ev_ext, 0));
     HB_CHECK(c, hipStreamWaitEvent(l.s_prep, c->ev_ext, 0));
   }
-  HB_CHECK(c, hipStreamWaitEvent(c->s_comb, c->ev_ext, 0));
   return HBTC_OK;
 }
 
