@@ -85,13 +85,18 @@ struct Lane {
 
 struct hbtc_ctx {
   int device = 0;
-  // Verification calls rotate over NL lanes (hbbft keeps up to 3 epochs in flight,
-  // src/honey_badger/builder.rs:37), so epoch k+1's item pass fills the SIMDs that epoch k's
-  // check levels and combine leave idle, and a small epoch's chain of check latencies overlaps
-  // two others; `stream` / `s_prep` / `s_comb` / `ev_*` / `ws_suffix` are the lane of the most
-  // recent verification (its combine runs on the same stream, after it).  NL lane streams plus
-  // the preparation stream = 4 streams = GPU_MAX_HW_QUEUES: each has a hardware queue of its own.
-  static constexpr int NL = 3;
+  // Verification calls rotate over NL lanes (hbbft processes the current epoch and up to
+  // max_future_epochs = 3 more, src/honey_badger/builder.rs:37, honey_badger.rs:122), so epoch
+  // k+1's item pass fills the SIMDs that epoch k's check levels and combine leave idle, and a
+  // small epoch's chain of check latencies overlaps three others; `stream` / `s_prep` /
+  // `s_comb` / `ev_*` / `ws_suffix` are the lane of the most recent verification (its combine
+  // runs on the same stream, after it).  Measured (C3 / 125-ciphertext slice / C2, ms per epoch):
+  // 2 lanes + a combine stream 107 / 24.4 / 45.3, 3 lanes 100.3 / 22.5 / 36.0, 4 lanes
+  // 97.5 / 20.7 / 35.8, 4 lanes with the preparation on the lane stream 98.0 / 22.2 / 38.9.
+#ifndef HBTC_LANES
+#define HBTC_LANES 4
+#endif
+  static constexpr int NL = HBTC_LANES;
   Lane lanes[NL];
   int lane = 0;
   int last_items_lane = -1;  // the lane of the most recent item pass (items_gate)
@@ -947,10 +952,10 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
       c->n_cu = prop.multiProcessorCount;
   }
-  // four streams (the NL lanes and the preparation), so each gets a hardware queue of its own
-  // (GPU_MAX_HW_QUEUES = 4): a stream sharing a queue would also stall behind the other stream's
-  // event waits.  The G2 preparation stream is shared by the lanes (its work is short and
-  // ordered anyway); a lane's combines run on the lane's own stream.
+  // NL lane streams and the preparation stream (GPU_MAX_HW_QUEUES = 4: with 4 lanes two streams
+  // share a hardware queue, which costs concurrency, never correctness: every wait is on an
+  // event recorded by work submitted earlier).  The G2 preparation stream is shared by the lanes
+  // (its work is short and ordered anyway); a lane's combines run on the lane's own stream.
   for (Lane& l : c->lanes)
     if (hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&l.ev_main, hipEventDisableTiming) != hipSuccess ||
