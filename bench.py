@@ -139,9 +139,10 @@ class Epoch:
             p = ctx.dev_alloc(arr.nbytes)
             ctx.dev_upload(p, arr)
             self.d[name] = p
-        # four sets of outputs, rotated per step: the library runs two verifications at once
-        # (its two lanes) while the combines of the two epochs before them still read their
-        # statuses, so epoch k writes the set epoch k-4's combine (and gather) has finished with
+        # N_OUT sets of outputs, rotated per step: the library keeps up to four epochs in flight
+        # (its four lanes, each verification followed by its combine), and under strong scaling
+        # the all-gather of a set runs after them, so epoch k writes the set epoch k-N_OUT's
+        # combine and gather have long finished with
         alloc = out_alloc or (lambda nbytes, i32: (ctx.dev_alloc(nbytes), None))
         self.out = []
         for j in range(N_OUT):
@@ -158,8 +159,8 @@ class Epoch:
     def step(self, ctx):
         """One epoch: the share checks, then the combines of the first t VERIFIED shares of
         every ciphertext (PublicKeySet::decrypt over ThresholdDecryption's verified share map,
-        td.rs:184).  The combines run on the library's combine stream behind this epoch's
-        verification, so they overlap the NEXT epoch's verification (pipelined epochs)."""
+        td.rs:184).  The combines run on the verification's lane behind it, while the next epochs'
+        verifications run on the library's other lanes (pipelined epochs)."""
         lib, h, d = ctx.lib, ctx.h, self.d
         self.cur = (self.cur + 1) % N_OUT
         j = self.cur
@@ -272,7 +273,7 @@ def max_over_ranks(elapsed, dist, device=None):
     return float(tt.item())
 
 
-N_OUT = 4  # output sets rotated per step (Epoch.step)
+N_OUT = 6  # output sets rotated per step (Epoch.step): four epochs in flight + two gathers
 
 FAMS = ["dec_verify", "rlc_items", "chk_tiles", "chk_tiles_w", "chk_subs", "chk_subs_w",
         "chk_leaves", "rlc_finalize", "lagrange", "comb_decode", "comb_digits", "combine", "prepare"]
