@@ -87,9 +87,13 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
         } else {
           const uint64_t r = rlc_scalar(key, item);
           const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
-          G1A pd;
-          g1_phi(pd, d);
-          jac_mul2_u32_uniform(S, d, ra, pd, rb);
+          Fq bx;  // phi(d) = (beta x, y)
+          {
+            Fq beta;
+            fq_set(beta, G1_BETA);
+            fq_mul(bx, d.x, beta);
+          }
+          if (!d.inf) g1_mul_glv_uniform(S, d, bx, ra, rb);
           if (!pk[id].inf) rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb);
         }
       }

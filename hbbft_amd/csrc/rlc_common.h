@@ -82,16 +82,22 @@ __device__ void rlc_reduce(Jac<F>* redA, Jac<F>* redB, const Jac<F>& q, uint32_t
   redB[lane] = z;
   __syncthreads();
   for (uint32_t s = 1; s < 64; s <<= 1) {
-    if ((lane & (2 * s - 1)) == 0) {
-      Jac<F> a = redA[lane], ar = redA[lane + s];
-      Jac<F> b = redB[lane], br = redB[lane + s];
-      jac_add(b, b, br);
-      Jac<F> sa = ar;
-      for (uint32_t d = 1; d < s; d <<= 1) jac_dbl(sa, sa);
-      jac_add(b, b, sa);
+    if ((lane & (2 * s - 1)) == 0) {  // one merge at a time (register pressure, as below)
+      Jac<F> b = redB[lane];
+      {
+        const Jac<F> br = redB[lane + s];
+        jac_add(b, b, br);
+      }
+      const Jac<F> ar = redA[lane + s];
+      {
+        Jac<F> sa = ar;
+        for (uint32_t d = 1; d < s; d <<= 1) jac_dbl(sa, sa);
+        jac_add(b, b, sa);
+      }
+      redB[lane] = b;
+      Jac<F> a = redA[lane];
       jac_add(a, a, ar);
       redA[lane] = a;
-      redB[lane] = b;
     }
     __syncthreads();
     if (s == 4 && (lane & 7) == 0) {
@@ -135,15 +141,23 @@ __device__ __forceinline__ void rlc_reduce_sp(G1J* redA, G1J* redB, const G1J& S
   __syncthreads();
   for (uint32_t s = 2; s < 64; s <<= 1) {
     if ((lane & (2 * s - 1)) < 2) {
-      G1J al = redA[lane], ar = redA[lane + s];
-      G1J bl = redB[lane], br = redB[lane + s];
-      jac_add(bl, bl, br);
-      G1J sa = ar;
-      for (uint32_t d = 1; d < s; d <<= 1) jac_dbl(sa, sa);
-      jac_add(bl, bl, sa);
+      // one merge at a time, so at most three points are live (register pressure: the active
+      // lanes only read entries of inactive ones besides their own, so the writes cannot race)
+      G1J bl = redB[lane];
+      {
+        const G1J br = redB[lane + s];
+        jac_add(bl, bl, br);
+      }
+      const G1J ar = redA[lane + s];
+      {
+        G1J sa = ar;
+        for (uint32_t d = 1; d < s; d <<= 1) jac_dbl(sa, sa);
+        jac_add(bl, bl, sa);
+      }
+      redB[lane] = bl;
+      G1J al = redA[lane];
       jac_add(al, al, ar);
       redA[lane] = al;
-      redB[lane] = bl;
     }
     __syncthreads();
     if (s == 4 && (lane & 7u) < 2) {
