@@ -55,7 +55,8 @@ MAD_U64_PEAK = 29.51e12
 # timing family -> kernel (hbtc_api.hip timed() families, rocprofv3 names)
 KERNEL_NAME = {"dec_verify": "k_dec_verify", "rlc_items": "k_rlc_items",
                "chk_tiles": "k_chk_plain<0>", "chk_tiles_w": "k_chk_weighted<0>",
-               "chk_subs": "k_chk_plain<1>", "chk_subs_w": "k_chk_weighted<1>",
+               "chk_halves": "k_chk_halves", "chk_halves_w": "k_chk_weighted<2>",
+               "chk_subs": "k_chk_plain<3>", "chk_subs_w": "k_chk_weighted<3>",
                "chk_leaves": "k_chk_leaves"}
 
 
@@ -275,7 +276,7 @@ def max_over_ranks(elapsed, dist, device=None):
 
 N_OUT = 6  # output sets rotated per step (Epoch.step): four epochs in flight + two gathers
 
-FAMS = ["dec_verify", "rlc_items", "chk_tiles", "chk_tiles_w", "chk_subs", "chk_subs_w",
+FAMS = ["dec_verify", "rlc_items", "chk_tiles", "chk_tiles_w", "chk_halves", "chk_halves_w", "chk_subs", "chk_subs_w",
         "chk_leaves", "rlc_finalize", "lagrange", "comb_decode", "comb_digits", "combine", "prepare"]
 
 

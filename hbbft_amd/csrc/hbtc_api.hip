@@ -564,8 +564,8 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   for (int i = 0; i < 8; ++i) key.k[i] = c->rd();
   TileSums* sums;
   G1A* dec;
-  uint32_t *counters, *sub_list, *leaves, *tw_list, *sw_list;
-  Fq2 *t_tiles, *t_subs;
+  uint32_t *counters, *sub_list, *leaves, *tw_list, *sw_list, *hw_list, *hl_list;
+  Fq2 *t_tiles, *t_subs, *t_halves;
   HB_TRY(wst(c, "rlc.sums", n_tiles, &sums));
   // two alternating buffers: a combine of the previous call may still read the other one
   c->lanes[c->lane].dec_flip ^= 1;
@@ -573,19 +573,25 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
   HB_TRY(guard_write(c, dec, (size_t)n_items * sizeof(G1A)));
   c->last_dec = {d_status, d_share, n_items, dec, nullptr};
-  // counters: [0] leaves, [1] listed tiles (sub-tile pass), [2] failing tiles, [3] failing subs
-  HB_TRY(wst(c, "rlc.counters", 4, &counters));
+  // counters: [0] leaves, [1] listed tiles (half / sub-tile pass), [2] failing tiles, [3] failing
+  // subs, [4] failing halves, [5] listed halves
+  HB_TRY(wst(c, "rlc.counters", 6, &counters));
   HB_TRY(wst(c, "rlc.sub_list", n_tiles, &sub_list));
   HB_TRY(wst(c, "rlc.tw_list", n_tiles, &tw_list));
   HB_TRY(wst(c, "rlc.sw_list", (size_t)8 * n_tiles, &sw_list));
   HB_TRY(wst(c, "rlc.t_tiles", (size_t)6 * n_tiles, &t_tiles));
   HB_TRY(wst(c, "rlc.t_subs", (size_t)48 * n_tiles, &t_subs));
+  HB_TRY(wst(c, "rlc.t_halves", (size_t)12 * n_tiles, &t_halves));
+  HB_TRY(wst(c, "rlc.hw_list", (size_t)2 * n_tiles, &hw_list));
+  HB_TRY(wst(c, "rlc.hl_list", (size_t)2 * n_tiles, &hl_list));
   HB_TRY(wst(c, "rlc.leaves", (size_t)2 * n_items, &leaves));
   uint32_t* leaf_count = counters;
   uint32_t* sub_count = counters + 1;
   uint32_t* tw_count = counters + 2;
   uint32_t* sw_count = counters + 3;
-  HB_CHECK(c, launch_zero_u32(c->stream, counters, 4));
+  uint32_t* hw_count = counters + 4;
+  uint32_t* hl_count = counters + 5;
+  HB_CHECK(c, launch_zero_u32(c->stream, counters, 6));
   const Suspects sus = suspects_of(c, ks, leaf_count, leaves);
   HB_TRY(items_gate(c));
   HB_TRY(timed(c, "rlc_items", [&] {
@@ -609,24 +615,33 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
                                h_aff, h_lines, w_aff, w_lines, h_st, w_st, d_status, leaf_count,
                                leaves);
       }));
-  } else {  // throughput form: plain first (k_chk_plain / k_chk_weighted)
+  } else {  // throughput form: plain first (k_chk_plain / k_chk_halves / k_chk_weighted)
     HB_TRY(timed(c, "chk_tiles", [&] {
-      return launch_chk_plain(c->stream, 0, n_tiles, n_tiles, nullptr, nullptr, tiles, sums, h_aff,
-                              h_lines, w_aff, w_lines, h_st, w_st, t_tiles, tw_count, tw_list);
+      return launch_chk_plain(c->stream, 0, n_tiles, n_tiles, nullptr, nullptr, nullptr, tiles, sums,
+                              h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_tiles, tw_count, tw_list);
     }));
     HB_TRY(timed(c, "chk_tiles_w", [&] {
-      return launch_chk_weighted(c->stream, 0, n_tiles, tw_count, tw_list, nullptr, tiles, sums,
-                                 h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_tiles, d_status,
+      return launch_chk_weighted(c->stream, 0, n_tiles, tw_count, tw_list, nullptr, nullptr, tiles,
+                                 sums, h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_tiles, d_status,
                                  sub_count, sub_list);
     }));
+    HB_TRY(timed(c, "chk_halves", [&] {
+      return launch_chk_halves(c->stream, n_tiles, sub_count, sub_list, tiles, sums, h_aff, h_lines,
+                               w_aff, w_lines, t_tiles, t_halves, hw_count, hw_list);
+    }));
+    HB_TRY(timed(c, "chk_halves_w", [&] {
+      return launch_chk_weighted(c->stream, 2, 2 * n_tiles, hw_count, hw_list, sub_list, nullptr,
+                                 tiles, sums, h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_halves,
+                                 d_status, hl_count, hl_list);
+    }));
     HB_TRY(timed(c, "chk_subs", [&] {
-      return launch_chk_plain(c->stream, 1, 8 * n_tiles, 0, sub_count, sub_list, tiles, sums, h_aff,
-                              h_lines, w_aff, w_lines, h_st, w_st, t_subs, sw_count, sw_list);
+      return launch_chk_plain(c->stream, 3, 8 * n_tiles, 0, hl_count, sub_list, hl_list, tiles, sums,
+                              h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_subs, sw_count, sw_list);
     }));
     HB_TRY(timed(c, "chk_subs_w", [&] {
-      return launch_chk_weighted(c->stream, 1, 8 * n_tiles, sw_count, sw_list, sub_list, tiles, sums,
-                                 h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_subs, d_status,
-                                 leaf_count, leaves);
+      return launch_chk_weighted(c->stream, 3, 8 * n_tiles, sw_count, sw_list, sub_list, hl_list,
+                                 tiles, sums, h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_subs,
+                                 d_status, leaf_count, leaves);
     }));
   }
   HB_TRY(timed(c, "chk_leaves", [&] {

@@ -123,8 +123,13 @@ __device__ __forceinline__ bool unit_values(Fq2& T, Fq2& Tw, const Fq2& e, const
 // ------------------------------------------------------------------------------ group levels
 // Plain first: a group's weighted check (needed only to locate a wrong share) runs only when
 // its plain check failed.  Every group of a level is one 6-lane check; a unit carries two
-// groups.  Level 0 = the 64-share tiles (group g = tile g), level 1 = the 8-share sub-tiles of
-// the listed tiles (group g = sub-tile g & 7 of tile sub_list[g >> 3]).
+// groups.  Level 0 = the 64-share tiles (group g = tile g); level 1 = the 8-share sub-tiles of
+// the listed tiles (group g = sub-tile g & 7 of tile sub_list[g >> 3], the paired schedules);
+// level 2 = the 32-share halves of the listed tiles (group g = half g & 1 of tile
+// sub_list[g >> 1]); level 3 = the 4 sub-tiles of the listed halves (half code list2[g >> 2],
+// sub-tile 4 (code & 1) + (g & 3) of tile sub_list[code >> 1]).  Halves between the tiles and
+// the sub-tiles cut a tile with two wrong shares from 8 sub-tile checks to 1 half check (the
+// other half's value is the tile's divided by it) plus the halves' own location.
 namespace {
 
 struct GroupRef {
@@ -134,26 +139,53 @@ struct GroupRef {
 
 template <int LEVEL>
 __device__ __forceinline__ GroupRef group_ref(uint32_t g, uint32_t n, const Tile* tiles,
-                                              const uint32_t* sub_list, const int32_t* h_status,
-                                              const int32_t* w_status) {
+                                              const uint32_t* sub_list, const uint32_t* list2,
+                                              const int32_t* h_status, const int32_t* w_status) {
   GroupRef r{0, 0, 8, 0, 0, false, false};
   if (g >= n) return r;
-  const uint32_t t = LEVEL == 0 ? g : sub_list[g >> 3];
+  uint32_t t, sub = 8;
+  if (LEVEL == 0) {
+    t = g;
+  } else if (LEVEL == 1) {
+    t = sub_list[g >> 3];
+    sub = g & 7u;
+  } else if (LEVEL == 2) {
+    t = sub_list[g >> 1];
+    sub = g & 1u;  // the half
+  } else {
+    const uint32_t code = list2[g >> 2];
+    t = sub_list[code >> 1];
+    sub = 4u * (code & 1u) + (g & 3u);
+  }
   const Tile tile = tiles[t];
   r.t = t;
   r.inst = tile.inst;
+  r.sub = sub;
   if (LEVEL == 0) {
     r.lo = tile.first;
     r.hi = tile.first + tile.count;
     r.inst_ok = h_status[tile.inst] == HBTC_ACCEPT && w_status[tile.inst] == HBTC_ACCEPT;
   } else {
-    r.sub = g & 7u;
-    r.lo = tile.first + r.sub * 8u;
-    r.hi = min(tile.first + tile.count, r.lo + 8u);
+    const uint32_t span = LEVEL == 2 ? 32u : 8u;
+    r.lo = tile.first + sub * span;
+    r.hi = min(tile.first + tile.count, r.lo + span);
     r.inst_ok = true;  // listed tiles belong to instances whose H and w decoded
   }
   r.active = r.lo < r.hi;
   return r;
+}
+
+// the (plain or weighted) G1 sums of a group
+template <int LEVEL>
+__device__ __forceinline__ void group_sums(G1J& S, G1J& P, const TileSums& ts, uint32_t sub,
+                                           bool weighted) {
+  if (LEVEL == 2) {
+    S = weighted ? ts.SHW[sub] : ts.SH[sub];
+    P = weighted ? ts.PHW[sub] : ts.PH[sub];
+  } else {
+    S = weighted ? ts.SW[sub] : ts.S[sub];
+    P = weighted ? ts.PW[sub] : ts.P[sub];
+  }
 }
 
 // 64-bit fingerprint of a GT value (canonical low words of coefficients 0 and 3), group-wide.
@@ -217,25 +249,23 @@ __device__ __forceinline__ int32_t locate_group(const Fq2& T, const Fq2& Tw, uin
 template <int LEVEL>
 __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_plain(
     uint32_t n_direct, const uint32_t* __restrict__ n_listed, const uint32_t* __restrict__ sub_list,
-    const Tile* __restrict__ tiles, const TileSums* __restrict__ sums,
+    const uint32_t* __restrict__ list2, const Tile* __restrict__ tiles,
+    const TileSums* __restrict__ sums,
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
     const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
     const int32_t* __restrict__ h_status, const int32_t* __restrict__ w_status,
     Fq2* __restrict__ Tbuf, uint32_t* __restrict__ fail_count, uint32_t* __restrict__ fail_list) {
   HBTC_LATENCY_PRIO();
-  const uint32_t n = LEVEL == 0 ? n_direct : *n_listed * 8u;
+  const uint32_t n = LEVEL == 0 ? n_direct : *n_listed * (LEVEL == 1 ? 8u : 4u);
   if (blockIdx.x * 2u * UNITS_PER_WAVE >= n) return;  // wave-uniform: grids are sized for the worst case
   const UnitLane ul = unit_lane();
   const uint32_t g = (blockIdx.x * UNITS_PER_WAVE + ul.unit) * 2u + ul.side;
-  const GroupRef r = group_ref<LEVEL>(ul.unit < UNITS_PER_WAVE ? g : n, n, tiles, sub_list,
+  const GroupRef r = group_ref<LEVEL>(ul.unit < UNITS_PER_WAVE ? g : n, n, tiles, sub_list, list2,
                                       h_status, w_status);
   G1J S, P;
   jac_set_inf(S);
   jac_set_inf(P);
-  if (r.active) {
-    S = sums[r.t].S[r.sub];
-    P = sums[r.t].P[r.sub];
-  }
+  if (r.active) group_sums<LEVEL>(S, P, sums[r.t], r.sub, false);
   const bool use1 = r.active && r.inst_ok && !jac_is_inf(S) && !h_aff[r.inst].inf;
   const bool use2 = r.active && r.inst_ok && !jac_is_inf(P) && !w_aff[r.inst].inf;
   Fq2 e;
@@ -248,6 +278,60 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_plain(
   if (ul.ps.k == 0) fail_list[atomicAdd(fail_count, 1u)] = g;
 }
 
+// Level 2: the halves of every listed tile i (tile sub_list[i]).  One pairing check per listed
+// tile: half 0's value T_0; half 1's is T_tile / T_0 (T_tile stored by k_chk_plain<0> at the
+// tile's index; GT values are cyclotomic, so the inverse is the conjugate).  A failing half
+// stores its value and joins the list of the weighted pass as code 2 i + h.
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_halves(
+    const uint32_t* __restrict__ n_listed, const uint32_t* __restrict__ tile_list,
+    const Tile* __restrict__ tiles, const TileSums* __restrict__ sums,
+    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
+    const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
+    const Fq2* __restrict__ Ttile, Fq2* __restrict__ Thalf, uint32_t* __restrict__ fail_count,
+    uint32_t* __restrict__ fail_list) {
+  HBTC_LATENCY_PRIO();
+  const uint32_t n = *n_listed;
+  if (blockIdx.x * 2u * UNITS_PER_WAVE >= n) return;
+  const UnitLane ul = unit_lane();
+  const uint32_t i = (blockIdx.x * UNITS_PER_WAVE + ul.unit) * 2u + ul.side;
+  const bool active = ul.unit < UNITS_PER_WAVE && i < n;
+  uint32_t t = 0, inst = 0, count = 0;
+  G1J S, P;
+  jac_set_inf(S);
+  jac_set_inf(P);
+  Fq2 T;
+  gt::set_one(T, ul.ps);
+  if (active) {
+    t = tile_list[i];
+    const Tile tile = tiles[t];
+    inst = tile.inst;
+    count = tile.count;
+    S = sums[t].SH[0];
+    P = sums[t].PH[0];
+    T = Ttile[(size_t)t * 6u + ul.ps.k];
+  }
+  const bool use1 = active && !jac_is_inf(S) && !h_aff[inst].inf;
+  const bool use2 = active && !jac_is_inf(P) && !w_aff[inst].inf;
+  Fq2 e0, e1;
+  pair_value(e0, S, use1, h_lines + (size_t)inst * MILLER_STEPS, P, use2,
+             w_lines + (size_t)inst * MILLER_STEPS, ul.ps);
+  {
+    Fq2 c0 = e0;
+    gt::conj(c0, ul.ps);
+    gt::mul(e1, T, c0, ul.ps);
+  }
+  const bool pass0 = gt::is_one(e0, ul.ps), pass1 = gt::is_one(e1, ul.ps);
+  if (!active) return;
+  if (!pass0) {
+    Thalf[(size_t)(2u * i) * 6u + ul.ps.k] = e0;
+    if (ul.ps.k == 0) fail_list[atomicAdd(fail_count, 1u)] = 2u * i;
+  }
+  if (count > 32u && !pass1) {
+    Thalf[(size_t)(2u * i + 1u) * 6u + ul.ps.k] = e1;
+    if (ul.ps.k == 0) fail_list[atomicAdd(fail_count, 1u)] = 2u * i + 1u;
+  }
+}
+
 #endif  // part 1
 
 #if HBTC_CHECK_IN(2)
@@ -257,8 +341,9 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_plain(
 template <int LEVEL>
 __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_weighted(
     const uint32_t* __restrict__ fail_count, const uint32_t* __restrict__ fail_list,
-    const uint32_t* __restrict__ sub_list_in, const Tile* __restrict__ tiles,
-    const TileSums* __restrict__ sums, const G2A* __restrict__ h_aff,
+    const uint32_t* __restrict__ sub_list_in, const uint32_t* __restrict__ list2,
+    const Tile* __restrict__ tiles, const TileSums* __restrict__ sums,
+    const G2A* __restrict__ h_aff,
     const Line* __restrict__ h_lines, const G2A* __restrict__ w_aff,
     const Line* __restrict__ w_lines, const int32_t* __restrict__ h_status,
     const int32_t* __restrict__ w_status, const Fq2* __restrict__ Tbuf,
@@ -270,15 +355,15 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_weighted(
   const uint32_t j = (blockIdx.x * UNITS_PER_WAVE + ul.unit) * 2u + ul.side;
   const bool listed = ul.unit < UNITS_PER_WAVE && j < n;
   const uint32_t g = listed ? fail_list[j] : 0u;
-  const GroupRef r = group_ref<LEVEL>(listed ? g : ~0u, ~0u, tiles, sub_list_in, h_status, w_status);
+  const GroupRef r = group_ref<LEVEL>(listed ? g : ~0u, ~0u, tiles, sub_list_in, list2, h_status,
+                                      w_status);
   G1J S, P;
   jac_set_inf(S);
   jac_set_inf(P);
   Fq2 T;
   gt::set_one(T, ul.ps);
   if (r.active) {
-    S = sums[r.t].SW[r.sub];
-    P = sums[r.t].PW[r.sub];
+    group_sums<LEVEL>(S, P, sums[r.t], r.sub, true);
     T = Tbuf[(size_t)g * 6u + ul.ps.k];
   }
   const bool use1 = r.active && !jac_is_inf(S) && !h_aff[r.inst].inf;
@@ -294,6 +379,8 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_weighted(
   }
   if (LEVEL == 0) {
     out_list[atomicAdd(out_count, 1u)] = r.t;
+  } else if (LEVEL == 2) {
+    out_list[atomicAdd(out_count, 1u)] = g;  // the half code 2 i + h
   } else {
     for (uint32_t i = r.lo; i < r.hi; ++i)
       if (status[i] == HBTC_RLC_PENDING) {
@@ -323,15 +410,12 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_pair(
   if (blockIdx.x * UNITS_PER_WAVE >= n) return;  // wave-uniform: grids are sized for the worst case
   const UnitLane ul = unit_lane();
   const uint32_t g = blockIdx.x * UNITS_PER_WAVE + ul.unit;
-  const GroupRef r = group_ref<LEVEL>(ul.unit < UNITS_PER_WAVE ? g : n, n, tiles, sub_list,
+  const GroupRef r = group_ref<LEVEL>(ul.unit < UNITS_PER_WAVE ? g : n, n, tiles, sub_list, nullptr,
                                       h_status, w_status);
   G1J S, P;
   jac_set_inf(S);
   jac_set_inf(P);
-  if (r.active) {
-    S = ul.side ? sums[r.t].SW[r.sub] : sums[r.t].S[r.sub];
-    P = ul.side ? sums[r.t].PW[r.sub] : sums[r.t].P[r.sub];
-  }
+  if (r.active) group_sums<LEVEL>(S, P, sums[r.t], r.sub, ul.side != 0);
   const bool use1 = r.active && r.inst_ok && !jac_is_inf(S) && !h_aff[r.inst].inf;
   const bool use2 = r.active && r.inst_ok && !jac_is_inf(P) && !w_aff[r.inst].inf;
   Fq2 e, T, Tw;
@@ -564,19 +648,36 @@ static inline uint32_t unit_blocks(uint64_t units) {
 
 #if HBTC_CHECK_IN(1)
 hipError_t launch_chk_plain(hipStream_t s, int level, uint32_t max_groups, uint32_t n_direct,
-                            const uint32_t* n_listed, const uint32_t* sub_list, const Tile* tiles,
+                            const uint32_t* n_listed, const uint32_t* sub_list,
+                            const uint32_t* list2, const Tile* tiles,
                             const TileSums* sums, const G2A* h_aff, const Line* h_lines,
                             const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
                             const int32_t* w_status, Fq2* Tbuf, uint32_t* fail_count,
                             uint32_t* fail_list) {
   if (max_groups == 0) return hipSuccess;
   const dim3 grid(unit_blocks(((uint64_t)max_groups + 1) / 2));
+#define HBTC_PLAIN_ARGS                                                                         \
+  grid, dim3(64), 0, s, n_direct, n_listed, sub_list, list2, tiles, sums, h_aff, h_lines, w_aff, \
+      w_lines, h_status, w_status, Tbuf, fail_count, fail_list
   if (level == 0)
-    hipLaunchKernelGGL(k_chk_plain<0>, grid, dim3(64), 0, s, n_direct, n_listed, sub_list, tiles, sums,
-                       h_aff, h_lines, w_aff, w_lines, h_status, w_status, Tbuf, fail_count, fail_list);
+    hipLaunchKernelGGL(k_chk_plain<0>, HBTC_PLAIN_ARGS);
+  else if (level == 1)
+    hipLaunchKernelGGL(k_chk_plain<1>, HBTC_PLAIN_ARGS);
   else
-    hipLaunchKernelGGL(k_chk_plain<1>, grid, dim3(64), 0, s, n_direct, n_listed, sub_list, tiles, sums,
-                       h_aff, h_lines, w_aff, w_lines, h_status, w_status, Tbuf, fail_count, fail_list);
+    hipLaunchKernelGGL(k_chk_plain<3>, HBTC_PLAIN_ARGS);
+#undef HBTC_PLAIN_ARGS
+  return hipGetLastError();
+}
+
+hipError_t launch_chk_halves(hipStream_t s, uint32_t max_tiles, const uint32_t* n_listed,
+                             const uint32_t* tile_list, const Tile* tiles, const TileSums* sums,
+                             const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
+                             const Line* w_lines, const Fq2* Ttile, Fq2* Thalf,
+                             uint32_t* fail_count, uint32_t* fail_list) {
+  if (max_tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_chk_halves, dim3(unit_blocks(((uint64_t)max_tiles + 1) / 2)), dim3(64), 0, s,
+                     n_listed, tile_list, tiles, sums, h_aff, h_lines, w_aff, w_lines, Ttile, Thalf,
+                     fail_count, fail_list);
   return hipGetLastError();
 }
 
@@ -585,21 +686,26 @@ hipError_t launch_chk_plain(hipStream_t s, int level, uint32_t max_groups, uint3
 #if HBTC_CHECK_IN(2)
 hipError_t launch_chk_weighted(hipStream_t s, int level, uint32_t max_groups,
                                const uint32_t* fail_count, const uint32_t* fail_list,
-                               const uint32_t* sub_list, const Tile* tiles, const TileSums* sums,
+                               const uint32_t* sub_list, const uint32_t* list2, const Tile* tiles,
+                               const TileSums* sums,
                                const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
                                const Line* w_lines, const int32_t* h_status,
                                const int32_t* w_status, const Fq2* Tbuf, int32_t* status,
                                uint32_t* out_count, uint32_t* out_list) {
   if (max_groups == 0) return hipSuccess;
   const dim3 grid(unit_blocks(((uint64_t)max_groups + 1) / 2));
+#define HBTC_WEIGHTED_ARGS                                                                     \
+  grid, dim3(64), 0, s, fail_count, fail_list, sub_list, list2, tiles, sums, h_aff, h_lines, w_aff, \
+      w_lines, h_status, w_status, Tbuf, status, out_count, out_list
   if (level == 0)
-    hipLaunchKernelGGL(k_chk_weighted<0>, grid, dim3(64), 0, s, fail_count, fail_list, sub_list, tiles,
-                       sums, h_aff, h_lines, w_aff, w_lines, h_status, w_status, Tbuf, status,
-                       out_count, out_list);
+    hipLaunchKernelGGL(k_chk_weighted<0>, HBTC_WEIGHTED_ARGS);
+  else if (level == 1)
+    hipLaunchKernelGGL(k_chk_weighted<1>, HBTC_WEIGHTED_ARGS);
+  else if (level == 2)
+    hipLaunchKernelGGL(k_chk_weighted<2>, HBTC_WEIGHTED_ARGS);
   else
-    hipLaunchKernelGGL(k_chk_weighted<1>, grid, dim3(64), 0, s, fail_count, fail_list, sub_list, tiles,
-                       sums, h_aff, h_lines, w_aff, w_lines, h_status, w_status, Tbuf, status,
-                       out_count, out_list);
+    hipLaunchKernelGGL(k_chk_weighted<3>, HBTC_WEIGHTED_ARGS);
+#undef HBTC_WEIGHTED_ARGS
   return hipGetLastError();
 }
 

@@ -47,6 +47,9 @@ struct TileSums {
   G1J P[9];   // sum r_i pk_i
   G1J SW[9];  // sum pos_i r_i d_i
   G1J PW[9];  // sum pos_i r_i pk_i
+  // the two 32-share halves (weights = position inside the half): the level between a failing
+  // tile and its sub-tiles in the plain-first schedule (hbtc_check.hip)
+  G1J SH[2], SHW[2], PH[2], PHW[2];
 };
 
 // Partial sums of one tile of SignatureShares (hbtc_sig.hip): S = sum r_i sigma_i in G2 and
@@ -87,16 +90,21 @@ hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n_tiles, const Tile* tile
 // lists the tile (level 0, out_list = sub_list) or the group's pending shares (level 1,
 // out_list = leaves as (item, instance) pairs).
 hipError_t launch_chk_plain(hipStream_t s, int level, uint32_t max_groups, uint32_t n_direct,
-                            const uint32_t* n_listed, const uint32_t* sub_list, const Tile* tiles,
-                            const TileSums* sums, const G2A* h_aff, const Line* h_lines,
-                            const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
-                            const int32_t* w_status, Fq2* Tbuf, uint32_t* fail_count,
-                            uint32_t* fail_list);
+                            const uint32_t* n_listed, const uint32_t* sub_list,
+                            const uint32_t* list2, const Tile* tiles, const TileSums* sums,
+                            const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
+                            const Line* w_lines, const int32_t* h_status, const int32_t* w_status,
+                            Fq2* Tbuf, uint32_t* fail_count, uint32_t* fail_list);
+hipError_t launch_chk_halves(hipStream_t s, uint32_t max_tiles, const uint32_t* n_listed,
+                             const uint32_t* tile_list, const Tile* tiles, const TileSums* sums,
+                             const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
+                             const Line* w_lines, const Fq2* Ttile, Fq2* Thalf,
+                             uint32_t* fail_count, uint32_t* fail_list);
 hipError_t launch_chk_weighted(hipStream_t s, int level, uint32_t max_groups,
                                const uint32_t* fail_count, const uint32_t* fail_list,
-                               const uint32_t* sub_list, const Tile* tiles, const TileSums* sums,
-                               const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
-                               const Line* w_lines, const int32_t* h_status,
+                               const uint32_t* sub_list, const uint32_t* list2, const Tile* tiles,
+                               const TileSums* sums, const G2A* h_aff, const Line* h_lines,
+                               const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
                                const int32_t* w_status, const Fq2* Tbuf, int32_t* status,
                                uint32_t* out_count, uint32_t* out_list);
 hipError_t launch_chk_pair(hipStream_t s, int level, bool to_leaves, uint32_t max_groups,

@@ -103,7 +103,8 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
   }
   rlc_list_leaf(sus, leaf, (uint32_t)item, tile.inst, lane);
   TileSums* ts = sums + blockIdx.x;
-  rlc_reduce_sp(redA, redB, S, P, lane, ts->S, ts->SW, ts->P, ts->PW);
+  rlc_reduce_sp(redA, redB, S, P, lane, ts->S, ts->SW, ts->P, ts->PW, ts->SH, ts->SHW, ts->PH,
+                ts->PHW);
 }
 #endif  // part 6
 

@@ -121,7 +121,8 @@ __device__ void rlc_reduce(Jac<F>* redA, Jac<F>* redB, const Jac<F>& q, uint32_t
 // groups of 8, [8] the tile.  Half the sequential merge chain of two separate reductions.
 __device__ __forceinline__ void rlc_reduce_sp(G1J* redA, G1J* redB, const G1J& S, const G1J& P,
                                               uint32_t lane, G1J* outS, G1J* outSW, G1J* outP,
-                                              G1J* outPW) {
+                                              G1J* outPW, G1J* outSH, G1J* outSHW, G1J* outPH,
+                                              G1J* outPHW) {
   const bool odd = (lane & 1u) != 0;
   G1J x = odd ? S : P, y;  // the value the neighbour lane needs
   {
@@ -167,6 +168,15 @@ __device__ __forceinline__ void rlc_reduce_sp(G1J* redA, G1J* redB, const G1J& S
       } else {
         outP[lane >> 3] = redA[lane];
         outPW[lane >> 3] = redB[lane];
+      }
+    }
+    if (s == 16 && (lane & 31u) < 2) {  // the 32-share halves
+      if ((lane & 31u) == 0) {
+        outSH[lane >> 5] = redA[lane];
+        outSHW[lane >> 5] = redB[lane];
+      } else {
+        outPH[lane >> 5] = redA[lane];
+        outPHW[lane >> 5] = redB[lane];
       }
     }
   }

@@ -397,7 +397,8 @@ int hbtc_merkle_validate_dev(hbtc_ctx* ctx, uint32_t n, uint32_t n_nodes, const 
 /* ---- kernel timing (HIP events on the context's stream) ---------------------------------- */
 /* Families: "prepare", "dec_verify", "sig_verify", "pair_verify", "lagrange" (selection +
  * Lagrange coefficients), "comb_decode", "comb_digits", "combine" (MSM bucket reduction), "skg_scalars", "skg_ack_rows",
- * "mul", "rlc_items", "chk_tiles", "chk_subs", "chk_leaves", "rlc_finalize", "rs", "merkle",
+ * "mul", "rlc_items", "chk_tiles", "chk_tiles_w", "chk_halves", "chk_halves_w", "chk_subs",
+ * "chk_subs_w", "chk_leaves", "rlc_finalize", "rs", "merkle",
  * "merkle_validate".  Reading
  * synchronises the stream. */
 int hbtc_timing_enable(hbtc_ctx* ctx, int enable);
