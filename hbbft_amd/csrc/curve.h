@@ -340,76 +340,79 @@ HD void jac_mul2_u32_uniform(Jac<F>& r, const Aff<F>& p, uint32_t a, const Aff<F
 // infinity and p != +-q; z3 = 2 Z1 H.  (p == +-q in that loop needs the running multiple of the
 // random-scalar prefix to equal the table point: probability ~2^-250, and a wrong sum only
 // makes its RLC group check fail, which falls back to the exact per-share checks.)
-HD void g1_madd_generic(G1J& r, const G1J& p, const Fq& qx, const Fq& qy) {
-  Fq z1z1, u2, s2, H, HH, I, J, rr, V, t;
-  fq_sqr(z1z1, p.z);
-  fq_mul(u2, qx, z1z1);
-  fq_mul(s2, qy, p.z);
-  fq_mul(s2, s2, z1z1);
-  fq_sub(H, u2, p.x);
-  fq_sub(rr, s2, p.y);
-  fq_sqr(HH, H);
-  fq_dbl(I, HH);
-  fq_dbl(I, I);
-  fq_mul(J, H, I);
-  fq_dbl(rr, rr);
-  fq_mul(V, p.x, I);
-  Fq x3, y3;
-  fq_sqr(x3, rr);
-  fq_sub(x3, x3, J);
-  fq_dbl(t, V);
-  fq_sub(x3, x3, t);
-  fq_sub(t, V, x3);
-  fq_mul(y3, rr, t);
-  fq_mul(t, p.y, J);
-  fq_dbl(t, t);
-  fq_sub(y3, y3, t);
-  fq_mul(r.z, p.z, H);
-  fq_dbl(r.z, r.z);
+template <class F>
+HD void jac_madd_generic(Jac<F>& r, const Jac<F>& p, const F& qx, const F& qy) {
+  F z1z1, u2, s2, H, HH, I, J, rr, V, t;
+  fsqr(z1z1, p.z);
+  fmul(u2, qx, z1z1);
+  fmul(s2, qy, p.z);
+  fmul(s2, s2, z1z1);
+  fsub(H, u2, p.x);
+  fsub(rr, s2, p.y);
+  fsqr(HH, H);
+  fdbl(I, HH);
+  fdbl(I, I);
+  fmul(J, H, I);
+  fdbl(rr, rr);
+  fmul(V, p.x, I);
+  F x3, y3;
+  fsqr(x3, rr);
+  fsub(x3, x3, J);
+  fdbl(t, V);
+  fsub(x3, x3, t);
+  fsub(t, V, x3);
+  fmul(y3, rr, t);
+  fmul(t, p.y, J);
+  fdbl(t, t);
+  fsub(y3, y3, t);
+  fmul(r.z, p.z, H);
+  fdbl(r.z, r.z);
   r.x = x3;
   r.y = y3;
 }
 
-// [a] d + [b] phi(d) for a G1 point d (not infinity, in G1) and 32-bit a, b: the uniform joint
-// double-and-add of jac_mul2_u32_uniform specialised to phi (phi(d) = (beta x, y) shares y with
-// d, so the table is d, beta x and d + phi(d): 60 registers instead of 72) with the generic
-// mixed addition (the running sum is infinity only before the first nonzero bit pair: then the
-// table point itself is taken).
-HD void g1_mul_glv_uniform(G1J& r, const G1A& d, const Fq& bx, uint32_t a, uint32_t b) {
-  G1A pq;  // d + phi(d) (never infinity: phi has no eigenvalue -1)
+// [a] d + [b] m(d) for an endomorphism m(x, y) = (c x, y) (G1: phi, c = beta; G2: -psi^2,
+// c = zeta in Fq) of a point d (not infinity, in the prime-order subgroup) and 32-bit a, b: the
+// uniform joint double-and-add of jac_mul2_u32_uniform specialised to an m that keeps y (the
+// table is d, c x and d + m(d): 5 coordinates instead of 6) with the generic mixed addition (the
+// running sum is infinity only before the first nonzero bit pair: then the table point itself
+// is taken).  mx = c x.
+template <class F>
+HD void glv_mul_uniform(Jac<F>& r, const Aff<F>& d, const F& mx, uint32_t a, uint32_t b) {
+  Aff<F> pq;  // d + m(d) (never infinity: m has no eigenvalue -1)
   {
-    G1J s;
+    Jac<F> s;
     jac_from_aff(s, d);
-    g1_madd_generic(s, s, bx, d.y);
-    Fq zi, zi2, zi3;
+    jac_madd_generic(s, s, mx, d.y);
+    F zi, zi2, zi3;
     finv_fast(zi, s.z);
-    fq_sqr(zi2, zi);
-    fq_mul(zi3, zi2, zi);
-    fq_mul(pq.x, s.x, zi2);
-    fq_mul(pq.y, s.y, zi3);
+    fsqr(zi2, zi);
+    fmul(zi3, zi2, zi);
+    fmul(pq.x, s.x, zi2);
+    fmul(pq.y, s.y, zi3);
   }
-  G1J acc;
+  Jac<F> acc;
   jac_set_inf(acc);
   for (int bit = 31; bit >= 0; --bit) {
     jac_dbl(acc, acc);
     const bool ba = ((a >> bit) & 1u) != 0, bb = ((b >> bit) & 1u) != 0;
-    Fq tx, ty;
-    fq_sel(tx, bb, ba ? pq.x : bx, d.x);
-    fq_sel(ty, ba && bb, pq.y, d.y);
+    F tx, ty;
+    fsel(tx, bb, ba ? pq.x : mx, d.x);
+    fsel(ty, ba && bb, pq.y, d.y);
     const bool first = jac_is_inf(acc);
-    G1J n;
-    g1_madd_generic(n, acc, tx, ty);
+    Jac<F> n;
+    jac_madd_generic(n, acc, tx, ty);
     {  // the sum is still infinity (leading zero bit pairs of this lane): take the table point
-      Fq one;
-      fq_one(one);
-      fq_sel(n.x, first, tx, n.x);
-      fq_sel(n.y, first, ty, n.y);
-      fq_sel(n.z, first, one, n.z);
+      F one;
+      fone(one);
+      fsel(n.x, first, tx, n.x);
+      fsel(n.y, first, ty, n.y);
+      fsel(n.z, first, one, n.z);
     }
     const bool take = ba || bb;
-    fq_sel(acc.x, take, n.x, acc.x);
-    fq_sel(acc.y, take, n.y, acc.y);
-    fq_sel(acc.z, take, n.z, acc.z);
+    fsel(acc.x, take, n.x, acc.x);
+    fsel(acc.y, take, n.y, acc.y);
+    fsel(acc.z, take, n.z, acc.z);
   }
   r = acc;
 }

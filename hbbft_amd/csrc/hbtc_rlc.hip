@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
             fq_set(beta, G1_BETA);
             fq_mul(bx, d.x, beta);
           }
-          if (!d.inf) g1_mul_glv_uniform(S, d, bx, ra, rb);
+          if (!d.inf) glv_mul_uniform(S, d, bx, ra, rb);
           if (!pk[id].inf) rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb);
         }
       }

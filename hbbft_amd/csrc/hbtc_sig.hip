@@ -19,28 +19,19 @@
 
 namespace hbtc {
 
-// -psi^2(q) = [mu] q on G2 (psi has eigenvalue x, mu = -x^2)
-__device__ __forceinline__ void g2_mu(G2A& r, const G2A& q) {
-  G2A t;
-  g2_psi(t.x, t.y, q);
-  t.inf = q.inf;
-  g2_psi(r.x, r.y, t);
-  fq2_neg(r.y, r.y);
-  r.inf = q.inf;
-}
-
-#ifndef HBTC_SIG_ITEMS_WAVES
-#define HBTC_SIG_ITEMS_WAVES 2
-#endif
+// Two instances (launch_sig_items picks by the call's size): W = 2, two waves per SIMD with one
+// LDS array (rlc_reduce1; more VGPR spills per wave, C4's 10^4 tiles: k_sig_items 106 -> 80 ms)
+// and W = 1, one wave per SIMD with two arrays (shorter waves: C2's 200 tiles, 13.3 -> 10.2 ms).
 // One wave per tile: decode every SignatureShare (zcash compressed G2 + subgroup check), r_i,
 // r_i sigma_i, r_i pk_i, then the plain and weighted tile / sub-tile sums in both groups.
-__global__ void __launch_bounds__(64, HBTC_SIG_ITEMS_WAVES) k_sig_items(
+template <int W>
+__global__ void __launch_bounds__(64, W) k_sig_items(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
     const uint8_t* __restrict__ sigs, const G1A* __restrict__ pk,
     const int32_t* __restrict__ pk_status, const PtXY* __restrict__ pk_tab, uint32_t n_pk,
     RlcKey key, Suspects sus, SigTileSums* __restrict__ sums, G2A* __restrict__ dec,
     int32_t* __restrict__ status) {
-  __shared__ G2J red2[2][64];  // reused for the G1 reduction
+  __shared__ G2J red2[W == 2 ? 1 : 2][64];  // reused for the G1 reduction (W = 2: 13.8 KB)
   G1J* red1 = reinterpret_cast<G1J*>(&red2[0][0]);
   const Tile tile = tiles[blockIdx.x];
   const uint32_t lane = threadIdx.x;
@@ -70,9 +61,15 @@ __global__ void __launch_bounds__(64, HBTC_SIG_ITEMS_WAVES) k_sig_items(
         } else {
           const uint64_t r = rlc_scalar(key, item);
           const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
-          G2A ms;
-          g2_mu(ms, sg);
-          jac_mul2_u32_uniform(S, sg, ra, ms, rb);
+          // -psi^2(sigma) = (zeta x, y): the G2 GLV map keeps y
+          Fq2 mx;
+          {
+            Fq zeta;
+            fq_set(zeta, G2_ZETA);
+            fq_mul(mx.c0, sg.x.c0, zeta);
+            fq_mul(mx.c1, sg.x.c1, zeta);
+          }
+          if (!sg.inf) glv_mul_uniform(S, sg, mx, ra, rb);
           if (!pk[id].inf) rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb);
         }
       }
@@ -82,8 +79,13 @@ __global__ void __launch_bounds__(64, HBTC_SIG_ITEMS_WAVES) k_sig_items(
   }
   rlc_list_leaf(sus, leaf, (uint32_t)item, tile.inst, lane);
   SigTileSums* ts = sums + blockIdx.x;
-  rlc_reduce<Fq2>(red2[0], red2[1], S, lane, ts->S, ts->SW);
-  rlc_reduce<Fq>(red1, red1 + 64, P, lane, ts->P, ts->PW);
+  if (W == 2) {
+    rlc_reduce1<Fq2>(red2[0], S, lane, ts->S, ts->SW);
+    rlc_reduce1<Fq>(red1, P, lane, ts->P, ts->PW);
+  } else {
+    rlc_reduce<Fq2>(red2[0], red2[W == 2 ? 0 : 1], S, lane, ts->S, ts->SW);
+    rlc_reduce<Fq>(red1, red1 + 64, P, lane, ts->P, ts->PW);
+  }
 }
 
 // Projective line table of one G2 sum: affine (one Fq2 inversion) then the 68 steps.
@@ -151,8 +153,12 @@ hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, 
                             const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,
                             SigTileSums* sums, G2A* dec, int32_t* status) {
   if (n_tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_sig_items, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk, pk_status,
-                     pk_tab, n_pk, key, sus, sums, dec, status);
+  if (n_tiles > 1024)  // more tiles than SIMDs: throughput form
+    hipLaunchKernelGGL(k_sig_items<2>, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk, pk_status,
+                       pk_tab, n_pk, key, sus, sums, dec, status);
+  else
+    hipLaunchKernelGGL(k_sig_items<1>, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk, pk_status,
+                       pk_tab, n_pk, key, sus, sums, dec, status);
   return hipGetLastError();
 }
 

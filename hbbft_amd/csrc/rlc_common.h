@@ -112,6 +112,53 @@ __device__ void rlc_reduce(Jac<F>* redA, Jac<F>* redB, const Jac<F>& q, uint32_t
   __syncthreads();  // the arrays are reused by the next reduction
 }
 
+// The same reduction with ONE LDS array (the plain sums A; the weighted sums B travel between
+// lanes by ds_bpermute): half the LDS of rlc_reduce, so a G2 tile (216-byte points) leaves room
+// for two waves per SIMD.  All 64 lanes run every exchange (converged control flow).
+template <class F>
+__device__ __forceinline__ void jac_shfl(Jac<F>& r, const Jac<F>& x, uint32_t src) {
+  const uint32_t* xs = reinterpret_cast<const uint32_t*>(&x);
+  uint32_t* rs = reinterpret_cast<uint32_t*>(&r);
+  const int addr = (int)((src & 63u) << 2);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(Jac<F>) / 4); ++i)
+    rs[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)xs[i]);
+}
+template <class F>
+__device__ void rlc_reduce1(Jac<F>* red, const Jac<F>& q, uint32_t lane, Jac<F>* outA, Jac<F>* outB) {
+  Jac<F> b;
+  jac_set_inf(b);
+  red[lane] = q;
+  __syncthreads();
+  for (uint32_t s = 1; s < 64; s <<= 1) {
+    const bool active = (lane & (2 * s - 1)) == 0;
+    {
+      Jac<F> br;
+      jac_shfl(br, b, lane + s);
+      if (active) jac_add(b, b, br);
+    }
+    if (active) {
+      Jac<F> sa = red[lane + s];
+      for (uint32_t d = 1; d < s; d <<= 1) jac_dbl(sa, sa);
+      jac_add(b, b, sa);
+      Jac<F> a = red[lane];
+      const Jac<F> ar = red[lane + s];
+      jac_add(a, a, ar);
+      red[lane] = a;  // active lanes read only inactive entries besides their own
+    }
+    __syncthreads();
+    if (s == 4 && (lane & 7u) == 0) {
+      outA[lane >> 3] = red[lane];
+      outB[lane >> 3] = b;
+    }
+  }
+  if (lane == 0) {
+    outA[8] = red[0];
+    outB[8] = b;
+  }
+  __syncthreads();  // the array is reused by the next reduction
+}
+
 // The two G1 sums of a DecryptionShare tile (S = sum r_i d_i, P = sum r_i pk_i), each with its
 // position-weighted sum, in ONE tree with every level's S and P merges on different lanes.
 // Level 1 pairs lanes (2m, 2m+1) in registers: the even lane forms the S pair, the odd lane the
