@@ -336,8 +336,8 @@ def host_buffer_line(ctx, ep, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--validators", dest="n", type=int, default=1000, help="validators N (f = (N-1)/3)")
     ap.add_argument("--cts", type=int, default=1000,
                     help="ciphertexts per epoch (strong: of the whole job; weak: per GPU)")
@@ -443,7 +443,7 @@ def main():
     # PMC passes of this command (tools/gpu_configs_pmc.sh -> tools/pmc_summary.py): separate
     # FETCH_SIZE / WRITE_SIZE / SQ passes, FETCH_SIZE doubled per the gfx950 note.
     traffic, pmc = None, {}
-    pmc_path = os.path.join(ROOT, "profiles", "r02d", "pmc_summary.json")
+    pmc_path = os.path.join(ROOT, "profiles", "r02f", "pmc_summary.json")
     if os.path.exists(pmc_path):
         summ = json.load(open(pmc_path))
         pmc = summ.get("hbtc::" + KERNEL_NAME[dom]) or summ.get("void hbtc::" + KERNEL_NAME[dom], {})
