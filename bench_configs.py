@@ -366,12 +366,22 @@ def bench_broadcast(ctx, n, value_bytes, steps, warmup):
     rstatus = np.empty(n, np.int32)
     log("bc: setup %.1fs (%d proofs, %d instances, shard_len %d)" % (time.time() - t0, n_pr, n, L))
 
+    # HBTC_BC_PHASE_SYNC=1: a sync between the phases, so each kernel's duration in a trace is
+    # its own (by default the three calls run on different verification lanes and overlap)
+    phase_sync = os.environ.get("HBTC_BC_PHASE_SYNC") == "1"
+
     def step():
         ctx._check(lib.hbtc_merkle_validate_dev(h, n_pr, n, d["voff"], d["values"], d["idx"], d["doff"],
                                                 d["digs"], d["roots"], d["status"]), "validate")
+        if phase_sync:
+            ctx.sync()
         ctx._check(lib.hbtc_rs_reconstruct_dev(h, k, p, L, n, d["recv"], N._ptr(present.reshape(-1)),
                                                N._ptr(rstatus)), "reconstruct")
+        if phase_sync:
+            ctx.sync()
         ctx._check(lib.hbtc_merkle_trees_dev(h, n, L, n, d["recv"], d["out"]), "trees")
+        if phase_sync:
+            ctx.sync()
 
     dt = timed_steps(ctx, step, steps, warmup)
     per_step = breakdown(ctx, steps, ["merkle_validate", "rs", "merkle"])
