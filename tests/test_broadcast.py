@@ -175,3 +175,27 @@ def test_gpu_rs_counts_refused(ctx):
     from hbbft_amd import _native as N
     with pytest.raises(N.HbtcError):
         ctx.rs_encode(200, 100, 4, np.zeros(300 * 4, np.uint8))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,p,ln", [(250, 6, 37), (254, 2, 8), (3, 253, 5), (86, 170, 1)])
+def test_gpu_rs_wide_codes_equal_oracle(ctx, k, p, ln):
+    """Codes at the GF(2^8) limit (k + p = 256): k up to 254 input rows per output row (the
+    kernel's LDS table block then exceeds 64 KB), odd shard lengths, one-byte shards; encode and
+    reconstruct equal the restatement."""
+    rng = np.random.default_rng(k * 1000 + p)
+    n_inst = 3
+    data = rng.integers(0, 256, (n_inst, k + p, ln), dtype=np.uint8)
+    enc = ctx.rs_encode(k, p, ln, data.copy()).reshape(n_inst, k + p, ln)
+    for i in range(n_inst):
+        exp = B.rs_encode([bytes(r) for r in data[i]], k, p)
+        assert [bytes(r) for r in enc[i]] == exp
+    present = np.ones((n_inst, k + p), np.uint8)
+    for i in range(n_inst):
+        present[i, rng.choice(k + p, p, replace=False)] = 0
+    recv = enc.copy()
+    recv[present == 0] = 0
+    out, st = ctx.rs_reconstruct(k, p, ln, recv.reshape(-1), present.reshape(-1))
+    from hbbft_amd import _native as N
+    assert (st == N.ACCEPT).all()
+    assert np.array_equal(out.reshape(n_inst, k + p, ln), enc)
