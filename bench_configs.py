@@ -52,6 +52,8 @@ G1_GEN = bytes.fromhex("97f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f
 G2_GEN = bytes.fromhex("93e02b6052719f607dacd3a088274f65596bd0d09920b61ab5da61bbdc7f5049334cf11213945d57e5ac7d055d042b7e"
                        "024aa2b2f08f0a91260805272dc51051c6e47ad4fa403b02b4510b647ae3d1770bac0326a805bbefd48056c8c121bdb8")
 SEED = 0x6862626674
+N_OUT = 6  # output sets rotated per step (bench.py's N_OUT)
+STEPS_DEFAULT = {"c2": 20, "c4": 6, "c5": 1, "bc": 20}
 
 
 def log(*a):
@@ -137,7 +139,11 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode=
     for k, arr in (("H", H), ("idx", idx), ("sigs", sigs)):
         d[k] = ctx.dev_alloc(arr.nbytes)
         ctx.dev_upload(d[k], arr)
-    for j in range(2):  # alternated per step: epoch k+1 verifies while epoch k combines
+    # N_OUT output sets rotated per step, as bench.py: the library keeps up to four calls in
+    # flight (its lanes, each verification followed by its combine), so step k writes the set
+    # whose combine (step k - N_OUT) has long finished; with two sets every third call waited
+    # for the combine two steps back
+    for j in range(N_OUT):
         d["status%d" % j] = ctx.dev_alloc(4 * total)
         d["out%d" % j] = ctx.dev_alloc(96 * n_inst)
         d["par%d" % j] = ctx.dev_alloc(n_inst)
@@ -147,7 +153,7 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode=
     cur = [0]
 
     def step():
-        cur[0] ^= 1
+        cur[0] = (cur[0] + 1) % N_OUT
         j = cur[0]
         ctx._check(lib.hbtc_verify_sig_shares_dev(h, ks, n_inst, d["H"], off, d["idx"], d["sigs"],
                                                   d["status%d" % j]), "verify_sig_shares_dev")
@@ -441,8 +447,10 @@ ctx_mode = [None]
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c2,c4,c5")
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default per config: c2 20, c4 6, c5 1, bc 20 -- enough "
+                         "for the pipelined calls to reach steady state)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 2; c5 1)")
     ap.add_argument("--inst", type=int, default=64, help="c4 coin instances on this GPU")
     ap.add_argument("--parts", type=int, default=1000, help="c5 Parts")
     ap.add_argument("--distinct", type=int, default=4, help="c5 distinct bivariate polynomials")
@@ -456,16 +464,18 @@ def main():
     ctx.set_verify_mode(ctx_mode[0])
     try:
         for c in args.configs.split(","):
+            steps = args.steps if args.steps is not None else STEPS_DEFAULT.get(c, 2)
+            warmup = args.warmup if args.warmup is not None else (1 if c == "c5" else 2)
             if c == "c2":
-                out = bench_coins(ctx, "c2", 100, 100, args.steps, args.warmup, args.corrupt,
+                out = bench_coins(ctx, "c2", 100, 100, steps, warmup, args.corrupt,
                                   args.corrupt_mode)
             elif c == "c4":
-                out = bench_coins(ctx, "c4", 10000, args.inst, args.steps, args.warmup, args.corrupt,
+                out = bench_coins(ctx, "c4", 10000, args.inst, steps, warmup, args.corrupt,
                                   args.corrupt_mode)
             elif c == "bc":
-                out = bench_broadcast(ctx, 256, args.bc_value, args.steps, args.warmup)
+                out = bench_broadcast(ctx, 256, args.bc_value, steps, warmup)
             elif c == "c5":
-                out = bench_skg(ctx, 1000, args.parts, args.distinct, args.steps, args.warmup)
+                out = bench_skg(ctx, 1000, args.parts, args.distinct, steps, warmup)
             else:
                 raise SystemExit("unknown config " + c)
             print(json.dumps(out), flush=True)
