@@ -107,6 +107,7 @@ struct hbtc_ctx {
   bool items_serial = true;
   int n_cu = 256;               // compute units of the device (check schedule, check_mode)
   int check_mode_forced = -1;  // HBTC_CHECK_MODE
+  bool g2_gls = true;          // G2 combines through the ψ split (HBTC_G2_GLS=0: 255-bit terms)
   std::string ws_suffix;
   hipStream_t stream = nullptr;  // main: items, checks, leaves
   hipStream_t s_prep = nullptr;  // per-instance G2 preparation, overlapped with the item pass
@@ -765,13 +766,14 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   return end_verify(c);
 }
 
-// Window width of a batch of n-term MSMs: minimise ceil(256/c) * (mixed adds + bucket adds) in
-// Fqm (mixed add 11, full add 16, segment scaling ~15 per bit per 8 buckets).
-uint32_t msm_window(uint32_t n) {
+// Window width of a batch of n-term MSMs of scalars < 2^bits: minimise W * (mixed adds + bucket
+// adds) in Fqm (mixed add 11, full add 16, segment scaling ~15 per bit per 8 buckets), W =
+// ceil((bits + 1) / c) windows (the signed recoding's last carry needs the extra bit).
+uint32_t msm_window(uint32_t n, uint32_t bits = 255) {
   uint32_t best = 4;
   double best_cost = 1e300;
   for (uint32_t c = 4; c <= 13; ++c) {
-    const double B = double(1u << (c - 1)), W = double((256 + c - 1) / c);
+    const double B = double(1u << (c - 1)), W = double((bits + c) / c);
     const double cost = W * (11.0 * n + 16.0 * B + (B / 8) * 15.0 * c) + W * c * 7.0;
     if (cost < best_cost) {
       best_cost = cost;
@@ -781,12 +783,34 @@ uint32_t msm_window(uint32_t n) {
   return best;
 }
 
-MsmPlan msm_plan(uint32_t n_msm, uint32_t n) {
+// Window width by the LONGEST per-lane chain instead (in Fqm): a segment thread of
+// k_msm_buckets walks 8n/B list terms (mixed adds), 8 rank sums and a small multiple; k_msm_wsum
+// adds S = B/8 segments; k_msm_final runs (bits + 1) doublings and W adds.  For batches too small
+// to fill the GPU the combine's time is this chain, not the total work.
+uint32_t msm_window_latency(uint32_t n, uint32_t bits) {
+  uint32_t best = 4;
+  double best_cost = 1e300;
+  for (uint32_t c = 4; c <= 13; ++c) {
+    const double B = double(1u << (c - 1)), S = B / 8, W = double((bits + c) / c);
+    const double cost = 11.0 * n / S + 16.0 * 8 + 23.0 * (c - 1) + 16.0 * S + 7.0 * (bits + 1) + 16.0 * W;
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = c;
+    }
+  }
+  return best;
+}
+
+MsmPlan msm_plan(uint32_t n_msm, uint32_t n, uint32_t bits = 255) {
   MsmPlan p;
   p.n_msm = n_msm;
   p.n = n;
-  p.c = msm_window(n);
-  p.W = (256 + p.c - 1) / p.c;
+  p.c = msm_window(n, bits);
+  if (bits <= 64) {  // the ψ-split G2 combines: short scalars, latency-bound batches
+    const uint64_t lanes = (uint64_t)n_msm * ((bits + p.c) / p.c) * std::max(1u, (1u << (p.c - 1)) / 8);
+    if (lanes < 65536) p.c = msm_window_latency(n, bits);
+  }
+  p.W = (bits + p.c) / p.c;
   return p;
 }
 
@@ -904,8 +928,23 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
     return launch_msm_decode_g2(sc, n_inst, t, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status,
                                 nullptr, d_aff, d_bad);
   }));
-  HB_TRY(msm_run<Fq2>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
-                      d_inst_status, d_out, d_parity));
+  if (c->g2_gls) {
+    // ψ = [x] on G2: four 64-bit terms per share (k_msm_gls_g2), so the Horner chain of the
+    // final pass is ~64 doublings instead of ~255 (the G2 combine is the lane's latency tail)
+    G2A* d_aff4;
+    uint32_t* d_sc4;
+    HB_TRY(wst(c, "comb.g2x4", 4 * terms, &d_aff4));
+    HB_TRY(wst(c, "comb.lws4", 4 * terms * 8, &d_sc4));
+    HB_TRY(timed_on(c, sc, "comb_digits", [&] {
+      return launch_msm_gls_g2(sc, n_inst, t, (const uint32_t*)d_lambda, d_aff, d_sc4, d_aff4);
+    }));
+    const MsmPlan plan4 = msm_plan(n_inst, 4 * t, 64);
+    HB_TRY(msm_run<Fq2>(c, sc, plan4, d_sc4, d_aff4, d_sel_cnt, t, d_bad, d_dup, d_inst_status,
+                        d_out, d_parity));
+  } else {
+    HB_TRY(msm_run<Fq2>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
+                        d_inst_status, d_out, d_parity));
+  }
   return note_comb_reads(c, {{d_idx, (size_t)n_items * 4}, {d_pts, n_items * pb},
                              {d_item_status, d_item_status ? (size_t)n_items * 4 : 0},
                              {dec2, dec2 ? n_items * sizeof(G2A) : 0}});
@@ -958,6 +997,7 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   hbtc_ctx* c = new hbtc_ctx();
   c->device = device;
   if (const char* e = getenv("HBTC_ITEMS_SERIAL")) c->items_serial = atoi(e) != 0;
+  if (const char* e = getenv("HBTC_G2_GLS")) c->g2_gls = atoi(e) != 0;
   if (const char* e = getenv("HBTC_CHECK_MODE")) {
     const std::string m(e);
     c->check_mode_forced = m == "plain" ? 0 : m == "pair3" ? 1 : m == "pair2" ? 2 : -1;

@@ -186,6 +186,10 @@ hipError_t launch_msm_gather_g1(hipStream_t s, uint32_t n_inst, uint32_t t, cons
                                 const uint32_t* sel_cnt, const G1A* dec, G1A* pts);
 hipError_t launch_msm_gather_g2(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_pos,
                                 const uint32_t* sel_cnt, const G2A* dec, G2A* pts);
+// G2 combine terms (lambda [n_msm][n] canonical, pts [n_msm][n]) -> 4n GLS terms per msm with
+// 64-bit scalars (sc4: 8 words each) and the points P, [u]P, [u^2]P, [u^3]P (hbtc_msm.hip)
+hipError_t launch_msm_gls_g2(hipStream_t s, uint32_t n_msm, uint32_t n, const uint32_t* lambda,
+                             const G2A* pts, uint32_t* sc4, G2A* pts4);
 hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
                                 const uint8_t* pts_c, const uint32_t* sel_pos,
                                 const uint32_t* sel_cnt, const int32_t* item_status,

@@ -623,6 +623,89 @@ hipError_t launch_msm_gather_g2(hipStream_t s, uint32_t n_inst, uint32_t t, cons
                                 const uint32_t* sel_cnt, const G2A* dec, G2A* pts) {
   return launch_msm_gather(s, n_inst, t, sel_pos, sel_cnt, dec, pts);
 }
+
+// GLS split of a G2 combine (ψ acts on G2 as [x], x = -u, u = |x| = 2^16 v): every term
+// λ P with λ < r < u^4 becomes four 64-bit terms
+//     λ P = d0 P + d1 [u]P + d2 [u^2]P + d3 [u^3]P,   λ = sum_j d_j u^j,  0 <= d_j < u,
+// [u]P = -ψ(P) = (ψ_x, -ψ_y), [u^2]P = ψ^2(P), [u^3]P = -ψ^3(P) -- so the Pippenger pass runs
+// over 65-bit windows (a Horner chain of ~64 doublings in k_msm_final instead of ~255) and the
+// result is the same point.  Term k of msm m goes to positions m * 4n + 4k + j; scalars are
+// written in the 8-word canonical layout k_msm_recode reads.
+__device__ __forceinline__ void gls_u_digits(const uint32_t* k, uint64_t d[4]) {
+  constexpr uint64_t V = BLS_X_ABS >> 16;  // 0xd20100000001
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = k[i];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const uint32_t lo16 = w[0] & 0xffffu;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = (w[i] >> 16) | (i < 7 ? w[i + 1] << 16 : 0u);
+    uint64_t rem = 0;  // < V < 2^48, so rem * 2^16 + 16 bits fits 64
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+      uint64_t cur = (rem << 16) | (w[i] >> 16);
+      const uint32_t qh = (uint32_t)(cur / V);
+      rem = cur - (uint64_t)qh * V;
+      cur = (rem << 16) | (w[i] & 0xffffu);
+      const uint32_t ql = (uint32_t)(cur / V);
+      rem = cur - (uint64_t)ql * V;
+      w[i] = (qh << 16) | ql;
+    }
+    d[j] = (rem << 16) | lo16;
+  }
+  d[3] = ((uint64_t)w[1] << 32) | w[0];  // the quotient after three divisions: < u
+}
+
+__global__ void __launch_bounds__(64) k_msm_gls_g2(uint64_t terms, uint32_t n,
+                                                   const uint32_t* __restrict__ lambda,
+                                                   const G2A* __restrict__ pts,
+                                                   uint32_t* __restrict__ sc4, G2A* __restrict__ pts4) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
+  const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (g >= terms) return;
+  uint64_t d[4];
+  gls_u_digits(lambda + g * 8, d);
+  const G2A p = pts[g];
+  G2A q[4];
+  q[0] = p;
+  Fq2 x1, y1, x2, y2, x3, y3;
+  g2_psi(x1, y1, p);
+  G2A t1;
+  t1.x = x1;
+  t1.y = y1;
+  t1.inf = p.inf;
+  g2_psi(x2, y2, t1);
+  G2A t2;
+  t2.x = x2;
+  t2.y = y2;
+  t2.inf = p.inf;
+  g2_psi(x3, y3, t2);
+  q[1].x = x1;
+  fq2_neg(q[1].y, y1);  // [u]P = -ψ(P)
+  q[2] = t2;            // [u^2]P = ψ^2(P)
+  q[3].x = x3;
+  fq2_neg(q[3].y, y3);  // [u^3]P = -ψ^3(P)
+  q[1].inf = q[2].inf = q[3].inf = p.inf;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    pts4[4 * g + j] = q[j];
+    uint32_t* o = sc4 + (4 * g + j) * 8;
+    o[0] = (uint32_t)d[j];
+    o[1] = (uint32_t)(d[j] >> 32);
+#pragma unroll
+    for (int i = 2; i < 8; ++i) o[i] = 0u;
+  }
+}
+
+hipError_t launch_msm_gls_g2(hipStream_t s, uint32_t n_msm, uint32_t n, const uint32_t* lambda,
+                             const G2A* pts, uint32_t* sc4, G2A* pts4) {
+  const uint64_t terms = (uint64_t)n_msm * n;
+  if (terms == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_msm_gls_g2, dim3(msm_blocks(terms, 64)), dim3(64), 0, s, terms, n, lambda, pts,
+                     sc4, pts4);
+  return hipGetLastError();
+}
 hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
                                 const uint8_t* pts_c, const uint32_t* sel_pos,
                                 const uint32_t* sel_cnt, const int32_t* item_status,
