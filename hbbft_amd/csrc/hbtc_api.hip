@@ -108,6 +108,7 @@ struct hbtc_ctx {
   int n_cu = 256;               // compute units of the device (check schedule, check_mode)
   int check_mode_forced = -1;  // HBTC_CHECK_MODE
   bool g2_gls = true;          // G2 combines through the ψ split (HBTC_G2_GLS=0: 255-bit terms)
+  bool g1_glv = true;          // G1 combines through the φ split (HBTC_G1_GLV=0: 255-bit terms)
   std::string ws_suffix;
   hipStream_t stream = nullptr;  // main: items, checks, leaves
   hipStream_t s_prep = nullptr;  // per-instance G2 preparation, overlapped with the item pass
@@ -806,7 +807,7 @@ MsmPlan msm_plan(uint32_t n_msm, uint32_t n, uint32_t bits = 255) {
   p.n_msm = n_msm;
   p.n = n;
   p.c = msm_window(n, bits);
-  if (bits <= 64) {  // the ψ-split G2 combines: short scalars, latency-bound batches
+  if (bits <= 128) {  // the φ / ψ-split combines: short scalars, often latency-bound batches
     const uint64_t lanes = (uint64_t)n_msm * ((bits + p.c) / p.c) * std::max(1u, (1u << (p.c - 1)) / 8);
     if (lanes < 65536) p.c = msm_window_latency(n, bits);
   }
@@ -910,8 +911,23 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
       return launch_msm_decode_g1(sc, n_inst, t, t, d_pts, d_sel_pos, d_sel_cnt, d_item_status,
                                   nullptr, d_aff, d_bad);
     }));
-    HB_TRY(msm_run<Fq>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
-                       d_inst_status, d_out, nullptr));
+    if (c->g1_glv) {
+      // φ = [-x^2] on G1: two 128-bit terms per share (k_msm_glv_g1), a Horner chain of ~128
+      // doublings instead of ~255
+      G1A* d_aff2;
+      uint32_t* d_sc2;
+      HB_TRY(wst(c, "comb.g1x2", 2 * terms, &d_aff2));
+      HB_TRY(wst(c, "comb.lws2", 2 * terms * 8, &d_sc2));
+      HB_TRY(timed_on(c, sc, "comb_digits", [&] {
+        return launch_msm_glv_g1(sc, n_inst, t, (const uint32_t*)d_lambda, d_aff, d_sc2, d_aff2);
+      }));
+      const MsmPlan plan2 = msm_plan(n_inst, 2 * t, 128);
+      HB_TRY(msm_run<Fq>(c, sc, plan2, d_sc2, d_aff2, d_sel_cnt, t, d_bad, d_dup, d_inst_status, d_out,
+                         nullptr));
+    } else {
+      HB_TRY(msm_run<Fq>(c, sc, plan, (const uint32_t*)d_lambda, d_aff, d_sel_cnt, t, d_bad, d_dup,
+                         d_inst_status, d_out, nullptr));
+    }
     return note_comb_reads(c, {{d_idx, (size_t)n_items * 4}, {d_pts, n_items * pb},
                                {d_item_status, d_item_status ? (size_t)n_items * 4 : 0},
                                {dec, dec ? n_items * sizeof(G1A) : 0}});
@@ -998,6 +1014,7 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   c->device = device;
   if (const char* e = getenv("HBTC_ITEMS_SERIAL")) c->items_serial = atoi(e) != 0;
   if (const char* e = getenv("HBTC_G2_GLS")) c->g2_gls = atoi(e) != 0;
+  if (const char* e = getenv("HBTC_G1_GLV")) c->g1_glv = atoi(e) != 0;
   if (const char* e = getenv("HBTC_CHECK_MODE")) {
     const std::string m(e);
     c->check_mode_forced = m == "plain" ? 0 : m == "pair3" ? 1 : m == "pair2" ? 2 : -1;

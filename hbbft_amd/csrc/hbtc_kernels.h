@@ -190,6 +190,9 @@ hipError_t launch_msm_gather_g2(hipStream_t s, uint32_t n_inst, uint32_t t, cons
 // 64-bit scalars (sc4: 8 words each) and the points P, [u]P, [u^2]P, [u^3]P (hbtc_msm.hip)
 hipError_t launch_msm_gls_g2(hipStream_t s, uint32_t n_msm, uint32_t n, const uint32_t* lambda,
                              const G2A* pts, uint32_t* sc4, G2A* pts4);
+// G1 combine terms -> 2n GLV terms per msm with 128-bit scalars: P, [u^2]P = -φ(P)
+hipError_t launch_msm_glv_g1(hipStream_t s, uint32_t n_msm, uint32_t n, const uint32_t* lambda,
+                             const G1A* pts, uint32_t* sc2, G1A* pts2);
 hipError_t launch_msm_decode_g1(hipStream_t s, uint32_t n_msm, uint32_t n, uint32_t stride,
                                 const uint8_t* pts_c, const uint32_t* sel_pos,
                                 const uint32_t* sel_cnt, const int32_t* item_status,

@@ -698,6 +698,50 @@ __global__ void __launch_bounds__(64) k_msm_gls_g2(uint64_t terms, uint32_t n,
   }
 }
 
+// GLV split of a G1 combine (φ = [-x^2] = [-u^2] on G1): λ P = e0 P + e1 [u^2]P with
+// λ = e0 + e1 u^2, 0 <= e_j < u^2 < 2^128 (the base-u digits paired: e0 = d0 + d1 u,
+// e1 = d2 + d3 u), [u^2]P = -φ(P) = (β x, -y).  Term k of msm m goes to 2k + j.
+__global__ void __launch_bounds__(64) k_msm_glv_g1(uint64_t terms, const uint32_t* __restrict__ lambda,
+                                                   const G1A* __restrict__ pts,
+                                                   uint32_t* __restrict__ sc2, G1A* __restrict__ pts2) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
+  const uint64_t g = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (g >= terms) return;
+  uint64_t d[4];
+  gls_u_digits(lambda + g * 8, d);
+  const G1A p = pts[g];
+  G1A q = p;
+  Fq beta;
+  fq_set(beta, G1_BETA);
+  fq_mul(q.x, p.x, beta);
+  fq_neg(q.y, p.y);
+  pts2[2 * g] = p;
+  pts2[2 * g + 1] = q;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    // e = d_lo + d_hi * u  (< u^2 < 2^128)
+    const uint64_t lo = d[2 * j], hi = d[2 * j + 1];
+    const uint64_t m_lo = hi * BLS_X_ABS, m_hi = __umul64hi(hi, BLS_X_ABS);
+    const uint64_t e_lo = m_lo + lo, e_hi = m_hi + (e_lo < lo ? 1u : 0u);
+    uint32_t* o = sc2 + (2 * g + j) * 8;
+    o[0] = (uint32_t)e_lo;
+    o[1] = (uint32_t)(e_lo >> 32);
+    o[2] = (uint32_t)e_hi;
+    o[3] = (uint32_t)(e_hi >> 32);
+#pragma unroll
+    for (int i = 4; i < 8; ++i) o[i] = 0u;
+  }
+}
+
+hipError_t launch_msm_glv_g1(hipStream_t s, uint32_t n_msm, uint32_t n, const uint32_t* lambda,
+                             const G1A* pts, uint32_t* sc2, G1A* pts2) {
+  const uint64_t terms = (uint64_t)n_msm * n;
+  if (terms == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_msm_glv_g1, dim3(msm_blocks(terms, 64)), dim3(64), 0, s, terms, lambda, pts, sc2,
+                     pts2);
+  return hipGetLastError();
+}
+
 hipError_t launch_msm_gls_g2(hipStream_t s, uint32_t n_msm, uint32_t n, const uint32_t* lambda,
                              const G2A* pts, uint32_t* sc4, G2A* pts4) {
   const uint64_t terms = (uint64_t)n_msm * n;
