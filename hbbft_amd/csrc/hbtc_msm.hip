@@ -184,26 +184,46 @@ __global__ void __launch_bounds__(LG_BS) k_lagrange_inv(uint32_t t, Fr* __restri
     xw[i] = pq;  // x_i is no longer needed: keep q's in-chunk exclusive prefix instead
     fr_mul(pq, pq, q[i]);
   }
+  // prefix products of the chunk products (q in C, x in X) and the suffix products of q (in
+  // IE) by log-step scans: 8 products deep instead of the 3 * 256 of one thread's walk
   C[tid] = pq;
   X[tid] = px;
+  IE[tid] = pq;
   __syncthreads();
-  if (tid == 0) {  // 3 * 256 products + one inversion, serial: small next to the O(t^2) pass
-    Fr acc, P;
-    limbs_set_const<8>(acc, FR_ONE);
-    limbs_set_const<8>(P, FR_ONE);
-    for (uint32_t u = 0; u < LG_BS; ++u) {
-      E[u] = acc;
-      fr_mul(acc, acc, C[u]);
-      fr_mul(P, P, X[u]);
+  Fr cp = pq, xp = px, sp = pq;
+  for (uint32_t off = 1; off < LG_BS; off <<= 1) {
+    Fr a, b, d;
+    const bool lo_ok = tid >= off, hi_ok = tid + off < LG_BS;
+    if (lo_ok) {
+      a = C[tid - off];
+      b = X[tid - off];
     }
-    Fr run;
-    fr_inv(run, acc);
-    for (int u = LG_BS - 1; u >= 0; --u) {
-      IE[u] = run;
-      fr_mul(run, run, C[u]);
+    if (hi_ok) d = IE[tid + off];
+    __syncthreads();
+    if (lo_ok) {
+      fr_mul(cp, cp, a);
+      fr_mul(xp, xp, b);
+      C[tid] = cp;
+      X[tid] = xp;
     }
-    X[0] = P;
+    if (hi_ok) {
+      fr_mul(sp, sp, d);
+      IE[tid] = sp;
+    }
+    __syncthreads();
   }
+  // C[u]: q over chunks 0..u;  X[LG_BS - 1]: P;  IE[u]: q over chunks u..LG_BS-1
+  Fr e_excl, s_excl;
+  limbs_set_const<8>(e_excl, FR_ONE);
+  limbs_set_const<8>(s_excl, FR_ONE);
+  if (tid > 0) e_excl = C[tid - 1];
+  if (tid + 1 < LG_BS) s_excl = IE[tid + 1];
+  __shared__ Fr INV_TOTAL;
+  if (tid == 0) fr_inv(INV_TOTAL, C[LG_BS - 1]);  // the one inversion
+  __syncthreads();
+  E[tid] = e_excl;
+  fr_mul(IE[tid], INV_TOTAL, s_excl);  // (q over chunks 0..tid)^-1
+  if (tid == 0) X[0] = X[LG_BS - 1];
   __syncthreads();
   const Fr P = X[0], e = E[tid];
   Fr inv_incl = IE[tid];  // inverse of the prefix of q through item i (starting at the chunk end)
