@@ -443,7 +443,7 @@ def main():
     # PMC passes of this command (tools/gpu_configs_pmc.sh -> tools/pmc_summary.py): separate
     # FETCH_SIZE / WRITE_SIZE / SQ passes, FETCH_SIZE doubled per the gfx950 note.
     traffic, pmc = None, {}
-    pmc_path = os.path.join(ROOT, "profiles", "r02f", "pmc_summary.json")
+    pmc_path = os.path.join(ROOT, "profiles", "r02g", "headline", "pmc_summary.json")
     if os.path.exists(pmc_path):
         summ = json.load(open(pmc_path))
         pmc = summ.get("hbtc::" + KERNEL_NAME[dom]) or summ.get("void hbtc::" + KERNEL_NAME[dom], {})
