@@ -336,7 +336,7 @@ def host_buffer_line(ctx, ep, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--validators", dest="n", type=int, default=1000, help="validators N (f = (N-1)/3)")
     ap.add_argument("--cts", type=int, default=1000,
