@@ -348,8 +348,14 @@ __device__ __forceinline__ void msm_generator(G2A& p) {
 // Term i of MSM k: the selected item sel_pos[k*t+i] (combines), else item k*stride+i of the
 // compressed array; terms i >= stride are the group generator (SyncKeyGen checks fold the
 // right-hand side [v]G into the MSM as one extra term).
+// G1: at most 256 VGPRs so two waves share a SIMD (uncapped, the fully inlined Fq product took
+// 256 + 2 AGPRs: one wave per SIMD for the 56 M commitment points of a SyncKeyGen era)
+#ifndef HBTC_MSM_DECODE_WAVES
+#define HBTC_MSM_DECODE_WAVES 2
+#endif
 template <class F, int NW>
-__global__ void __launch_bounds__(64) k_msm_decode(uint32_t n_inst, uint32_t t, uint32_t stride,
+__global__ void __launch_bounds__(64, (sizeof(F) == sizeof(Fq) ? HBTC_MSM_DECODE_WAVES : 1))
+    k_msm_decode(uint32_t n_inst, uint32_t t, uint32_t stride,
                                                    const uint8_t* __restrict__ pts,
                                                    const uint32_t* __restrict__ sel_pos,
                                                    const uint32_t* __restrict__ sel_cnt,
