@@ -353,6 +353,10 @@ __device__ __forceinline__ void msm_generator(G2A& p) {
 #ifndef HBTC_MSM_DECODE_WAVES
 #define HBTC_MSM_DECODE_WAVES 2
 #endif
+// the G1 bucket walk likewise (256 + 15 AGPRs uncapped)
+#ifndef HBTC_MSM_BUCKET_WAVES
+#define HBTC_MSM_BUCKET_WAVES 2
+#endif
 template <class F, int NW>
 __global__ void __launch_bounds__(64, (sizeof(F) == sizeof(Fq) ? HBTC_MSM_DECODE_WAVES : 1))
     k_msm_decode(uint32_t n_inst, uint32_t t, uint32_t stride,
@@ -440,7 +444,8 @@ __device__ __forceinline__ uint32_t msm_rank(const uint32_t* ro, uint32_t B, uin
 // [r_lo, r_hi): tot = sum_r (r_hi - r) B'_r, run = sum_r B'_r (B'_r = the slice's part of
 // bucket rank r, bucket b = B - r), so the slice's share of sum_b b B_b is tot + [B - r_hi] run.
 template <class F>
-__global__ void __launch_bounds__(64) k_msm_buckets(uint64_t n_lanes, uint32_t n, uint32_t c,
+__global__ void __launch_bounds__(64, (sizeof(F) == sizeof(Fq) ? HBTC_MSM_BUCKET_WAVES : 1))
+    k_msm_buckets(uint64_t n_lanes, uint32_t n, uint32_t c,
                                                     uint32_t W, const Aff<F>* __restrict__ pts,
                                                     const uint32_t* __restrict__ list,
                                                     const uint32_t* __restrict__ roff,
