@@ -280,7 +280,11 @@ bool hash_offsets_ok(uint32_t n, const uint32_t* offsets) {
 // GPU candidates of hash_g2 / hash_g1_g2 (one lane per message): the seed, the ChaCha stream
 // and G2::rand's draw loop before [h2] — the host path's code (k_g2_clear_cofactor finishes).
 // g1_c48 != null: hash_g1_g2(u_i, v_i), the seed message (|v| > 64 ? sha3(v) : v) || u_i.
-__global__ void __launch_bounds__(64) k_hash_cand(uint32_t n, const uint8_t* __restrict__ g1_c48,
+#ifndef HBTC_HASH_CAND_WAVES
+#define HBTC_HASH_CAND_WAVES 2
+#endif
+// two waves per SIMD (256 VGPRs + spills; uncapped 256 + 61 AGPRs ran one)
+__global__ void __launch_bounds__(64, HBTC_HASH_CAND_WAVES) k_hash_cand(uint32_t n, const uint8_t* __restrict__ g1_c48,
                                                   const uint8_t* __restrict__ msgs,
                                                   const uint32_t* __restrict__ offsets,
                                                   G2A* __restrict__ cand) {
