@@ -2,7 +2,7 @@
 # Final check of the round: the whole -m gpu suite, smoke(), the default bench line and the
 # secondary configs (c2, c4, bc, c5), each under its own time limit; the first failure ends it.
 cd "$(dirname "$0")/.." || exit 1
-O=gpurun_out/final
+O=gpurun_out/${OUT_DIR:-final}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit $?
