@@ -79,7 +79,7 @@ class Epoch:
     shares of the whole epoch with an invalid encoding."""
 
     def __init__(self, ctx, n, n_ct, seed, corrupt_frac=0.01, corrupt_mode="uniform", ct_range=None,
-                 out_alloc=None):
+                 out_alloc=None, load_keyset=True):
         rng = random.Random(seed)
         self.n, self.n_ct = n, n_ct
         self.f = (n - 1) // 3
@@ -98,8 +98,11 @@ class Epoch:
         self.a, self.b = a, b
         pk, st = ctx.g1_mul(G1_GEN, scalars_bytes(sks))
         assert not st.any()
-        self.keyset, bad = ctx.keyset_load(pk)
-        assert bad == 0
+        self.pk = pk
+        self.keyset = None
+        if load_keyset:  # (a node loads the key set on every device itself)
+            self.keyset, bad = ctx.keyset_load(pk)
+            assert bad == 0
         rs, hs = [], []
         for k in range(a, b):
             rk = random.Random(seed * 1000003 + k)
@@ -201,7 +204,8 @@ class Epoch:
             for p, t in o.values():
                 if t is None:
                     ctx.dev_free(p)
-        ctx.keyset_free(self.keyset)
+        if self.keyset is not None:
+            ctx.keyset_free(self.keyset)
 
 
 class StrongGather:
@@ -242,6 +246,72 @@ class StrongGather:
         return a["status"].cpu().numpy(), a["g"].cpu().numpy().reshape(-1), a["cst"].cpu().numpy()
 
 
+class NodeEpoch:
+    """The C3 epoch on a one-process node (hbtc_node_*, `--node`): device slot d holds whole
+    ciphertexts [first[d], first[d+1]) (hbtc_shard_instances, balanced by share count) resident
+    in its HBM; a step enqueues every slot's verification, then every slot's combines of its own
+    ciphertexts (hbtc_node_verify_dec_shares_dev / hbtc_node_combine_dec_verified_dev, one host
+    thread per device).  No collective: the slots' verdicts and combined points are disjoint
+    slices of the epoch, final where they are computed (one process owns every device)."""
+
+    def __init__(self, node, args, slices):
+        self.node = node
+        self.ctxs = [node.context(d) for d in range(len(node.devices))]
+        self.eps = [Epoch(c, args.n, args.cts, SEED, args.corrupt, args.corrupt_mode, ct_range=slices[d][0],
+                          load_keyset=False) for d, c in enumerate(self.ctxs)]
+        self.keyset, bad = node.keyset_load(self.eps[0].pk)
+        assert bad == 0
+        self.t = self.eps[0].t
+        self.total = sum(ep.total for ep in self.eps)
+        self.m = sum(ep.m for ep in self.eps)
+        self.n, self.f = self.eps[0].n, self.eps[0].f
+        self.parts = []
+        for j in range(N_OUT):
+            specs = [{"offsets": ep.offsets, "d_H_c96": ep.d["H"], "d_w_c96": ep.d["w"], "d_idx": ep.d["idx"],
+                      "d_items": ep.d["shares"], "d_status": ep.ptr(j, "status"), "d_out": ep.ptr(j, "g"),
+                      "d_inst_status": ep.ptr(j, "cst")} if ep.m else {} for ep in self.eps]
+            self.parts.append(node.parts(specs))
+        self.cur = 0
+
+    def step(self, ctx=None):
+        self.cur = (self.cur + 1) % N_OUT
+        for ep in self.eps:
+            ep.cur = self.cur
+        parts, _ = self.parts[self.cur]
+        self.node.verify_dec_shares_dev(self.keyset, parts)
+        self.node.combine_dec_verified_dev(parts, self.t)
+
+    def check(self, ctx, args):
+        self.node.sync()
+        st, g, cst = [], [], []
+        for c, ep in zip(self.ctxs, self.eps):
+            if ep.m:
+                a, b, x = ep.results(c)
+                st.append(a)
+                g.append(b)
+                cst.append(x)
+        st, g, cst = np.concatenate(st), np.concatenate(g), np.concatenate(cst)
+        expected = np.concatenate([ep.expected for ep in self.eps])
+        want, _ = ctx.g1_mul(G1_GEN, scalars_bytes(_all_master_r(args, self.eps[0])))
+        return (int((st != expected).sum()), bool((cst == 0).all() and bytes(g) == bytes(want)),
+                int((st == N.ACCEPT).sum()))
+
+
+def timed_node(nep, steps, warmup):
+    """timed() for the node: W untimed steps, then K steps bracketed by node-wide syncs."""
+    c0 = nep.ctxs[0]
+    c0.timing_enable(True)
+    for _ in range(warmup):
+        nep.step()
+    nep.node.sync()
+    c0.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        nep.step()
+    nep.node.sync()
+    return time.perf_counter() - t0
+
+
 def cpu_baseline(ep, budget_s):
     """The oracle (threshold_crypto restatement) on a bounded sample of the same workload: per
     share the reference's verify_decryption_share = hash_g1_g2(u, v) + two full pairings, plus
@@ -272,6 +342,23 @@ def max_over_ranks(elapsed, dist, device=None):
     tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     return float(tt.item())
+
+
+# committed rocprofv3 summaries of this command (kernel trace + PMC passes), newest first
+PROFILE_DIRS = ("profiles/r03/headline", "profiles/r02g/headline")
+
+
+def rocprof_avg_ms(csv_path, kernel):
+    """Average duration (ms) of `kernel` in a committed rocprofv3 --stats kernel table."""
+    import csv
+    if not os.path.exists(csv_path):
+        return None
+    with open(csv_path, newline="") as fh:
+        for row in csv.DictReader(fh):
+            name = row["Name"].split("(")[0]
+            if name.endswith("hbtc::" + kernel):
+                return round(float(row["AverageNs"]) / 1e6, 3)
+    return None
 
 
 N_OUT = 6  # output sets rotated per step (Epoch.step): four epochs in flight + two gathers
@@ -309,28 +396,47 @@ def timed(ctx, ep, steps, warmup, dist=None, gather=None, sync_all=None):
     return time.perf_counter() - t0
 
 
-def host_buffer_line(ctx, ep, steps):
-    """The epoch through the host-buffer entry points (what an FFI caller holding wire bytes
-    does): hbtc_verify_dec_shares (H2D of shares + idx, verification, D2H of the statuses), the
-    first t ACCEPTed shares of every ciphertext picked on the host, hbtc_combine_dec (H2D of
-    those shares, combine, D2H of the points)."""
+def host_buffer_line(ctx, ep, steps, warmup=2):
+    """The epoch through the pipelined host-buffer entry point (what an FFI caller holding wire
+    bytes does, hbtc_dec_epoch_submit / hbtc_wait): per epoch, the compressed shares, indices,
+    H and w go from host memory through pinned staging to the device, the shares are verified,
+    the first t verified shares of every ciphertext combined, and statuses and points come back
+    to host memory -- all inside the timed region.  Up to four epochs are in flight (hbbft's
+    current epoch + max_future_epochs = 3), so epoch k's copies overlap the others' kernels."""
+    from collections import deque
     sh = ep.host_shares.reshape(-1)
-    m, n = ep.m, ep.n
+    n_sets = 6
+    outs = [None] * n_sets
+    inflight = deque()
+
+    def run(k):
+        if len(inflight) == 4:
+            inflight.popleft().wait()
+        p = ctx.dec_epoch_submit(ep.keyset, ep.H, ep.w, ep.offsets, ep.idx, sh, ep.t, outs[k % n_sets])
+        outs[k % n_sets] = p.outs
+        inflight.append(p)
+        return p
+
+    for k in range(warmup):
+        run(k)
+    while inflight:
+        inflight.popleft().wait()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        st = ctx.verify_dec_shares(ep.keyset, ep.H, ep.w, None, ep.idx, sh, offsets=ep.offsets)
-        acc = (st == N.ACCEPT).reshape(m, n)
-        sel = acc & (np.cumsum(acc, axis=1) <= ep.t)
-        counts = sel.sum(axis=1)
-        flat = sel.reshape(-1)
-        g, cst = ctx.combine_dec(counts, ep.idx[flat], ep.host_shares[flat].reshape(-1), ep.t)
+    last = None
+    for k in range(steps):
+        last = run(warmup + k)
+    while inflight:
+        inflight.popleft().wait()
     elapsed = time.perf_counter() - t0
-    ok = bool((st == ep.expected).all() and (cst == 0).all()
-              and b"".join(g) == bytes(ep.want_g(ctx)))
+    st, g, cst = last.outs
+    ok = bool((st[:ep.total] == ep.expected).all() and (cst[:ep.m] == 0).all()
+              and g[:ep.m].tobytes() == bytes(ep.want_g(ctx)))
     return {"value": round(ep.total * steps / elapsed, 1), "unit": "shares/s",
-            "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "results_ok": ok,
-            "path": "hbtc_verify_dec_shares + hbtc_combine_dec (host buffers: H2D of compressed "
-                    "shares/idx and D2H of statuses/points inside the timed region)"}
+            "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "warmup": warmup,
+            "results_ok": ok,
+            "path": "hbtc_dec_epoch_submit + hbtc_wait (host buffers, up to 4 epochs in flight: pinned "
+                    "staging, H2D of compressed shares / idx / H / w, verification, combine of the first t "
+                    "verified shares, D2H of statuses and points inside the timed region)"}
 
 
 def main():
@@ -350,6 +456,15 @@ def main():
                          "(default); per_share: one pairing check per share")
     ap.add_argument("--corrupt", type=float, default=0.01, help="fraction of wrong shares")
     ap.add_argument("--corrupt-mode", choices=["uniform", "senders"], default="uniform")
+    ap.add_argument("--node", action="store_true",
+                    help="with --gpus N > 1 in ONE process (no torchrun): a multi-device node "
+                         "(hbtc_node_*_dev) splits the epoch by whole ciphertexts over N GPUs; no "
+                         "collective, no torch.distributed")
+    ap.add_argument("--slots", default=None,
+                    help="--node device slots, e.g. 0,0 (two contexts on GPU 0: a rehearsal)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise torch.distributed and run the strong-scaling merge even at "
+                         "WORLD_SIZE 1 (torchrun --nproc-per-node 1: exercises the RCCL path on one GPU)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend of the merge (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the sharded path with several ranks on one GPU)")
@@ -358,9 +473,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    strong = args.scaling == "strong" and world > 1
+    if args.node and world == 1 and (args.gpus > 1 or args.slots):
+        return node_main(args)
+    use_dist = world > 1 or args.force_dist
+    strong = args.scaling == "strong" and use_dist
     dist, torch, dev = None, None, None
-    if world > 1:
+    if use_dist:
         import torch
         import torch.distributed as dist
         local = local % max(1, torch.cuda.device_count())
@@ -442,15 +560,23 @@ def main():
     # HBM traffic and VALU instruction count of the same kernel from the committed rocprofv3
     # PMC passes of this command (tools/gpu_configs_pmc.sh -> tools/pmc_summary.py): separate
     # FETCH_SIZE / WRITE_SIZE / SQ passes, FETCH_SIZE doubled per the gfx950 note.
-    traffic, pmc = None, {}
-    pmc_path = os.path.join(ROOT, "profiles", "r02g", "headline", "pmc_summary.json")
-    if os.path.exists(pmc_path):
-        summ = json.load(open(pmc_path))
+    traffic, pmc, prof_dir = None, {}, None
+    for cand in PROFILE_DIRS:
+        if os.path.exists(os.path.join(ROOT, cand, "pmc_summary.json")):
+            prof_dir = cand
+            break
+    rocprof_ms = None
+    if prof_dir:
+        summ = json.load(open(os.path.join(ROOT, prof_dir, "pmc_summary.json")))
         pmc = summ.get("hbtc::" + KERNEL_NAME[dom]) or summ.get("void hbtc::" + KERNEL_NAME[dom], {})
         if "hbm_read_bytes" in pmc and "hbm_write_bytes" in pmc:
             traffic = pmc["hbm_read_bytes"] + pmc["hbm_write_bytes"]
+        rocprof_ms = rocprof_avg_ms(os.path.join(ROOT, prof_dir, "kt_kernel_stats.csv"), KERNEL_NAME[dom])
     if strong:
-        par = "strong: one epoch sharded by whole ciphertexts over %d GPU(s) (hbtc_shard_instances), RCCL all-gather of statuses + combined points" % world
+        coll = ("RCCL (nccl backend) all-gather over xGMI" if args.backend == "nccl"
+                else "gloo all-gather of host copies (rehearsal, not the product merge)")
+        par = ("strong: one epoch sharded by whole ciphertexts over %d rank(s), one process per GPU "
+               "(hbtc_shard_instances), %s of statuses + combined points" % (world, coll))
     elif world > 1:
         par = "weak: an independent epoch per GPU (%d GPUs), no collective" % world
     else:
@@ -478,7 +604,11 @@ def main():
         "accepted_per_step": n_acc,
         "mode": args.mode,
         "exact_single_share_checks_per_step_rank0": leaves,
-        "kernel_ms_per_step_rank0": per_step,
+        "kernel_event_spans_ms_per_step_rank0": per_step,
+        "kernel_event_spans_note": ("HIP-event spans per kernel family on the library's streams, summed "
+                                    "per step: the four verification lanes and the preparation stream "
+                                    "overlap, so the spans add up to more than ms_per_step; kernel "
+                                    "durations are roofline.rocprof_avg_ms_per_launch (rocprofv3)"),
         "roofline": {
             "bound": "valu-int (v_mad_u64_u32)",
             "kernel": KERNEL_NAME[dom],
@@ -490,13 +620,19 @@ def main():
             "traffic_unit": "bytes per launch (HBM read + write, rocprofv3 PMC)",
             "fqm_per_launch": fqm_per_launch[dom],
             "kernel_ms_per_launch": round(dom_avg_s * 1e3, 3),
+            "kernel_ms_per_launch_source": "HIP events on the kernel's stream, this run (the span can "
+                                           "include time the kernel shares the CUs with other lanes)",
+            "rocprof_avg_ms_per_launch": rocprof_ms,
+            "frac_at_rocprof_duration": (round(fqm_per_launch[dom] * consts["mad_u64_u32_per_fqm"]
+                                               / (rocprof_ms * 1e-3) / MAD_U64_PEAK, 4) if rocprof_ms else None),
+            "profile_dir": prof_dir,
             "pmc": {k: pmc[k] for k in ("vgpr", "scratch_bytes_per_lane", "valu_busy",
                                         "hbm_read_bytes", "hbm_write_bytes") if k in pmc} or None,
             "valu_insts_per_launch": pmc.get("counters_mean_per_dispatch", {}).get("SQ_INSTS_VALU"),
         },
     }
     if world == 1 and not args.no_extra:
-        out["host_buffers"] = host_buffer_line(ctx, ep, max(1, min(args.steps, 2)))
+        out["host_buffers"] = host_buffer_line(ctx, ep, args.steps, min(args.warmup, 2))
         if args.corrupt_mode == "uniform":
             out["adversarial"] = adversarial_line(ctx, args, ep)
     if rank == 0 and not args.no_cpu:
@@ -508,6 +644,52 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def node_main(args):
+    """--node: the epoch on a one-process multi-device node (NodeEpoch)."""
+    from hbbft_amd import shard
+    slots = [int(x) for x in args.slots.split(",")] if args.slots else list(range(args.gpus))
+    ctx = N.Context(slots[0])
+    node = N.Node(slots)
+    node.set_verify_mode(N.MODE_RLC if args.mode == "rlc" else N.MODE_PER_SHARE)
+    offsets_all = np.arange(0, args.n * args.cts + 1, args.n, dtype=np.uint32)
+    slices = shard.instance_slices(len(slots), offsets_all)
+    t0 = time.time()
+    nep = NodeEpoch(node, args, slices)
+    log("node: setup %.1fs (%d shares over %d slots)" % (time.time() - t0, nep.total, len(slots)))
+    elapsed = timed_node(nep, args.steps, args.warmup)
+    mism, comb_ok, n_acc = nep.check(ctx, args)
+    per = {f: round(nep.ctxs[0].timing_read(f)[0] / args.steps, 3) for f in FAMS
+           if nep.ctxs[0].timing_read(f)[1]}
+    log("node: %.3fs for %d steps; slot-0 event spans ms/step %s; mismatches %d, combine ok %s"
+        % (elapsed, args.steps, per, mism, comb_ok))
+    if mism or not comb_ok:
+        raise SystemExit("node: results differ from the construction (%d mismatches, combine %s)" % (mism, comb_ok))
+    n_gpus = len(set(slots))
+    out = {
+        "metric": "verified BLS12-381 shares/sec (whole node) at N=1000; combines/sec",
+        "value": round(nep.total * args.steps / elapsed, 1), "unit": "shares/s", "n_gpus": n_gpus,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "u32 (381-bit Montgomery limbs)",
+        "data": "synthetic (seeded key set, shares generated on device; %s + 8 bad encodings)"
+                % ("%g%% wrong shares" % (100 * args.corrupt) if args.corrupt_mode == "uniform"
+                   else "f = %d Byzantine senders send wrong shares on every ciphertext" % nep.f),
+        "config": {"workload": "C3 HoneyBadger epoch: %d ciphertexts x %d DecryptionShares verified + %d G1 "
+                               "combines (t=%d)" % (args.cts, args.n, args.cts, nep.t),
+                   "N": args.n, "f": nep.f, "t": nep.t, "ciphertexts": args.cts,
+                   "shares_per_step": nep.total,
+                   "parallelism": "node: one process, %d device slot(s) on %d GPU(s) (hbtc_node_*_dev), whole "
+                                  "ciphertexts per slot (hbtc_shard_instances); no collective (disjoint "
+                                  "outputs)" % (len(slots), n_gpus)},
+        "combines_per_s": round(args.cts * args.steps / elapsed, 1),
+        "accepted_per_step": n_acc, "mode": args.mode,
+        "kernel_event_spans_ms_per_step_slot0": per,
+    }
+    print(json.dumps(out), flush=True)
+    node.close()
+    ctx.close()
 
 
 def _all_expected(dist, ep, torch, dev, slices):

@@ -10,7 +10,10 @@ checked against the construction after timing:
       (PublicKeyShare::verify, src/coin.rs:151) + 100 G2 combines of the first t=34 verified
       shares (combine_signatures + parity, src/coin.rs:185-191,173).  Inputs resident in HBM.
   c4  N=10,000: I coin instances x 10^4 SignatureShares + I G2 Pippenger combines (t=3334).
-      SURVEY §8 shards the I=64 instances over 8 GPUs; this 1-GPU line runs --inst of them.
+      BASELINE config 4 shards the I=64 instances over 8 GPUs: `--gpus 8` runs them on a
+      one-process node (hbtc_node_*_dev: whole instances per GPU, every GPU verifies and
+      combines its own instances, no collective); `--slots 0,0` rehearses the node path with
+      two contexts on one GPU.
   c5  SyncKeyGen N=1000, one node's view of an era: 1000 Parts (row.commitment() ==
       commit.row(x), src/sync_key_gen.rs:366), then the 10^6 Acks: each Ack value addressed to
       us decrypted (SecretKey::decrypt = hash_g1_g2 + Ciphertext::verify + sk u + pad,
@@ -113,16 +116,13 @@ def corrupt_positions(rng, n, n_inst, frac, mode):
     return rng.sample(range(total), int(total * frac))
 
 
-def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode="uniform"):
-    """c2 / c4: n_inst coin instances x n SignatureShares + n_inst combines (first t verified)."""
+def coin_inputs(ctx, n, n_inst, corrupt=0.01, corrupt_mode="uniform"):
+    """A coin epoch generated on the device (setup): key set, H per instance, shares, expected
+    statuses, the master key and the instances' H scalars (for the combine's construction)."""
     rng = random.Random(SEED + n)
-    t0 = time.time()
     master, sks = key_shares(rng, n)
-    t = (n - 1) // 3 + 1
     pk, st = ctx.g1_mul(G1_GEN, fr_bytes(sks))
     assert not st.any()
-    ks, bad = ctx.keyset_load(pk)
-    assert bad == 0
     hs = [rng.randrange(1, R) for _ in range(n_inst)]
     H, _ = ctx.g2_mul(G2_GEN, fr_bytes(hs))
     total = n * n_inst
@@ -133,67 +133,208 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode=
         expected[j] = N.REJECT
     sigs, st = ctx.g2_mul(G2_GEN, fr_bytes(scal))
     assert not st.any()
-    offsets = np.arange(0, total + 1, n, dtype=np.uint32)
-    idx = np.tile(np.arange(n, dtype=np.uint32), n_inst)
-    d = {}
-    for k, arr in (("H", H), ("idx", idx), ("sigs", sigs)):
-        d[k] = ctx.dev_alloc(arr.nbytes)
-        ctx.dev_upload(d[k], arr)
-    # N_OUT output sets rotated per step, as bench.py: the library keeps up to four calls in
-    # flight (its lanes, each verification followed by its combine), so step k writes the set
-    # whose combine (step k - N_OUT) has long finished; with two sets every third call waited
-    # for the combine two steps back
-    for j in range(N_OUT):
-        d["status%d" % j] = ctx.dev_alloc(4 * total)
-        d["out%d" % j] = ctx.dev_alloc(96 * n_inst)
-        d["par%d" % j] = ctx.dev_alloc(n_inst)
-        d["cst%d" % j] = ctx.dev_alloc(4 * n_inst)
-    log("%s: setup %.1fs (%d shares)" % (name, time.time() - t0, total))
-    lib, h, off = ctx.lib, ctx.h, N._ptr(offsets)
-    cur = [0]
+    return {"pk": pk, "H": H, "sigs": sigs, "expected": expected, "master": master, "hs": hs,
+            "offsets": np.arange(0, total + 1, n, dtype=np.uint32),
+            "idx": np.tile(np.arange(n, dtype=np.uint32), n_inst), "t": (n - 1) // 3 + 1}
 
-    def step():
-        cur[0] = (cur[0] + 1) % N_OUT
-        j = cur[0]
-        ctx._check(lib.hbtc_verify_sig_shares_dev(h, ks, n_inst, d["H"], off, d["idx"], d["sigs"],
+
+class CoinRunner:
+    """The coin epoch on ONE context: every instance's shares verified, then the combines of the
+    first t verified shares (hbtc_verify_sig_shares_dev + hbtc_combine_sigs_verified_dev)."""
+
+    def __init__(self, ctx, inp, n_inst):
+        self.ctx, self.n_inst, self.t = ctx, n_inst, inp["t"]
+        self.offsets = inp["offsets"]
+        self.total = int(self.offsets[-1])
+        self.ks, bad = ctx.keyset_load(inp["pk"])
+        assert bad == 0
+        self.d = {}
+        for k in ("H", "idx", "sigs"):
+            arr = inp[k]
+            self.d[k] = ctx.dev_alloc(arr.nbytes)
+            ctx.dev_upload(self.d[k], arr)
+        # N_OUT output sets rotated per step, as bench.py: the library keeps up to four calls in
+        # flight (its lanes, each verification followed by its combine), so step k writes the set
+        # whose combine (step k - N_OUT) has long finished
+        for j in range(N_OUT):
+            self.d["status%d" % j] = ctx.dev_alloc(4 * self.total)
+            self.d["out%d" % j] = ctx.dev_alloc(96 * n_inst)
+            self.d["par%d" % j] = ctx.dev_alloc(n_inst)
+            self.d["cst%d" % j] = ctx.dev_alloc(4 * n_inst)
+        self.cur = 0
+
+    def step(self):
+        ctx, d, lib, h = self.ctx, self.d, self.ctx.lib, self.ctx.h
+        self.cur = (self.cur + 1) % N_OUT
+        j = self.cur
+        off = N._ptr(self.offsets)
+        ctx._check(lib.hbtc_verify_sig_shares_dev(h, self.ks, self.n_inst, d["H"], off, d["idx"], d["sigs"],
                                                   d["status%d" % j]), "verify_sig_shares_dev")
-        ctx._check(lib.hbtc_combine_sigs_verified_dev(h, n_inst, off, d["idx"], d["sigs"],
-                                                      d["status%d" % j], t, d["out%d" % j],
+        ctx._check(lib.hbtc_combine_sigs_verified_dev(h, self.n_inst, off, d["idx"], d["sigs"],
+                                                      d["status%d" % j], self.t, d["out%d" % j],
                                                       d["par%d" % j], d["cst%d" % j]),
                    "combine_sigs_verified_dev")
 
-    elapsed = timed_steps(ctx, step, steps, warmup)
-    per = breakdown(ctx, steps, COIN_FAMS)
-    j = cur[0]
-    stv = np.empty(total, np.int32)
-    ctx.dev_download(stv, d["status%d" % j])
-    out = np.empty(96 * n_inst, np.uint8)
-    ctx.dev_download(out, d["out%d" % j])
-    cst = np.empty(n_inst, np.int32)
-    ctx.dev_download(cst, d["cst%d" % j])
-    want, _ = ctx.g2_mul(G2_GEN, fr_bytes([master * hh % R for hh in hs]))
-    mism = int((stv != expected).sum())
+    def sync(self):
+        self.ctx.sync()
+
+    def results(self):
+        j, d, ctx = self.cur, self.d, self.ctx
+        st = np.empty(self.total, np.int32)
+        out = np.empty(96 * self.n_inst, np.uint8)
+        par = np.empty(self.n_inst, np.uint8)
+        cst = np.empty(self.n_inst, np.int32)
+        for arr, name in ((st, "status"), (out, "out"), (par, "par"), (cst, "cst")):
+            ctx.dev_download(arr, d["%s%d" % (name, j)])
+        return st, out, par, cst
+
+    def free(self):
+        for p in self.d.values():
+            self.ctx.dev_free(p)
+        self.ctx.keyset_free(self.ks)
+
+
+class NodeCoinRunner:
+    """The same coin epoch on a multi-device node in ONE process (hbtc_node_*): device slot d
+    holds whole instances [first[d], first[d+1]) (hbtc_shard_instances, balanced by share
+    count) resident in its HBM; each step enqueues every slot's verification and then every
+    slot's combine of its own instances (hbtc_node_verify_sig_shares_dev /
+    hbtc_node_combine_sigs_verified_dev: one host thread per device for the enqueue, no
+    synchronisation).  Instances never cross devices, so there is no exchange: each device's
+    verdicts and combined signatures are final where they are computed."""
+
+    def __init__(self, node, inp, n_inst):
+        from hbbft_amd import shard
+        self.node, self.n_inst, self.t = node, n_inst, inp["t"]
+        n_dev = len(node.devices)
+        if n_inst < n_dev:
+            raise SystemExit("node coin bench: %d instances cannot be split over %d devices as whole "
+                             "instances" % (n_inst, n_dev))
+        off = inp["offsets"]
+        self.total = int(off[-1])
+        self.first = [int(x) for x in shard.instance_plan(n_dev, off)]
+        self.ks, bad = node.keyset_load(inp["pk"])
+        assert bad == 0
+        self.ctxs = [node.context(d) for d in range(n_dev)]
+        self.slots = []
+        for d, c in enumerate(self.ctxs):
+            a, b = self.first[d], self.first[d + 1]
+            lo, hi = int(off[a]), int(off[b])
+            sl = {"a": a, "b": b, "lo": lo, "hi": hi, "offsets": (off[a:b + 1] - off[a]).astype(np.uint32),
+                  "mem": {}}
+            for name, arr in (("H", inp["H"].reshape(-1, 96)[a:b]), ("idx", inp["idx"][lo:hi]),
+                              ("sigs", inp["sigs"].reshape(-1, 96)[lo:hi])):
+                arr = np.ascontiguousarray(arr).reshape(-1)
+                p = c.dev_alloc(max(arr.nbytes, 16))
+                if arr.nbytes:
+                    c.dev_upload(p, arr)
+                sl["mem"][name] = p
+            for j in range(N_OUT):
+                for name, nb in (("status", 4 * (hi - lo)), ("out", 96 * (b - a)), ("par", b - a),
+                                 ("cst", 4 * (b - a))):
+                    sl["mem"]["%s%d" % (name, j)] = c.dev_alloc(max(nb, 16))
+            self.slots.append(sl)
+        self.parts = []
+        for j in range(N_OUT):
+            specs = []
+            for sl in self.slots:
+                m = sl["mem"]
+                specs.append({"offsets": sl["offsets"], "d_H_c96": m["H"], "d_idx": m["idx"],
+                              "d_items": m["sigs"], "d_status": m["status%d" % j], "d_out": m["out%d" % j],
+                              "d_out_parity": m["par%d" % j], "d_inst_status": m["cst%d" % j]})
+            self.parts.append(node.parts(specs))
+        self.cur = 0
+
+    def step(self):
+        self.cur = (self.cur + 1) % N_OUT
+        parts, _ = self.parts[self.cur]
+        self.node.verify_sig_shares_dev(self.ks, parts)
+        self.node.combine_sigs_verified_dev(parts, self.t)
+
+    def sync(self):
+        self.node.sync()
+
+    def results(self):
+        j = self.cur
+        st = np.empty(self.total, np.int32)
+        out = np.empty(96 * self.n_inst, np.uint8)
+        par = np.empty(self.n_inst, np.uint8)
+        cst = np.empty(self.n_inst, np.int32)
+        for c, sl in zip(self.ctxs, self.slots):
+            a, b, lo, hi, m = sl["a"], sl["b"], sl["lo"], sl["hi"], sl["mem"]
+            if b == a:
+                continue
+            for arr, name, x, y, w in ((st, "status", lo, hi, 1), (out, "out", 96 * a, 96 * b, 1),
+                                       (par, "par", a, b, 1), (cst, "cst", a, b, 1)):
+                tmp = np.empty(y - x, arr.dtype)
+                c.dev_download(tmp, m["%s%d" % (name, j)])
+                arr[x:y] = tmp
+        return st, out, par, cst
+
+    def free(self):
+        for c, sl in zip(self.ctxs, self.slots):
+            for p in sl["mem"].values():
+                c.dev_free(p)
+        self.node.keyset_free(self.ks)
+
+
+def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode="uniform", node=None,
+                keep_arrays=False):
+    """c2 / c4: n_inst coin instances x n SignatureShares + n_inst combines (first t verified).
+    node: a hbtc Node (one process, several device slots) instead of the single context."""
+    t0 = time.time()
+    inp = coin_inputs(ctx, n, n_inst, corrupt, corrupt_mode)
+    t, total = inp["t"], n * n_inst
+    run = NodeCoinRunner(node, inp, n_inst) if node is not None else CoinRunner(ctx, inp, n_inst)
+    log("%s: setup %.1fs (%d shares%s)" % (name, time.time() - t0, total,
+                                           ", node of %d slots" % len(node.devices) if node else ""))
+    tctx = run.ctxs[0] if node is not None else ctx
+    tctx.timing_enable(True)
+    for _ in range(warmup):
+        run.step()
+    run.sync()
+    tctx.timing_reset()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        run.step()
+    run.sync()
+    elapsed = time.perf_counter() - t1
+    per = breakdown(tctx, steps, COIN_FAMS)
+    stv, out, par, cst = run.results()
+    want, _ = ctx.g2_mul(G2_GEN, fr_bytes([inp["master"] * hh % R for hh in inp["hs"]]))
+    mism = int((stv != inp["expected"]).sum())
     comb_ok = bool((cst == 0).all() and bytes(out) == bytes(want))
     if mism or not comb_ok:
         raise SystemExit("%s: results differ from the construction (%d mismatches, combine %s)"
                          % (name, mism, comb_ok))
-    for p in d.values():
-        ctx.dev_free(p)
-    ctx.keyset_free(ks)
-    return {
+    run.free()
+    n_gpus = len(set(node.devices)) if node is not None else 1
+    if node is not None:
+        par_s = ("node: one process, %d device slot(s) on %d GPU(s) (hbtc_node_*_dev), whole instances per "
+                 "slot (hbtc_shard_instances), each slot verifies and combines its own instances; no "
+                 "collective (disjoint outputs)" % (len(node.devices), n_gpus))
+    else:
+        par_s = "1 GPU"
+    res = {
         "metric": "verified BLS12-381 SignatureShares/sec; combines/sec",
-        "value": round(total * steps / elapsed, 1), "unit": "shares/s", "n_gpus": 1,
+        "value": round(total * steps / elapsed, 1), "unit": "shares/s", "n_gpus": n_gpus,
         "steps": steps, "warmup": warmup, "ms_per_step": round(elapsed / steps * 1e3, 3),
-        "higher_is_better": True, "dtype": "u32 (381-bit Montgomery limbs)",
+        "higher_is_better": True, "scaling": "strong", "dtype": "u32 (381-bit Montgomery limbs)",
         "data": "synthetic (seeded key set, shares generated on device; %s)"
                 % ("%g%% wrong shares" % (100 * corrupt) if corrupt_mode == "uniform"
                    else "f = %d Byzantine senders sign wrongly in every instance" % ((n - 1) // 3)),
         "mode": "rlc" if ctx_mode[0] == N.MODE_RLC else "per_share",
         "config": {"workload": "%s: %d coin instances x %d SignatureShares verified + %d G2 combines (t=%d)"
-                   % (name, n_inst, n, n_inst, t), "N": n, "t": t, "instances": n_inst},
+                   % (name, n_inst, n, n_inst, t), "N": n, "t": t, "instances": n_inst,
+                   "parallelism": par_s},
         "combines_per_s": round(n_inst * steps / elapsed, 2),
         "kernel_ms_per_step": per, "mismatches": mism, "combine_ok": comb_ok,
     }
+    if node is not None:
+        res["kernel_ms_per_step_note"] = "event spans of device slot 0 only"
+    if keep_arrays:
+        res["_arrays"] = (stv, out, par, cst)
+    return res
 
 
 def bench_skg(ctx, n, n_parts, n_distinct, steps, warmup):
@@ -451,7 +592,13 @@ def main():
                     help="timed steps (default per config: c2 20, c4 6, c5 1, bc 20 -- enough "
                          "for the pipelined calls to reach steady state)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 2; c5 1)")
-    ap.add_argument("--inst", type=int, default=64, help="c4 coin instances on this GPU")
+    ap.add_argument("--inst", type=int, default=64, help="c4 coin instances (of the whole node)")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="c2 / c4: devices of a one-process node (hbtc_node_*_dev, whole instances per "
+                         "GPU); 1 = a single context")
+    ap.add_argument("--slots", default=None,
+                    help="c2 / c4: explicit device slots of the node, e.g. 0,0 (two contexts on GPU 0: "
+                         "a rehearsal of the node path on one GPU)")
     ap.add_argument("--parts", type=int, default=1000, help="c5 Parts")
     ap.add_argument("--distinct", type=int, default=4, help="c5 distinct bivariate polynomials")
     ap.add_argument("--bc-value", type=int, default=65536, help="bc: bytes per proposed value")
@@ -462,16 +609,21 @@ def main():
     ctx = N.Context(0)
     ctx_mode[0] = N.MODE_RLC if args.mode == "rlc" else N.MODE_PER_SHARE
     ctx.set_verify_mode(ctx_mode[0])
+    node = None
+    slots = [int(x) for x in args.slots.split(",")] if args.slots else list(range(args.gpus))
+    if len(slots) > 1:
+        node = N.Node(slots)
+        node.set_verify_mode(ctx_mode[0])
     try:
         for c in args.configs.split(","):
             steps = args.steps if args.steps is not None else STEPS_DEFAULT.get(c, 2)
             warmup = args.warmup if args.warmup is not None else (1 if c == "c5" else 2)
             if c == "c2":
                 out = bench_coins(ctx, "c2", 100, 100, steps, warmup, args.corrupt,
-                                  args.corrupt_mode)
+                                  args.corrupt_mode, node=node)
             elif c == "c4":
                 out = bench_coins(ctx, "c4", 10000, args.inst, steps, warmup, args.corrupt,
-                                  args.corrupt_mode)
+                                  args.corrupt_mode, node=node)
             elif c == "bc":
                 out = bench_broadcast(ctx, 256, args.bc_value, steps, warmup)
             elif c == "c5":
@@ -480,6 +632,8 @@ def main():
                 raise SystemExit("unknown config " + c)
             print(json.dumps(out), flush=True)
     finally:
+        if node is not None:
+            node.close()
         ctx.close()
 
 

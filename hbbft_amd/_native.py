@@ -120,7 +120,24 @@ SIGNATURES = {
     "hbtc_node_verify_sig_shares": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P]),
     "hbtc_node_combine_dec": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P]),
     "hbtc_node_combine_sigs": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P, _P]),
+    "hbtc_dec_epoch_submit": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P, _U32, _P, _P, _P,
+                                     ctypes.POINTER(ctypes.c_uint64)]),
+    "hbtc_sig_epoch_submit": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _U32, _P, _P, _P, _P,
+                                     ctypes.POINTER(ctypes.c_uint64)]),
+    "hbtc_wait": (_I32, [_P, ctypes.c_uint64]),
+    "hbtc_node_verify_sig_shares_dev": (_I32, [_P, _U32, _P]),
+    "hbtc_node_verify_dec_shares_dev": (_I32, [_P, _U32, _P]),
+    "hbtc_node_combine_sigs_verified_dev": (_I32, [_P, _P, _U32]),
+    "hbtc_node_combine_dec_verified_dev": (_I32, [_P, _P, _U32]),
+    "hbtc_node_sync": (_I32, [_P]),
 }
+
+
+class NodePart(ctypes.Structure):
+    """include/hbtc.h hbtc_node_part: one device's part of a device-resident node batch."""
+    _fields_ = [("n_inst", _U32), ("offsets", _P), ("d_H_c96", _P), ("d_w_c96", _P),
+                ("d_idx", _P), ("d_items", _P), ("d_status", _P), ("d_out", _P),
+                ("d_out_parity", _P), ("d_inst_status", _P)]
 
 _lib = None
 
@@ -269,6 +286,16 @@ def _offsets(counts_or_offsets, is_offsets):
 class Context:
     """One hbtc context (one GPU).  Methods take host data (bytes / numpy) and return numpy."""
 
+    @classmethod
+    def borrowed(cls, handle, device):
+        """A non-owning view of a context created elsewhere (a node's device slot)."""
+        c = cls.__new__(cls)
+        c.lib = load()
+        c.h = ctypes.c_void_p(handle)
+        c.device = device
+        c._borrowed = True
+        return c
+
     def __init__(self, device=0):
         self.lib = load()
         h = ctypes.c_void_p()
@@ -280,7 +307,8 @@ class Context:
 
     def close(self):
         if getattr(self, "h", None):
-            self.lib.hbtc_ctx_destroy(self.h)
+            if not getattr(self, "_borrowed", False):
+                self.lib.hbtc_ctx_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -348,6 +376,49 @@ class Context:
                                                     _ptr(off), _ptr(ix), _ptr(sb), _ptr(st)),
                     "hbtc_verify_dec_shares")
         return st
+
+    # ---- pipelined host-buffer epochs (hbtc_*_epoch_submit / hbtc_wait)
+    class Pending:
+        """A submitted epoch: its output arrays (filled by wait()) and the inputs kept alive."""
+
+        def __init__(self, ctx, ticket, outs, keep):
+            self.ctx, self.ticket, self.outs, self._keep = ctx, ticket, outs, keep
+
+        def wait(self):
+            self.ctx._check(self.ctx.lib.hbtc_wait(self.ctx.h, self.ticket), "hbtc_wait")
+            return self.outs
+
+    def dec_epoch_submit(self, keyset, H, w, offsets, idx, shares, t, outs=None):
+        """Submit one epoch of DecryptionShares (verification + combine of the first t verified
+        shares per ciphertext, t = 0: verification only); returns a Pending whose wait() gives
+        (status, g [n_ct, 48], combine status).  `outs` reuses output arrays."""
+        off = np.ascontiguousarray(offsets, dtype=np.uint32)
+        n_ct, n = off.size - 1, int(off[-1])
+        Hb, wb, sb = _join(H, 96), _join(w, 96), _join(shares, 48)
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        if outs is None:
+            outs = (np.empty(max(n, 1), np.int32), np.empty((max(n_ct, 1), 48), np.uint8),
+                    np.empty(max(n_ct, 1), np.int32))
+        tk = ctypes.c_uint64()
+        self._check(self.lib.hbtc_dec_epoch_submit(self.h, keyset, n_ct, _ptr(Hb), _ptr(wb), _ptr(off), _ptr(ix),
+                                                   _ptr(sb), t, _ptr(outs[0]), _ptr(outs[1]), _ptr(outs[2]),
+                                                   ctypes.byref(tk)), "hbtc_dec_epoch_submit")
+        return Context.Pending(self, tk.value, outs, (off,))
+
+    def sig_epoch_submit(self, keyset, H, offsets, idx, sigs, t, outs=None):
+        """The SignatureShare epoch (coins): wait() gives (status, sig [n, 96], parity, combine status)."""
+        off = np.ascontiguousarray(offsets, dtype=np.uint32)
+        n_inst, n = off.size - 1, int(off[-1])
+        Hb, sb = _join(H, 96), _join(sigs, 96)
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        if outs is None:
+            outs = (np.empty(max(n, 1), np.int32), np.empty((max(n_inst, 1), 96), np.uint8),
+                    np.empty(max(n_inst, 1), np.uint8), np.empty(max(n_inst, 1), np.int32))
+        tk = ctypes.c_uint64()
+        self._check(self.lib.hbtc_sig_epoch_submit(self.h, keyset, n_inst, _ptr(Hb), _ptr(off), _ptr(ix), _ptr(sb),
+                                                   t, _ptr(outs[0]), _ptr(outs[1]), _ptr(outs[2]),
+                                                   _ptr(outs[3]), ctypes.byref(tk)), "hbtc_sig_epoch_submit")
+        return Context.Pending(self, tk.value, outs, (off,))
 
     def verify_sigs(self, pks, H, sigs):
         pk, Hb, sb = _join(pks, 48), _join(H, 96), _join(sigs, 96)
@@ -700,3 +771,49 @@ class Node:
         self._check(self.lib.hbtc_node_combine_sigs(self.h, n, _ptr(off), _ptr(ix), _ptr(sg), t, _ptr(out),
                                                     _ptr(par), _ptr(st)), "hbtc_node_combine_sigs")
         return [bytes(out[96 * k:96 * k + 96]) for k in range(n)], par[:n], st[:n]
+
+    # ---- device-resident parts (one per device slot; include/hbtc.h hbtc_node_part)
+    def context(self, slot):
+        """Device slot `slot`'s context (owned by the node) for allocation and copies."""
+        h = self.lib.hbtc_node_context(self.h, int(slot))
+        if not h:
+            raise HbtcError("hbtc_node_context(%d): no such slot" % slot)
+        return Context.borrowed(h, self.devices[slot])
+
+    @staticmethod
+    def parts(specs):
+        """specs: per slot a dict of NodePart fields (device pointers as ints / c_void_p, the
+        host `offsets` as a uint32 array, kept alive by the returned tuple)."""
+        arr = (NodePart * len(specs))()
+        keep = []
+        for i, sp in enumerate(specs):
+            off = sp.get("offsets")
+            if off is not None:
+                off = np.ascontiguousarray(off, dtype=np.uint32)
+                keep.append(off)
+                arr[i].offsets = off.ctypes.data
+                arr[i].n_inst = off.size - 1
+            for k, v in sp.items():
+                if k in ("offsets", "n_inst"):
+                    continue
+                setattr(arr[i], k, v.value if isinstance(v, ctypes.c_void_p) else v)
+        return arr, keep
+
+    def verify_sig_shares_dev(self, keyset, parts):
+        self._check(self.lib.hbtc_node_verify_sig_shares_dev(self.h, keyset, parts),
+                    "hbtc_node_verify_sig_shares_dev")
+
+    def verify_dec_shares_dev(self, keyset, parts):
+        self._check(self.lib.hbtc_node_verify_dec_shares_dev(self.h, keyset, parts),
+                    "hbtc_node_verify_dec_shares_dev")
+
+    def combine_sigs_verified_dev(self, parts, t):
+        self._check(self.lib.hbtc_node_combine_sigs_verified_dev(self.h, parts, t),
+                    "hbtc_node_combine_sigs_verified_dev")
+
+    def combine_dec_verified_dev(self, parts, t):
+        self._check(self.lib.hbtc_node_combine_dec_verified_dev(self.h, parts, t),
+                    "hbtc_node_combine_dec_verified_dev")
+
+    def sync(self):
+        self._check(self.lib.hbtc_node_sync(self.h), "hbtc_node_sync")

@@ -106,7 +106,15 @@ def validate_proofs(ctx, proofs, num_nodes, expected_index=None):
     with expected_index, the sender's node index == proof.index.  Returns a bool array."""
     if not proofs:
         return np.zeros(0, bool)
-    st = ctx.merkle_validate(num_nodes, [p.value for p in proofs], [p.index for p in proofs],
+    if not 0 < num_nodes < 1 << 31:
+        raise ValueError("validate_proofs: num_nodes out of range")
+    # The wire index is a usize (u64).  The device walk takes a u32: an index of 2^32 or more
+    # walks exactly like 2^32 - 1 (index ^ 1 >= the level size on every level while the node
+    # count is below 2^31, so no digest is consumed), so one Byzantine Echo with a huge index
+    # gets its own verdict (valid iff it has no digests and its leaf hash is the root, as in the
+    # reference) instead of failing the whole batch.
+    ix = [p.index if 0 <= p.index < 1 << 32 else (1 << 32) - 1 for p in proofs]
+    st = ctx.merkle_validate(num_nodes, [p.value for p in proofs], ix,
                              [p.digests for p in proofs], [p.root_hash for p in proofs])
     ok = st == N.ACCEPT
     if expected_index is not None:
@@ -122,9 +130,41 @@ def glue_shards(values, k):
     return data[4:4 + struct.unpack(">I", data[:4])[0]]
 
 
+# SHA3-256 of the empty string (FIPS 202): the digest of an empty leaf
+_SHA3_EMPTY = bytes.fromhex("a7ffc6f8bf1ed76651c14756a061d662f580ff4de43b49fa82d80a4b80f8434a")
+
+
+def _sha3_many(ctx, blobs):
+    """SHA3-256 of each byte string on the GPU, one hbtc_merkle_trees call per distinct length
+    (the root of a one-leaf tree is that leaf's digest)."""
+    out, by_len = [None] * len(blobs), {}
+    for i, b in enumerate(blobs):
+        by_len.setdefault(len(b), []).append(i)
+    for ln, ids in by_len.items():
+        if ln == 0:
+            for i in ids:
+                out[i] = _SHA3_EMPTY
+            continue
+        dig = ctx.merkle_trees(1, ln, np.frombuffer(b"".join(blobs[i] for i in ids), np.uint8).copy())
+        for r, i in enumerate(ids):
+            out[i] = bytes(dig[r, -1])
+    return out
+
+
+def _ragged_root(ctx, leaves):
+    """MerkleTree::from_vec(leaves).root_hash() for leaves of any lengths (merkle.rs:19-32: the
+    odd digest of a level is carried up unhashed)."""
+    cur = _sha3_many(ctx, leaves)
+    while len(cur) > 1:
+        h = _sha3_many(ctx, [cur[i] + cur[i + 1] for i in range(0, len(cur) - 1, 2)])
+        cur = [h[j // 2] if j + 1 < len(cur) else cur[j] for j in range(0, len(cur), 2)]
+    return cur[0]
+
+
 def decode_batch(ctx, leaf_values_per_inst, root_hashes, num_faulty):
     """decode_from_shards (broadcast.rs:461-493) for several instances of one network (every
-    leaf list has N entries, bytes or None; an instance's present shards share one length).
+    leaf list has N entries, bytes or None).  Reed-Solomon instances need one shard length
+    (IncorrectShardSize otherwise); the trivial coding (no parity shards) takes any lengths.
     Returns the decoded value or None per instance, as the reference."""
     out = [None] * len(leaf_values_per_inst)
     if not leaf_values_per_inst:
@@ -135,6 +175,13 @@ def decode_batch(ctx, leaf_values_per_inst, root_hashes, num_faulty):
     by_len = {}
     for i, lv in enumerate(leaf_values_per_inst):
         lens = {len(v) for v in lv if v is not None}
+        if p == 0 and all(v is not None for v in lv) and (len(lens) != 1 or 0 in lens):
+            # Coding::Trivial checks presence only (broadcast.rs:449-455): the tree is built over
+            # the leaves as they are, whatever their lengths
+            leaves = [bytes(v) for v in lv]
+            if _ragged_root(ctx, leaves) == bytes(root_hashes[i]):
+                out[i] = glue_shards(leaves, k)
+            continue
         if len(lens) != 1 or 0 in lens:  # IncorrectShardSize / nothing present / empty shards
             continue
         by_len.setdefault(lens.pop(), []).append(i)

@@ -148,6 +148,25 @@ struct hbtc_ctx {
     uint32_t n_out = 0, n_in = 0;
   };
   std::map<std::string, GfPlan> gf_plans;
+  // Asynchronous host-buffer epochs (hbtc_*_epoch_submit / hbtc_wait): at most one ticket per
+  // lane in flight, its inputs and outputs in pinned staging owned by that lane.
+  struct Ticket {
+    uint64_t id = 0;
+    bool active = false;
+    hipEvent_t ev = nullptr;
+    void* h_in = nullptr;
+    size_t in_cap = 0;
+    void* h_out = nullptr;
+    size_t out_cap = 0;
+    int32_t* status = nullptr;
+    uint8_t* out = nullptr;
+    uint8_t* parity = nullptr;
+    int32_t* inst_status = nullptr;
+    size_t n_items = 0, n_inst = 0, pt = 0;
+    bool combined = false;
+  };
+  Ticket tickets[NL];
+  uint64_t next_ticket = 1;
   std::random_device rd;
   bool timing = false;
   std::vector<Span> spans;
@@ -985,6 +1004,118 @@ int point_mul_host(hbtc_ctx* c, int group, uint32_t n, const uint8_t* base,
   return sync(c);
 }
 
+// ---------------------------------------------------------------- asynchronous host epochs
+size_t round256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int pinned_grow(hbtc_ctx* c, void** h, size_t* cap, size_t bytes) {
+  if (*cap >= bytes && *h) return HBTC_OK;
+  if (*h) HB_CHECK(c, hipHostFree(*h));
+  *h = nullptr;
+  *cap = 0;
+  const size_t want = bytes + bytes / 4 + 256;
+  HB_CHECK(c, hipHostMalloc(h, want, hipHostMallocDefault));
+  *cap = want;
+  return HBTC_OK;
+}
+
+// The ticket's results are on the host: copy them out of the pinned staging into the caller's
+// buffers.
+int finish_ticket(hbtc_ctx* c, hbtc_ctx::Ticket& T) {
+  if (!T.active) return HBTC_OK;
+  HB_CHECK(c, hipEventSynchronize(T.ev));
+  const uint8_t* o = static_cast<const uint8_t*>(T.h_out);
+  size_t off = 0;
+  memcpy(T.status, o, 4 * T.n_items);
+  off = round256(4 * T.n_items);
+  if (T.combined) {
+    memcpy(T.out, o + off, T.pt * T.n_inst);
+    off += round256(T.pt * T.n_inst);
+    if (T.parity) memcpy(T.parity, o + off, T.n_inst);
+    off += round256(T.n_inst);
+    memcpy(T.inst_status, o + off, 4 * T.n_inst);
+  }
+  T.active = false;
+  return HBTC_OK;
+}
+
+// One epoch from host buffers without blocking: inputs into the next lane's pinned staging,
+// H2D, verification, the combine of the first t verified shares of every instance (t > 0) and
+// D2H of the results, all on that lane's stream (group 1: DecryptionShares, 2: SignatureShares).
+int epoch_submit(hbtc_ctx* c, int group, uint32_t keyset_id, uint32_t n_inst, const uint8_t* H,
+                 const uint8_t* w, const uint32_t* offsets, const uint32_t* idx, const uint8_t* items,
+                 uint32_t t, int32_t* status, uint8_t* out, uint8_t* parity, int32_t* inst_status,
+                 uint64_t* ticket) {
+  uint32_t n;
+  HB_TRY(check_offsets(c, n_inst, offsets, &n));
+  const size_t pt = group == 1 ? 48 : 96;
+  const int l = (c->lane + 1) % hbtc_ctx::NL;
+  hbtc_ctx::Ticket& T = c->tickets[l];
+  HB_TRY(finish_ticket(c, T));  // the lane's previous epoch (its staging is reused)
+  if (!T.ev) HB_CHECK(c, hipEventCreateWithFlags(&T.ev, hipEventDisableTiming));
+  select_lane(c, l);
+  const size_t sH = 96 * (size_t)n_inst, sW = group == 1 ? sH : 0, sI = 4 * (size_t)n, sP = pt * n;
+  const size_t oW = round256(sH), oI = oW + round256(sW), oP = oI + round256(sI);
+  HB_TRY(pinned_grow(c, &T.h_in, &T.in_cap, oP + sP));
+  uint8_t* hi = static_cast<uint8_t*>(T.h_in);
+  if (sH) memcpy(hi, H, sH);
+  if (sW) memcpy(hi + oW, w, sW);
+  if (sI) memcpy(hi + oI, idx, sI);
+  if (sP) memcpy(hi + oP, items, sP);
+  void *d_H, *d_w = nullptr, *d_idx, *d_items, *d_st, *d_out = nullptr, *d_par = nullptr, *d_cst = nullptr;
+  HB_TRY(ws(c, "ep.H", sH, &d_H));
+  if (sW) HB_TRY(ws(c, "ep.w", sW, &d_w));
+  HB_TRY(ws(c, "ep.idx", sI, &d_idx));
+  HB_TRY(ws(c, "ep.items", sP, &d_items));
+  HB_TRY(ws(c, "ep.status", 4 * (size_t)n, &d_st));
+  HB_TRY(guard_write(c, d_H, sH));
+  HB_TRY(guard_write(c, d_idx, sI));
+  HB_TRY(guard_write(c, d_items, sP));
+  if (sH) HB_CHECK(c, hipMemcpyAsync(d_H, hi, sH, hipMemcpyHostToDevice, c->stream));
+  if (sW) HB_CHECK(c, hipMemcpyAsync(d_w, hi + oW, sW, hipMemcpyHostToDevice, c->stream));
+  if (sI) HB_CHECK(c, hipMemcpyAsync(d_idx, hi + oI, sI, hipMemcpyHostToDevice, c->stream));
+  if (sP) HB_CHECK(c, hipMemcpyAsync(d_items, hi + oP, sP, hipMemcpyHostToDevice, c->stream));
+  const bool comb = t > 0 && n_inst > 0;
+  {
+    PinLane pin(c);  // the uploads above went to lane l: verification and combine stay there
+    if (group == 1)
+      HB_TRY(dec_shares_dev(c, keyset_id, n_inst, (const uint8_t*)d_H, (const uint8_t*)d_w, offsets,
+                            (const uint32_t*)d_idx, (const uint8_t*)d_items, (int32_t*)d_st));
+    else
+      HB_TRY(sig_shares_dev(c, keyset_id, n_inst, (const uint8_t*)d_H, offsets, (const uint32_t*)d_idx,
+                            (const uint8_t*)d_items, (int32_t*)d_st));
+    if (comb) {
+      HB_TRY(ws(c, "ep.out", pt * n_inst, &d_out));
+      if (group == 2) HB_TRY(ws(c, "ep.par", n_inst, &d_par));
+      HB_TRY(ws(c, "ep.cst", 4 * (size_t)n_inst, &d_cst));
+      HB_TRY(combine_dev(c, group, n_inst, offsets, (const uint32_t*)d_idx, (const uint8_t*)d_items, t,
+                         (uint8_t*)d_out, (uint8_t*)d_par, (int32_t*)d_cst, (const int32_t*)d_st));
+      HB_TRY(stream_after(c, c->stream, c->s_comb, c->ev_comb));
+    }
+  }
+  const size_t q1 = round256(4 * (size_t)n), q2 = q1 + round256(pt * n_inst), q3 = q2 + round256(n_inst);
+  HB_TRY(pinned_grow(c, &T.h_out, &T.out_cap, q3 + 4 * (size_t)n_inst + 16));
+  uint8_t* ho = static_cast<uint8_t*>(T.h_out);
+  if (n) HB_CHECK(c, hipMemcpyAsync(ho, d_st, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  if (comb) {
+    HB_CHECK(c, hipMemcpyAsync(ho + q1, d_out, pt * n_inst, hipMemcpyDeviceToHost, c->stream));
+    if (d_par) HB_CHECK(c, hipMemcpyAsync(ho + q2, d_par, n_inst, hipMemcpyDeviceToHost, c->stream));
+    HB_CHECK(c, hipMemcpyAsync(ho + q3, d_cst, 4 * (size_t)n_inst, hipMemcpyDeviceToHost, c->stream));
+  }
+  HB_CHECK(c, hipEventRecord(T.ev, c->stream));
+  T.status = status;
+  T.out = out;
+  T.parity = group == 2 ? parity : nullptr;
+  T.inst_status = inst_status;
+  T.n_items = n;
+  T.n_inst = n_inst;
+  T.pt = pt;
+  T.combined = comb;
+  T.active = true;
+  T.id = c->next_ticket++;
+  *ticket = T.id;
+  return HBTC_OK;
+}
+
 struct Guard {
   hbtc_ctx* c;
   std::lock_guard<std::mutex> lk;
@@ -1080,6 +1211,12 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
     (void)hipFree(kv.second.out_rows);
     (void)hipFree(kv.second.in_rows);
     (void)hipFree(kv.second.tabs);
+  }
+  for (auto& tk : c->tickets) {
+    if (tk.active && tk.ev) (void)hipEventSynchronize(tk.ev);
+    if (tk.ev) (void)hipEventDestroy(tk.ev);
+    if (tk.h_in) (void)hipHostFree(tk.h_in);
+    if (tk.h_out) (void)hipHostFree(tk.h_out);
   }
   for (auto& kv : c->stages) {
     if (kv.second.h) (void)hipHostFree(kv.second.h);
@@ -1361,6 +1498,43 @@ int hbtc_unframe_points_dev(hbtc_ctx* c, uint32_t n, uint32_t point_size, const 
   HB_TRY(lane_async(c, {rng(d_framed, (size_t)n * (point_size + 8))}, {rng(d_items, (size_t)n * point_size)}));
   HB_TRY(timed(c, "unframe", [&] { return launch_unframe(c->stream, n, point_size, d_framed, d_items); }));
   return end_verify(c);
+}
+
+int hbtc_dec_epoch_submit(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t* H_c96,
+                          const uint8_t* w_c96, const uint32_t* offsets, const uint32_t* idx,
+                          const uint8_t* share_c48, uint32_t t, int32_t* status, uint8_t* out_g_c48,
+                          int32_t* inst_status, uint64_t* ticket) {
+  if (!c || !ticket || (n_ct && (!H_c96 || !w_c96 || !offsets))) return HBTC_ERR_ARG;
+  Guard g(c);
+  uint32_t n;
+  HB_TRY(check_offsets(c, n_ct, offsets, &n));
+  if (n && (!idx || !share_c48 || !status)) return fail(c, HBTC_ERR_ARG, "NULL item array");
+  if (t && n_ct && (!out_g_c48 || !inst_status)) return fail(c, HBTC_ERR_ARG, "NULL combine output");
+  return epoch_submit(c, 1, keyset_id, n_ct, H_c96, w_c96, offsets, idx, share_c48, t, status, out_g_c48,
+                      nullptr, inst_status, ticket);
+}
+
+int hbtc_sig_epoch_submit(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8_t* H_c96,
+                          const uint32_t* offsets, const uint32_t* idx, const uint8_t* sig_c96,
+                          uint32_t t, int32_t* status, uint8_t* out_sig_c96, uint8_t* out_parity,
+                          int32_t* inst_status, uint64_t* ticket) {
+  if (!c || !ticket || (n_inst && (!H_c96 || !offsets))) return HBTC_ERR_ARG;
+  Guard g(c);
+  uint32_t n;
+  HB_TRY(check_offsets(c, n_inst, offsets, &n));
+  if (n && (!idx || !sig_c96 || !status)) return fail(c, HBTC_ERR_ARG, "NULL item array");
+  if (t && n_inst && (!out_sig_c96 || !out_parity || !inst_status))
+    return fail(c, HBTC_ERR_ARG, "NULL combine output");
+  return epoch_submit(c, 2, keyset_id, n_inst, H_c96, nullptr, offsets, idx, sig_c96, t, status, out_sig_c96,
+                      out_parity, inst_status, ticket);
+}
+
+int hbtc_wait(hbtc_ctx* c, uint64_t ticket) {
+  if (!c || ticket == 0) return HBTC_ERR_ARG;
+  Guard g(c);
+  for (auto& T : c->tickets)
+    if (T.active && T.id == ticket) return finish_ticket(c, T);
+  return ticket < c->next_ticket ? HBTC_OK : fail(c, HBTC_ERR_ARG, "unknown ticket");
 }
 
 int hbtc_verify_dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct,
@@ -2109,7 +2283,9 @@ int gf_plan(hbtc_ctx* c, const std::string& key, const std::vector<uint32_t>& ou
   auto it = c->gf_plans.find(key);
   if (it == c->gf_plans.end()) {
     if (c->gf_plans.size() >= 256) {  // presence patterns are few per era; bound the cache anyway
-      HB_CHECK(c, hipStreamSynchronize(c->stream));
+      // a gf_apply launched on ANY lane may still read these tables (rs_*_dev calls rotate
+      // lanes): drain every lane before freeing
+      HB_TRY(sync(c));
       for (auto& kv : c->gf_plans) {
         (void)hipFree(kv.second.out_rows);
         (void)hipFree(kv.second.in_rows);

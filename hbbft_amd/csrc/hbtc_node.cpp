@@ -285,3 +285,65 @@ int hbtc_node_combine_sigs(hbtc_node* nd, uint32_t n_inst, const uint32_t* offse
 }
 
 }  // extern "C"
+
+// ---- device-resident parts (asynchronous per device) ---------------------------------------
+namespace {
+template <class F>
+int node_parts(hbtc_node* nd, const hbtc_node_part* parts, F&& call) {
+  if (!nd || !parts) return HBTC_ERR_ARG;
+  for (size_t d = 0; d < nd->ctx.size(); ++d)
+    if (parts[d].n_inst && !offsets_ok(parts[d].n_inst, parts[d].offsets))
+      return node_fail(nd, HBTC_ERR_ARG, "part " + std::to_string(d) + ": bad offsets");
+  return run_devices(nd, [&](size_t d) { return parts[d].n_inst ? call(d, parts[d]) : HBTC_OK; });
+}
+}  // namespace
+
+extern "C" {
+
+int hbtc_node_verify_sig_shares_dev(hbtc_node* nd, uint32_t keyset_id, const hbtc_node_part* parts) {
+  if (!nd) return HBTC_ERR_ARG;
+  std::lock_guard<std::mutex> lk(nd->mu);
+  return node_parts(nd, parts, [&](size_t d, const hbtc_node_part& p) {
+    uint32_t ks;
+    if (keyset_of(nd, keyset_id, d, &ks) != HBTC_OK) return HBTC_ERR_NO_KEYSET;
+    return hbtc_verify_sig_shares_dev(nd->ctx[d], ks, p.n_inst, p.d_H_c96, p.offsets, p.d_idx,
+                                      p.d_items, p.d_status);
+  });
+}
+
+int hbtc_node_verify_dec_shares_dev(hbtc_node* nd, uint32_t keyset_id, const hbtc_node_part* parts) {
+  if (!nd) return HBTC_ERR_ARG;
+  std::lock_guard<std::mutex> lk(nd->mu);
+  return node_parts(nd, parts, [&](size_t d, const hbtc_node_part& p) {
+    uint32_t ks;
+    if (keyset_of(nd, keyset_id, d, &ks) != HBTC_OK) return HBTC_ERR_NO_KEYSET;
+    return hbtc_verify_dec_shares_dev(nd->ctx[d], ks, p.n_inst, p.d_H_c96, p.d_w_c96, p.offsets,
+                                      p.d_idx, p.d_items, p.d_status);
+  });
+}
+
+int hbtc_node_combine_sigs_verified_dev(hbtc_node* nd, const hbtc_node_part* parts, uint32_t t) {
+  if (!nd) return HBTC_ERR_ARG;
+  std::lock_guard<std::mutex> lk(nd->mu);
+  return node_parts(nd, parts, [&](size_t d, const hbtc_node_part& p) {
+    return hbtc_combine_sigs_verified_dev(nd->ctx[d], p.n_inst, p.offsets, p.d_idx, p.d_items,
+                                          p.d_status, t, p.d_out, p.d_out_parity, p.d_inst_status);
+  });
+}
+
+int hbtc_node_combine_dec_verified_dev(hbtc_node* nd, const hbtc_node_part* parts, uint32_t t) {
+  if (!nd) return HBTC_ERR_ARG;
+  std::lock_guard<std::mutex> lk(nd->mu);
+  return node_parts(nd, parts, [&](size_t d, const hbtc_node_part& p) {
+    return hbtc_combine_dec_verified_dev(nd->ctx[d], p.n_inst, p.offsets, p.d_idx, p.d_items,
+                                         p.d_status, t, p.d_out, p.d_inst_status);
+  });
+}
+
+int hbtc_node_sync(hbtc_node* nd) {
+  if (!nd) return HBTC_ERR_ARG;
+  std::lock_guard<std::mutex> lk(nd->mu);
+  return run_devices(nd, [&](size_t d) { return hbtc_sync(nd->ctx[d]); });
+}
+
+}  // extern "C"

@@ -58,11 +58,10 @@ def fr_from_wire(b, pos=0):
 
 
 def fr_value_from_wire(b):
-    """A whole message holding one FieldWrap<Fr> (an Ack value); trailing bytes are refused."""
-    v, end = fr_from_wire(b)
-    if end != len(bytes(b)):
-        raise WireError("trailing bytes")
-    return v
+    """A message holding one FieldWrap<Fr> (an Ack value).  bincode 1.0's `deserialize` stops
+    after the last field and ignores what follows (no trailing-bytes check before bincode 1.3's
+    Options), so bytes appended after the value are ignored here too."""
+    return fr_from_wire(b)[0]
 
 
 def poly_to_wire(coeffs):
@@ -74,7 +73,7 @@ def poly_from_wire(b):
     if len(b) < 8:
         raise WireError("short Poly")
     n = struct.unpack_from("<Q", b)[0]
-    if 8 + 40 * n != len(b):
+    if 8 + 40 * n > len(b):  # short; bytes after the last coefficient are ignored (bincode 1.0)
         raise WireError("bad Poly length")
     out, pos = [], 8
     for _ in range(n):

@@ -166,6 +166,29 @@ int hbtc_hash_g2_batch_gpu(hbtc_ctx* ctx, uint32_t n, const uint8_t* msgs, const
 int hbtc_hash_g1_g2_batch_gpu(hbtc_ctx* ctx, uint32_t n, const uint8_t* g1_c48,
                               const uint8_t* msgs, const uint32_t* offsets, uint8_t* out_c96);
 
+/* ---- pipelined host-buffer epochs ------------------------------------------------------------ */
+/* The batch queue's epoch call without blocking (hbbft keeps the current epoch and up to
+ * max_future_epochs = 3 more in flight, src/honey_badger/builder.rs:37; the batch points are
+ * ThresholdDecryption::remove_invalid_shares, src/threshold_decryption.rs:136-149, and the
+ * epoch's coin / decryption queues).  A submit copies the inputs into pinned staging of the next
+ * verification lane and enqueues, on that lane: H2D, the verification (as hbtc_verify_*_shares),
+ * then, for t > 0, the combine of the FIRST t ACCEPTed items of every instance (as
+ * hbtc_combine_*_verified_dev: the shares hbbft keeps, coin.rs:185-191, td.rs:184), and D2H of
+ * every result; it returns a ticket at once.  hbtc_wait(ticket) blocks until that epoch's results
+ * are in the caller's output buffers, which must stay valid until then (inputs may be reused as
+ * soon as submit returns).  At most four epochs are in flight per context: a fifth submit first
+ * completes the oldest (its outputs written as by hbtc_wait).  Waiting on a completed ticket
+ * returns HBTC_OK. */
+int hbtc_dec_epoch_submit(hbtc_ctx* ctx, uint32_t keyset_id, uint32_t n_ct, const uint8_t* H_c96,
+                          const uint8_t* w_c96, const uint32_t* offsets, const uint32_t* idx,
+                          const uint8_t* share_c48, uint32_t t, int32_t* status, uint8_t* out_g_c48,
+                          int32_t* inst_status, uint64_t* ticket);
+int hbtc_sig_epoch_submit(hbtc_ctx* ctx, uint32_t keyset_id, uint32_t n_inst, const uint8_t* H_c96,
+                          const uint32_t* offsets, const uint32_t* idx, const uint8_t* sig_c96,
+                          uint32_t t, int32_t* status, uint8_t* out_sig_c96, uint8_t* out_parity,
+                          int32_t* inst_status, uint64_t* ticket);
+int hbtc_wait(hbtc_ctx* ctx, uint64_t ticket);
+
 /* ---- batched scalar multiplication -------------------------------------------------------- */
 /* out_i = k_i * P_i with 32-byte little-endian scalars (any value < 2^256).  base_stride is 1
  * for one base per item or 0 for a single shared base.  status[i] = ACCEPT or DECODE_ERR. */
@@ -301,6 +324,34 @@ int hbtc_node_combine_dec(hbtc_node* node, uint32_t n_ct, const uint32_t* offset
 int hbtc_node_combine_sigs(hbtc_node* node, uint32_t n_inst, const uint32_t* offsets,
                            const uint32_t* idx, const uint8_t* sig_c96, uint32_t t,
                            uint8_t* out_sig_c96, uint8_t* out_parity, int32_t* inst_status);
+
+/* Device-resident node calls: the batch is already split over the node's devices, part d living
+ * on device slot d (one hbtc_node_part per slot, in slot order; a part with n_inst == 0 is
+ * skipped).  The shard plans below give the parts: whole instances per device
+ * (hbtc_shard_instances), or item slices whose sub-instances share their parent's H / w
+ * (hbtc_shard_items).  Every device's call is enqueued on its own context from its own host
+ * thread and the call returns without waiting for the GPUs (hbtc_node_sync waits); semantics
+ * and statuses are those of the single-context *_dev calls.  The combines read the statuses the
+ * verification of the SAME parts wrote, so their parts must hold whole instances (a split
+ * instance's sub-instances are gathered onto one device by the caller first). */
+typedef struct {
+  uint32_t n_inst;          /* instances (or sub-instances) of this part                      */
+  const uint32_t* offsets;  /* HOST array, n_inst + 1 entries, offsets[0] == 0                 */
+  const uint8_t* d_H_c96;   /* device: H per instance (verification only)                    */
+  const uint8_t* d_w_c96;   /* device: w per ciphertext (decryption shares only)             */
+  const uint32_t* d_idx;    /* device: node index per item                                    */
+  const uint8_t* d_items;   /* device: compressed items (48 B decryption, 96 B signature)     */
+  int32_t* d_status;        /* device: item statuses (written by verification, read by combine) */
+  uint8_t* d_out;           /* device: combined points (48 / 96 B per instance; combine only)  */
+  uint8_t* d_out_parity;    /* device: Signature::parity per instance (signature combine only) */
+  int32_t* d_inst_status;   /* device: combine status per instance (combine only)              */
+} hbtc_node_part;
+int hbtc_node_verify_sig_shares_dev(hbtc_node* node, uint32_t keyset_id, const hbtc_node_part* parts);
+int hbtc_node_verify_dec_shares_dev(hbtc_node* node, uint32_t keyset_id, const hbtc_node_part* parts);
+int hbtc_node_combine_sigs_verified_dev(hbtc_node* node, const hbtc_node_part* parts, uint32_t t);
+int hbtc_node_combine_dec_verified_dev(hbtc_node* node, const hbtc_node_part* parts, uint32_t t);
+/* Wait for every device's enqueued work. */
+int hbtc_node_sync(hbtc_node* node);
 
 /* The node's shard plans (host code, no GPU), for callers that run one process per GPU and
  * merge with their own collective (bench.py: RCCL all-gather of statuses and combined points).

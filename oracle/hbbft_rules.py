@@ -171,7 +171,7 @@ def _poly_from_wire(b):
     if len(b) < 8:
         raise ValueError("Poly")
     n = int.from_bytes(b[:8], "little")
-    if 8 + 40 * n != len(b):
+    if 8 + 40 * n > len(b):  # bincode 1.0 ignores bytes after the last field
         raise ValueError("Poly length")
     out, pos = [], 8
     for _ in range(n):
@@ -239,9 +239,7 @@ class SyncKeyGen:
         if ser_val is None:
             return fault("ValueDecryption")
         try:
-            val, end = _fr_from_wire(ser_val)
-            if end != len(ser_val):
-                raise ValueError("trailing")
+            val, _ = _fr_from_wire(ser_val)  # trailing bytes ignored, as bincode 1.0 does
         except ValueError:
             return fault("ValueDeserialization")
         if not self.value_matches(part["commit"], s_idx, val):

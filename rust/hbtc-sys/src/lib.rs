@@ -47,6 +47,7 @@ pub struct Batch<'a> {
 impl<'a> Batch<'a> {
     fn check(&self, item_size: usize) {
         assert!(!self.offsets.is_empty() && self.offsets[0] == 0, "offsets[0] must be 0");
+        assert!(self.offsets.windows(2).all(|w| w[0] <= w[1]), "offsets must be non-decreasing");
         let n = *self.offsets.last().unwrap() as usize;
         assert_eq!(self.idx.len(), n, "one node index per item");
         assert_eq!(self.items.len(), n * item_size, "item bytes");
@@ -155,7 +156,12 @@ impl Context {
     /// SecretKey::decrypt for a batch under one key: (plaintexts in the msgs layout, status).
     pub fn decrypt(&self, sk_le32: &[u8; 32], u_c48: &[u8], w_c96: &[u8], msgs: &[u8], offsets: &[u32])
         -> Result<(Vec<u8>, Vec<i32>)> {
+        assert!(!offsets.is_empty() && offsets[0] == 0, "offsets[0] must be 0");
+        assert!(offsets.windows(2).all(|w| w[0] <= w[1]), "offsets must be non-decreasing");
         let n = offsets.len() - 1;
+        assert!(offsets[n] as usize <= msgs.len(), "offsets past the message bytes");
+        assert_eq!(u_c48.len(), 48 * n, "one compressed G1 u per ciphertext");
+        assert_eq!(w_c96.len(), 96 * n, "one compressed G2 w per ciphertext");
         let (mut out, mut st) = (vec![0u8; msgs.len()], vec![0i32; n]);
         self.ok(unsafe {
             ffi::hbtc_decrypt(self.raw, n as u32, sk_le32.as_ptr(), u_c48.as_ptr(), w_c96.as_ptr(), msgs.as_ptr(),
@@ -198,6 +204,7 @@ impl Node {
     }
 
     pub fn keyset_load(&self, pk_shares_c48: &[u8]) -> Result<(u32, u32)> {
+        assert_eq!(pk_shares_c48.len() % 48, 0);
         let (mut id, mut bad) = (0u32, 0u32);
         self.ok(unsafe {
             ffi::hbtc_node_keyset_load(self.raw, pk_shares_c48.as_ptr(), (pk_shares_c48.len() / 48) as u32, &mut id,
@@ -208,6 +215,8 @@ impl Node {
 
     pub fn verify_dec_shares(&self, keyset: u32, h_c96: &[u8], w_c96: &[u8], b: &Batch) -> Result<Vec<i32>> {
         b.check(48);
+        assert_eq!(h_c96.len(), 96 * b.n_inst() as usize);
+        assert_eq!(w_c96.len(), 96 * b.n_inst() as usize);
         let mut st = vec![0i32; b.n_items()];
         self.ok(unsafe {
             ffi::hbtc_node_verify_dec_shares(self.raw, keyset, b.n_inst(), h_c96.as_ptr(), w_c96.as_ptr(),
@@ -218,6 +227,7 @@ impl Node {
 
     pub fn verify_sig_shares(&self, keyset: u32, h_c96: &[u8], b: &Batch) -> Result<Vec<i32>> {
         b.check(96);
+        assert_eq!(h_c96.len(), 96 * b.n_inst() as usize);
         let mut st = vec![0i32; b.n_items()];
         self.ok(unsafe {
             ffi::hbtc_node_verify_sig_shares(self.raw, keyset, b.n_inst(), h_c96.as_ptr(), b.offsets.as_ptr(),

@@ -171,6 +171,49 @@ def test_gpu_decode_batch_equal_oracle(ctx, n):
 
 
 @pytest.mark.gpu
+def test_gpu_validate_proofs_oversized_index(ctx):
+    """A wire index (usize) of 2^32 or more: Proof::validate walks no level with it, so it is
+    valid iff it has no digests and its leaf hash is the root; the other proofs of the batch
+    keep their own verdicts, and the expected-index check rejects it."""
+    from hbbft_amd import broadcast as G
+    n, f = 7, 2
+    _, _, root, ps = B.send_shards(b"oversized", n, f)
+    v0 = ps[0][0]
+    lone = hashlib.sha3_256(v0).digest()
+    var = [ps[3], (v0, 1 << 40, [], lone), (v0, 1 << 32, ps[0][2], root), (v0, (1 << 64) - 1, [], lone),
+           (v0, (1 << 32) - 1, [], lone), ps[5]]
+    exp = [B.proof_validate(x, n) for x in var]
+    assert exp == [True, True, False, True, True, True]
+    got = G.validate_proofs(ctx, [G.Proof(*x) for x in var], n)
+    assert list(got) == exp
+    got = G.validate_proofs(ctx, [G.Proof(*x) for x in var], n, expected_index=[3, 1, 0, 0, 0, 5])
+    assert list(got) == [True, False, False, False, False, True]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_gpu_trivial_coding_ragged_leaves(ctx, n):
+    """Coding::Trivial (no parity shards, N <= 3) checks presence only: leaves of different
+    lengths (and empty ones) are hashed as they are, and the value glued if the root matches."""
+    from hbbft_amd import broadcast as G
+    rng = random.Random(50 + n)
+    leafs, roots, exp = [], [], []
+    for inst in range(8):
+        lv = [bytes(rng.randrange(256) for _ in range(rng.choice([0, 1, 3, 4, 9, 40])))
+              for _ in range(n)]
+        if inst % 2 == 0:  # a prefix that glues to a value
+            lv[0] = (3).to_bytes(4, "big") + b"abc" + lv[0]
+        root = B.merkle_levels(lv)[1] if inst != 5 else bytes(32)
+        if inst == 7 and n > 1:
+            lv[1] = None  # missing: TooFewShardsPresent
+        leafs.append(lv)
+        roots.append(root)
+        exp.append(B.decode_from_shards(lv, 0, root))
+    assert G.decode_batch(ctx, leafs, roots, 0) == exp
+    assert any(v is not None for v in exp)
+
+
+@pytest.mark.gpu
 def test_gpu_rs_counts_refused(ctx):
     from hbbft_amd import _native as N
     with pytest.raises(N.HbtcError):

@@ -8,7 +8,7 @@ sizes, workspaces, counters and tile lists the benchmarks time are the ones test
   C3  1000 ciphertexts x 1000 DecryptionShares + 1000 G1 combines (uniform 1 % and the
       sender-concentrated 33 % pattern), plus a per-share-mode slice of 40 ciphertexts
   C4  64 coin instances x 10^4 SignatureShares + 64 combines of t = 3334 (property: statuses
-      from the construction, combine == master_sk * H, combined signature verifies)
+      from the construction, combine == master_sk * H), on one context and on a two-slot node
   C5  one node's SyncKeyGen era at N = 1000: 1000 Parts (56 280-point commitments) and 10^6 Acks
 """
 import numpy as np
@@ -95,12 +95,46 @@ def test_c2_full_against_construction(ctx):
     assert out["mismatches"] == 0 and out["combine_ok"]
 
 
-@pytest.mark.timeout(600)
-def test_c4_full_64_instances_by_property(ctx):
+@pytest.mark.timeout(900)
+def test_c4_full_64_instances_single_context_and_node(ctx):
+    """BASELINE config 4 at full size (64 x 10^4 SignatureShares + 64 combines of t = 3334): on
+    one context, and on a one-process node of two device slots (two contexts on this GPU:
+    hbtc_node_*_dev with whole instances per slot, the path `bench_configs.py c4 --gpus N`
+    runs on N GPUs).  Both equal the construction, and each other bit for bit (statuses,
+    combined signatures, parities, combine statuses)."""
     bench_configs.ctx_mode[0] = N.MODE_RLC
-    out = bench_configs.bench_coins(ctx, "c4", 10000, 64, 1, 0, 0.01)
-    assert out["mismatches"] == 0 and out["combine_ok"]
-    assert out["config"]["instances"] == 64 and out["config"]["t"] == 3334
+    a = bench_configs.bench_coins(ctx, "c4", 10000, 64, 1, 0, 0.01, keep_arrays=True)
+    assert a["mismatches"] == 0 and a["combine_ok"]
+    assert a["config"]["instances"] == 64 and a["config"]["t"] == 3334
+    node = N.Node([0, 0])
+    try:
+        node.set_verify_mode(N.MODE_RLC)
+        b = bench_configs.bench_coins(ctx, "c4", 10000, 64, 2, 1, 0.01, node=node, keep_arrays=True)
+    finally:
+        node.close()
+    assert b["mismatches"] == 0 and b["combine_ok"]
+    assert b["config"]["parallelism"].startswith("node: one process, 2 device slot(s) on 1 GPU(s)")
+    for x, y in zip(a["_arrays"], b["_arrays"]):
+        assert x.shape == y.shape and (x == y).all()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("slots", [[0, 0, 0], [0, 0, 0, 0, 0, 0, 0, 0]])
+def test_c2_node_slots_equal_single_context(ctx, slots):
+    """C2 (100 x 100 SignatureShares, 33 % sender-concentrated) on a node of 3 and 8 slots (100
+    instances cut unevenly by share count): equal to the single context bit for bit."""
+    bench_configs.ctx_mode[0] = N.MODE_RLC
+    a = bench_configs.bench_coins(ctx, "c2", 100, 100, 1, 0, 0.0, "senders", keep_arrays=True)
+    node = N.Node(slots)
+    try:
+        node.set_verify_mode(N.MODE_RLC)
+        b = bench_configs.bench_coins(ctx, "c2", 100, 100, 3, 1, 0.0, "senders", node=node,
+                                      keep_arrays=True)
+    finally:
+        node.close()
+    assert a["mismatches"] == 0 and b["mismatches"] == 0 and a["combine_ok"] and b["combine_ok"]
+    for x, y in zip(a["_arrays"], b["_arrays"]):
+        assert (x == y).all()
 
 
 @pytest.mark.timeout(600)

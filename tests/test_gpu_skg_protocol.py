@@ -134,11 +134,13 @@ def _messages(ctx, rng, n, t, our, pub_keys):
         cm, _ = ctx.g1_mul(G1, b)
         commits[p] = [bytes(cm[48 * i:48 * i + 48]) for i in range(len(b))]
 
-    def part(p, tamper_row=False, bad_ct=False, short=False):
+    def part(p, tamper_row=False, bad_ct=False, short=False, extra=b""):
         rows = [skg._bivar_row(polys[p], t, i + 1) for i in range(n)]
         if tamper_row:
             rows[our][0] = (rows[our][0] + 1) % R
-        cts = skg.encrypt_batch(ctx, pks, [wire.poly_to_wire(r) for r in rows])
+        ser = [wire.poly_to_wire(r) for r in rows]
+        ser[our] += extra  # bytes after the last coefficient: ignored by bincode 1.0
+        cts = skg.encrypt_batch(ctx, pks, ser)
         if bad_ct:
             c = cts[our]
             cts[our] = skg.Ciphertext(c.u, c.v, cts[(our + 1) % n].w)
@@ -176,7 +178,9 @@ def _messages(ctx, rng, n, t, our, pub_keys):
         ("ack", 3, ack(3, 0, bad_ct=True)),              # ValueDecryption
         ("ack", 2, ack(2, 3, raw=b"\x21" + bytes(39))),  # ValueDeserialization (bad length)
         ("ack", 3, ack(3, 3, raw=wire.fr_to_wire(0)[:8] + (R + 1).to_bytes(32, "big"))),  # >= r
-        ("part", 2, part(2)),                            # ok now
+        ("ack", 2, ack(2, 0, raw=wire.fr_to_wire(_bivar_eval(polys[0], t, 3, our + 1))
+                        + b"\x07\x07")),                 # ok: appended bytes ignored (bincode 1.0)
+        ("part", 2, part(2, extra=b"\x01\x02\x03")),        # ok now, appended bytes ignored
         ("ack", 3, ack(3, 2)),                           # ok
         ("ack", 0, ack(0, 2)),                           # ok
         ("ack", 1, ack(1, 2)),                           # ok: Part 2 complete (3 > 2t acks)
