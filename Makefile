@@ -26,6 +26,12 @@ all: lib hosttest oracle
 
 lib: $(LIB)
 
+# the one-block asm Fq product / squaring (generated; `make gen-fips` after editing the generator)
+.PHONY: gen-fips
+gen-fips:
+	python3 tools/gen_fips_asm.py --selftest
+	python3 tools/gen_fips_asm.py > $(CSRC)/fq_fips_asm.h
+
 $(BUILD):
 	mkdir -p $(BUILD)
 

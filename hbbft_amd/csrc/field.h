@@ -58,6 +58,15 @@
 
 #include "bls_constants.h"
 #include "fq_fips.h"
+// One inline-asm block per product / squaring (tools/gen_fips_asm.py): no per-statement s_nop
+// padding, and a squaring with 222 instead of 288 MACs.  HBTC_FIPS_ONEBLOCK=0 keeps the
+// C++-glued product of fq_fips.h for both.
+#ifndef HBTC_FIPS_ONEBLOCK
+#define HBTC_FIPS_ONEBLOCK 1
+#endif
+#if HBTC_FIPS_ONEBLOCK
+#include "fq_fips_asm.h"
+#endif
 
 #ifndef HBTC_FQ_UNROLL
 #define HBTC_FQ_UNROLL 1
@@ -247,23 +256,44 @@ extern unsigned long long hbtc_fqm_count;
 // translation unit whose hot loops hold few product sites (the cooperative GT kernels,
 // hbtc_check.hip) defines HBTC_FQMUL_INLINE; HBTC_FQMUL_CIOS selects round 1's CIOS loop.
 #if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ void fq_mul_dev(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+#if HBTC_FIPS_ONEBLOCK
+  fips::mont_mul_asm(r, a, b);
+#else
+  mont_mul_fips(r, a, b, FQ_P, FQ_NP);
+#endif
+}
+__device__ __forceinline__ void fq_sqr_dev(uint32_t* r, const uint32_t* a) {
+#if HBTC_FIPS_ONEBLOCK
+  fips::mont_sqr_asm(r, a);
+#else
+  mont_mul_fips(r, a, a, FQ_P, FQ_NP);
+#endif
+}
 __device__ __attribute__((noinline)) Fq fq_mul_call(Fq a, Fq b) {
   Fq r;
-  mont_mul_fips(r.v, a.v, b.v, FQ_P, FQ_NP);
+  fq_mul_dev(r.v, a.v, b.v);
+  return r;
+}
+__device__ __attribute__((noinline)) Fq fq_sqr_call(Fq a) {
+  Fq r;
+  fq_sqr_dev(r.v, a.v);
   return r;
 }
 #endif
 #if defined(__HIP_DEVICE_COMPILE__) && defined(HBTC_FQMUL_INLINE)
-HD void fq_mul(Fq& r, const Fq& a, const Fq& b) { mont_mul_fips(r.v, a.v, b.v, FQ_P, FQ_NP); }
+HD void fq_mul(Fq& r, const Fq& a, const Fq& b) { fq_mul_dev(r.v, a.v, b.v); }
+HD void fq_sqr(Fq& r, const Fq& a) { fq_sqr_dev(r.v, a.v); }
 #elif defined(__HIP_DEVICE_COMPILE__) && !defined(HBTC_FQMUL_CIOS)
 HD void fq_mul(Fq& r, const Fq& a, const Fq& b) { r = fq_mul_call(a, b); }
+HD void fq_sqr(Fq& r, const Fq& a) { r = fq_sqr_call(a); }
 #else
 HD void fq_mul(Fq& r, const Fq& a, const Fq& b) {
   HBTC_COUNT_FQ_MUL();
   mont_mul<12, HBTC_FQ_UNROLL>(r, a, b, FQ_P, FQ_NP);
 }
+HD void fq_sqr(Fq& r, const Fq& a) { fq_mul(r, a, a); }  // counted as one Fqm
 #endif
-HD void fq_sqr(Fq& r, const Fq& a) { fq_mul(r, a, a); }
 // Product through the single out-of-line copy on the device (code-size-bound callers).
 HD void fq_mul_ol(Fq& r, const Fq& a, const Fq& b) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -308,6 +338,11 @@ HD void fq_from_mont(Fq& r, const Fq& a) {
   fq_canon(r, t);
 }
 
+HD void fq_sel(Fq& r, bool c, const Fq& a, const Fq& b) {  // r = c ? a : b (no branch)
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+}
+
 // a^e for a constant 12-limb exponent e (square-and-multiply, MSB first)
 HDN void fq_pow_const(Fq& r, const Fq& a, const uint32_t* e) {
   Fq acc;
@@ -324,10 +359,80 @@ HDN void fq_pow_const(Fq& r, const Fq& a, const uint32_t* e) {
 
 HD void fq_inv(Fq& r, const Fq& a) { fq_pow_const(r, a, EXP_P_MINUS_2); }
 
-HD void fq_sel(Fq& r, bool c, const Fq& a, const Fq& b) {  // r = c ? a : b (no branch)
-#pragma unroll
-  for (int i = 0; i < 12; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+// a^e for a constant exponent by a left-to-right sliding window of width 3 over the odd powers
+// a, a^3, a^5, a^7 (4 Fq of table): for the 379-bit (p-3)/4 of the square roots, 378 squarings +
+// ~95 multiplications instead of 379 + 190.  The schedule is computed at compile time: each step
+// squares `nsq` times, then multiplies by table entry `idx` (idx 4: no multiplication).
+struct PowStep {
+  uint16_t nsq;
+  uint8_t idx;
+};
+struct PowPlan {
+  PowStep s[400];
+  int n = 0;
+  uint8_t first = 0;
+};
+constexpr int pow_bit(const uint32_t* e, int i) { return (int)((e[i >> 5] >> (i & 31)) & 1u); }
+constexpr PowPlan pow_plan(const uint32_t* e) {
+  PowPlan pl{};
+  int i = 383;
+  while (i >= 0 && !pow_bit(e, i)) --i;
+  auto window = [&](int top, int& low) {  // odd window [top .. low], at most 3 bits
+    low = top - 2 < 0 ? 0 : top - 2;
+    while (!pow_bit(e, low)) ++low;
+    int v = 0;
+    for (int b = top; b >= low; --b) v = 2 * v + pow_bit(e, b);
+    return v;
+  };
+  int low = 0;
+  pl.first = (uint8_t)((window(i, low) - 1) / 2);
+  i = low - 1;
+  int nsq = 0;
+  while (i >= 0) {
+    if (!pow_bit(e, i)) {
+      ++nsq;
+      --i;
+      continue;
+    }
+    const int v = window(i, low);
+    nsq += i - low + 1;
+    pl.s[pl.n++] = PowStep{(uint16_t)nsq, (uint8_t)((v - 1) / 2)};
+    nsq = 0;
+    i = low - 1;
+  }
+  if (nsq) pl.s[pl.n++] = PowStep{(uint16_t)nsq, 4};
+  return pl;
 }
+HBTC_CONST PowPlan POW_SQRT_PLAN = pow_plan(EXP_P_MINUS_3_DIV_4);
+
+HDN void fq_pow_window(Fq& r, const Fq& a, const PowPlan& pl) {
+  Fq t0 = a, t1, t2, t3, a2;
+  fq_sqr(a2, a);
+  fq_mul(t1, t0, a2);
+  fq_mul(t2, t1, a2);
+  fq_mul(t3, t2, a2);
+  Fq acc;
+  fq_sel(acc, pl.first == 0, t0, t1);
+  fq_sel(acc, pl.first == 2, t2, acc);
+  fq_sel(acc, pl.first == 3, t3, acc);
+#pragma unroll 1
+  for (int k = 0; k < pl.n; ++k) {
+    const PowStep st = pl.s[k];
+#pragma unroll 1
+    for (int q = 0; q < st.nsq; ++q) fq_sqr(acc, acc);
+    if (st.idx == 0) {
+      fq_mul(acc, acc, t0);
+    } else if (st.idx == 1) {
+      fq_mul(acc, acc, t1);
+    } else if (st.idx == 2) {
+      fq_mul(acc, acc, t2);
+    } else if (st.idx == 3) {
+      fq_mul(acc, acc, t3);
+    }
+  }
+  r = acc;
+}
+
 
 // Wave-wide OR of a predicate (the device loops below stay wave-uniform); the host build has
 // one "lane".
@@ -425,7 +530,7 @@ HD void fq_inv_binary(Fq& r, const Fq& a_mont) {
 // Returns true and r = sqrt(a) if a is a square (p = 3 mod 4: a^((p+1)/4)).
 HD bool fq_sqrt(Fq& r, const Fq& a) {
   Fq t, y;
-  fq_pow_const(t, a, EXP_P_MINUS_3_DIV_4);  // a^((p-3)/4)
+  fq_pow_window(t, a, POW_SQRT_PLAN);  // a^((p-3)/4)
   fq_mul(y, t, a);                          // a^((p+1)/4)
   Fq y2;
   fq_sqr(y2, y);
@@ -608,7 +713,7 @@ HDN bool fq2_sqrt(Fq2& r, const Fq2& a) {
     fq_mul(d, d, half);
   }
   Fq tt, x0;
-  fq_pow_const(tt, d, EXP_P_MINUS_3_DIV_4);  // t = delta^((p-3)/4)
+  fq_pow_window(tt, d, POW_SQRT_PLAN);  // t = delta^((p-3)/4)
   fq_mul(x0, tt, d);                         // x0 = delta^((p+1)/4)
   Fq chk;
   fq_mul(chk, tt, x0);  // delta^((p-1)/2) = +-1

@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""Generate hbbft_amd/csrc/fq_fips_asm.h: the Fq Montgomery product and squaring as ONE inline-asm
+block each (product scanning, carry-out MACs), for gfx950.
+
+Why one block: hipcc pads every inline-asm statement with an `s_nop 0` (it cannot see the
+hazards inside), and the C++-glued form of fq_fips.h issues ~75 statements per product; the
+column shifts and the Montgomery digit need the two 32-bit halves of the 64-bit accumulator,
+which an asm operand cannot name, so the accumulator, its overflow word and the squaring's
+cross-product accumulator are pinned to fixed VGPRs (HBTC_FIPS_*), named literally below; the
+carries go through VCC.
+
+Squaring: a^2 = sum_i a_i^2 2^(64i) + sum_i a_i 2^(32i) * 2 a_{>i}, and 2 a_{>i} is written with
+limbs that fit 32 bits: t_{i+1} = (2 a_{i+1}) mod 2^32 and t_j = (2 a_j mod 2^32) + (a_{j-1} >> 31)
+for j >= i + 2 (the dropped top bit of each doubled limb reappears in the next limb; the row sum
+telescopes to exactly 2 a_{>i}).  So the 66 cross products use one of two precomputed doubled
+limb vectors (23 shifts / v_alignbit outside the asm), every term is non-negative and the column
+accumulation is the product's: 78 + 144 = 222 MACs and ~540 instructions instead of 288 and ~660.
+Bounds as fq_fips.h: inputs < 2p, result < 2p; every 96-bit column sum fits.
+
+Usage: tools/gen_fips_asm.py > hbbft_amd/csrc/fq_fips_asm.h
+"""
+
+ACC = "v[%d:%d]"
+
+
+def gen_mul(square):
+    # operand numbering: outputs r0..r11 (%0..%11), q0..q11 (%12..%23); inputs a0..a11, then
+    # b0..b11 (mul only), then p0..p11 (SGPR), np (SGPR)
+    R = lambda i: "%%%d" % i
+    Q = lambda i: "%%%d" % (12 + i)
+    A = lambda i: "%%%d" % (24 + i)
+    if square:
+        B = A
+        D2 = lambda j: "%%%d" % (36 + j)       # j = 1..11 -> %37..%47 (%36 unused slot: a'' of 0)
+        D1 = lambda j: "%%%d" % (48 + j - 2)   # j = 2..11 -> %48..%57
+        P = lambda i: "%%%d" % (58 + i)
+        NP = "%70"
+    else:
+        B = lambda i: "%%%d" % (36 + i)
+        P = lambda i: "%%%d" % (48 + i)
+        NP = "%60"
+    acc = "v[\" HBTC_XS(HBTC_FIPS_ACC0) \":\" HBTC_XS(HBTC_FIPS_ACC1) \"]"
+    lo = "v\" HBTC_XS(HBTC_FIPS_ACC0) \""
+    hi = "v\" HBTC_XS(HBTC_FIPS_ACC1) \""
+    c2 = "v\" HBTC_XS(HBTC_FIPS_C2) \""
+    xacc = "v[\" HBTC_XS(HBTC_FIPS_X0) \":\" HBTC_XS(HBTC_FIPS_X1) \"]"
+    xlo = "v\" HBTC_XS(HBTC_FIPS_X0) \""
+    xhi = "v\" HBTC_XS(HBTC_FIPS_X1) \""
+    xc2 = "v\" HBTC_XS(HBTC_FIPS_XC2) \""
+    cc = "vcc"
+    lines = []
+    emit = lines.append
+
+    def mac(x, y, fresh):
+        emit("v_mad_u64_u32 %s, %s, %s, %s, %s" % (acc, cc, x, y, acc))
+        if fresh:
+            emit("v_addc_co_u32_e64 %s, %s, 0, 0, %s" % (c2, cc, cc))
+        else:
+            emit("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (c2, cc, c2, cc))
+
+    def xmac(x, y, first):
+        if first:
+            emit("v_mad_u64_u32 %s, %s, %s, %s, 0" % (xacc, cc, x, y))
+            emit("v_mov_b32 %s, 0" % xc2)
+        else:
+            emit("v_mad_u64_u32 %s, %s, %s, %s, %s" % (xacc, cc, x, y, xacc))
+            emit("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (xc2, cc, xc2, cc))
+
+    emit("v_mov_b32 %s, 0" % lo)
+    emit("v_mov_b32 %s, 0" % hi)
+    for k in range(23):
+        lo_i, hi_i = (0, k) if k < 12 else (k - 11, 11)
+        fresh = True
+        if square:
+            # row i: a_i * (2 a_{>i}) = a_i * sum_{j>i} t_j^(i) 2^(32j), t_{i+1}^(i) = D2(i+1) =
+            # (2 a_{i+1}) mod 2^32, t_j^(i) = D1(j) = (2 a_j mod 2^32) + top bit of a_{j-1}
+            # for j >= i + 2 (the top bits cancel along the row): every term non-negative
+            for i in range(lo_i, hi_i + 1):
+                j = k - i
+                if i < j:
+                    mac(A(i), D2(j) if j == i + 1 else D1(j), fresh)
+                    fresh = False
+                elif i == j:
+                    mac(A(i), A(i), fresh)
+                    fresh = False
+        else:
+            for i in range(lo_i, hi_i + 1):
+                mac(A(i), B(k - i), fresh)
+                fresh = False
+        qhi = k - 1 if k < 12 else 11
+        for i in range(lo_i, qhi + 1):
+            mac(Q(i), P(k - i), fresh)
+            fresh = False
+        if k < 12:
+            emit("v_mul_lo_u32 %s, %s, %s" % (Q(k), lo, NP))
+            mac(Q(k), P(0), fresh)
+        else:
+            emit("v_mov_b32 %s, %s" % (R(k - 12), lo))
+        emit("v_mov_b32 %s, %s" % (lo, hi))
+        emit("v_mov_b32 %s, %s" % (hi, c2))
+    emit("v_mov_b32 %s, %s" % (R(11), lo))
+    return lines
+
+
+def block(name, square):
+    body = gen_mul(square)
+    text = "\n".join('      "%s\\n\\t"' % l for l in body)
+    outs = ", ".join('"=&v"(r[%d])' % i for i in range(12)) + ",\n        " + \
+        ", ".join('"=&v"(q[%d])' % i for i in range(12))
+    ins = ", ".join('"v"(a[%d])' % i for i in range(12))
+    if square:
+        ins += ",\n        " + ", ".join('"v"(d2[%d])' % i for i in range(12))
+        ins += ",\n        " + ", ".join('"v"(d1[%d])' % i for i in range(2, 12))
+    else:
+        ins += ",\n        " + ", ".join('"v"(b[%d])' % i for i in range(12))
+    ins += ",\n        " + ", ".join('"s"(FQ_P[%d])' % i for i in range(12)) + ', "s"(FQ_NP)'
+    clob = '"v" HBTC_XS(HBTC_FIPS_ACC0), "v" HBTC_XS(HBTC_FIPS_ACC1), "v" HBTC_XS(HBTC_FIPS_C2), "vcc"'
+    args = "uint32_t* r, const uint32_t* a" + ("" if square else ", const uint32_t* b")
+    prep = ""
+    if square:
+        prep = """  uint32_t d2[12], d1[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) d2[j] = a[j] << 1;
+#pragma unroll
+  for (int j = 1; j < 12; ++j) d1[j] = (a[j] << 1) | (a[j - 1] >> 31);
+"""
+    return """__device__ __forceinline__ void %s(%s) {
+  uint32_t q[12];
+%s  asm volatile(
+%s
+      : %s
+      : %s
+      : %s);
+}
+""" % (name, args, prep, text, outs, ins, clob)
+
+
+def main():
+    print("""// GENERATED by tools/gen_fips_asm.py -- do not edit.
+// Fq Montgomery product and squaring for gfx950, each one inline-asm block (see the generator's
+// docstring): product scanning with carry-out MACs, the 64-bit column accumulator, its overflow
+// word and the squaring's cross accumulator pinned to HBTC_FIPS_* registers (override before
+// including to move them), the modulus limbs in SGPRs.  Only VALU instructions on registers.
+#pragma once
+#include <cstdint>
+#if defined(__HIP_DEVICE_COMPILE__)
+#ifndef HBTC_FIPS_ACC0
+#define HBTC_FIPS_ACC0 2
+#define HBTC_FIPS_ACC1 3
+#define HBTC_FIPS_C2 4
+#define HBTC_FIPS_XC2 5
+#define HBTC_FIPS_X0 6
+#define HBTC_FIPS_X1 7
+#endif
+#define HBTC_S(x) #x
+#define HBTC_XS(x) HBTC_S(x)
+namespace hbtc {
+namespace fips {
+""")
+    print(block("mont_mul_asm", False))
+    print(block("mont_sqr_asm", True))
+    print("""}  // namespace fips
+}  // namespace hbtc
+#endif""")
+
+
+if __name__ == "__main__" and "--selftest" not in __import__("sys").argv:
+    main()
+
+
+def selftest(trials=300):
+    """Execute the generated instruction lists on Python integers (VCC as one lane's carry bit)
+    and compare with a*b*2^-384 mod p for random a, b < 2p."""
+    import random
+    import re
+    P = 0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab
+    NP = (-pow(P, -1, 1 << 32)) % (1 << 32)
+    M32 = (1 << 32) - 1
+    rng = random.Random(5)
+    for square in (False, True):
+        prog = gen_mul(square)
+        for _ in range(trials):
+            a = rng.randrange(2 * P)
+            b = a if square else rng.randrange(2 * P)
+            al = [(a >> (32 * i)) & M32 for i in range(12)]
+            bl = [(b >> (32 * i)) & M32 for i in range(12)]
+            ops = {}
+            for i in range(12):
+                ops[24 + i] = al[i]
+                ops[58 + i if square else 48 + i] = (P >> (32 * i)) & M32
+            if square:
+                for j in range(12):
+                    ops[36 + j] = (al[j] << 1) & M32
+                for j in range(2, 12):
+                    ops[48 + j - 2] = ((al[j] << 1) | (al[j - 1] >> 31)) & M32
+                ops[70] = NP
+            else:
+                for i in range(12):
+                    ops[36 + i] = bl[i]
+                ops[60] = NP
+            reg = {"lo": 0, "hi": 0, "c2": 0}
+            vcc = [0]
+
+            def val(t):
+                t = t.strip()
+                if t == "0":
+                    return 0
+                if t.startswith("%"):
+                    return ops[int(t[1:])]
+                if "ACC0" in t and "ACC1" in t:
+                    return reg["lo"] | (reg["hi"] << 32)
+                if "ACC0" in t:
+                    return reg["lo"]
+                if "ACC1" in t:
+                    return reg["hi"]
+                if "C2" in t:
+                    return reg["c2"]
+                raise ValueError(t)
+
+            def store(t, v):
+                t = t.strip()
+                if t.startswith("%"):
+                    ops[int(t[1:])] = v & M32
+                elif "ACC0" in t and "ACC1" in t:
+                    reg["lo"], reg["hi"] = v & M32, (v >> 32) & M32
+                elif "ACC0" in t:
+                    reg["lo"] = v & M32
+                elif "ACC1" in t:
+                    reg["hi"] = v & M32
+                elif "C2" in t:
+                    reg["c2"] = v & M32
+                else:
+                    raise ValueError(t)
+
+            for line in prog:
+                op, rest = line.split(" ", 1)
+                args = [x for x in re.split(r",(?![^\[]*\])", rest)]
+                if op == "v_mad_u64_u32":
+                    d, _, x, y, z = args
+                    s = val(x) * val(y) + val(z)
+                    vcc[0] = s >> 64
+                    store(d, s & ((1 << 64) - 1))
+                elif op == "v_addc_co_u32_e64":
+                    d, _, x, y, _c = args
+                    s = val(x) + val(y) + vcc[0]
+                    vcc[0] = s >> 32
+                    store(d, s)
+                elif op == "v_mul_lo_u32":
+                    d, x, y = args
+                    store(d, val(x) * val(y))
+                elif op == "v_mov_b32":
+                    d, x = args
+                    store(d, val(x))
+                else:
+                    raise ValueError(op)
+            r = sum(ops[i] << (32 * i) for i in range(12))
+            want = a * b * pow(2, -384, P) % P
+            assert r < 2 * P and r % P == want, ("square" if square else "mul", hex(a), hex(b))
+    print("selftest ok")
+
+
+if __name__ == "__main__" and len(__import__("sys").argv) > 1 and __import__("sys").argv[1] == "--selftest":
+    selftest()

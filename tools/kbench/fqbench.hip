@@ -9,15 +9,23 @@
 #include <vector>
 #include "field.h"
 #include "fq_fips.h"
+#include "fq_fips_asm.h"
 using namespace hbtc;
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
 constexpr int ITERS = 512;
 
+// V 0-2: products (rolled / unrolled CIOS, C++-glued FIPS); 3: one-block asm FIPS product;
+// 4: squaring through the FIPS product; 5: one-block asm FIPS squaring (b ignored)
 template <int V>
 __device__ __forceinline__ void mulv(Fq& r, const Fq& a, const Fq& b) {
   if constexpr (V == 0) mont_mul<12, 1>(r, a, b, FQ_P, FQ_NP);
   else if constexpr (V == 1) mont_mul<12, 12>(r, a, b, FQ_P, FQ_NP);
-  else mont_mul_fips(r.v, a.v, b.v, FQ_P, FQ_NP);
+  else if constexpr (V == 2) mont_mul_fips(r.v, a.v, b.v, FQ_P, FQ_NP);
+  else if constexpr (V == 4) mont_mul_fips(r.v, a.v, a.v, FQ_P, FQ_NP);
+#if defined(__HIP_DEVICE_COMPILE__)
+  else if constexpr (V == 3) fips::mont_mul_asm(r.v, a.v, b.v);
+  else fips::mont_sqr_asm(r.v, a.v);
+#endif
 }
 
 template <int V, int ILP, int WAVES>
@@ -64,21 +72,32 @@ int main() {
   CHK(hipMalloc(&d_out, sizeof(Fq) * nthreads));
   CHK(hipMemcpy(d_in, h.data(), sizeof(Fq) * 1024, hipMemcpyHostToDevice));
   // cross-check
-  std::vector<Fq> r0(1024), r1(1024), r2(1024);
-  hipLaunchKernelGGL(k_check<0>, dim3(16), dim3(64), 0, 0, d_in, d_out);
-  CHK(hipMemcpy(r0.data(), d_out, sizeof(Fq) * 1024, hipMemcpyDeviceToHost));
-  hipLaunchKernelGGL(k_check<1>, dim3(16), dim3(64), 0, 0, d_in, d_out);
-  CHK(hipMemcpy(r1.data(), d_out, sizeof(Fq) * 1024, hipMemcpyDeviceToHost));
-  hipLaunchKernelGGL(k_check<2>, dim3(16), dim3(64), 0, 0, d_in, d_out);
-  CHK(hipMemcpy(r2.data(), d_out, sizeof(Fq) * 1024, hipMemcpyDeviceToHost));
-  int bad = 0;
+  std::vector<Fq> rv[6];
+  auto chk = [&](auto kern, int v) {
+    rv[v].resize(1024);
+    hipLaunchKernelGGL(kern, dim3(16), dim3(64), 0, 0, d_in, d_out);
+    CHK(hipMemcpy(rv[v].data(), d_out, sizeof(Fq) * 1024, hipMemcpyDeviceToHost));
+  };
+  chk(k_check<0>, 0);
+  chk(k_check<1>, 1);
+  chk(k_check<2>, 2);
+  chk(k_check<3>, 3);
+  chk(k_check<4>, 4);
+  chk(k_check<5>, 5);
+  int bad = 0, bad_sq = 0;
   for (int i = 0; i < 1024; ++i) {
-    Fq hr;
+    Fq hr, hs;
     mont_mul<12, 1>(hr, h[i], h[(i * 7 + 3) & 1023], FQ_P, FQ_NP);
     fq_canon(hr, hr);
-    for (int l = 0; l < 12; ++l) bad += (r0[i].v[l] != hr.v[l]) + (r1[i].v[l] != hr.v[l]) + (r2[i].v[l] != hr.v[l]);
+    mont_mul<12, 1>(hs, h[i], h[i], FQ_P, FQ_NP);
+    fq_canon(hs, hs);
+    for (int l = 0; l < 12; ++l) {
+      for (int v = 0; v < 4; ++v) bad += rv[v][i].v[l] != hr.v[l];
+      for (int v = 4; v < 6; ++v) bad_sq += rv[v][i].v[l] != hs.v[l];
+    }
   }
-  printf("cross-check vs host CIOS: %s (%d limb mismatches)\n", bad ? "FAIL" : "ok", bad);
+  printf("cross-check vs host CIOS: products %s (%d limb mismatches), squarings %s (%d)\n",
+         bad ? "FAIL" : "ok", bad, bad_sq ? "FAIL" : "ok", bad_sq);
   hipEvent_t a, b;
   CHK(hipEventCreate(&a));
   CHK(hipEventCreate(&b));
@@ -104,8 +123,9 @@ int main() {
   run(NAME " ILP1 4w/SIMD", k_mul<V, 1, 4>, 1024, 1);                                  \
   run(NAME " ILP2 4w/SIMD", k_mul<V, 2, 4>, 1024, 2);                                  \
   run(NAME " ILP1 8w/SIMD", k_mul<V, 1, 8>, 2048, 1);
-  RUNV(0, "CIOS rolled")
-  RUNV(1, "CIOS unrolled")
-  RUNV(2, "FIPS asm")
+  RUNV(2, "FIPS asm (C++ glued)")
+  RUNV(3, "FIPS one-block asm")
+  RUNV(4, "sqr via FIPS product")
+  RUNV(5, "sqr one-block asm")
   return 0;
 }
