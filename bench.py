@@ -345,7 +345,7 @@ def max_over_ranks(elapsed, dist, device=None):
 
 
 # committed rocprofv3 summaries of this command (kernel trace + PMC passes), newest first
-PROFILE_DIRS = ("profiles/r03/headline", "profiles/r02g/headline")
+PROFILE_DIRS = ("profiles/r03/headline", "profiles/r03/headline_a", "profiles/r02g/headline")
 
 
 def rocprof_avg_ms(csv_path, kernel):
@@ -515,6 +515,16 @@ def main():
     elapsed = max_over_ranks(elapsed, dist, dev if args.backend == "nccl" else None)
     breakdown = {f: ctx.timing_read(f) for f in FAMS}
     leaves = ctx.rlc_last_leaves() if args.mode == "rlc" else ep.total
+    # the same epoch once more with nothing else in flight (after the timed region): the dominant
+    # kernel's duration on an otherwise idle chip, beside its pipelined duration above (where
+    # the other lanes' check levels and combines share the CUs with it)
+    iso = {}
+    if gather is None:
+        ctx.sync()
+        ctx.timing_reset()
+        ep.step(ctx)
+        ctx.sync()
+        iso = {f: ctx.timing_read(f) for f in FAMS}
     if strong:
         # the merged whole epoch on every rank, against the whole epoch's construction
         st, g, cst = gather.merged()
@@ -626,6 +636,12 @@ def main():
             "frac_at_rocprof_duration": (round(fqm_per_launch[dom] * consts["mad_u64_u32_per_fqm"]
                                                / (rocprof_ms * 1e-3) / MAD_U64_PEAK, 4) if rocprof_ms else None),
             "profile_dir": prof_dir,
+            "kernel_ms_per_launch_isolated": (round(iso[dom][0] / iso[dom][1], 3) if iso.get(dom, (0, 0))[1]
+                                              else None),
+            "frac_isolated": (round(fqm_per_launch[dom] * consts["mad_u64_u32_per_fqm"]
+                                    / (iso[dom][0] / iso[dom][1] * 1e-3) / MAD_U64_PEAK, 4)
+                              if iso.get(dom, (0, 0))[1] else None),
+            "isolated_note": "one extra epoch after the timed region with no other epoch in flight",
             "pmc": {k: pmc[k] for k in ("vgpr", "scratch_bytes_per_lane", "valu_busy",
                                         "hbm_read_bytes", "hbm_write_bytes") if k in pmc} or None,
             "valu_insts_per_launch": pmc.get("counters_mean_per_dispatch", {}).get("SQ_INSTS_VALU"),
@@ -733,7 +749,8 @@ def adversarial_line(ctx, args, base):
             "data": "f = %d Byzantine senders send wrong shares on every ciphertext (%d of %d shares) + 8 bad encodings"
                     % (ep.f, ep.f * ep.m, ep.total),
             "accepted_per_step": n_acc, "exact_single_share_checks_per_step": leaves,
-            "kernel_ms_per_step": per}
+            "kernel_event_spans_ms_per_step": per,
+            "kernel_event_spans_note": "HIP-event spans: they include queueing behind the other lanes' kernels (k_rlc_finalize runs ~0.02 ms in rocprofv3 traces)"}
 
 
 if __name__ == "__main__":

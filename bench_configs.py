@@ -102,6 +102,27 @@ def breakdown(ctx, steps, fams):
     return out
 
 
+MAD_U64_PEAK = 29.51e12  # measured v_mad_u64_u32 lane-ops/s (bench.py MAD_U64_PEAK)
+
+
+def roofline_line(ctx, family, kernel, fqm_per_launch, note):
+    """The dominant kernel's VALU-integer roofline point: algorithmic Fqm per launch (tools/
+    fqm_count.cpp -> bench/roofline_constants.json) x 288 v_mad_u64_u32 / its average HIP-event
+    span on its stream (this run)."""
+    ms, n = ctx.timing_read(family)
+    if not n:
+        return None
+    avg_s = ms / n / 1e3
+    consts = json.load(open(os.path.join(ROOT, "bench", "roofline_constants.json")))
+    achieved = fqm_per_launch * consts["mad_u64_u32_per_fqm"] / avg_s / 1e12
+    return {"bound": "valu-int (v_mad_u64_u32)", "kernel": kernel, "achieved": round(achieved, 3),
+            "peak": MAD_U64_PEAK / 1e12, "unit": "T mad_u64_u32/s",
+            "frac": round(achieved / (MAD_U64_PEAK / 1e12), 4), "traffic": None,
+            "fqm_per_launch": fqm_per_launch, "kernel_ms_per_launch": round(avg_s * 1e3, 3),
+            "kernel_ms_per_launch_source": "HIP-event span on the kernel's stream, this run",
+            "work_unit": note}
+
+
 COIN_FAMS = ["prepare", "sig_verify", "sig_items", "sig_lines", "chk_tiles", "chk_subs",
              "chk_leaves", "rlc_finalize", "lagrange", "comb_decode", "comb_digits", "combine"]
 
@@ -279,7 +300,7 @@ class NodeCoinRunner:
 
 
 def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode="uniform", node=None,
-                keep_arrays=False):
+                keep_arrays=False, cpu_budget=0.0):
     """c2 / c4: n_inst coin instances x n SignatureShares + n_inst combines (first t verified).
     node: a hbtc Node (one process, several device slots) instead of the single context."""
     t0 = time.time()
@@ -300,6 +321,11 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode=
     run.sync()
     elapsed = time.perf_counter() - t1
     per = breakdown(tctx, steps, COIN_FAMS)
+    consts = json.load(open(os.path.join(ROOT, "bench", "roofline_constants.json")))
+    items0 = (run.slots[0]["hi"] - run.slots[0]["lo"]) if node is not None else total
+    roof = roofline_line(tctx, "sig_items", "k_sig_items", consts["sig_rlc_item"] * items0,
+                         "sig_rlc_item Fqm (G2 decode + subgroup test, [a]s + [b](-psi^2 s), r pk from "
+                         "the fixed-base table, tile-tree share) x %d SignatureShares per launch" % items0)
     stv, out, par, cst = run.results()
     want, _ = ctx.g2_mul(G2_GEN, fr_bytes([inp["master"] * hh % R for hh in inp["hs"]]))
     mism = int((stv != inp["expected"]).sum())
@@ -328,16 +354,26 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode=
                    % (name, n_inst, n, n_inst, t), "N": n, "t": t, "instances": n_inst,
                    "parallelism": par_s},
         "combines_per_s": round(n_inst * steps / elapsed, 2),
-        "kernel_ms_per_step": per, "mismatches": mism, "combine_ok": comb_ok,
+        "kernel_event_spans_ms_per_step": per, "mismatches": mism, "combine_ok": comb_ok,
     }
+    res["roofline"] = roof
     if node is not None:
-        res["kernel_ms_per_step_note"] = "event spans of device slot 0 only"
+        res["kernel_event_spans_note"] = "event spans of device slot 0 only"
+    if cpu_budget and node is None:
+        try:
+            from oracle.cbaseline import run_sig_share_baseline
+            nonce = ("Nonce for Honey Badger %s@0:2:0" % ("[" + ", ".join(["0x" + "ab" * 48] * 4) + "]")).encode()
+            res["cpu_baseline"] = run_sig_share_baseline(inp["sigs"][:96 * n], inp["pk"], nonce, cpu_budget)
+            res["cpu_baseline"]["sample"] += (" (a synthetic %d-byte nonce: hash_g2 of it is not the bench's H, "
+                                              "so the pairings reject; the work per share is the same)" % len(nonce))
+        except Exception as e:  # the baseline is reported, never the product path
+            res["cpu_baseline"] = {"error": repr(e)}
     if keep_arrays:
         res["_arrays"] = (stv, out, par, cst)
     return res
 
 
-def bench_skg(ctx, n, n_parts, n_distinct, steps, warmup):
+def bench_skg(ctx, n, n_parts, n_distinct, steps, warmup, cpu_budget=0.0):
     """c5: one node's SyncKeyGen view at N=n (t = (n-1)/3): n_parts Parts, then n_parts x n Acks."""
     rng = random.Random(SEED + 5)
     t0 = time.time()
@@ -442,6 +478,22 @@ def bench_skg(ctx, n, n_parts, n_distinct, steps, warmup):
     am = int((ast != ack_expect).sum()) + int((ack_dst != N.ACCEPT).sum())
     if pm or am:
         raise SystemExit("c5: results differ from the construction (%d Part, %d Ack mismatches)" % (pm, am))
+    consts = json.load(open(os.path.join(ROOT, "bench", "roofline_constants.json")))
+    dec_ms, dec_n = ctx.timing_read("comb_decode")
+    # decodes per step: every Part's commitment (n_parts x m points), plus the commitment of each
+    # Part whose row failed (its Acks go through an RLC MSM over the commitment again)
+    n_dec = (n_parts + int((part_expect != N.ACCEPT).sum())) * m
+    roof = roofline_line(ctx, "comb_decode", "k_msm_decode<Fq, 12>",
+                         consts["dec_share"]["decode"] * n_dec * steps // max(dec_n, 1),
+                         "G1 decode + subgroup test Fqm (dec_share.decode) x the commitment points one "
+                         "launch decodes (%d per step over %d launches)" % (n_dec, dec_n // max(steps, 1)))
+    cpu = None
+    if cpu_budget:
+        try:
+            from oracle.cbaseline import run_skg_ack_baseline
+            cpu = run_skg_ack_baseline(n, t, cpu_budget)
+        except Exception as e:  # reported, never the product path
+            cpu = {"error": repr(e)}
     tp = t_parts[0] / steps
     td = t_dec[0] / steps
     ta = elapsed / steps - tp
@@ -457,7 +509,8 @@ def bench_skg(ctx, n, n_parts, n_distinct, steps, warmup):
         "parts_ms": round(tp * 1e3, 3), "acks_ms": round(ta * 1e3, 3),
         "acks_decrypt_ms": round(td * 1e3, 3),
         "parts_per_s": round(n_parts / tp, 1), "acks_per_s": round(n_acks / ta, 1),
-        "kernel_ms_per_step": per, "mismatches": pm + am,
+        "kernel_event_spans_ms_per_step": per, "mismatches": pm + am,
+        "roofline": roof, "cpu_baseline": cpu,
     }
 
 
@@ -573,7 +626,7 @@ def bench_broadcast(ctx, n, value_bytes, steps, warmup):
                    "shard_len": L},
         "values_decoded_per_s": round(n / (dt / steps), 1),
         "input_bytes_per_step": int(n_pr * L + digs.size + n * (n - f) * L),
-        "kernel_ms_per_step": per_step, "results_ok": ok,
+        "kernel_event_spans_ms_per_step": per_step, "results_ok": ok,
         "cpu_baseline": {"value": round(n_pr / cpu_step, 1), "unit": "proofs/s (with the epoch's decodes)",
                          "cores": 1, "kind": "port",
                          "sample": "2048 Proof::validate + 2 decode_from_shards (first call builds the "
@@ -603,6 +656,7 @@ def main():
     ap.add_argument("--distinct", type=int, default=4, help="c5 distinct bivariate polynomials")
     ap.add_argument("--bc-value", type=int, default=65536, help="bc: bytes per proposed value")
     ap.add_argument("--mode", choices=["rlc", "per_share"], default="rlc")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baselines")
     ap.add_argument("--corrupt", type=float, default=0.01)
     ap.add_argument("--corrupt-mode", choices=["uniform", "senders"], default="uniform")
     args = ap.parse_args()
@@ -620,14 +674,15 @@ def main():
             warmup = args.warmup if args.warmup is not None else (1 if c == "c5" else 2)
             if c == "c2":
                 out = bench_coins(ctx, "c2", 100, 100, steps, warmup, args.corrupt,
-                                  args.corrupt_mode, node=node)
+                                  args.corrupt_mode, node=node, cpu_budget=0.0 if args.no_cpu else 10.0)
             elif c == "c4":
                 out = bench_coins(ctx, "c4", 10000, args.inst, steps, warmup, args.corrupt,
-                                  args.corrupt_mode, node=node)
+                                  args.corrupt_mode, node=node, cpu_budget=0.0 if args.no_cpu else 10.0)
             elif c == "bc":
                 out = bench_broadcast(ctx, 256, args.bc_value, steps, warmup)
             elif c == "c5":
-                out = bench_skg(ctx, 1000, args.parts, args.distinct, steps, warmup)
+                out = bench_skg(ctx, 1000, args.parts, args.distinct, steps, warmup,
+                                cpu_budget=0.0 if args.no_cpu else 10.0)
             else:
                 raise SystemExit("unknown config " + c)
             print(json.dumps(out), flush=True)

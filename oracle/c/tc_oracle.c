@@ -1431,3 +1431,116 @@ uint64_t tco_bench_dec_shares(int mode, int threads, double budget_s, const uint
   free(pw);
   return done;
 }
+
+/* Per SignatureShare, threshold_crypto's PublicKeyShare::verify as hbbft's Coin calls it
+ * (src/coin.rs:151), including the serde decode of the share: decode(sig) [on-curve + [r]Q],
+ * H = hash_g2(nonce) (recomputed per call, as the reference does), decode(pk_i),
+ * pairing(pk_i, H) == pairing(G1, sig).  Share i uses pk48[i] (n_shares of each). */
+typedef struct {
+  const uint8_t *sigs, *pks, *nonce;
+  size_t nonce_len;
+  uint32_t n_shares, first, stride;
+  double budget_s;
+  uint32_t done, accepted;
+} sjob;
+static void* sworker(void* arg) {
+  sjob* j = (sjob*)arg;
+  const double t0 = now_s();
+  for (uint32_t i = j->first; i < j->n_shares; i += j->stride) {
+    g2a s;
+    if (tco_g2_decompress(j->sigs + 96 * i, &s, 1) == 0) {
+      uint8_t H[96];
+      tco_hash_g2(j->nonce, j->nonce_len, H);
+      g2a h;
+      g1a pk, g;
+      tco_g2_decompress(H, &h, 0);
+      tco_g1_decompress(j->pks + 48 * i, &pk, 1);
+      g = G1GEN;
+      fp12 e1, e2;
+      pairing(&e1, &pk, &h);
+      pairing(&e2, &g, &s);
+      j->accepted += f12_eq(&e1, &e2);
+    }
+    j->done++;
+    if (now_s() - t0 > j->budget_s) break;
+  }
+  return NULL;
+}
+uint64_t tco_bench_sig_shares(int threads, double budget_s, const uint8_t* sigs96, const uint8_t* pks48,
+                              uint32_t n_shares, const uint8_t* nonce, size_t nonce_len, double* wall_s,
+                              uint64_t* accepted) {
+  tco_init();
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+  sjob* jobs = (sjob*)calloc(threads, sizeof(sjob));
+  const double t0 = now_s();
+  for (int k = 0; k < threads; ++k) {
+    sjob* j = &jobs[k];
+    j->sigs = sigs96;
+    j->pks = pks48;
+    j->nonce = nonce;
+    j->nonce_len = nonce_len;
+    j->n_shares = n_shares;
+    j->first = (uint32_t)k;
+    j->stride = (uint32_t)threads;
+    j->budget_s = budget_s;
+    pthread_create(&th[k], NULL, sworker, j);
+  }
+  uint64_t done = 0, acc = 0;
+  for (int k = 0; k < threads; ++k) {
+    pthread_join(th[k], NULL);
+    done += jobs[k].done;
+    acc += jobs[k].accepted;
+  }
+  *wall_s = now_s() - t0;
+  if (accepted) *accepted = acc;
+  free(th);
+  free(jobs);
+  return done;
+}
+
+/* G1 scalar multiplications (255-bit scalars, pairing 0.14's double-and-add) of the generator on
+ * `threads` threads for budget_s seconds: the unit of BivarCommitment::evaluate, which the
+ * reference runs (t+1)^2 times per Ack (src/sync_key_gen.rs:493).  Returns multiplications done. */
+typedef struct {
+  double budget_s;
+  uint64_t seed;
+  uint32_t done;
+} mjob;
+static void* mworker(void* arg) {
+  mjob* j = (mjob*)arg;
+  const double t0 = now_s();
+  uint64_t s = j->seed;
+  g1a base = G1GEN;
+  while (now_s() - t0 < j->budget_s) {
+    uint64_t k[4];
+    for (int i = 0; i < 4; ++i) {
+      s = s * 6364136223846793005ull + 1442695040888963407ull;
+      k[i] = s;
+    }
+    k[3] &= 0x3fffffffffffffffull;
+    g1j r;
+    g1_mul(&r, &base, k, 4);
+    j->done++;
+  }
+  return NULL;
+}
+uint64_t tco_bench_g1_mul(int threads, double budget_s, double* wall_s) {
+  tco_init();
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+  mjob* jobs = (mjob*)calloc(threads, sizeof(mjob));
+  const double t0 = now_s();
+  for (int k = 0; k < threads; ++k) {
+    jobs[k].budget_s = budget_s;
+    jobs[k].seed = 0x9e3779b97f4a7c15ull * (uint64_t)(k + 1);
+    pthread_create(&th[k], NULL, mworker, &jobs[k]);
+  }
+  uint64_t done = 0;
+  for (int k = 0; k < threads; ++k) {
+    pthread_join(th[k], NULL);
+    done += jobs[k].done;
+  }
+  *wall_s = now_s() - t0;
+  free(th);
+  free(jobs);
+  return done;
+}

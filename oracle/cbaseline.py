@@ -31,6 +31,12 @@ _lib.tco_bench_dec_shares.restype = ctypes.c_uint64
 _lib.tco_bench_dec_shares.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, _B, ctypes.c_uint32,
                                       _B, _B, _B, ctypes.c_size_t, _B,
                                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint64)]
+_lib.tco_bench_sig_shares.restype = ctypes.c_uint64
+_lib.tco_bench_sig_shares.argtypes = [ctypes.c_int, ctypes.c_double, _B, _B, ctypes.c_uint32, _B,
+                                      ctypes.c_size_t, ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_uint64)]
+_lib.tco_bench_g1_mul.restype = ctypes.c_uint64
+_lib.tco_bench_g1_mul.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]
 _lib.tco_init()
 
 
@@ -168,3 +174,44 @@ def run_dec_share_baseline(ep, budget_s, cores=None):
                                     "2-pair multi-Miller loop + one final exponentiation per share"
                                     % (done_o, wall_o)},
     }
+
+
+def run_sig_share_baseline(sigs96, pks48, nonce, budget_s, cores=None):
+    """bench_configs.py c2 / c4 cpu_baseline: the reference-faithful PublicKeyShare::verify
+    (src/coin.rs:151: serde decode of the share, hash_g2(nonce) per call, two full pairings) on
+    every usable core, over real shares of the benchmark's first instance (share i with its
+    sender's pk)."""
+    cpus = host_cpus()
+    cores = cores or cpus["usable"]
+    n = len(pks48) // 48
+    wall, acc = ctypes.c_double(), ctypes.c_uint64()
+    done = _lib.tco_bench_sig_shares(cores, budget_s, bytes(sigs96), bytes(pks48), n, bytes(nonce), len(nonce),
+                                     ctypes.byref(wall), ctypes.byref(acc))
+    return {"value": round(done / wall.value, 2), "unit": "shares/s", "cores": cores, "host_cpus": cpus,
+            "kind": "port",
+            "impl": "C restatement of threshold_crypto 0.1 / pairing 0.14 (oracle/c/tc_oracle.c), pthreads",
+            "sample": "%d SignatureShare checks of instance 0 in %.1fs: per share serde decode ([r]Q subgroup "
+                      "check) + hash_g2(nonce) + two full pairings, as Coin calls PublicKeyShare::verify "
+                      "(src/coin.rs:151)" % (done, wall.value)}
+
+
+def run_skg_ack_baseline(n, t, budget_s, cores=None):
+    """bench_configs.py c5 cpu_baseline: the reference's Ack check is
+    commit.evaluate(x, y) == val * G1 (src/sync_key_gen.rs:493), i.e. (t+1)^2 G1 scalar
+    multiplications per Ack (BivarCommitment::evaluate over the (t+1)^2 coefficient grid) plus
+    the Ack value's SecretKey::decrypt (two pairings, :483).  At N = 1000 one Ack is ~112k
+    scalar multiplications, so the sample times the scalar multiplication on every usable core
+    and reports the Acks/s that rate gives (the decrypt's pairings are left out: a lower bound on
+    the reference's time, an upper bound on its rate)."""
+    cpus = host_cpus()
+    cores = cores or cpus["usable"]
+    wall = ctypes.c_double()
+    done = _lib.tco_bench_g1_mul(cores, budget_s, ctypes.byref(wall))
+    per_ack = (t + 1) ** 2
+    rate = done / wall.value
+    return {"value": round(rate / per_ack, 4), "unit": "acks/s (projected from the timed scalar multiplications)",
+            "cores": cores, "host_cpus": cpus, "kind": "port",
+            "impl": "C restatement of pairing 0.14's G1 double-and-add (oracle/c/tc_oracle.c), pthreads",
+            "sample": "%d G1 scalar multiplications in %.1fs (%.0f /s); one Ack = (t+1)^2 = %d of them "
+                      "(commit.evaluate at N = %d, t = %d), decrypt pairings excluded"
+                      % (done, wall.value, rate, per_ack, n, t)}
