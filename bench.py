@@ -454,6 +454,9 @@ def main():
     ap.add_argument("--mode", choices=["rlc", "per_share"], default="rlc",
                     help="rlc: batched random-linear-combination checks with exact fallback "
                          "(default); per_share: one pairing check per share")
+    ap.add_argument("--rlc-bits", type=int, choices=[64, 128], default=64,
+                    help="RLC scalar size (hbtc_set_rlc_bits): soundness 2^-64 (default) or 2^-128 "
+                         "per group check")
     ap.add_argument("--corrupt", type=float, default=0.01, help="fraction of wrong shares")
     ap.add_argument("--corrupt-mode", choices=["uniform", "senders"], default="uniform")
     ap.add_argument("--node", action="store_true",
@@ -492,6 +495,7 @@ def main():
     ctx = N.Context(local)
     t0 = time.time()
     ctx.set_verify_mode(N.MODE_RLC if args.mode == "rlc" else N.MODE_PER_SHARE)
+    ctx.set_rlc_bits(args.rlc_bits)
     gather, slices = None, None
     if strong:
         from hbbft_amd import shard
@@ -552,7 +556,7 @@ def main():
     # algorithmic Fqm per launch of each kernel family (tools/fqm_count.cpp)
     fqm_per_launch = {
         "dec_verify": consts["dec_share"]["total"] * ep.total,
-        "rlc_items": consts["rlc_item"] * ep.total,
+        "rlc_items": consts["rlc_item" if args.rlc_bits == 64 else "rlc_item_128"] * ep.total,
         # the plain 2-pair check of every tile (serial Fqm count of one check; the cooperative
         # kernel issues more lane-level work than this)
         "chk_tiles": consts["rlc_group_check"] * n_tiles,
@@ -613,6 +617,7 @@ def main():
         "combines_per_s": round(combines, 1),
         "accepted_per_step": n_acc,
         "mode": args.mode,
+        "rlc_bits": args.rlc_bits,
         "exact_single_share_checks_per_step_rank0": leaves,
         "kernel_event_spans_ms_per_step_rank0": per_step,
         "kernel_event_spans_note": ("HIP-event spans per kernel family on the library's streams, summed "
@@ -669,6 +674,7 @@ def node_main(args):
     ctx = N.Context(slots[0])
     node = N.Node(slots)
     node.set_verify_mode(N.MODE_RLC if args.mode == "rlc" else N.MODE_PER_SHARE)
+    node.set_rlc_bits(args.rlc_bits)
     offsets_all = np.arange(0, args.n * args.cts + 1, args.n, dtype=np.uint32)
     slices = shard.instance_slices(len(slots), offsets_all)
     t0 = time.time()

@@ -75,6 +75,7 @@ SIGNATURES = {
     "hbtc_skg_check_parts": (_I32, [_P, _U32, _U32, _U32, _P, _P, _P]),
     "hbtc_skg_check_acks": (_I32, [_P, _U32, _U32, _U32, _P, _P, _P, _U32, _P, _P, _P, _P]),
     "hbtc_set_verify_mode": (_I32, [_P, _I32]),
+    "hbtc_set_rlc_bits": (_I32, [_P, _U32]),
     "hbtc_sha3_256": (_I32, [_P, _SZ, _P]),
     "hbtc_hash_g2": (_I32, [_P, _SZ, _P]),
     "hbtc_hash_g1_g2": (_I32, [_P, _P, _SZ, _P]),
@@ -114,6 +115,7 @@ SIGNATURES = {
     "hbtc_node_devices": (_I32, [_P]),
     "hbtc_node_context": (_P, [_P, _I32]),
     "hbtc_node_set_verify_mode": (_I32, [_P, _I32]),
+    "hbtc_node_set_rlc_bits": (_I32, [_P, _U32]),
     "hbtc_node_keyset_load": (_I32, [_P, _P, _U32, ctypes.POINTER(_U32), ctypes.POINTER(_U32)]),
     "hbtc_node_keyset_free": (_I32, [_P, _U32]),
     "hbtc_node_verify_dec_shares": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P, _P]),
@@ -657,6 +659,10 @@ class Context:
         MODE_PER_SHARE: one pairing check per share."""
         self._check(self.lib.hbtc_set_verify_mode(self.h, int(mode)), "hbtc_set_verify_mode")
 
+    def set_rlc_bits(self, bits):
+        """RLC scalar size: 64 (default, <= 2^-64 per group check) or 128 (<= 2^-128)."""
+        self._check(self.lib.hbtc_set_rlc_bits(self.h, int(bits)), "hbtc_set_rlc_bits")
+
     def set_check_schedule(self, schedule):
         """HBTC_CHECK_* (include/hbtc.h): -1 auto, 0 plain-first, 1 paired + sub-tiles, 2 paired -> leaves."""
         self._check(self.lib.hbtc_set_check_schedule(self.h, int(schedule)), "hbtc_set_check_schedule")
@@ -716,6 +722,9 @@ class Node:
 
     def set_verify_mode(self, mode):
         self._check(self.lib.hbtc_node_set_verify_mode(self.h, int(mode)), "hbtc_node_set_verify_mode")
+
+    def set_rlc_bits(self, bits):
+        self._check(self.lib.hbtc_node_set_rlc_bits(self.h, int(bits)), "hbtc_node_set_rlc_bits")
 
     def keyset_load(self, pk_shares):
         pk = _join(pk_shares, 48)

@@ -376,9 +376,10 @@ HD void jac_madd_generic(Jac<F>& r, const Jac<F>& p, const F& qx, const F& qy) {
 // uniform joint double-and-add of jac_mul2_u32_uniform specialised to an m that keeps y (the
 // table is d, c x and d + m(d): 5 coordinates instead of 6) with the generic mixed addition (the
 // running sum is infinity only before the first nonzero bit pair: then the table point itself
-// is taken).  mx = c x.
+// is taken).  mx = c x.  a, b < 2^nbits (nbits = 32 or 64: the 64- / 128-bit RLC scalars).
 template <class F>
-HD void glv_mul_uniform(Jac<F>& r, const Aff<F>& d, const F& mx, uint32_t a, uint32_t b) {
+HD void glv_mul_uniform(Jac<F>& r, const Aff<F>& d, const F& mx, uint64_t a, uint64_t b,
+                        int nbits = 32) {
   Aff<F> pq;  // d + m(d) (never infinity: m has no eigenvalue -1)
   {
     Jac<F> s;
@@ -393,7 +394,8 @@ HD void glv_mul_uniform(Jac<F>& r, const Aff<F>& d, const F& mx, uint32_t a, uin
   }
   Jac<F> acc;
   jac_set_inf(acc);
-  for (int bit = 31; bit >= 0; --bit) {
+#pragma unroll 1
+  for (int bit = nbits - 1; bit >= 0; --bit) {
     jac_dbl(acc, acc);
     const bool ba = ((a >> bit) & 1u) != 0, bb = ((b >> bit) & 1u) != 0;
     F tx, ty;

@@ -45,7 +45,7 @@ struct DevBuf {
 struct Keyset {
   G1A* pk = nullptr;
   int32_t* st = nullptr;
-  PtXY* tab = nullptr;  // fixed-base tables (n * PK_TAB_WIN * 256 points, ~98 KB per share)
+  PtXY* tab = nullptr;  // fixed-base tables (n * PK_TAB_WIN * 256 points, ~196 KB per share)
   uint32_t* last_bad = nullptr;  // sender tracking: the call that last flagged each sender
   uint32_t* rejects = nullptr;   // per-sender REJECT counts of the running call
   uint32_t calls = 0;            // RLC verification calls on this key set
@@ -124,6 +124,7 @@ struct hbtc_ctx {
   std::map<std::string, DevBuf> bufs;
   int verify_mode = HBTC_MODE_RLC;
   bool track_senders = true;
+  uint32_t rlc_bits = 64;  // hbtc_set_rlc_bits
   const uint32_t* last_leaf_count = nullptr;  // device counter of the last RLC call
   // Device ranges that combines still read, each with the event recorded after that combine:
   // work on another lane that writes an overlapping range waits on it first (combines run
@@ -583,6 +584,7 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles));
   RlcKey key;
   for (int i = 0; i < 8; ++i) key.k[i] = c->rd();
+  key.bits = c->rlc_bits;
   TileSums* sums;
   G1A* dec;
   uint32_t *counters, *sub_list, *leaves, *tw_list, *sw_list, *hw_list, *hl_list;
@@ -715,6 +717,7 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   HB_TRY(make_tiles(c, n_inst, offsets, &tiles, &n_tiles));
   RlcKey key;
   for (int i = 0; i < 8; ++i) key.k[i] = c->rd();
+  key.bits = c->rlc_bits;
   constexpr uint32_t LEAF_CHUNK = 1u << 15;
   const size_t n_tables = std::max<size_t>((size_t)16 * n_tiles, LEAF_CHUNK);
   SigTileSums* sums;
@@ -2022,6 +2025,13 @@ int hbtc_set_sender_tracking(hbtc_ctx* c, int enable) {
   if (!c) return HBTC_ERR_ARG;
   Guard g(c);
   c->track_senders = enable != 0;
+  return HBTC_OK;
+}
+
+int hbtc_set_rlc_bits(hbtc_ctx* c, uint32_t bits) {
+  if (!c || (bits != 64 && bits != 128)) return HBTC_ERR_ARG;
+  Guard g(c);
+  c->rlc_bits = bits;
   return HBTC_OK;
 }
 

@@ -38,6 +38,7 @@ __device__ __forceinline__ bool is_suspect(const Suspects& s, uint32_t id) {
 }
 struct RlcKey {
   uint32_t k[8];  // ChaCha20 key, fresh from the host's random source for every call
+  uint32_t bits;  // 64: r_i = a_i + b_i mu with 32-bit halves (default); 128: 64-bit halves
 };
 // Partial sums of one tile: [0..7] the 8-share sub-tiles, [8] the whole tile.  The weighted
 // sums carry the position of every share inside its group (0..7 in a sub-tile, 0..63 in the
@@ -65,8 +66,11 @@ constexpr uint32_t PLINES_FQ2 = 3 * MILLER_STEPS;
 
 // Fixed-base table of every public-key share (built once per key set, resident in HBM):
 // tab[(i * PK_TAB_WIN + w) * 256 + v] = v * 2^(8w) * pk_i (affine, v >= 1), so [a] pk_i for a
-// 32-bit a is PK_TAB_WIN = 4 mixed additions and no doublings.
-constexpr int PK_TAB_WIN = 4;
+// 32-bit a is 4 mixed additions and no doublings (windows 0..3), for a 64-bit a (128-bit RLC
+// scalars, hbtc_set_rlc_bits) 8 (windows 0..7).
+constexpr int PK_TAB_WIN = 8;
+// windows the scalar halves of an RLC call use
+__host__ __device__ constexpr int rlc_windows(uint32_t bits) { return bits == 128 ? 8 : 4; }
 struct PtXY {
   Fq x, y;
 };

@@ -192,6 +192,12 @@ int hbtc_node_set_verify_mode(hbtc_node* nd, int mode) {
   return run_devices(nd, [&](size_t d) { return hbtc_set_verify_mode(nd->ctx[d], mode); });
 }
 
+int hbtc_node_set_rlc_bits(hbtc_node* nd, uint32_t bits) {
+  if (!nd) return HBTC_ERR_ARG;
+  std::lock_guard<std::mutex> lk(nd->mu);
+  return run_devices(nd, [&](size_t d) { return hbtc_set_rlc_bits(nd->ctx[d], bits); });
+}
+
 int hbtc_node_keyset_load(hbtc_node* nd, const uint8_t* pk_c48, uint32_t n, uint32_t* keyset_id,
                           uint32_t* n_bad) {
   if (!nd || !pk_c48 || !keyset_id || n == 0) return HBTC_ERR_ARG;

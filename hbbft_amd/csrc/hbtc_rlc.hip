@@ -85,16 +85,17 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
         if (is_suspect(sus, id)) {
           st = HBTC_RLC_LEAF;  // straight to an exact check, outside the group sums
         } else {
-          const uint64_t r = rlc_scalar(key, item);
-          const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
+          uint64_t ra, rb;
+          rlc_scalar(key, item, ra, rb);
           Fq bx;  // phi(d) = (beta x, y)
           {
             Fq beta;
             fq_set(beta, G1_BETA);
             fq_mul(bx, d.x, beta);
           }
-          if (!d.inf) glv_mul_uniform(S, d, bx, ra, rb);
-          if (!pk[id].inf) rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb);
+          if (!d.inf) glv_mul_uniform(S, d, bx, ra, rb, (int)key.bits / 2);
+          if (!pk[id].inf)
+            rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb, rlc_windows(key.bits));
         }
       }
     }

@@ -59,8 +59,8 @@ __global__ void __launch_bounds__(64, W) k_sig_items(
         if (is_suspect(sus, id)) {
           st = HBTC_RLC_LEAF;  // straight to an exact check, outside the group sums
         } else {
-          const uint64_t r = rlc_scalar(key, item);
-          const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
+          uint64_t ra, rb;
+          rlc_scalar(key, item, ra, rb);
           // -psi^2(sigma) = (zeta x, y): the G2 GLV map keeps y
           Fq2 mx;
           {
@@ -69,8 +69,9 @@ __global__ void __launch_bounds__(64, W) k_sig_items(
             fq_mul(mx.c0, sg.x.c0, zeta);
             fq_mul(mx.c1, sg.x.c1, zeta);
           }
-          if (!sg.inf) glv_mul_uniform(S, sg, mx, ra, rb);
-          if (!pk[id].inf) rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb);
+          if (!sg.inf) glv_mul_uniform(S, sg, mx, ra, rb, (int)key.bits / 2);
+          if (!pk[id].inf)
+            rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb, rlc_windows(key.bits));
         }
       }
     }

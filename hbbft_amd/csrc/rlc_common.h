@@ -18,13 +18,17 @@ __device__ __forceinline__ void rlc_load_words(uint32_t* w, const uint8_t* base,
   }
 }
 
-// ChaCha20 block (RFC 8439 layout: constants, 8 key words, counter, 3 nonce words) -> the
-// two 32-bit words [2j, 2j+1] of block `ctr`, combined into the 64-bit scalar r_i.
+// The scalar r_i = a + b mu of item i from a ChaCha20 block (RFC 8439 layout: constants, 8 key
+// words, counter, 3 nonce words).  64-bit mode (key.bits = 64): a and b are the 32-bit words
+// [2j, 2j+1] of block i / 8 (j = i mod 8); 128-bit mode: a and b are the 64-bit pairs of words
+// [4j, 4j+1], [4j+2, 4j+3] of block i / 4 (j = i mod 4), under a different nonce word.
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int s) { return (x << s) | (x >> (32 - s)); }
-static __device__ uint64_t rlc_scalar(const RlcKey& key, uint64_t item) {
+static __device__ void rlc_scalar(const RlcKey& key, uint64_t item, uint64_t& a, uint64_t& b) {
+  const bool wide = key.bits == 128;
+  const uint64_t blk = wide ? item >> 2 : item >> 3;
   uint32_t st[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
                      key.k[0], key.k[1], key.k[2], key.k[3], key.k[4], key.k[5], key.k[6], key.k[7],
-                     (uint32_t)(item >> 3), (uint32_t)(item >> 35), 0x68626266u, 0x72726c63u};
+                     (uint32_t)blk, (uint32_t)(blk >> 32), 0x68626266u, wide ? 0x32313172u : 0x72726c63u};
   uint32_t x[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) x[i] = st[i];
@@ -43,15 +47,33 @@ static __device__ uint64_t rlc_scalar(const RlcKey& key, uint64_t item) {
     QR(0, 5, 10, 15) QR(1, 6, 11, 12) QR(2, 7, 8, 13) QR(3, 4, 9, 14)
   }
 #undef QR
-  const int j = (int)(item & 7);
-  uint32_t lo = 0, hi = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if (i == j) {
-      lo = x[2 * i] + st[2 * i];
-      hi = x[2 * i + 1] + st[2 * i + 1];
-    }
-  return ((uint64_t)hi << 32) | lo;
+  for (int i = 0; i < 16; ++i) x[i] += st[i];
+  if (wide) {
+    const int j = (int)(item & 3);
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i == j) {
+        w0 = x[4 * i];
+        w1 = x[4 * i + 1];
+        w2 = x[4 * i + 2];
+        w3 = x[4 * i + 3];
+      }
+    a = ((uint64_t)w1 << 32) | w0;
+    b = ((uint64_t)w3 << 32) | w2;
+  } else {
+    const int j = (int)(item & 7);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i == j) {
+        lo = x[2 * i];
+        hi = x[2 * i + 1];
+      }
+    a = lo;
+    b = hi;
+  }
 }
 
 // Append the wave's tracked-sender items to the leaf list: one atomic per wave.  Called by all
@@ -237,11 +259,13 @@ __device__ __forceinline__ void rlc_reduce_sp(G1J* redA, G1J* redB, const G1J& S
   __syncthreads();
 }
 
-// [a] pk + [b] phi(pk) from the key set's fixed-base table (8 mixed additions, no doublings).
-static __device__ void rlc_pk_mul(G1J& r, const PtXY* __restrict__ tab, uint32_t a, uint32_t b) {
+// [a] pk + [b] phi(pk) from the key set's fixed-base table (2 nwin mixed additions, no
+// doublings; nwin = 4 for 32-bit a, b, 8 for 64-bit).
+static __device__ void rlc_pk_mul(G1J& r, const PtXY* __restrict__ tab, uint64_t a, uint64_t b,
+                                  int nwin) {
   jac_set_inf(r);
-#pragma unroll
-  for (int w = 0; w < PK_TAB_WIN; ++w) {
+#pragma unroll 1
+  for (int w = 0; w < nwin; ++w) {
     const uint32_t va = (a >> (8 * w)) & 0xffu, vb = (b >> (8 * w)) & 0xffu;
     if (va) {
       const PtXY e = tab[w * 256 + va];

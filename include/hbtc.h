@@ -308,6 +308,8 @@ const char* hbtc_node_last_error(hbtc_node* node);
 int hbtc_node_devices(hbtc_node* node);
 hbtc_ctx* hbtc_node_context(hbtc_node* node, int device_slot);
 int hbtc_node_set_verify_mode(hbtc_node* node, int mode);
+/* hbtc_set_rlc_bits on every device of the node. */
+int hbtc_node_set_rlc_bits(hbtc_node* node, uint32_t bits);
 int hbtc_node_keyset_load(hbtc_node* node, const uint8_t* pk_shares_c48, uint32_t n,
                           uint32_t* keyset_id, uint32_t* n_bad);
 int hbtc_node_keyset_free(hbtc_node* node, uint32_t keyset_id);
@@ -367,17 +369,26 @@ int hbtc_shard_instances(uint32_t n_dev, uint32_t n_inst, const uint32_t* offset
 
 /* ---- verification strategy ----------------------------------------------------------------- */
 /* HBTC_MODE_RLC (default): shares of one instance are checked together by a random linear
- * combination (fresh 64-bit ChaCha20 scalars per call, prime-order points only) in groups of
+ * combination (fresh ChaCha20 scalars per call, 64-bit by default, 128-bit with
+ * hbtc_set_rlc_bits; prime-order points only) in groups of
  * 64 consecutive shares; failing groups are split 64 -> 8 -> 1 share; a group with exactly one
  * wrong share is resolved by a position-weighted second combination (the wrong share located
  * without per-share pairings), the rest get the exact pairing check.  The decisions equal the
  * per-share decisions except with probability <= 2^-64 per group check (<= 2^-58 per located
- * group).
+ * group); <= 2^-128 (2^-122) with 128-bit scalars.
  * HBTC_MODE_PER_SHARE: every share gets its own 2-pair pairing check (the reference's count).
  * Applies to hbtc_verify_dec_shares[_dev]. */
 #define HBTC_MODE_PER_SHARE 0
 #define HBTC_MODE_RLC 1
 int hbtc_set_verify_mode(hbtc_ctx* ctx, int mode);
+/* Size of the RLC scalars r_i = a_i + b_i mu (mu = -x^2 mod r, the GLV eigenvalue; DESIGN.md §4,
+ * "Soundness"): 64 (default: 32-bit halves, 2^64 distinct scalars, a wrong share survives a group
+ * check with probability <= 2^-64, <= 2^-58 per located group) or 128 (64-bit halves, 2^128
+ * distinct scalars: <= 2^-128 per group check, <= 2^-122 per located group, matching BLS12-381's
+ * ~2^-128 security level; the item passes do twice the doublings and table additions).  Any
+ * other value: HBTC_ERR_ARG.  Applies to the RLC calls of hbtc_verify_dec_shares[_dev] and
+ * hbtc_verify_sig_shares[_dev]. */
+int hbtc_set_rlc_bits(hbtc_ctx* ctx, uint32_t bits);
 /* Sender tracking (default on, RLC mode): a sender with many shares REJECTed (at least 1/8 of
  * the call's average shares per sender) by one of the last 16 RLC calls on a key set has its
  * shares checked one by one, outside the group sums, so f Byzantine senders who lie in every

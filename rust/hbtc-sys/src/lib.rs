@@ -104,6 +104,11 @@ impl Context {
         self.ok(unsafe { ffi::hbtc_set_verify_mode(self.raw, mode) })
     }
 
+    /// RLC scalar size: 64 (default) or 128 bits (soundness 2^-64 / 2^-128 per group check).
+    pub fn set_rlc_bits(&self, bits: u32) -> Result<()> {
+        self.ok(unsafe { ffi::hbtc_set_rlc_bits(self.raw, bits) })
+    }
+
     /// PublicKeyShare::verify for every SignatureShare of every coin instance (H = hash_g2(nonce)).
     pub fn verify_sig_shares(&self, keyset: u32, h_c96: &[u8], b: &Batch) -> Result<Vec<i32>> {
         b.check(96);

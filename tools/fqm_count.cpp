@@ -142,6 +142,21 @@ int main() {
   jac_dbl(ts, ts);
   const unsigned long long jdbl = hbtc_fqm_count;
   const unsigned long long rlc_item = rlc_item_mults + (2 * (189 * jadd + 57 * jdbl) + 63) / 64;
+  // 128-bit RLC scalars (hbtc_set_rlc_bits): 64-bit halves, so 32 more doublings and 32 more
+  // mixed additions in the joint double-and-add (half the bits set) and 8 more table additions
+  // (4 with phi)
+  unsigned long long rlc_item_128 = 0;
+  {
+    hbtc_fqm_count = 0;
+    G1J tm = rd;
+    jac_add_aff(tm, tm, gen1);
+    const unsigned long long madd1 = hbtc_fqm_count;
+    hbtc_fqm_count = 0;
+    G1A pq;
+    g1_phi(pq, gen1);
+    const unsigned long long phi1 = hbtc_fqm_count;
+    rlc_item_128 = rlc_item + 32 * jdbl + 32 * madd1 + 8 * madd1 + 4 * phi1;
+  }
   // SignatureShare RLC item (k_sig_items): G2 decode + subgroup test, -psi^2(sigma) = (zeta x, y)
   // (2 Fqm), r * sigma = [a] sigma + [b] (-psi^2 sigma) (joint 32-bit double-and-add in G2, 16 of
   // 32 bits set per half), r * pk from the fixed-base table (8 G1 mixed additions + 4 phi), and
@@ -243,7 +258,7 @@ int main() {
          sig_decode, mlfv, fe, sig_decode + mlfv + fe);
   printf("  \"g1_combine_item\": %llu,\n  \"g2_combine_item\": %llu,\n", comb1, comb2);
   printf("  \"g1_msm_combine\": %llu,\n", msm_combine);
-  printf("  \"rlc_item\": %llu,\n  \"sig_rlc_item\": %llu,\n  \"rlc_group_check\": %llu\n}\n", rlc_item,
-         sig_rlc_item, rlc_group);
+  printf("  \"rlc_item\": %llu,\n  \"rlc_item_128\": %llu,\n  \"sig_rlc_item\": %llu,\n"
+         "  \"rlc_group_check\": %llu\n}\n", rlc_item, rlc_item_128, sig_rlc_item, rlc_group);
   return 0;
 }
