@@ -730,8 +730,9 @@ def _all_master_r(args, ep):
 def adversarial_line(ctx, args, base):
     """The same configuration under BFT's worst case: f = 333 Byzantine senders send wrong
     shares on every ciphertext (33 % of all shares, concentrated by sender).  A fresh key set,
-    so the first epoch finds the liars through failing groups (reported as first_epoch_ms);
-    the timed steps then run with the liars tracked (hbtc_set_sender_tracking, default on)."""
+    so the first epoch's call starts with a probe pass over its first ciphertexts that finds the
+    liars (reported as first_epoch_ms); the timed steps then run with the liars tracked
+    (hbtc_set_sender_tracking, default on)."""
     base.free(ctx)
     ep = Epoch(ctx, args.n, args.cts, SEED, 0.0, "senders")
     ctx.sync()
@@ -740,8 +741,8 @@ def adversarial_line(ctx, args, base):
     ctx.sync()
     first = time.perf_counter() - t0
     first_leaves = ctx.rlc_last_leaves() if args.mode == "rlc" else ep.total
-    steps = max(1, min(args.steps, 2))
-    elapsed = timed(ctx, ep, steps, 0)
+    steps = max(1, min(args.steps, 6))
+    elapsed = timed(ctx, ep, steps, 1)
     per = {f: round(ctx.timing_read(f)[0] / steps, 3) for f in FAMS if ctx.timing_read(f)[1]}
     leaves = ctx.rlc_last_leaves() if args.mode == "rlc" else ep.total
     mism, comb_ok, n_acc = ep.check(ctx)

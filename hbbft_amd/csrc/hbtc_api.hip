@@ -125,6 +125,8 @@ struct hbtc_ctx {
   int verify_mode = HBTC_MODE_RLC;
   bool track_senders = true;
   uint32_t rlc_bits = 64;  // hbtc_set_rlc_bits
+  bool probe_cold = true;  // probe pass on a cold key set (HBTC_PROBE=0: off)
+  uint64_t probes = 0;     // probe passes run
   const uint32_t* last_leaf_count = nullptr;  // device counter of the last RLC call
   // Device ranges that combines still read, each with the event recorded after that combine:
   // work on another lane that writes an overlapping range waits on it first (combines run
@@ -542,6 +544,19 @@ int check_mode(hbtc_ctx* c, uint32_t n_tiles) {
 }
 
 // ---------------------------------------------------------------- device-pointer cores
+// The per-ciphertext G2 preparation of a DecryptionShare call (decoded H / w, statuses, lines).
+struct G2Prep {
+  const G2A* h_aff;
+  const int32_t* h_st;
+  const Line* h_lines;
+  const G2A* w_aff;
+  const int32_t* w_st;
+  const Line* w_lines;
+};
+uint32_t probe_size(const hbtc_ctx* c, const Keyset* ks, uint32_t n_ct);
+int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets,
+                 const uint32_t* d_idx, const uint8_t* d_share, int32_t* d_status, const G2Prep& pp);
+
 int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t* d_H,
                    const uint8_t* d_w, const uint32_t* offsets, const uint32_t* d_idx,
                    const uint8_t* d_share, int32_t* d_status) {
@@ -581,6 +596,47 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   w_aff = h_aff + n_ct;
   w_st = h_st + n_ct;
   w_lines = h_lines + (size_t)n_ct * MILLER_STEPS;
+  const G2Prep prep{h_aff, h_st, h_lines, w_aff, w_st, w_lines};
+  // Cold key set (no RLC call on it yet, sender tracking on): a probe pass over the first
+  // ciphertexts finds the senders who lie on all of them before the call proper, so f Byzantine
+  // senders do not send most of the first epoch's shares to the exact checks.
+  const uint32_t n_probe = probe_size(c, ks, n_ct);
+  if (n_probe) {
+    HB_TRY(rlc_dec_pass(c, ks, n_probe, offsets, d_idx, d_share, nullptr, prep));
+    ++c->probes;
+  }
+  HB_TRY(rlc_dec_pass(c, ks, n_ct, offsets, d_idx, d_share, d_status, prep));
+  return end_verify(c);
+}
+
+// Instances of a call's probe pass: n_ct / 16 (at most 64) on a cold key set, else 0.
+uint32_t probe_size(const hbtc_ctx* c, const Keyset* ks, uint32_t n_ct) {
+  if (!c->track_senders || !c->probe_cold || ks->calls != 0 || n_ct < 32) return 0;
+  return std::min<uint32_t>(64u, n_ct / 16u);
+}
+
+// One RLC pass over instances [0, n_ct) of a call whose G2 preparation is `pp`: tiles, item pass,
+// group-check levels, leaves, final statuses into d_status.  d_status == nullptr: the probe pass
+// (statuses into scratch, its own workspace: only its sender-tracking counts matter).
+int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets,
+                 const uint32_t* d_idx, const uint8_t* d_share, int32_t* d_status, const G2Prep& pp) {
+  const bool probe = d_status == nullptr;
+  const uint32_t n_items = offsets[n_ct];
+  const std::string suffix0 = c->ws_suffix;
+  struct Restore {
+    hbtc_ctx* c;
+    std::string s;
+    ~Restore() { c->ws_suffix = s; }
+  } restore{c, suffix0};
+  if (probe) {
+    c->ws_suffix = suffix0 + ".probe";
+    HB_TRY(wst(c, "rlc.status", n_items, &d_status));
+  }
+  const G2A *h_aff = pp.h_aff, *w_aff = pp.w_aff;
+  const int32_t *h_st = pp.h_st, *w_st = pp.w_st;
+  const Line *h_lines = pp.h_lines, *w_lines = pp.w_lines;
+  Tile* tiles;
+  uint32_t n_tiles;
   HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles));
   RlcKey key;
   for (int i = 0; i < 8; ++i) key.k[i] = c->rd();
@@ -591,11 +647,15 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   Fq2 *t_tiles, *t_subs, *t_halves;
   HB_TRY(wst(c, "rlc.sums", n_tiles, &sums));
   // two alternating buffers: a combine of the previous call may still read the other one
-  c->lanes[c->lane].dec_flip ^= 1;
-  HB_TRY(wst(c, c->lanes[c->lane].dec_flip ? "rlc.dec1" : "rlc.dec0", n_items, &dec));
-  HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
-  HB_TRY(guard_write(c, dec, (size_t)n_items * sizeof(G1A)));
-  c->last_dec = {d_status, d_share, n_items, dec, nullptr};
+  if (probe) {
+    HB_TRY(wst(c, "rlc.dec0", n_items, &dec));
+  } else {
+    c->lanes[c->lane].dec_flip ^= 1;
+    HB_TRY(wst(c, c->lanes[c->lane].dec_flip ? "rlc.dec1" : "rlc.dec0", n_items, &dec));
+    HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
+    HB_TRY(guard_write(c, dec, (size_t)n_items * sizeof(G1A)));
+    c->last_dec = {d_status, d_share, n_items, dec, nullptr};
+  }
   // counters: [0] leaves, [1] listed tiles (half / sub-tile pass), [2] failing tiles, [3] failing
   // subs, [4] failing halves, [5] listed halves
   HB_TRY(wst(c, "rlc.counters", 6, &counters));
@@ -671,14 +731,13 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
     return launch_chk_leaves(c->stream, n_items, leaf_count, leaves, d_idx, dec, ks->pk, h_aff,
                              h_lines, w_aff, w_lines, d_status);
   }));
-  c->last_leaf_count = leaf_count;
-  HB_TRY(timed(c, "rlc_finalize", [&] {
+  if (!probe) c->last_leaf_count = leaf_count;
+  return timed(c, "rlc_finalize", [&] {
     return launch_rlc_finalize(c->stream, n_tiles, tiles, h_st, w_st, d_status, d_idx, ks->n,
                                ks->rejects + (size_t)c->lane * ks->n,
                                const_cast<uint32_t*>(sus.last_bad), sus.now,
                                track_threshold(ks, n_items));
-  }));
-  return end_verify(c);
+  });
 }
 
 int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8_t* d_H,
@@ -1149,6 +1208,7 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (const char* e = getenv("HBTC_ITEMS_SERIAL")) c->items_serial = atoi(e) != 0;
   if (const char* e = getenv("HBTC_G2_GLS")) c->g2_gls = atoi(e) != 0;
   if (const char* e = getenv("HBTC_G1_GLV")) c->g1_glv = atoi(e) != 0;
+  if (const char* e = getenv("HBTC_PROBE")) c->probe_cold = atoi(e) != 0;
   if (const char* e = getenv("HBTC_CHECK_MODE")) {
     const std::string m(e);
     c->check_mode_forced = m == "plain" ? 0 : m == "pair3" ? 1 : m == "pair2" ? 2 : -1;

@@ -49,6 +49,9 @@ namespace hbtc {
 // here and contribute the identity; a ciphertext whose own H / w failed to decode is resolved
 // by k_rlc_finalize.  Needs nothing from the per-ciphertext preparation, so it runs
 // concurrently with k_g2_prepare on another stream.
+#ifndef HBTC_ITEMS_PRIO
+#define HBTC_ITEMS_PRIO 0  // wave priority of the item pass (experiments: 3 = above the check levels)
+#endif
 #ifndef HBTC_ITEMS_WAVES
 #define HBTC_ITEMS_WAVES 2  // minimum waves per SIMD the register allocation must allow (1: 153 ms, 2: 86 ms, 3: 161 ms per C3 launch)
 #endif
@@ -58,6 +61,9 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
     const int32_t* __restrict__ pk_status, const PtXY* __restrict__ pk_tab, uint32_t n_pk,
     RlcKey key, Suspects sus, TileSums* __restrict__ sums, G1A* __restrict__ dec,
     int32_t* __restrict__ status) {
+#if HBTC_ITEMS_PRIO > 0
+  __builtin_amdgcn_s_setprio(HBTC_ITEMS_PRIO);
+#endif
   __shared__ G1J redA[64];
   __shared__ G1J redB[64];
   const Tile tile = tiles[blockIdx.x];
