@@ -18,7 +18,8 @@ MSM_PARTS := 8 9
 SKG_PARTS := 10
 KOBJS := $(foreach p,$(PARTS),$(BUILD)/hbtc_kernels.p$(p).o) $(foreach p,$(RLC_PARTS),$(BUILD)/hbtc_rlc.p$(p).o) \
          $(foreach p,$(MSM_PARTS),$(BUILD)/hbtc_msm.p$(p).o) $(foreach p,$(SKG_PARTS),$(BUILD)/hbtc_skg.p$(p).o) \
-         $(BUILD)/hbtc_check.c1.o $(BUILD)/hbtc_check.c2.o $(BUILD)/hbtc_sig.o $(BUILD)/hbtc_bcast.o
+         $(BUILD)/hbtc_check.c1.o $(BUILD)/hbtc_check.c2.o $(BUILD)/hbtc_sig.o $(BUILD)/hbtc_pb.o \
+         $(BUILD)/hbtc_bcast.o
 LIB := hbbft_amd/libhbtc.so
 
 .PHONY: all lib hosttest oracle clean resources roofline-constants
@@ -65,6 +66,10 @@ $(BUILD)/hbtc_check.c%.o: $(CSRC)/hbtc_check.hip $(HDRS) | $(BUILD)
 
 # the G2 item pass, all helpers inlined (no calls; the product itself stays out of line)
 $(BUILD)/hbtc_sig.o: $(CSRC)/hbtc_sig.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DHBTC_INLINE_ALL -c $< -o $@
+
+# the pair-batch item pass (Ciphertext::verify / PublicKey::verify by RLC), helpers inlined
+$(BUILD)/hbtc_pb.o: $(CSRC)/hbtc_pb.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_INLINE_ALL -c $< -o $@
 
 # Reliable Broadcast: Reed-Solomon over GF(2^8), SHA3 Merkle trees and proofs

@@ -473,7 +473,7 @@ def bench_skg(ctx, n, n_parts, n_distinct, steps, warmup, cpu_budget=0.0):
     t_parts[0] = t_dec[0] = 0.0
     elapsed = timed_steps(ctx, step, steps, 0)
     per = breakdown(ctx, steps, ["skg_scalars", "skg_ack_rows", "comb_decode", "comb_digits",
-                                 "combine", "mul", "hash", "pair_verify"])
+                                 "combine", "mul", "hash", "pb_items", "pb_lines", "pb_ml", "pb_checks", "pair_verify"])
     pm = int((pst != part_expect).sum())
     am = int((ast != ack_expect).sum()) + int((ack_dst != N.ACCEPT).sum())
     if pm or am:

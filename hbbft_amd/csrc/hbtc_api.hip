@@ -1372,6 +1372,72 @@ int hbtc_verify_sig_shares(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, con
   return sync(c);
 }
 
+// e(A_i, Q_i) == e(G1, W_i) for n items in device memory (A null: the G1 generator; Q trusted:
+// our own hash output, decoded without the subgroup check; statuses ACCEPT / REJECT /
+// DECODE_ERR as k_pair_verify's).  RLC mode: the pair-batch path of hbtc_pb.hip in chunks of
+// PB_CHUNK items (the per-item line tables are 19.6 KB each): item pass, Q line tables, partial
+// Miller products per 8-item sub-tile, the 64-item tile checks, the 8-item sub-tiles of failing tiles, the exact k_pair_verify of the
+// items of failing sub-tiles.  Per-share mode: k_pair_verify for every item.
+constexpr uint32_t PB_CHUNK = 1u << 18;
+int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_q, bool q_trusted,
+                  const uint8_t* d_w, int32_t* d_status) {
+  if (c->verify_mode == HBTC_MODE_PER_SHARE) {
+    return timed(c, "pair_verify", [&] {
+      return launch_pair_verify(c->stream, n, d_a, d_q, nullptr, d_w, d_status);
+    });
+  }
+  for (uint32_t base = 0; base < n; base += PB_CHUNK) {
+    const uint32_t m = std::min(PB_CHUNK, n - base);
+    const uint32_t T = (m + 63) / 64;
+    G1A* rA;
+    G2A* qdec;
+    SigTileSums* sums;
+    Fq2 *qtab, *wtab, *fbuf;
+    uint32_t *winf, *counters, *tlist, *leaves;
+    HB_TRY(wst(c, "pb.ra", m, &rA));
+    HB_TRY(wst(c, "pb.qdec", m, &qdec));
+    HB_TRY(wst(c, "pb.sums", T, &sums));
+    HB_TRY(wst(c, "pb.qtab", (size_t)m * PLINES_FQ2, &qtab));
+    HB_TRY(wst(c, "pb.wtab", (size_t)8 * T * PLINES_FQ2, &wtab));
+    HB_TRY(wst(c, "pb.winf", (size_t)8 * T, &winf));
+    HB_TRY(wst(c, "pb.fbuf", (size_t)8 * T * 6, &fbuf));
+    HB_TRY(wst(c, "pb.counters", 2, &counters));
+    HB_TRY(wst(c, "pb.tlist", T, &tlist));
+    HB_TRY(wst(c, "pb.leaves", m, &leaves));
+    const uint8_t* a = d_a ? d_a + (size_t)48 * base : nullptr;
+    const uint8_t* q = d_q + (size_t)96 * base;
+    const uint8_t* w = d_w + (size_t)96 * base;
+    int32_t* st = d_status + base;
+    RlcKey key;
+    for (int i = 0; i < 8; ++i) key.k[i] = c->rd();
+    key.bits = c->rlc_bits;
+    HB_CHECK(c, launch_zero_u32(c->stream, counters, 2));
+    HB_TRY(timed(c, "pb_items", [&] {
+      return launch_pb_items(c->stream, m, a, q, q_trusted, w, key, rA, qdec, sums, st);
+    }));
+    HB_TRY(timed(c, "pb_lines", [&] { return launch_pb_lines(c->stream, m, qdec, st, qtab); }));
+    HB_TRY(timed(c, "pb_ml", [&] { return launch_pb_ml(c->stream, m, rA, qtab, st, fbuf); }));
+    HB_TRY(timed(c, "pb_checks", [&] {
+      const hipError_t e = launch_plines(c->stream, 3, T, 0, nullptr, nullptr, nullptr, sums, nullptr,
+                                         wtab, winf);
+      if (e != hipSuccess) return e;
+      return launch_pb_fe(c->stream, 0, T, m, T, nullptr, nullptr, fbuf, wtab, winf, st, counters,
+                          tlist);
+    }));
+    HB_TRY(timed(c, "pb_checks", [&] {
+      const hipError_t e = launch_plines(c->stream, 4, 8 * T, 0, counters, tlist, nullptr, sums,
+                                         nullptr, wtab, winf);
+      if (e != hipSuccess) return e;
+      return launch_pb_fe(c->stream, 1, 8 * T, m, 0, counters, tlist, fbuf, wtab, winf, st,
+                          counters + 1, leaves);
+    }));
+    HB_TRY(timed(c, "pair_verify", [&] {
+      return launch_pair_verify(c->stream, m, a, q, nullptr, w, st, leaves, counters + 1);
+    }));
+  }
+  return HBTC_OK;
+}
+
 int hbtc_verify_sigs(hbtc_ctx* c, uint32_t n, const uint8_t* pk, const uint8_t* H,
                      const uint8_t* sig, int32_t* status) {
   if (!c || (n && (!pk || !H || !sig || !status))) return HBTC_ERR_ARG;
@@ -1383,10 +1449,8 @@ int hbtc_verify_sigs(hbtc_ctx* c, uint32_t n, const uint8_t* pk, const uint8_t* 
   HB_TRY(upload(c, "in2", sig, (size_t)96 * n, &d_sig));
   HB_TRY(ws(c, "out0", (size_t)4 * n, &d_st));
   // e(pk, H) == e(G1, sig)
-  HB_TRY(timed(c, "pair_verify", [&] {
-    return launch_pair_verify(c->stream, n, (const uint8_t*)d_pk, (const uint8_t*)d_H, nullptr,
-                              (const uint8_t*)d_sig, (int32_t*)d_st);
-  }));
+  HB_TRY(pb_verify_dev(c, n, (const uint8_t*)d_pk, (const uint8_t*)d_H, false, (const uint8_t*)d_sig,
+                       (int32_t*)d_st));
   HB_TRY(download(c, status, d_st, (size_t)4 * n));
   return sync(c);
 }
@@ -1401,11 +1465,9 @@ int hbtc_verify_ciphertexts(hbtc_ctx* c, uint32_t n, const uint8_t* u, const uin
   HB_TRY(upload(c, "in1", H, (size_t)96 * n, &d_H));
   HB_TRY(upload(c, "in2", w, (size_t)96 * n, &d_w));
   HB_TRY(ws(c, "out0", (size_t)4 * n, &d_st));
-  // e(G1, w) == e(u, H)
-  HB_TRY(timed(c, "pair_verify", [&] {
-    return launch_pair_verify(c->stream, n, nullptr, (const uint8_t*)d_w, (const uint8_t*)d_u,
-                              (const uint8_t*)d_H, (int32_t*)d_st);
-  }));
+  // e(G1, w) == e(u, H), checked as e(u, H) == e(G1, w)
+  HB_TRY(pb_verify_dev(c, n, (const uint8_t*)d_u, (const uint8_t*)d_H, false, (const uint8_t*)d_w,
+                       (int32_t*)d_st));
   HB_TRY(download(c, status, d_st, (size_t)4 * n));
   return sync(c);
 }
@@ -2217,10 +2279,9 @@ int hbtc_decrypt(hbtc_ctx* c, uint32_t n, const uint8_t* sk_le32, const uint8_t*
   HB_TRY(ws(c, "out0", (size_t)4 * n, &d_st));
   HB_TRY(ws(c, "out1", (size_t)48 * n, &d_g));
   HB_TRY(ws(c, "out2", (size_t)4 * n, &d_gst));
-  HB_TRY(timed(c, "pair_verify", [&] {
-    return launch_pair_verify(c->stream, n, nullptr, (const uint8_t*)d_w, (const uint8_t*)d_u,
-                              (const uint8_t*)d_H, (int32_t*)d_st);
-  }));
+  // H is this call's own hash output (cofactor cleared: in the subgroup by construction)
+  HB_TRY(pb_verify_dev(c, n, (const uint8_t*)d_u, (const uint8_t*)d_H, true, (const uint8_t*)d_w,
+                       (int32_t*)d_st));
   HB_TRY(timed(c, "mul", [&] {
     return launch_point_mul(c->stream, 1, n, (const uint8_t*)d_u, 1, (const uint8_t*)d_k, 0,
                             (uint8_t*)d_g, (int32_t*)d_gst);

@@ -779,4 +779,179 @@ hipError_t launch_sigchk_leaves(hipStream_t s, uint32_t base, uint32_t chunk,
 
 #endif
 
+#if HBTC_CHECK_IN(1)
+// ------------------------------------------------------------------------------ pair batches
+// e(A_i, Q_i) == e(G1, W_i) batches (hbtc_pb.hip).  A group's value is
+//     FE( conj( prod_i f_{|x|,Q_i}(r_i A_i) * f_{|x|,W}(-G1) ) ),  W = the group's sum of r_i W_i:
+// every pair is an affine G1 point with a projective line table.  The Miller loops are cut by
+// 8-item sub-tile so a batch yields enough independent chains to fill the chip: k_pb_ml runs one
+// 6-lane group per sub-tile (its items' pairs share the 63 squarings) and stores the partial
+// product; k_pb_fe runs one group per checked group: the product of its partials (a tile: 8),
+// the Miller loop of its W sum at -G1, the final exponentiation.  Level 0: the 64-item tiles;
+// level 1: the 8 sub-tiles of failing tiles (their partials are reused).  A passing group
+// ACCEPTs its pending items; a failing tile is listed for level 1, a failing sub-tile's pending
+// items for the exact per-item checks.
+constexpr uint32_t PB_GROUPS_PER_WAVE = 10;
+
+namespace {
+// f *= prod_{p < bound} line_p: the pair loader sets, per lane, the line's A (Fq2, every lane),
+// `prod` (lanes 0, 1: C.c{k} y; lanes 2, 3: B.c{k-2} x; zero elsewhere) and whether pair p is
+// used; `bound` is wave-uniform (groups with fewer pairs mark the rest unused).  The 63
+// squarings are shared by all pairs.  Unconjugated (x < 0: the caller conjugates the product).
+template <class Loader>
+__device__ __forceinline__ void pb_miller(Fq2& f, uint32_t bound, const Loader& load, const Pos& ps) {
+  gt::set_one(f, ps);
+  int j = 0;
+  bool first = true;
+#pragma unroll 1
+  for (int bit = 62; bit >= 0; --bit) {
+    const bool add = ((BLS_X_ABS >> bit) & 1ull) != 0;
+#pragma unroll 1
+    for (int rep = 0; rep < (add ? 2 : 1); ++rep) {
+      if (rep == 0 && !first) gt::sqr(f, f, ps);
+      first = false;
+#pragma unroll 1
+      for (uint32_t p = 0; p < bound; ++p) {
+        Fq2 A;
+        Fq prod;
+        bool u;
+        load(p, j, A, prod, u);
+        gt::mul_line_t<true, true>(f, prod, 0, A, prod, 2, prod, 0, u, ps);
+      }
+      ++j;
+    }
+  }
+}
+
+// The per-lane line values of one pair at step j: table L (3 Fq2 per step), affine point (x, y).
+__device__ __forceinline__ void pb_line_values(const Fq2* L, const Fq& x, const Fq& y, bool u,
+                                               uint32_t k, Fq2& A, Fq& prod) {
+  fq2_zero(A);
+  fq_zero(prod);
+  if (u) {
+    A = L[0];
+    const Fq2& BC = k < 2 ? L[2] : L[1];
+    const Fq& m = (k & 1u) ? BC.c1 : BC.c0;
+    fq_mul(prod, m, k < 2 ? y : x);
+    if (k >= 4) fq_zero(prod);
+  }
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
+}  // namespace
+
+// Partial Miller products of the 8-item sub-tiles: group g = items [8g, 8g + 8) of the chunk.
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_pb_ml(uint32_t n_items, const G1A* __restrict__ rA,
+                                                           const Fq2* __restrict__ qtab,
+                                                           const int32_t* __restrict__ status,
+                                                           Fq2* __restrict__ fbuf) {
+  HBTC_LATENCY_PRIO();
+  const uint32_t n_groups = (n_items + 7u) / 8u;
+  if (blockIdx.x * PB_GROUPS_PER_WAVE >= n_groups) return;  // wave-uniform
+  const Pos ps = gt::pos();
+  const uint32_t slot = gt::lane_id() / 6u;
+  const uint32_t g = blockIdx.x * PB_GROUPS_PER_WAVE + slot;
+  const bool active = slot < PB_GROUPS_PER_WAVE && g < n_groups;
+  const uint32_t lo = active ? 8u * g : 0u;
+  const uint32_t cnt = active ? min(8u, n_items - lo) : 0u;
+  uint32_t use = 0;  // pending items whose r A is finite (A = O or Q = O: the pair is 1)
+  for (uint32_t q = 0; q < cnt; ++q)
+    if (status[lo + q] == HBTC_RLC_PENDING && !rA[lo + q].inf) use |= 1u << q;
+  const uint32_t k = ps.k;
+  Fq2 f;
+  pb_miller(f, wave_max(cnt), [&](uint32_t p, int j, Fq2& A, Fq& prod, bool& u) {
+    u = ((use >> p) & 1u) != 0;
+    const uint32_t i = lo + (u ? p : 0u);
+    pb_line_values(qtab + ((size_t)i * MILLER_STEPS + j) * 3, rA[i].x, rA[i].y, u, k, A, prod);
+  }, ps);
+  if (active) fbuf[(size_t)g * 6 + k] = f;
+}
+
+// Group checks from the partials: level 0 group g = tile g (partials 8g .. 8g + 7); level 1
+// group g = sub-tile g & 7 of tile list[g >> 3] (one partial).
+template <int LEVEL>
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_pb_fe(
+    uint32_t n_items, uint32_t n_direct, const uint32_t* __restrict__ n_listed,
+    const uint32_t* __restrict__ list, const Fq2* __restrict__ fbuf, const Fq2* __restrict__ wtab,
+    const uint32_t* __restrict__ winf, int32_t* __restrict__ status, uint32_t* __restrict__ out_count,
+    uint32_t* __restrict__ out_list) {
+  HBTC_LATENCY_PRIO();
+  const uint32_t n_groups = LEVEL == 0 ? n_direct : *n_listed * 8u;
+  if (blockIdx.x * PB_GROUPS_PER_WAVE >= n_groups) return;  // wave-uniform
+  const Pos ps = gt::pos();
+  const uint32_t slot = gt::lane_id() / 6u;
+  const uint32_t g = blockIdx.x * PB_GROUPS_PER_WAVE + slot;
+  const bool active = slot < PB_GROUPS_PER_WAVE && g < n_groups;
+  const uint32_t k = ps.k;
+  uint32_t t = 0, s0 = 0, ns = 0;  // partials [s0, s0 + ns)
+  if (active) {
+    t = LEVEL == 0 ? g : list[g >> 3];
+    s0 = LEVEL == 0 ? 8u * t : 8u * t + (g & 7u);
+    const uint32_t n_subs = (n_items + 7u) / 8u;
+    ns = s0 < n_subs ? min(LEVEL == 0 ? 8u : 1u, n_subs - s0) : 0u;
+  }
+  const bool w_use = active && winf[g] == 0;
+  Fq gx, ngy;  // -G1
+  fq_set(gx, G1_GEN_X);
+  fq_set(ngy, G1_GEN_Y);
+  fq_neg(ngy, ngy);
+  const Fq2* wt = wtab + (size_t)g * PLINES_FQ2;
+  Fq2 f;
+  pb_miller(f, 1u, [&](uint32_t, int j, Fq2& A, Fq& prod, bool& u) {
+    u = w_use;
+    pb_line_values(wt + 3 * j, gx, ngy, u, k, A, prod);
+  }, ps);
+#pragma unroll 1
+  for (uint32_t s = 0; s < wave_max(ns); ++s) {
+    Fq2 x;
+    gt::set_one(x, ps);
+    if (s < ns) x = fbuf[(size_t)(s0 + s) * 6 + k];
+    gt::mul(f, f, x, ps);
+  }
+  gt::conj(f, ps);
+  Fq2 e;
+  gt::final_exp(e, f, ps);
+  const bool ok = gt::is_one(e, ps);
+  if (!active) return;
+  const uint32_t lo = 8u * s0, hi = min(n_items, 8u * (s0 + ns));
+  if (ok) {
+    for (uint32_t q = lo + k; q < hi; q += 6u)
+      if (status[q] == HBTC_RLC_PENDING) status[q] = HBTC_ACCEPT;
+  } else if (LEVEL == 0) {
+    if (k == 0) out_list[atomicAdd(out_count, 1u)] = t;
+  } else if (k == 0) {
+    for (uint32_t q = lo; q < hi; ++q)
+      if (status[q] == HBTC_RLC_PENDING) out_list[atomicAdd(out_count, 1u)] = q;
+  }
+}
+
+hipError_t launch_pb_ml(hipStream_t s, uint32_t n_items, const G1A* rA, const Fq2* qtab,
+                        const int32_t* status, Fq2* fbuf) {
+  if (n_items == 0) return hipSuccess;
+  const uint32_t groups = (n_items + 7u) / 8u;
+  hipLaunchKernelGGL(k_pb_ml, dim3((groups + PB_GROUPS_PER_WAVE - 1) / PB_GROUPS_PER_WAVE), dim3(64), 0, s,
+                     n_items, rA, qtab, status, fbuf);
+  return hipGetLastError();
+}
+
+hipError_t launch_pb_fe(hipStream_t s, int level, uint32_t max_groups, uint32_t n_items,
+                        uint32_t n_direct, const uint32_t* n_listed, const uint32_t* list,
+                        const Fq2* fbuf, const Fq2* wtab, const uint32_t* winf, int32_t* status,
+                        uint32_t* out_count, uint32_t* out_list) {
+  if (max_groups == 0) return hipSuccess;
+  const dim3 grid((max_groups + PB_GROUPS_PER_WAVE - 1) / PB_GROUPS_PER_WAVE);
+  if (level == 0)
+    hipLaunchKernelGGL(k_pb_fe<0>, grid, dim3(64), 0, s, n_items, n_direct, n_listed, list, fbuf, wtab,
+                       winf, status, out_count, out_list);
+  else
+    hipLaunchKernelGGL(k_pb_fe<1>, grid, dim3(64), 0, s, n_items, n_direct, n_listed, list, fbuf, wtab,
+                       winf, status, out_count, out_list);
+  return hipGetLastError();
+}
+#endif
+
 }  // namespace hbtc

@@ -166,7 +166,28 @@ hipError_t launch_sig_verify(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
                              const int32_t* pk_status, uint32_t n_pk, const G2A* h_aff,
                              const int32_t* h_status, const Line* h_lines, int32_t* status);
 hipError_t launch_pair_verify(hipStream_t s, uint32_t n, const uint8_t* a1, const uint8_t* a2,
-                              const uint8_t* b1, const uint8_t* b2, int32_t* status);
+                              const uint8_t* b1, const uint8_t* b2, int32_t* status,
+                              const uint32_t* list = nullptr, const uint32_t* count = nullptr);
+// ---- pair batches e(A_i, Q_i) == e(G1, W_i) by RLC (hbtc_pb.hip, checks in hbtc_check.hip)
+// items: decode A (null: the G1 generator), Q (q_trusted: no subgroup check), W; r_i A_i (affine)
+// -> rA, decoded Q -> Qdec, the plain sums of r_i W_i per 64-item tile and 8-item sub-tile (S[]
+// of SigTileSums), statuses PENDING / DECODE_ERR
+hipError_t launch_pb_items(hipStream_t s, uint32_t n, const uint8_t* a_c48, const uint8_t* q_c96,
+                           bool q_trusted, const uint8_t* w_c96, RlcKey key, G1A* rA, G2A* Qdec,
+                           SigTileSums* sums, int32_t* status);
+// projective line tables (PLINES_FQ2 per item) of the pending items' Q
+hipError_t launch_pb_lines(hipStream_t s, uint32_t n, const G2A* Qdec, const int32_t* status,
+                           Fq2* tables);
+// partial Miller products of the 8-item sub-tiles (6 Fq2 per sub-tile into fbuf)
+hipError_t launch_pb_ml(hipStream_t s, uint32_t n_items, const G1A* rA, const Fq2* qtab,
+                        const int32_t* status, Fq2* fbuf);
+// group checks from the partials: level 0 every tile (n_direct), level 1 the 8 sub-tiles of the
+// *n_listed tiles of list; failing tiles -> out_list (level 0), failing sub-tiles' pending items
+// -> out_list (level 1)
+hipError_t launch_pb_fe(hipStream_t s, int level, uint32_t max_groups, uint32_t n_items,
+                        uint32_t n_direct, const uint32_t* n_listed, const uint32_t* list,
+                        const Fq2* fbuf, const Fq2* wtab, const uint32_t* winf, int32_t* status,
+                        uint32_t* out_count, uint32_t* out_list);
 // k_i P_i; base_stride / scalar_stride 0 = one base / scalar for every item
 hipError_t launch_point_mul(hipStream_t s, int group, uint32_t n, const uint8_t* base,
                             uint32_t base_stride, const uint8_t* scalars, uint32_t scalar_stride,

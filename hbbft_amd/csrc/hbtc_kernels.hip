@@ -316,13 +316,19 @@ __global__ void __launch_bounds__(64) k_sig_verify(
 #if HBTC_IN_PART(4)
 // Generic e(a1, a2) == e(b1, b2) with every argument per item; a null G1 pointer means the
 // G1 generator.  verify_sigs: (pk, H) vs (G1, sig).  verify_ciphertexts: (G1, w) vs (u, H).
+// With `count` non-null: only the *count items list[0 ..) (the exact checks behind a failing
+// pair-batch group, hbtc_pb.hip).
 __global__ void __launch_bounds__(64) k_pair_verify(uint32_t n, const uint8_t* __restrict__ a1,
                                                     const uint8_t* __restrict__ a2,
                                                     const uint8_t* __restrict__ b1,
                                                     const uint8_t* __restrict__ b2,
-                                                    int32_t* __restrict__ status) {
-  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= n) return;
+                                                    int32_t* __restrict__ status,
+                                                    const uint32_t* __restrict__ list,
+                                                    const uint32_t* __restrict__ count) {
+  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+  if (count) n = *count;
+  if (g >= n) return;
+  const uint32_t i = count ? list[g] : g;
   uint32_t w[24];
   G1A A1, B1;
   G2A A2, B2;
@@ -459,10 +465,11 @@ hipError_t launch_sig_verify(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
 
 #if HBTC_IN_PART(4)
 hipError_t launch_pair_verify(hipStream_t s, uint32_t n, const uint8_t* a1, const uint8_t* a2,
-                              const uint8_t* b1, const uint8_t* b2, int32_t* status) {
+                              const uint8_t* b1, const uint8_t* b2, int32_t* status,
+                              const uint32_t* list, const uint32_t* count) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_pair_verify, dim3(blocks_for(n, 64)), dim3(64), 0, s, n, a1, a2, b1, b2,
-                     status);
+                     status, list, count);
   return hipGetLastError();
 }
 

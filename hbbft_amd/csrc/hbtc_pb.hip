@@ -1,0 +1,121 @@
+// Random-linear-combination batch verification of pairing equalities with a per-item G2
+// argument:  e(A_i, Q_i) == e(G1, W_i)  for every item i of a batch.  It is the fast path of
+//   hbtc_verify_ciphertexts / hbtc_decrypt: Ciphertext::verify, e(G1, w) == e(u, H) with
+//       H = hash_g1_g2(u, v) (A = u, Q = H, W = w; SecretKey::decrypt of the SyncKeyGen rows and
+//       Ack values, /root/reference/src/sync_key_gen.rs:358,481-484), and
+//   hbtc_verify_sigs: PublicKey::verify, e(pk, H) == e(G1, sigma) (A = pk, Q = H, W = sigma;
+//       src/coin.rs:192-197, dynamic_honey_badger/votes.rs:154).
+// The reference evaluates two full pairings per item.  Here, for a group G of consecutive items
+// and ChaCha20 scalars r_i drawn per call (hbtc_rlc.hip explains the scalars and the bounds):
+//     every item valid  =>  prod_G e(r_i A_i, Q_i) * e(-G1, sum_G r_i W_i) == 1
+// one multi-Miller loop of |G| + 1 pairs and ONE final exponentiation per group, instead of
+// |G| pairs of pairings.  Groups are 64-item tiles, then the 8-item sub-tiles of failing tiles,
+// then exact per-item checks (k_pair_verify) of failing sub-tiles.
+//
+// Every pair has an affine G1 point and a G2 argument that varies, so every line table is
+// projective (A, B, C per Miller step, pairing.h g2_proj_lines): k_pb_lines builds the table of
+// each item's Q_i, k_plines (hbtc_sig.hip, modes 3 / 4) those of the groups' W sums, and
+// k_pb_check (hbtc_check.hip) evaluates them on the cooperative GT arithmetic of gt6.h.
+#include "rlc_common.h"
+
+namespace hbtc {
+
+// One wave per tile of 64 consecutive items: decode A (G1, subgroup check; null = the G1
+// generator), W and Q (G2, subgroup checks; Q trusted = our own hash output, in the subgroup by
+// construction: on-curve decode only), draw r_i, store r_i A_i (affine) and the decoded Q_i, and
+// sum r_i W_i over the tile and its 8 sub-tiles.  An item that fails to decode gets DECODE_ERR
+// and contributes nothing.
+__global__ void __launch_bounds__(64, 2) k_pb_items(uint32_t n, const uint8_t* __restrict__ a_c48,
+                                                    const uint8_t* __restrict__ q_c96, bool q_trusted,
+                                                    const uint8_t* __restrict__ w_c96, RlcKey key,
+                                                    G1A* __restrict__ rA, G2A* __restrict__ Qdec,
+                                                    SigTileSums* __restrict__ sums,
+                                                    int32_t* __restrict__ status) {
+  __shared__ G2J red[64];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t i = blockIdx.x * 64u + lane;
+  G2J S;
+  jac_set_inf(S);
+  if (i < n) {
+    uint32_t w[24];
+    G1A A;
+    G2A Q, W;
+    bool ok = true;
+    if (a_c48) {
+      rlc_load_words(w, a_c48, i, 12);
+      ok = g1_decompress(A, w);
+    } else {
+      fq_set(A.x, G1_GEN_X);
+      fq_set(A.y, G1_GEN_Y);
+      A.inf = 0;
+    }
+    rlc_load_words(w, q_c96, i, 24);
+    ok = g2_decompress(Q, w, !q_trusted) && ok;
+    rlc_load_words(w, w_c96, i, 24);
+    ok = g2_decompress(W, w) && ok;
+    G1A ra;
+    ra.inf = 1;
+    if (ok) {
+      uint64_t a, b;
+      rlc_scalar(key, i, a, b);
+      const int nbits = (int)key.bits / 2;
+      if (!A.inf && !Q.inf) {  // r A, affine (one binary-Euclid inversion)
+        Fq bx, beta;
+        fq_set(beta, G1_BETA);
+        fq_mul(bx, A.x, beta);
+        G1J t;
+        glv_mul_uniform(t, A, bx, a, b, nbits);
+        if (!jac_is_inf(t)) {
+          Fq zi, zi2, zi3;
+          finv_fast(zi, t.z);
+          fq_sqr(zi2, zi);
+          fq_mul(zi3, zi2, zi);
+          fq_mul(ra.x, t.x, zi2);
+          fq_mul(ra.y, t.y, zi3);
+          ra.inf = 0;
+        }
+      }
+      if (!W.inf) {  // r W = [a] W + [b] (-psi^2 W), -psi^2 (x, y) = (zeta x, y)
+        Fq2 mx;
+        Fq zeta;
+        fq_set(zeta, G2_ZETA);
+        fq_mul(mx.c0, W.x.c0, zeta);
+        fq_mul(mx.c1, W.x.c1, zeta);
+        glv_mul_uniform(S, W, mx, a, b, nbits);
+      }
+    }
+    rA[i] = ra;
+    Qdec[i] = Q;
+    status[i] = ok ? HBTC_RLC_PENDING : HBTC_DECODE_ERR;
+  }
+  rlc_reduce_plain<Fq2>(red, S, lane, sums[blockIdx.x].S);
+}
+
+// The projective line table of every pending item's Q_i (one lane per item).
+__global__ void __launch_bounds__(64) k_pb_lines(uint32_t n, const G2A* __restrict__ Qdec,
+                                                 const int32_t* __restrict__ status,
+                                                 Fq2* __restrict__ tables) {
+  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  if (i >= n || status[i] != HBTC_RLC_PENDING) return;
+  const G2A Q = Qdec[i];
+  if (Q.inf) return;  // the pair is unused (e(A, O) = 1)
+  g2_proj_lines(tables + (size_t)i * PLINES_FQ2, Q);
+}
+
+hipError_t launch_pb_items(hipStream_t s, uint32_t n, const uint8_t* a_c48, const uint8_t* q_c96,
+                           bool q_trusted, const uint8_t* w_c96, RlcKey key, G1A* rA, G2A* Qdec,
+                           SigTileSums* sums, int32_t* status) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pb_items, dim3((n + 63) / 64), dim3(64), 0, s, n, a_c48, q_c96, q_trusted, w_c96,
+                     key, rA, Qdec, sums, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_pb_lines(hipStream_t s, uint32_t n, const G2A* Qdec, const int32_t* status,
+                           Fq2* tables) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pb_lines, dim3((n + 63) / 64), dim3(64), 0, s, n, Qdec, status, tables);
+  return hipGetLastError();
+}
+
+}  // namespace hbtc

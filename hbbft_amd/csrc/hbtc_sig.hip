@@ -124,14 +124,21 @@ __global__ void __launch_bounds__(64) k_plines(int mode, uint32_t max_groups, ui
                                                uint32_t* __restrict__ inf) {
   HBTC_LATENCY_PRIO();
   const uint32_t g = blockIdx.x * 64 + threadIdx.x;
-  // mode 2: leaves [base, base + max_groups) of the list (chunks keep the tables bounded)
-  const uint32_t c = mode == 0 ? 0u : *count;
-  const uint32_t n = mode == 0 ? max_groups
+  // mode 2: leaves [base, base + max_groups) of the list (chunks keep the tables bounded);
+  // modes 3 / 4 (pair-batch path, hbtc_pb.hip): the plain sum of every tile / of the 8 sub-tiles
+  // of the listed tiles
+  const uint32_t c = (mode == 0 || mode == 3) ? 0u : *count;
+  const uint32_t n = (mode == 0 || mode == 3) ? max_groups
                    : mode == 1 ? c * 16u
+                   : mode == 4 ? c * 8u
                                : (c > base ? min(c - base, max_groups) : 0u);
   if (g >= n) return;
   G2J S;
-  if (mode == 0) {
+  if (mode == 3) {
+    S = sums[g].S[8];
+  } else if (mode == 4) {
+    S = sums[list[g >> 3]].S[g & 7u];
+  } else if (mode == 0) {
     const uint32_t t = g >> 1;
     S = (g & 1u) ? sums[t].SW[8] : sums[t].S[8];
   } else if (mode == 1) {

@@ -134,6 +134,27 @@ __device__ void rlc_reduce(Jac<F>* redA, Jac<F>* redB, const Jac<F>& q, uint32_t
   __syncthreads();  // the arrays are reused by the next reduction
 }
 
+// Plain tree sum of the per-lane points over the wave: out[0..7] the aligned groups of 8, out[8]
+// the whole wave (no position-weighted sums: the pair-batch path locates by splitting).
+template <class F>
+__device__ void rlc_reduce_plain(Jac<F>* red, const Jac<F>& q, uint32_t lane, Jac<F>* out) {
+  red[lane] = q;
+  __syncthreads();
+#pragma unroll 1
+  for (uint32_t s = 1; s < 64; s <<= 1) {
+    if ((lane & (2 * s - 1)) == 0) {
+      Jac<F> a = red[lane];
+      const Jac<F> b = red[lane + s];
+      jac_add(a, a, b);
+      red[lane] = a;
+    }
+    __syncthreads();
+    if (s == 4 && (lane & 7u) == 0) out[lane >> 3] = red[lane];
+  }
+  if (lane == 0) out[8] = red[0];
+  __syncthreads();
+}
+
 // The same reduction with ONE LDS array (the plain sums A; the weighted sums B travel between
 // lanes by ds_bpermute): half the LDS of rlc_reduce, so a G2 tile (216-byte points) leaves room
 // for two waves per SIMD.  All 64 lanes run every exchange (converged control flow).
