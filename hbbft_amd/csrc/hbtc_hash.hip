@@ -147,11 +147,6 @@ HASH_HD void fq_rand(Fq& r, ChaCha04& rng) {
   }
 }
 
-const Limbs<16> G2_COFACTOR = {{0x1c7238e5u, 0xcf1c38e3u, 0x786f0c70u, 0x1616ec6eu, 0x3a6691aeu,
-                                0x21537e29u, 0x4d9e82efu, 0xa628f1cbu, 0x2e5a7ddfu, 0xa68a205bu,
-                                0x47085abau, 0xcd91de45u, 0x2876a202u, 0x091d5079u, 0x5414e7f1u,
-                                0x05d543a9u}};
-
 // One draw of G2::rand's loop: x, greatest, get_point_from_x.  False if x^3 + b is not a square
 // (the loop draws again).
 HASH_HD bool g2_rand_candidate(G2A& p, ChaCha04& rng) {
@@ -180,7 +175,7 @@ void g2_rand(G2A& out, ChaCha04& rng) {
     G2A p;
     if (!g2_rand_candidate(p, rng)) continue;
     G2J q;
-    jac_mul_limbs<Fq2, 16>(q, p, G2_COFACTOR);  // scale_by_cofactor (full h2)
+    g2_clear_cofactor(q, p);  // scale_by_cofactor (full h2, curve.h)
     if (jac_is_inf(q)) continue;
     jac_to_aff(out, q);
     return;
@@ -382,13 +377,12 @@ hipError_t launch_zero_u32(hipStream_t s, uint32_t* p, size_t n) {
 // [h2] P for candidates P (one lane each) -> compressed G2 words; st = 1 if [h2] P = O (the
 // host then continues G2::rand's loop itself).
 __global__ void __launch_bounds__(64) k_g2_clear_cofactor(uint32_t n, const G2A* __restrict__ in,
-                                                          Limbs<16> h2,
                                                           uint32_t* __restrict__ out_w,
                                                           int32_t* __restrict__ st) {
   const uint32_t i = blockIdx.x * 64 + threadIdx.x;
   if (i >= n) return;
   G2J q;
-  jac_mul_limbs<Fq2, 16>(q, in[i], h2);
+  g2_clear_cofactor(q, in[i]);
   if (jac_is_inf(q)) {
     st[i] = 1;
     return;
@@ -406,7 +400,7 @@ hipError_t launch_g2_clear_cofactor(hipStream_t s, uint32_t n, const G2A* in, ui
                                     int32_t* st) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_g2_clear_cofactor, dim3((n + 63) / 64), dim3(64), 0, s, n, in,
-                     G2_COFACTOR, reinterpret_cast<uint32_t*>(out_c96), st);
+                     reinterpret_cast<uint32_t*>(out_c96), st);
   return hipGetLastError();
 }
 
