@@ -14,18 +14,23 @@
 //
 // Every pair has an affine G1 point and a G2 argument that varies, so every line table is
 // projective (A, B, C per Miller step, pairing.h g2_proj_lines): k_pb_lines builds the table of
-// each item's Q_i, k_plines (hbtc_sig.hip, modes 3 / 4) those of the groups' W sums, and
-// k_pb_check (hbtc_check.hip) evaluates them on the cooperative GT arithmetic of gt6.h.
+// each item's Q_i, k_plines (hbtc_sig.hip, modes 3 / 4) those of the groups' W sums; k_pb_ml
+// (Miller partials per 8-item sub-tile) and k_pb_fe (group products, final exponentiations) in
+// hbtc_check.hip evaluate them on the cooperative GT arithmetic of gt6.h.
 #include "rlc_common.h"
 
 namespace hbtc {
+
+#ifndef HBTC_PB_ITEMS_WAVES
+#define HBTC_PB_ITEMS_WAVES 2
+#endif
 
 // One wave per tile of 64 consecutive items: decode A (G1, subgroup check; null = the G1
 // generator), W and Q (G2, subgroup checks; Q trusted = our own hash output, in the subgroup by
 // construction: on-curve decode only), draw r_i, store r_i A_i (affine) and the decoded Q_i, and
 // sum r_i W_i over the tile and its 8 sub-tiles.  An item that fails to decode gets DECODE_ERR
 // and contributes nothing.
-__global__ void __launch_bounds__(64, 2) k_pb_items(uint32_t n, const uint8_t* __restrict__ a_c48,
+__global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n, const uint8_t* __restrict__ a_c48,
                                                     const uint8_t* __restrict__ q_c96, bool q_trusted,
                                                     const uint8_t* __restrict__ w_c96, RlcKey key,
                                                     G1A* __restrict__ rA, G2A* __restrict__ Qdec,

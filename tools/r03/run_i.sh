@@ -16,3 +16,9 @@ step 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu 
 step 300 python3 -u bench_configs.py --configs c5 --no-cpu > $O/bench_c5.json 2> $O/bench_c5.err
 step 300 python3 -u bench_configs.py --configs c2,c4 --no-cpu > $O/bench_c2_c4.json 2> $O/bench_c2_c4.err
 echo done >&2
+step 200 python3 -u bench.py --cts 125 --no-extra --no-cpu > $O/bench_125.json 2> $O/bench_125.err
+step 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt125 -o kt -- python3 bench.py --cts 125 --no-extra --no-cpu --steps 20 --warmup 2 > $O/kt125.log 2>&1
+echo done2 >&2
+step 200 python3 -u tools/pb_probe.py 262144 2 > $O/probe_w2.txt 2>&1
+step 200 env HBTC_LIB_PATH=hbbft_amd/libhbtc_pbw1.so python3 -u tools/pb_probe.py 262144 2 > $O/probe_w1.txt 2>&1
+echo done >&2
