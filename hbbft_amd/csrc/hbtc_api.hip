@@ -1380,7 +1380,7 @@ int hbtc_verify_sig_shares(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, con
 // items of failing sub-tiles.  Per-share mode: k_pair_verify for every item.
 constexpr uint32_t PB_CHUNK = 1u << 18;
 int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_q, bool q_trusted,
-                  const uint8_t* d_w, int32_t* d_status) {
+                  const uint8_t* d_w, int32_t* d_status, G1A* d_adec = nullptr) {
   if (c->verify_mode == HBTC_MODE_PER_SHARE) {
     return timed(c, "pair_verify", [&] {
       return launch_pair_verify(c->stream, n, d_a, d_q, nullptr, d_w, d_status);
@@ -1413,7 +1413,8 @@ int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_
     key.bits = c->rlc_bits;
     HB_CHECK(c, launch_zero_u32(c->stream, counters, 2));
     HB_TRY(timed(c, "pb_items", [&] {
-      return launch_pb_items(c->stream, m, a, q, q_trusted, w, key, rA, qdec, sums, st);
+      return launch_pb_items(c->stream, m, a, q, q_trusted, w, key, rA, qdec, sums, st,
+                             d_adec ? d_adec + base : nullptr);
     }));
     HB_TRY(timed(c, "pb_lines", [&] { return launch_pb_lines(c->stream, m, qdec, st, qtab); }));
     HB_TRY(timed(c, "pb_ml", [&] { return launch_pb_ml(c->stream, m, rA, qtab, st, fbuf); }));
@@ -2256,6 +2257,40 @@ int hbtc_hash_g1_g2_batch_gpu(hbtc_ctx* c, uint32_t n, const uint8_t* g1_c48, co
   return hash_batch_gpu(c, n, g1_c48, msgs, offsets, out_c96);
 }
 
+// k (canonical, < r, 8 little-endian limbs) = k1 x^2 + k0 with k0 < x^2 and k1 < 2^128 (k < r <
+// x^4): binary long division by x^2 = 0xac45a4010001a4020000000100000000.
+static void split_by_x2(const uint32_t* k, uint32_t* k0, uint32_t* k1) {
+  static const uint32_t X2[4] = {0x00000000u, 0x00000001u, 0x0001a402u, 0xac45a401u};
+  uint32_t rem[5] = {0, 0, 0, 0, 0};
+  uint32_t q[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int bit = 255; bit >= 0; --bit) {
+    for (int j = 4; j > 0; --j) rem[j] = (rem[j] << 1) | (rem[j - 1] >> 31);  // rem = 2 rem + bit
+    rem[0] = (rem[0] << 1) | ((k[bit >> 5] >> (bit & 31)) & 1u);
+    bool ge = rem[4] != 0;
+    if (!ge) {
+      ge = true;
+      for (int j = 3; j >= 0; --j)
+        if (rem[j] != X2[j]) {
+          ge = rem[j] > X2[j];
+          break;
+        }
+    }
+    if (ge) {
+      uint64_t borrow = 0;
+      for (int j = 0; j < 5; ++j) {
+        const uint64_t d = (uint64_t)rem[j] - (j < 4 ? X2[j] : 0u) - borrow;
+        rem[j] = (uint32_t)d;
+        borrow = (d >> 63) & 1u;
+      }
+      q[bit >> 5] |= 1u << (bit & 31);
+    }
+  }
+  for (int j = 0; j < 4; ++j) {
+    k0[j] = rem[j];
+    k1[j] = q[j];
+  }
+}
+
 int hbtc_decrypt(hbtc_ctx* c, uint32_t n, const uint8_t* sk_le32, const uint8_t* u_c48,
                  const uint8_t* w_c96, const uint8_t* msgs, const uint32_t* offsets, uint8_t* out,
                  int32_t* status) {
@@ -2280,12 +2315,26 @@ int hbtc_decrypt(hbtc_ctx* c, uint32_t n, const uint8_t* sk_le32, const uint8_t*
   HB_TRY(ws(c, "out1", (size_t)48 * n, &d_g));
   HB_TRY(ws(c, "out2", (size_t)4 * n, &d_gst));
   // H is this call's own hash output (cofactor cleared: in the subgroup by construction)
+  const bool rlc = c->verify_mode == HBTC_MODE_RLC;
+  G1A* d_adec = nullptr;
+  if (rlc) HB_TRY(wst(c, "dec.adec", n, &d_adec));
   HB_TRY(pb_verify_dev(c, n, (const uint8_t*)d_u, (const uint8_t*)d_H, true, (const uint8_t*)d_w,
-                       (int32_t*)d_st));
-  HB_TRY(timed(c, "mul", [&] {
-    return launch_point_mul(c->stream, 1, n, (const uint8_t*)d_u, 1, (const uint8_t*)d_k, 0,
-                            (uint8_t*)d_g, (int32_t*)d_gst);
-  }));
+                       (int32_t*)d_st, d_adec));
+  if (rlc) {
+    // g = sk u on the u decoded by the pair batch, for the ciphertexts that verify:
+    // sk = k0 + k1 x^2 (k0 < x^2), [sk] u = [k0] u + [k1] (beta x, -y)
+    uint32_t k0[4], k1[4];
+    split_by_x2(k.v, k0, k1);
+    HB_TRY(timed(c, "mul", [&] {
+      return launch_pb_mul_glv(c->stream, n, d_adec, (const int32_t*)d_st, k0, k1, (uint8_t*)d_g);
+    }));
+    HB_CHECK(c, hipMemsetAsync(d_gst, 0, (size_t)4 * n, c->stream));  // statuses are in d_st
+  } else {
+    HB_TRY(timed(c, "mul", [&] {
+      return launch_point_mul(c->stream, 1, n, (const uint8_t*)d_u, 1, (const uint8_t*)d_k, 0,
+                              (uint8_t*)d_g, (int32_t*)d_gst);
+    }));
+  }
   std::vector<uint8_t> gb((size_t)n * 48);
   std::vector<int32_t> gst(n);
   HB_TRY(download(c, status, d_st, (size_t)4 * n));

@@ -174,7 +174,10 @@ hipError_t launch_pair_verify(hipStream_t s, uint32_t n, const uint8_t* a1, cons
 // of SigTileSums), statuses PENDING / DECODE_ERR
 hipError_t launch_pb_items(hipStream_t s, uint32_t n, const uint8_t* a_c48, const uint8_t* q_c96,
                            bool q_trusted, const uint8_t* w_c96, RlcKey key, G1A* rA, G2A* Qdec,
-                           SigTileSums* sums, int32_t* status);
+                           SigTileSums* sums, int32_t* status, G1A* adec = nullptr);
+// g_i = [k0 + k1 x^2] A_i (compressed) for the ACCEPTed items, zero bytes for the others
+hipError_t launch_pb_mul_glv(hipStream_t s, uint32_t n, const G1A* adec, const int32_t* status,
+                             const uint32_t* k0, const uint32_t* k1, uint8_t* out_c48);
 // projective line tables (PLINES_FQ2 per item) of the pending items' Q
 hipError_t launch_pb_lines(hipStream_t s, uint32_t n, const G2A* Qdec, const int32_t* status,
                            Fq2* tables);

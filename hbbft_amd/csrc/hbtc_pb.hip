@@ -35,7 +35,8 @@ __global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n
                                                     const uint8_t* __restrict__ w_c96, RlcKey key,
                                                     G1A* __restrict__ rA, G2A* __restrict__ Qdec,
                                                     SigTileSums* __restrict__ sums,
-                                                    int32_t* __restrict__ status) {
+                                                    int32_t* __restrict__ status,
+                                                    G1A* __restrict__ adec) {
   __shared__ G2J red[64];
   const uint32_t lane = threadIdx.x;
   const uint32_t i = blockIdx.x * 64u + lane;
@@ -91,6 +92,7 @@ __global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n
     }
     rA[i] = ra;
     Qdec[i] = Q;
+    if (adec) adec[i] = A;  // the decoded A for the caller (hbtc_decrypt's g = sk u)
     status[i] = ok ? HBTC_RLC_PENDING : HBTC_DECODE_ERR;
   }
   rlc_reduce_plain<Fq2>(red, S, lane, sums[blockIdx.x].S);
@@ -109,10 +111,91 @@ __global__ void __launch_bounds__(64) k_pb_lines(uint32_t n, const G2A* __restri
 
 hipError_t launch_pb_items(hipStream_t s, uint32_t n, const uint8_t* a_c48, const uint8_t* q_c96,
                            bool q_trusted, const uint8_t* w_c96, RlcKey key, G1A* rA, G2A* Qdec,
-                           SigTileSums* sums, int32_t* status) {
+                           SigTileSums* sums, int32_t* status, G1A* adec) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_pb_items, dim3((n + 63) / 64), dim3(64), 0, s, n, a_c48, q_c96, q_trusted, w_c96,
-                     key, rA, Qdec, sums, status);
+                     key, rA, Qdec, sums, status, adec);
+  return hipGetLastError();
+}
+
+// g_i = [k] A_i for the ACCEPTed items of a pair batch (hbtc_decrypt: g = sk u), from the decoded
+// A_i and the host's split k = k0 + k1 x^2 (k0 < x^2, k1 < 2^128): [k] A = [k0] A + [k1] m(A)
+// with m(A) = -phi(A) = (beta x, -y) = [x^2] A on G1 -- a joint 128-bit double-and-add whose
+// bits are the same on every lane (no divergence) over {A, m(A), A + m(A)}, instead of a fresh
+// decode and a 255-bit double-and-add (k_point_mul).  Other items: zero bytes.
+__global__ void __launch_bounds__(64) k_pb_mul_glv(uint32_t n, const G1A* __restrict__ adec,
+                                                   const int32_t* __restrict__ status,
+                                                   Limbs<4> k0, Limbs<4> k1,
+                                                   uint32_t* __restrict__ out_w) {
+  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  if (i >= n) return;
+  uint32_t w[12];
+  for (int j = 0; j < 12; ++j) w[j] = 0;
+  if (status[i] == HBTC_ACCEPT) {
+    const G1A A = adec[i];
+    G1A m, am;
+    {
+      Fq beta;
+      fq_set(beta, G1_BETA);
+      fq_mul(m.x, A.x, beta);
+      fq_neg(m.y, A.y);
+      m.inf = A.inf;
+      G1J s;
+      jac_from_aff(s, A);
+      jac_add_aff(s, s, m);  // [1 + x^2] A: O only for A = O
+      am.inf = jac_is_inf(s) ? 1u : 0u;
+      if (!am.inf) {
+        Fq zi, zi2, zi3;
+        finv_fast(zi, s.z);
+        fq_sqr(zi2, zi);
+        fq_mul(zi3, zi2, zi);
+        fq_mul(am.x, s.x, zi2);
+        fq_mul(am.y, s.y, zi3);
+      }
+    }
+    G1J acc;
+    jac_set_inf(acc);
+#pragma unroll 1
+    for (int bit = 127; bit >= 0; --bit) {
+      jac_dbl(acc, acc);
+      const bool ba = ((k0.v[bit >> 5] >> (bit & 31)) & 1u) != 0;
+      const bool bb = ((k1.v[bit >> 5] >> (bit & 31)) & 1u) != 0;
+      if (ba && bb)
+        jac_add_aff(acc, acc, am);
+      else if (ba)
+        jac_add_aff(acc, acc, A);
+      else if (bb)
+        jac_add_aff(acc, acc, m);
+    }
+    G1A g;
+    g.inf = jac_is_inf(acc) ? 1u : 0u;
+    if (!g.inf) {
+      Fq zi, zi2, zi3;
+      finv_fast(zi, acc.z);
+      fq_sqr(zi2, zi);
+      fq_mul(zi3, zi2, zi);
+      fq_mul(g.x, acc.x, zi2);
+      fq_mul(g.y, acc.y, zi3);
+    } else {
+      fq_zero(g.x);
+      fq_zero(g.y);
+    }
+    g1_compress(w, g);
+  }
+  uint4* o = reinterpret_cast<uint4*>(out_w + 12 * (size_t)i);
+  for (int k = 0; k < 3; ++k) o[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+}
+
+hipError_t launch_pb_mul_glv(hipStream_t s, uint32_t n, const G1A* adec, const int32_t* status,
+                             const uint32_t* k0, const uint32_t* k1, uint8_t* out_c48) {
+  if (n == 0) return hipSuccess;
+  Limbs<4> a, b;
+  for (int j = 0; j < 4; ++j) {
+    a.v[j] = k0[j];
+    b.v[j] = k1[j];
+  }
+  hipLaunchKernelGGL(k_pb_mul_glv, dim3((n + 63) / 64), dim3(64), 0, s, n, adec, status, a, b,
+                     reinterpret_cast<uint32_t*>(out_c48));
   return hipGetLastError();
 }
 
