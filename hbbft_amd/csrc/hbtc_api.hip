@@ -525,6 +525,14 @@ uint32_t track_threshold(const Keyset* ks, uint32_t n_items) {
   return t ? (uint32_t)t : 1u;
 }
 
+// REJECTs that flag a sender in a probe pass: half of the probe's average shares per sender (>= 2).
+// A probe is small, so the call threshold (1/8 of the average) would flag honest senders hit by one
+// stray corrupted share -- their shares would then take the exact checks for 16 calls.
+uint32_t probe_threshold(const Keyset* ks, uint32_t n_items) {
+  const uint64_t t = (uint64_t)n_items / (2ull * ks->n);
+  return t > 2 ? (uint32_t)t : 2u;
+}
+
 // Group-check schedule of one RLC call.  The plain-first form (5 levels: plain and weighted
 // checks of tiles, then of sub-tiles, then leaves) does the least work and is right when the
 // call fills the chip; a call with few tiles (a rank's slice under strong scaling, a small
@@ -736,7 +744,7 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
     return launch_rlc_finalize(c->stream, n_tiles, tiles, h_st, w_st, d_status, d_idx, ks->n,
                                ks->rejects + (size_t)c->lane * ks->n,
                                const_cast<uint32_t*>(sus.last_bad), sus.now,
-                               track_threshold(ks, n_items));
+                               probe ? probe_threshold(ks, n_items) : track_threshold(ks, n_items));
   });
 }
 
