@@ -7,6 +7,8 @@ TAG=${1:-r03}
 O=gpurun_out/prof_$TAG
 mkdir -p $O
 export TMPDIR=/tmp
+# no cold-key-set probe pass: its small first call would join the per-dispatch means
+export HBTC_PROBE=0
 step() {
   local lim=$1; shift
   echo "== $*" >&2
