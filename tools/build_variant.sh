@@ -21,7 +21,7 @@ for o in build/*.o; do
     src=${stem%%.*}
     part=""
     if [[ $stem == *.p* ]]; then part="-DHBTC_PART=${stem##*.p}"; fi
-    if [[ $stem == hbtc_check.c* ]]; then src=hbtc_check; part="-DHBTC_CHECK_PART=${stem##*.c}"; fi
+    if [[ $stem == hbtc_check.c* ]]; then src=hbtc_check; part="-DHBTC_CHECK_PART=${stem##*.c} -DHBTC_GT_INLINE"; fi
     base=""
     case $stem in hbtc_rlc.p6|hbtc_msm.p8) base="-DHBTC_INLINE_ALL -DHBTC_FQMUL_INLINE";; hbtc_sig|hbtc_pb) base="-DHBTC_INLINE_ALL";; esac
     $HIPCC $FLAGS $part $base ${extra[$stem]} -c "hbbft_amd/csrc/$src.hip" -o "$out/$stem.o" &
