@@ -114,10 +114,11 @@ HD void mul2_fq(Fq2& r, const Fq2& a, const Fq& y) {
 }
 
 // ------------------------------------------------------------------------------ GT operations
-// Out-of-line on the device: the glue of the final exponentiation and the location search
-// call these a few dozen times per check, so one copy each keeps the kernels inside the
-// instruction cache; their by-reference operands cost ~100 dwords of stack traffic per call
-// against ~10^4 instructions of work.
+// Out-of-line on the device unless HBTC_GT_INLINE: the glue of the final exponentiation and the
+// location search call these a few dozen times per check; their by-reference operands cost
+// ~100 dwords of stack traffic per call.  The check kernels are built with HBTC_GT_INLINE
+// (Makefile): scratch 960 -> ~330 B/lane at the same C3 throughput, the latency-bound small
+// calls slightly faster.
 #if defined(__HIP_DEVICE_COMPILE__) && defined(HBTC_GT_INLINE)
 #define GTN __device__ __forceinline__
 #elif defined(__HIP_DEVICE_COMPILE__)
