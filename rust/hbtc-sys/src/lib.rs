@@ -13,6 +13,7 @@
 //!   SyncKeyGen::handle_part / handle_ack                  skg_check_parts / skg_check_acks / decrypt
 #![allow(clippy::too_many_arguments)]
 pub mod ffi;
+pub mod queues;
 
 use std::ffi::CStr;
 use std::os::raw::c_int;
@@ -130,6 +131,34 @@ impl Context {
         self.ok(unsafe {
             ffi::hbtc_verify_dec_shares(self.raw, keyset, b.n_inst(), h_c96.as_ptr(), w_c96.as_ptr(),
                                         b.offsets.as_ptr(), b.idx.as_ptr(), b.items.as_ptr(), st.as_mut_ptr())
+        })?;
+        Ok(st)
+    }
+
+    /// PublicKey::verify for n (pk, H, sigma) triples: e(pk, H) == e(G1, sigma) (src/coin.rs:192-197).
+    pub fn verify_sigs(&self, pk_c48: &[u8], h_c96: &[u8], sig_c96: &[u8]) -> Result<Vec<i32>> {
+        assert_eq!(pk_c48.len() % 48, 0);
+        let n = pk_c48.len() / 48;
+        assert_eq!(h_c96.len(), 96 * n, "one H per signature");
+        assert_eq!(sig_c96.len(), 96 * n, "one signature per key");
+        let mut st = vec![0i32; n];
+        self.ok(unsafe {
+            ffi::hbtc_verify_sigs(self.raw, n as u32, pk_c48.as_ptr(), h_c96.as_ptr(), sig_c96.as_ptr(),
+                                  st.as_mut_ptr())
+        })?;
+        Ok(st)
+    }
+
+    /// Ciphertext::verify for n (u, H, w) triples: e(G1, w) == e(u, H) (src/threshold_decryption.rs:98).
+    pub fn verify_ciphertexts(&self, u_c48: &[u8], h_c96: &[u8], w_c96: &[u8]) -> Result<Vec<i32>> {
+        assert_eq!(u_c48.len() % 48, 0);
+        let n = u_c48.len() / 48;
+        assert_eq!(h_c96.len(), 96 * n, "one H per ciphertext");
+        assert_eq!(w_c96.len(), 96 * n, "one w per ciphertext");
+        let mut st = vec![0i32; n];
+        self.ok(unsafe {
+            ffi::hbtc_verify_ciphertexts(self.raw, n as u32, u_c48.as_ptr(), h_c96.as_ptr(), w_c96.as_ptr(),
+                                         st.as_mut_ptr())
         })?;
         Ok(st)
     }
