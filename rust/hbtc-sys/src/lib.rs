@@ -163,6 +163,44 @@ impl Context {
         Ok(st)
     }
 
+    /// BivarCommitment::row(x) == row.commitment() for every Part (x = our_idx + 1): commits holds
+    /// per Part the (t+1)(t+2)/2 compressed points, rows per Part t+1 Fr (32-byte LE each).
+    pub fn skg_check_parts(&self, t: u32, our_idx: u32, commits_c48: &[u8], rows_le32: &[u8]) -> Result<Vec<i32>> {
+        let m = ((t + 1) * (t + 2) / 2) as usize;
+        assert_eq!(commits_c48.len() % (48 * m), 0);
+        let n_parts = commits_c48.len() / (48 * m);
+        assert_eq!(rows_le32.len(), 32 * (t as usize + 1) * n_parts, "t + 1 row coefficients per Part");
+        let mut st = vec![0i32; n_parts];
+        self.ok(unsafe {
+            ffi::hbtc_skg_check_parts(self.raw, n_parts as u32, t, our_idx, commits_c48.as_ptr(), rows_le32.as_ptr(),
+                                      st.as_mut_ptr())
+        })?;
+        Ok(st)
+    }
+
+    /// BivarCommitment::evaluate(x, y) == val G1 for every Ack value (x = our_idx + 1, y = sender
+    /// + 1), against Part ack_part[i]'s commitment; row_ok[p] != 0: Part p's verified row (rows)
+    /// gives the scalar fast path.
+    pub fn skg_check_acks(&self, t: u32, our_idx: u32, commits_c48: &[u8], rows_le32: &[u8], row_ok: &[u8],
+                          ack_part: &[u32], ack_sender: &[u32], vals_le32: &[u8]) -> Result<Vec<i32>> {
+        let m = ((t + 1) * (t + 2) / 2) as usize;
+        assert_eq!(commits_c48.len() % (48 * m), 0);
+        let n_parts = commits_c48.len() / (48 * m);
+        assert_eq!(rows_le32.len(), 32 * (t as usize + 1) * n_parts);
+        assert_eq!(row_ok.len(), n_parts);
+        let n = ack_part.len();
+        assert!(ack_part.iter().all(|&p| (p as usize) < n_parts), "ack_part out of range");
+        assert_eq!(ack_sender.len(), n);
+        assert_eq!(vals_le32.len(), 32 * n);
+        let mut st = vec![0i32; n];
+        self.ok(unsafe {
+            ffi::hbtc_skg_check_acks(self.raw, n_parts as u32, t, our_idx, commits_c48.as_ptr(), rows_le32.as_ptr(),
+                                     row_ok.as_ptr(), n as u32, ack_part.as_ptr(), ack_sender.as_ptr(),
+                                     vals_le32.as_ptr(), st.as_mut_ptr())
+        })?;
+        Ok(st)
+    }
+
     /// combine_signatures over the first t shares of every instance: (signatures, parities, status).
     pub fn combine_sigs(&self, b: &Batch, t: u32) -> Result<(Vec<u8>, Vec<u8>, Vec<i32>)> {
         b.check(96);

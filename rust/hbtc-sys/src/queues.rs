@@ -548,3 +548,237 @@ impl<K: Ord + Clone, N: Ord + Clone> DecryptionEpoch<K, N> {
         pending.push((k.clone(), e, items));
     }
 }
+
+// ===================================================================================== SyncKeyGen
+/// A threshold_crypto Ciphertext (u, v, w) as it arrives.
+#[derive(Clone)]
+pub struct WireCt {
+    pub u: [u8; 48],
+    pub v: Vec<u8>,
+    pub w: [u8; 96],
+}
+
+/// The bincode decoding the replay needs (threshold_crypto's serde, provided by the caller):
+/// a Part row -> t + 1 Fr (32-byte LE), an Ack value -> one Fr; None where serde refuses it.
+pub trait SkgCodec {
+    fn row(&self, plain: &[u8]) -> Option<Vec<[u8; 32]>>;
+    fn value(&self, plain: &[u8]) -> Option<[u8; 32]>;
+}
+
+pub enum SkgMsg<N> {
+    Part { sender: N, commit_c48: Vec<u8>, rows: Vec<WireCt> },
+    Ack { sender: N, proposer: u32, values: Vec<WireCt> },
+}
+
+/// The outcome of one queued message (sync_key_gen.rs:338-398): a Part is ignored (None), valid
+/// (our Ack is then built by the caller from `row`) or faulty; an Ack yields its faults.
+pub enum SkgOutcome<N> {
+    PartIgnored,
+    PartValid { proposer: u32, row: Vec<[u8; 32]> },
+    PartInvalid(N),
+    Ack(Vec<(N, &'static str)>),
+}
+
+struct Proposal {
+    commit: Vec<u8>,
+    acks: BTreeSet<u32>,
+    values: BTreeMap<u32, [u8; 32]>,
+    our_row: Option<Vec<[u8; 32]>>,
+}
+
+/// One node's SyncKeyGen message handling with batched crypto (the Rust form of
+/// `hbbft_amd/skg.py`): decrypt every queued ciphertext addressed to us in one `decrypt` call,
+/// check every decoded row in one `skg_check_parts` call and every decoded value in one
+/// `skg_check_acks` call against the commitment of the FIRST Part of its proposer (the only one
+/// the reference stores, :346-354), then replay in order with the reference's fault order
+/// NodeCount -> SenderExist -> DuplicateAck -> ValueDecryption -> ValueDeserialization ->
+/// ValueInvalid (:467-495).
+pub struct SkgQueue<N: Ord + Clone> {
+    index: BTreeMap<N, u32>,
+    our_idx: Option<u32>,
+    sec_key_le32: [u8; 32],
+    t: u32,
+    parts: BTreeMap<u32, Proposal>,
+    queue: Vec<SkgMsg<N>>,
+}
+
+impl<N: Ord + Clone> SkgQueue<N> {
+    pub fn new(node_ids: &[N], our_id: &N, sec_key_le32: [u8; 32], t: u32) -> Self {
+        let ids: BTreeSet<N> = node_ids.iter().cloned().collect();
+        let index: BTreeMap<N, u32> = ids.iter().cloned().enumerate().map(|(i, n)| (n, i as u32)).collect();
+        let our_idx = index.get(our_id).copied();
+        SkgQueue { index, our_idx, sec_key_le32, t, parts: BTreeMap::new(), queue: Vec::new() }
+    }
+
+    pub fn handle(&mut self, msg: SkgMsg<N>) {
+        self.queue.push(msg);
+    }
+
+    /// Ack values received so far for proposer p (node index + 1 -> Fr), for `generate`.
+    pub fn values(&self, p: u32) -> Option<&BTreeMap<u32, [u8; 32]>> {
+        self.parts.get(&p).map(|s| &s.values)
+    }
+
+    pub fn is_complete(&self, p: u32) -> bool {
+        self.parts.get(&p).map_or(false, |s| s.acks.len() > 2 * self.t as usize)
+    }
+
+    pub fn flush(&mut self, ctx: &Context, codec: &dyn SkgCodec) -> Result<Vec<SkgOutcome<N>>> {
+        let q = std::mem::take(&mut self.queue);
+        let n = self.index.len();
+        let t = self.t;
+        // 1. the ciphertexts addressed to us, decrypted in one batch
+        let mut jobs: Vec<usize> = Vec::new();
+        let (mut us, mut ws, mut vs, mut off) = (Vec::new(), Vec::new(), Vec::new(), vec![0u32]);
+        if let Some(our) = self.our_idx {
+            for (m, msg) in q.iter().enumerate() {
+                let (sender, cts, is_ack) = match msg {
+                    SkgMsg::Part { sender, rows, .. } => (sender, rows, false),
+                    SkgMsg::Ack { sender, values, .. } => (sender, values, true),
+                };
+                if !self.index.contains_key(sender) || (is_ack && cts.len() != n) {
+                    continue;
+                }
+                if let Some(c) = cts.get(our as usize) {
+                    jobs.push(m);
+                    us.extend_from_slice(&c.u);
+                    ws.extend_from_slice(&c.w);
+                    vs.extend_from_slice(&c.v);
+                    off.push(vs.len() as u32);
+                }
+            }
+        }
+        let mut plain: BTreeMap<usize, Option<Vec<u8>>> = BTreeMap::new();
+        if !jobs.is_empty() {
+            let (out, st) = ctx.decrypt(&self.sec_key_le32, &us, &ws, &vs, &off)?;
+            for (j, m) in jobs.iter().enumerate() {
+                let p = if st[j] == ACCEPT { Some(out[off[j] as usize..off[j + 1] as usize].to_vec()) } else { None };
+                plain.insert(*m, p);
+            }
+        }
+        // 2. decode; the commitment every message is checked against (first Part per proposer)
+        let mut first: BTreeMap<u32, Vec<u8>> = self.parts.iter().map(|(p, s)| (*p, s.commit.clone())).collect();
+        let mut commit_of: BTreeMap<usize, u32> = BTreeMap::new();  // message -> proposer whose commitment applies
+        let mut rows: BTreeMap<usize, Option<Vec<[u8; 32]>>> = BTreeMap::new();
+        let mut vals: BTreeMap<usize, Option<[u8; 32]>> = BTreeMap::new();
+        for (m, msg) in q.iter().enumerate() {
+            match msg {
+                SkgMsg::Part { sender, commit_c48, .. } => {
+                    let s = match self.index.get(sender) { Some(&s) => s, None => continue };
+                    if !first.contains_key(&s) {
+                        first.insert(s, commit_c48.clone());
+                        commit_of.insert(m, s);
+                    }
+                    if let Some(Some(p)) = plain.get(&m) {
+                        rows.insert(m, codec.row(p).filter(|r| r.len() == t as usize + 1));
+                    }
+                }
+                SkgMsg::Ack { sender, proposer, .. } => {
+                    if !self.index.contains_key(sender) {
+                        continue;
+                    }
+                    if let Some(Some(p)) = plain.get(&m) {
+                        vals.insert(m, codec.value(p));
+                    }
+                    if first.contains_key(proposer) {
+                        commit_of.insert(m, *proposer);
+                    }
+                }
+            }
+        }
+        // 3. batched checks
+        let our = self.our_idx.unwrap_or(0);
+        let mut row_ok: BTreeMap<usize, bool> = BTreeMap::new();
+        let pm: Vec<usize> = rows.iter().filter(|(m, r)| r.is_some() && commit_of.contains_key(m)).map(|(m, _)| *m).collect();
+        if !pm.is_empty() {
+            let cm: Vec<u8> = pm.iter().flat_map(|m| first[&commit_of[m]].iter().copied()).collect();
+            let rb: Vec<u8> = pm.iter().flat_map(|m| rows[m].as_ref().unwrap().iter().flat_map(|c| c.iter().copied())).collect();
+            let st = ctx.skg_check_parts(t, our, &cm, &rb)?;
+            for (m, s) in pm.iter().zip(st) {
+                row_ok.insert(*m, s == ACCEPT);
+            }
+        }
+        let mut val_ok: BTreeMap<usize, bool> = BTreeMap::new();
+        let am: Vec<usize> = vals.iter().filter(|(m, v)| v.is_some() && commit_of.contains_key(m)).map(|(m, _)| *m).collect();
+        if !am.is_empty() {
+            // one commitment per distinct proposer, with our verified row when we have one
+            let props: Vec<u32> = am.iter().map(|m| commit_of[m]).collect::<BTreeSet<_>>().into_iter().collect();
+            let pos: BTreeMap<u32, u32> = props.iter().enumerate().map(|(i, p)| (*p, i as u32)).collect();
+            let zero_row = vec![[0u8; 32]; t as usize + 1];
+            let (mut cm, mut rb, mut ok) = (Vec::new(), Vec::new(), Vec::new());
+            for p in &props {
+                cm.extend_from_slice(&first[p]);
+                let row = self.parts.get(p).and_then(|s| s.our_row.clone()).or_else(|| {
+                    pm.iter().find(|m| commit_of[*m] == *p && row_ok.get(*m).copied().unwrap_or(false))
+                        .and_then(|m| rows[m].clone())
+                });
+                ok.push(row.is_some() as u8);
+                for c in row.as_ref().unwrap_or(&zero_row) {
+                    rb.extend_from_slice(c);
+                }
+            }
+            let ack_part: Vec<u32> = am.iter().map(|m| pos[&commit_of[m]]).collect();
+            let ack_sender: Vec<u32> = am.iter().map(|m| match &q[*m] {
+                SkgMsg::Ack { sender, .. } => self.index[sender],
+                SkgMsg::Part { .. } => unreachable!(),
+            }).collect();
+            let vb: Vec<u8> = am.iter().flat_map(|m| vals[m].unwrap().to_vec()).collect();
+            let st = ctx.skg_check_acks(t, our, &cm, &rb, &ok, &ack_part, &ack_sender, &vb)?;
+            for (m, s) in am.iter().zip(st) {
+                val_ok.insert(*m, s == ACCEPT);
+            }
+        }
+        // 4. replay in order (:338-381 Parts, :387-396 / :462-498 Acks)
+        let mut out = Vec::with_capacity(q.len());
+        for (m, msg) in q.into_iter().enumerate() {
+            out.push(match msg {
+                SkgMsg::Part { sender, commit_c48, rows: cts } => {
+                    let s = match self.index.get(&sender) { Some(&s) => s, None => { out.push(SkgOutcome::PartIgnored); continue; } };
+                    if self.parts.contains_key(&s) {
+                        SkgOutcome::PartIgnored  // multiple parts: ignored
+                    } else {
+                        self.parts.insert(s, Proposal { commit: commit_c48, acks: BTreeSet::new(), values: BTreeMap::new(), our_row: None });
+                        match self.our_idx {
+                            None => SkgOutcome::PartIgnored,
+                            Some(o) if o as usize >= cts.len() || plain.get(&m).map_or(true, |p| p.is_none()) => SkgOutcome::PartIgnored,
+                            Some(_) => match (rows.get(&m).cloned().flatten(), row_ok.get(&m).copied().unwrap_or(false)) {
+                                (Some(row), true) => {
+                                    self.parts.get_mut(&s).unwrap().our_row = Some(row.clone());
+                                    SkgOutcome::PartValid { proposer: s, row }
+                                }
+                                _ => SkgOutcome::PartInvalid(sender),
+                            },
+                        }
+                    }
+                }
+                SkgMsg::Ack { sender, proposer, values } => {
+                    let s = match self.index.get(&sender) { Some(&s) => s, None => { out.push(SkgOutcome::Ack(Vec::new())); continue; } };
+                    let fault = |kind: &'static str| SkgOutcome::Ack(vec![(sender.clone(), kind)]);
+                    if values.len() != n {
+                        fault("NodeCount")
+                    } else if !self.parts.contains_key(&proposer) {
+                        fault("SenderExist")
+                    } else if self.parts[&proposer].acks.contains(&s) {
+                        fault("DuplicateAck")
+                    } else {
+                        self.parts.get_mut(&proposer).unwrap().acks.insert(s);
+                        if self.our_idx.is_none() {
+                            SkgOutcome::Ack(Vec::new())
+                        } else if plain.get(&m).map_or(true, |p| p.is_none()) {
+                            fault("ValueDecryption")
+                        } else if vals.get(&m).map_or(true, |v| v.is_none()) {
+                            fault("ValueDeserialization")
+                        } else if !val_ok.get(&m).copied().unwrap_or(false) {
+                            fault("ValueInvalid")
+                        } else {
+                            let v = vals[&m].unwrap();
+                            self.parts.get_mut(&proposer).unwrap().values.insert(s + 1, v);
+                            SkgOutcome::Ack(Vec::new())
+                        }
+                    }
+                }
+            });
+        }
+        Ok(out)
+    }
+}
