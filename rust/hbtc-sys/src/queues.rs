@@ -731,10 +731,12 @@ impl<N: Ord + Clone> SkgQueue<N> {
         // 4. replay in order (:338-381 Parts, :387-396 / :462-498 Acks)
         let mut out = Vec::with_capacity(q.len());
         for (m, msg) in q.into_iter().enumerate() {
-            out.push(match msg {
+            let outcome = match msg {
                 SkgMsg::Part { sender, commit_c48, rows: cts } => {
-                    let s = match self.index.get(&sender) { Some(&s) => s, None => { out.push(SkgOutcome::PartIgnored); continue; } };
-                    if self.parts.contains_key(&s) {
+                    let s = match self.index.get(&sender) { Some(&s) => s, None => u32::MAX };
+                    if s == u32::MAX {
+                        SkgOutcome::PartIgnored  // not a node
+                    } else if self.parts.contains_key(&s) {
                         SkgOutcome::PartIgnored  // multiple parts: ignored
                     } else {
                         self.parts.insert(s, Proposal { commit: commit_c48, acks: BTreeSet::new(), values: BTreeMap::new(), our_row: None });
@@ -752,9 +754,11 @@ impl<N: Ord + Clone> SkgQueue<N> {
                     }
                 }
                 SkgMsg::Ack { sender, proposer, values } => {
-                    let s = match self.index.get(&sender) { Some(&s) => s, None => { out.push(SkgOutcome::Ack(Vec::new())); continue; } };
+                    let s = match self.index.get(&sender) { Some(&s) => s, None => u32::MAX };
                     let fault = |kind: &'static str| SkgOutcome::Ack(vec![(sender.clone(), kind)]);
-                    if values.len() != n {
+                    if s == u32::MAX {
+                        SkgOutcome::Ack(Vec::new())  // not a node
+                    } else if values.len() != n {
                         fault("NodeCount")
                     } else if !self.parts.contains_key(&proposer) {
                         fault("SenderExist")
@@ -777,7 +781,8 @@ impl<N: Ord + Clone> SkgQueue<N> {
                         }
                     }
                 }
-            });
+            };
+            out.push(outcome);
         }
         Ok(out)
     }
