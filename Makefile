@@ -40,7 +40,9 @@ $(BUILD)/hbtc_kernels.p%.o: $(CSRC)/hbtc_kernels.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=$* -c $< -o $@
 
 # part 6 (per-item G1 work) is built with every helper and the Fq product inlined: no calls
-# (each call saves / restores live registers through scratch; 72.6 -> 67.9 ms per C3 launch)
+# (each call saves / restores live registers through scratch; 72.6 -> 67.9 ms per C3 launch).
+# The shared-subroutine product (HBTC_FQMUL_SR) is 1.2 MB -> 150 KB of code here but no faster
+# (isolated 48.5 vs 49.9 ms): the pass is VALU-issue-bound, not instruction-fetch-bound.
 $(BUILD)/hbtc_rlc.p6.o: $(CSRC)/hbtc_rlc.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_PART=6 -DHBTC_INLINE_ALL -DHBTC_FQMUL_INLINE -c $< -o $@
 
@@ -64,16 +66,21 @@ $(BUILD)/hbtc_skg.p%.o: $(CSRC)/hbtc_skg.hip $(HDRS) | $(BUILD)
 # with the GT helpers (gt6.h mul / frob / exp_by_x) inlined: 960 -> ~330 B/lane of scratch (the
 # by-reference operands of the calls went through the stack), C3 unchanged, the 125-ciphertext
 # slice 18.3 -> 17.8 ms per epoch (profiles/r03/gt_inline/)
+# with the Fq product / squaring as ONE shared subroutine each (HBTC_FQMUL_SR, fq_fips_sr.h):
+# straight-line Fq2 products instead of the rolled select loop, ~100 B/lane less scratch; C3
+# 11.35 -> 11.62 M shares/s (profiles/r03/fq_sr/)
 $(BUILD)/hbtc_check.c%.o: $(CSRC)/hbtc_check.hip $(HDRS) | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -DHBTC_CHECK_PART=$* -DHBTC_GT_INLINE -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DHBTC_CHECK_PART=$* -DHBTC_GT_INLINE -DHBTC_FQMUL_SR -c $< -o $@
 
-# the G2 item pass, all helpers inlined (no calls; the product itself stays out of line)
+# the G2 item pass, all helpers inlined, the product as the shared subroutine (no ABI calls:
+# C2 658k -> 696k, C4 3.67M -> 3.93M shares/s with the check kernels, profiles/r03/fq_sr/)
 $(BUILD)/hbtc_sig.o: $(CSRC)/hbtc_sig.hip $(HDRS) | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -DHBTC_INLINE_ALL -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DHBTC_INLINE_ALL -DHBTC_FQMUL_SR -c $< -o $@
 
-# the pair-batch item pass (Ciphertext::verify / PublicKey::verify by RLC), helpers inlined
+# the pair-batch item pass (Ciphertext::verify / PublicKey::verify by RLC), helpers inlined,
+# the product as the shared subroutine
 $(BUILD)/hbtc_pb.o: $(CSRC)/hbtc_pb.hip $(HDRS) | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -DHBTC_INLINE_ALL -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DHBTC_INLINE_ALL -DHBTC_FQMUL_SR -c $< -o $@
 
 # Reliable Broadcast: Reed-Solomon over GF(2^8), SHA3 Merkle trees and proofs
 $(BUILD)/hbtc_bcast.o: $(CSRC)/hbtc_bcast.hip $(HDRS) | $(BUILD)

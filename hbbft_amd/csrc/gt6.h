@@ -81,6 +81,25 @@ HD void fq2_xi_if(Fq2& r, bool t, const Fq2& a) {
 // Fq2 product (Karatsuba) with ONE Fq multiplication site in a rolled 3-step loop: with the
 // ~660-instruction product-scanning multiply inlined, three sites per Fq2 product put the
 // cooperative kernels far past the instruction cache; the operand selects cost ~10%.
+// With the product as a shared subroutine (HBTC_FQMUL_SR) a site is a few dozen instructions:
+// straight-line Karatsuba, no operand selects.
+#if defined(__HIP_DEVICE_COMPILE__) && defined(HBTC_FQMUL_SR)
+HD void mul2(Fq2& r, const Fq2& a, const Fq2& b) {
+  Fq sa, sb, t0, t1, t2;
+  fq_add(sa, a.c0, a.c1);
+  fq_add(sb, b.c0, b.c1);
+  fq_mul(t0, a.c0, b.c0);
+  fq_mul(t1, a.c1, b.c1);
+  fq_mul(t2, sa, sb);
+  fq_sub(r.c0, t0, t1);
+  fq_sub(t2, t2, t0);
+  fq_sub(r.c1, t2, t1);
+}
+HD void mul2_fq(Fq2& r, const Fq2& a, const Fq& y) {
+  fq_mul(r.c0, a.c0, y);
+  fq_mul(r.c1, a.c1, y);
+}
+#else
 HD void mul2(Fq2& r, const Fq2& a, const Fq2& b) {
   Fq sa, sb;
   fq_add(sa, a.c0, a.c1);
@@ -112,6 +131,7 @@ HD void mul2_fq(Fq2& r, const Fq2& a, const Fq& y) {
   }
   r.c0 = t0;
 }
+#endif
 
 // ------------------------------------------------------------------------------ GT operations
 // Out-of-line on the device unless HBTC_GT_INLINE: the glue of the final exponentiation and the

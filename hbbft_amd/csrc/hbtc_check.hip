@@ -18,7 +18,9 @@
 // them (the plain group tries positions [0, half), the weighted group [half, count) starting
 // from T^half), with a wave-wide early exit once every failing unit has its answer.
 // few product sites per hot loop (gt6.h's rolled Fq2 product): inline the multiplication
+#ifndef HBTC_FQMUL_SR
 #define HBTC_FQMUL_INLINE
+#endif
 #include "gt6.h"
 #include "hbtc_kernels.h"
 

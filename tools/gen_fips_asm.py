@@ -20,6 +20,8 @@ Bounds as fq_fips.h: inputs < 2p, result < 2p; every 96-bit column sum fits.
 Usage: tools/gen_fips_asm.py > hbbft_amd/csrc/fq_fips_asm.h
 """
 
+import re
+
 ACC = "v[%d:%d]"
 
 
@@ -164,7 +166,214 @@ namespace fips {
 #endif""")
 
 
-if __name__ == "__main__" and "--selftest" not in __import__("sys").argv:
+
+# ------------------------------------------------------------------------------ subroutines
+# fq_fips_sr.h: the same two instruction lists as ONE shared subroutine each (module-level asm),
+# entered by s_swappc from a short call-site block, for translation units whose hot loops hold
+# many product sites (an inlined copy is ~5.6 KB of code: a point doubling plus a mixed addition
+# inline ~100 KB, past the 64 KB instruction cache, and the waves then stall on instruction
+# fetch).  Calling convention (every register fixed; the call-site asm names them as operands
+# and clobbers, so the compiler keeps nothing else there across a call):
+#   a: v8..v19 (the result overwrites it: r_j is written at column 12 + j, after the last read
+#   of a_j and b_j at column j + 11), b / the squaring's doubled limbs t_j: v20..v31, the
+#   squaring's carried doubled limbs: v32..v41, q: v42..v53, accumulators v54..v59, the modulus
+#   s48..s59, -p^-1 s60, target s[62:63], return address s[64:65] (below s72: at 8 waves per
+#   SIMD the registers from s72 up are reserved).
+SR_A, SR_B, SR_D1, SR_Q, SR_ACC, SR_P, SR_NP, SR_TGT, SR_RET = 8, 20, 32, 42, 54, 48, 60, 62, 64
+P_MOD = 0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab
+NP_MOD = (-pow(P_MOD, -1, 1 << 32)) % (1 << 32)
+
+
+def sr_body(square):
+    """gen_mul's list with every operand on its fixed register."""
+    acc = {
+        'v[" HBTC_XS(HBTC_FIPS_ACC0) ":" HBTC_XS(HBTC_FIPS_ACC1) "]': "v[%d:%d]" % (SR_ACC, SR_ACC + 1),
+        'v[" HBTC_XS(HBTC_FIPS_X0) ":" HBTC_XS(HBTC_FIPS_X1) "]': "v[%d:%d]" % (SR_ACC + 4, SR_ACC + 5),
+        'v" HBTC_XS(HBTC_FIPS_ACC0) "': "v%d" % SR_ACC,
+        'v" HBTC_XS(HBTC_FIPS_ACC1) "': "v%d" % (SR_ACC + 1),
+        'v" HBTC_XS(HBTC_FIPS_C2) "': "v%d" % (SR_ACC + 2),
+        'v" HBTC_XS(HBTC_FIPS_XC2) "': "v%d" % (SR_ACC + 3),
+        'v" HBTC_XS(HBTC_FIPS_X0) "': "v%d" % (SR_ACC + 4),
+        'v" HBTC_XS(HBTC_FIPS_X1) "': "v%d" % (SR_ACC + 5),
+    }
+
+    def reg(n):
+        if n < 12:
+            return "v%d" % (SR_A + n)            # r (overwrites a)
+        if n < 24:
+            return "v%d" % (SR_Q + n - 12)       # q
+        if n < 36:
+            return "v%d" % (SR_A + n - 24)       # a
+        if square:
+            if n < 48:
+                return "v%d" % (SR_B + n - 36)   # t_j (j = n - 36)
+            if n < 58:
+                return "v%d" % (SR_D1 + n - 48)  # carried doubled limbs, j = n - 46
+            if n < 70:
+                return "s%d" % (SR_P + n - 58)
+            return "s%d" % SR_NP
+        if n < 48:
+            return "v%d" % (SR_B + n - 36)
+        if n < 60:
+            return "s%d" % (SR_P + n - 48)
+        return "s%d" % SR_NP
+
+    out = []
+    for line in gen_mul(square):
+        for k in sorted(acc, key=len, reverse=True):
+            line = line.replace(k, acc[k])
+        out.append(re.sub(r"%(\d+)", lambda m: reg(int(m.group(1))), line))
+    return out
+
+
+def sr_text(label, square):
+    lines = [".p2align 8", "%s:" % label]
+    lines += ["s_mov_b32 s%d, 0x%08x" % (SR_P + i, (P_MOD >> (32 * i)) & 0xFFFFFFFF) for i in range(12)]
+    lines.append("s_mov_b32 s%d, 0x%08x" % (SR_NP, NP_MOD))
+    lines += sr_body(square)
+    lines.append("s_setpc_b64 s[%d:%d]" % (SR_RET, SR_RET + 1))
+    return lines
+
+
+def sr_call(name, label, square):
+    outs = ", ".join('"={v%d}"(r[%d])' % (SR_A + i, i) for i in range(12))
+    ins = ", ".join('"{v%d}"(a[%d])' % (SR_A + i, i) for i in range(12))
+    if square:
+        ins += ",\n        " + ", ".join('"{v%d}"(t[%d])' % (SR_B + j, j) for j in range(1, 12))
+        ins += ",\n        " + ", ".join('"{v%d}"(u[%d])' % (SR_D1 + j - 2, j) for j in range(2, 12))
+    else:
+        ins += ",\n        " + ", ".join('"{v%d}"(b[%d])' % (SR_B + i, i) for i in range(12))
+    clob = []
+    if square:
+        clob += ['"v%d"' % SR_B]  # t_0 is not an input
+    clob += ['"v%d"' % v for v in range(SR_Q, SR_ACC + 6)]
+    clob += ['"s%d"' % s for s in range(SR_P, SR_RET + 2)]
+    clob += ['"vcc"', '"scc"']
+    args = "uint32_t* r, const uint32_t* a" + ("" if square else ", const uint32_t* b")
+    prep = ""
+    if square:
+        prep = """  uint32_t t[12], u[12];
+#pragma unroll
+  for (int j = 1; j < 12; ++j) t[j] = a[j] << 1;
+#pragma unroll
+  for (int j = 2; j < 12; ++j) u[j] = (a[j] << 1) | (a[j - 1] >> 31);
+"""
+    call = ('      "s_getpc_b64 s[%d:%d]\\n\\t"\n' % (SR_TGT, SR_TGT + 1) +
+            '      "s_add_u32 s%d, s%d, %s@rel32@lo+4\\n\\t"\n' % (SR_TGT, SR_TGT, label) +
+            '      "s_addc_u32 s%d, s%d, %s@rel32@hi+12\\n\\t"\n' % (SR_TGT + 1, SR_TGT + 1, label) +
+            '      "s_swappc_b64 s[%d:%d], s[%d:%d]"' % (SR_RET, SR_RET + 1, SR_TGT, SR_TGT + 1))
+    return """__device__ __forceinline__ void %s(%s) {
+%s  asm volatile(
+%s
+      : %s
+      : %s
+      : %s);
+}
+""" % (name, args, prep, call, outs, ins, ", ".join(clob))
+
+
+def main_sr():
+    print("""// GENERATED by tools/gen_fips_asm.py --sr -- do not edit.
+// The Fq Montgomery product and squaring of fq_fips_asm.h as ONE shared subroutine each, called
+// with s_swappc from a four-instruction call-site block (see the generator: calling convention,
+// and why: code size of the hot loops vs the instruction cache).  Device builds that define
+// HBTC_FQMUL_SR only.  Only VALU instructions on registers, plus the SALU modulus setup and the
+// branches.
+#pragma once
+#include <cstdint>
+#if defined(__HIP_DEVICE_COMPILE__)""")
+    # The subroutines live in the code of a never-launched kernel of each translation unit
+    # (file-scope asm is not emitted in the device compilation): an s_endpgm, then the bodies.
+    print('static __global__ void __launch_bounds__(64) hbtc_fq_sr_holder() {')
+    print('  asm volatile(')
+    print('    "s_endpgm\\n"')
+    for label, square in (("hbtc_fqmul_sr", False), ("hbtc_fqsqr_sr", True)):
+        for l in sr_text(label, square):
+            print('    "%s\\n"' % l)
+    print('    ::: "memory");')
+    print('}')
+    print("""namespace hbtc {
+namespace fips {
+""")
+    print(sr_call("mont_mul_sr", "hbtc_fqmul_sr", False))
+    print(sr_call("mont_sqr_sr", "hbtc_fqsqr_sr", True))
+    print("""}  // namespace fips
+}  // namespace hbtc
+#endif""")
+
+
+def selftest_sr(trials=200):
+    """Run the subroutine bodies on a concrete register file (VCC as one lane's carry bit)."""
+    import random
+    M32 = (1 << 32) - 1
+    rng = random.Random(9)
+    for square in (False, True):
+        prog = sr_text("x", square)[2:-1]
+        for _ in range(trials):
+            a = rng.randrange(2 * P_MOD)
+            b = a if square else rng.randrange(2 * P_MOD)
+            regs = {}
+            for i in range(12):
+                regs["v%d" % (SR_A + i)] = (a >> (32 * i)) & M32
+            al = [(a >> (32 * i)) & M32 for i in range(12)]
+            if square:
+                for j in range(1, 12):
+                    regs["v%d" % (SR_B + j)] = (al[j] << 1) & M32
+                for j in range(2, 12):
+                    regs["v%d" % (SR_D1 + j - 2)] = ((al[j] << 1) | (al[j - 1] >> 31)) & M32
+            else:
+                for i in range(12):
+                    regs["v%d" % (SR_B + i)] = (b >> (32 * i)) & M32
+            vcc = 0
+
+            def val(t):
+                t = t.strip()
+                if t.startswith("0x") or t.isdigit():
+                    return int(t, 0)
+                m = re.fullmatch(r"v\[(\d+):(\d+)\]", t)
+                if m:
+                    return regs["v" + m.group(1)] | (regs["v" + m.group(2)] << 32)
+                return regs[t]
+
+            def store(t, v):
+                t = t.strip()
+                m = re.fullmatch(r"v\[(\d+):(\d+)\]", t)
+                if m:
+                    regs["v" + m.group(1)] = v & M32
+                    regs["v" + m.group(2)] = (v >> 32) & M32
+                else:
+                    regs[t] = v & M32
+
+            for line in prog:
+                op, rest = line.split(" ", 1)
+                args = re.split(r",(?![^\[]*\])", rest)
+                if op in ("s_mov_b32", "v_mov_b32"):
+                    store(args[0], val(args[1]))
+                elif op == "v_mad_u64_u32":
+                    d, _, x, y, z = args
+                    s = val(x) * val(y) + val(z)
+                    vcc = s >> 64
+                    store(d, s & ((1 << 64) - 1))
+                elif op == "v_addc_co_u32_e64":
+                    d, _, x, y, _c = args
+                    s = val(x) + val(y) + vcc
+                    vcc = s >> 32
+                    store(d, s)
+                elif op == "v_mul_lo_u32":
+                    d, x, y = args
+                    store(d, val(x) * val(y))
+                else:
+                    raise ValueError(op)
+            r = sum(regs["v%d" % (SR_A + i)] << (32 * i) for i in range(12))
+            want = a * b * pow(2, -384, P_MOD) % P_MOD
+            assert r < 2 * P_MOD and r % P_MOD == want, ("sr square" if square else "sr mul", hex(a), hex(b))
+    print("selftest_sr ok")
+
+
+if __name__ == "__main__" and len(__import__("sys").argv) > 1 and __import__("sys").argv[1] == "--sr":
+    main_sr()
+
+if __name__ == "__main__" and len(__import__("sys").argv) == 1:
     main()
 
 
@@ -261,3 +470,4 @@ def selftest(trials=300):
 
 if __name__ == "__main__" and len(__import__("sys").argv) > 1 and __import__("sys").argv[1] == "--selftest":
     selftest()
+    selftest_sr()

@@ -15,7 +15,8 @@ using namespace hbtc;
 constexpr int ITERS = 512;
 
 // V 0-2: products (rolled / unrolled CIOS, C++-glued FIPS); 3: one-block asm FIPS product;
-// 4: squaring through the FIPS product; 5: one-block asm FIPS squaring (b ignored)
+// 4: squaring through the FIPS product; 5: one-block asm FIPS squaring (b ignored); 6 / 7: the
+// product / squaring as the shared subroutine of fq_fips_sr.h (build with -DHBTC_FQMUL_SR)
 template <int V>
 __device__ __forceinline__ void mulv(Fq& r, const Fq& a, const Fq& b) {
   if constexpr (V == 0) mont_mul<12, 1>(r, a, b, FQ_P, FQ_NP);
@@ -24,7 +25,9 @@ __device__ __forceinline__ void mulv(Fq& r, const Fq& a, const Fq& b) {
   else if constexpr (V == 4) mont_mul_fips(r.v, a.v, a.v, FQ_P, FQ_NP);
 #if defined(__HIP_DEVICE_COMPILE__)
   else if constexpr (V == 3) fips::mont_mul_asm(r.v, a.v, b.v);
-  else fips::mont_sqr_asm(r.v, a.v);
+  else if constexpr (V == 5) fips::mont_sqr_asm(r.v, a.v);
+  else if constexpr (V == 6) fips::mont_mul_sr(r.v, a.v, b.v);  // subroutine (fq_fips_sr.h)
+  else fips::mont_sqr_sr(r.v, a.v);
 #endif
 }
 
@@ -72,7 +75,7 @@ int main() {
   CHK(hipMalloc(&d_out, sizeof(Fq) * nthreads));
   CHK(hipMemcpy(d_in, h.data(), sizeof(Fq) * 1024, hipMemcpyHostToDevice));
   // cross-check
-  std::vector<Fq> rv[6];
+  std::vector<Fq> rv[8];
   auto chk = [&](auto kern, int v) {
     rv[v].resize(1024);
     hipLaunchKernelGGL(kern, dim3(16), dim3(64), 0, 0, d_in, d_out);
@@ -84,6 +87,8 @@ int main() {
   chk(k_check<3>, 3);
   chk(k_check<4>, 4);
   chk(k_check<5>, 5);
+  chk(k_check<6>, 6);
+  chk(k_check<7>, 7);
   int bad = 0, bad_sq = 0;
   for (int i = 0; i < 1024; ++i) {
     Fq hr, hs;
@@ -92,8 +97,8 @@ int main() {
     mont_mul<12, 1>(hs, h[i], h[i], FQ_P, FQ_NP);
     fq_canon(hs, hs);
     for (int l = 0; l < 12; ++l) {
-      for (int v = 0; v < 4; ++v) bad += rv[v][i].v[l] != hr.v[l];
-      for (int v = 4; v < 6; ++v) bad_sq += rv[v][i].v[l] != hs.v[l];
+      for (int v : {0, 1, 2, 3, 6}) bad += rv[v][i].v[l] != hr.v[l];
+      for (int v : {4, 5, 7}) bad_sq += rv[v][i].v[l] != hs.v[l];
     }
   }
   printf("cross-check vs host CIOS: products %s (%d limb mismatches), squarings %s (%d)\n",
@@ -127,5 +132,7 @@ int main() {
   RUNV(3, "FIPS one-block asm")
   RUNV(4, "sqr via FIPS product")
   RUNV(5, "sqr one-block asm")
+  RUNV(6, "FIPS subroutine (s_swappc)")
+  RUNV(7, "sqr subroutine (s_swappc)")
   return 0;
 }
