@@ -133,6 +133,16 @@ HD void mul2_fq(Fq2& r, const Fq2& a, const Fq& y) {
 }
 #endif
 
+// The short operand-choice loops of the line product, the easy part and the Miller step stay
+// rolled where the product is inlined (code size: instruction cache); with the shared-subroutine
+// product they are unrolled, so the operand choices are compile-time.  (Unrolling mul's and
+// sqr's term loops too hoists their operand fetches: 220 -> 960 B/lane of scratch.)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(HBTC_FQMUL_SR) && !defined(HBTC_GT_ROLLED)
+#define HBTC_GT_SMALL_LOOP HBTC_PRAGMA(unroll)
+#else
+#define HBTC_GT_SMALL_LOOP HBTC_PRAGMA(unroll 1)
+#endif
+
 // ------------------------------------------------------------------------------ GT operations
 // Out-of-line on the device unless HBTC_GT_INLINE: the glue of the final exponentiation and the
 // location search call these a few dozen times per check; their by-reference operands cost
@@ -228,7 +238,7 @@ HD void mul_line_t(Fq2& f, const Fq& pa, uint32_t a, const Fq2& Ad, const Fq& pb
   const uint32_t k = ps.k;
   Fq2 acc;
   fq2_zero(acc);
-#pragma unroll 1
+HBTC_GT_SMALL_LOOP
   for (uint32_t t = 0; t < 3; ++t) {
     // term t: f_k A, f_{k-2} B (xi if k < 2), f_{k-3} Y (xi if k < 3)
     const uint32_t fk = t == 0 ? k : (t == 1 ? (k >= 2 ? k - 2 : k + 4) : (k >= 3 ? k - 3 : k + 3));
@@ -389,7 +399,7 @@ HD void easy_part(Fq2& r, const Fq2& f, const Pos& ps) {
   const uint32_t k = ps.k;
   // t_m = tx * x * x' - ty * y * y'
   Fq2 z0, z1;
-#pragma unroll 1
+HBTC_GT_SMALL_LOOP
   for (uint32_t t = 0; t < 2; ++t) {
     Fq2 x, y, q, sx, px, py;
     // the square term, then the product term: (n1 n2), (n0 n1), (n0 n2)
@@ -533,7 +543,7 @@ HD void miller2_t(Fq2& f, const MillerArg& m1, const MillerArg& m2, const Pos& p
                            : reinterpret_cast<const Fq*>(m2.lines + j);
       const Fq* Lr1 = k < 4 ? L1 : L2;
       Fq p1, p2;
-#pragma unroll 1
+HBTC_GT_SMALL_LOOP
       for (uint32_t t = 0; t < 2; ++t) {
         Fq q;
         fq_mul(q, t == 0 ? Lr1[c1] : L2[c2], t == 0 ? s1 : s2);
