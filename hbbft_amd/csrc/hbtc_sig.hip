@@ -22,6 +22,8 @@ namespace hbtc {
 // Two instances (launch_sig_items picks by the call's size): W = 2, two waves per SIMD with one
 // LDS array (rlc_reduce1; more VGPR spills per wave, C4's 10^4 tiles: k_sig_items 106 -> 80 ms)
 // and W = 1, one wave per SIMD with two arrays (shorter waves: C2's 200 tiles, 13.3 -> 10.2 ms).
+// Re-measured with the shared-subroutine product (2.5 KB / 0.7 KB of scratch per lane): C4 161
+// ms per step with W = 2 against 171 with W = 1 (profiles/r03/sig_waves/).
 // One wave per tile: decode every SignatureShare (zcash compressed G2 + subgroup check), r_i,
 // r_i sigma_i, r_i pk_i, then the plain and weighted tile / sub-tile sums in both groups.
 template <int W>
@@ -156,12 +158,16 @@ __global__ void __launch_bounds__(64) k_plines(int mode, uint32_t max_groups, ui
 
 static inline uint32_t sig_blocks(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
 
+#ifndef HBTC_SIG_ITEMS_W2_MIN
+#define HBTC_SIG_ITEMS_W2_MIN 1024u  // tiles above which the two-wave form runs
+#endif
+
 hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* sigs, const G1A* pk, const int32_t* pk_status,
                             const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,
                             SigTileSums* sums, G2A* dec, int32_t* status) {
   if (n_tiles == 0) return hipSuccess;
-  if (n_tiles > 1024)  // more tiles than SIMDs: throughput form
+  if (n_tiles > HBTC_SIG_ITEMS_W2_MIN)  // more tiles than SIMDs: throughput form
     hipLaunchKernelGGL(k_sig_items<2>, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk, pk_status,
                        pk_tab, n_pk, key, sus, sums, dec, status);
   else
