@@ -6,7 +6,8 @@
 // (/root/reference/src/threshold_decryption.rs:159): for a group G of shares of one
 // ciphertext, T = e(sum r_i d_i, H) e(-sum r_i pk_i, w) == 1 iff (except with probability
 // 2^-64) every share of G is valid; T_w, the same with position-weighted r_i, locates a single
-// wrong share as the p with T_w == T^p (hbtc_rlc.hip explains both).
+// wrong share as the weight w with T_w == T^w (hbtc_rlc.hip explains both; share i of a group of
+// 2^k has the weight bitrev_k(i), rlc_common.h).
 //
 // Levels:
 //   k_chk_tiles   every 64-share tile: (plain, weighted) unit; a failing tile's single wrong
@@ -83,9 +84,18 @@ __device__ __forceinline__ void pair_value(Fq2& e, const G1J& S, bool use1, cons
   gt::final_exp(e, f, ps);
 }
 
-// Single-error location for a failing unit: smallest p < count with Tw == T^p, or -1.  The
-// group on side 0 tries [0, half), side 1 tries [half, count) from T^half (half = 2^lg).
-// Every lane of the wave runs the loop; `need` is false on units that passed or are idle.
+// The trees of the item passes give share i of a group of 2^k the weight bitrev_k(i)
+// (rlc_common.h): the position of weight w, or -1 past the group's count.
+__device__ __forceinline__ int32_t weight_pos(int32_t w, int k, uint32_t count) {
+  if (w < 0) return -1;
+  const uint32_t i = __builtin_bitreverse32((uint32_t)w) >> (32 - k);
+  return i < count ? (int32_t)i : -1;
+}
+
+// Single-error location for a failing unit of a group of 2^(lg+1) shares: the weight w with
+// Tw == T^w (unique: T has prime order), mapped to its position, or -1.  The group on side 0
+// tries [0, half), side 1 tries [half, 2 half) from T^half (half = 2^lg).  Every lane of the wave
+// runs the loop; `need` is false on units that passed or are idle.
 __device__ __forceinline__ int32_t locate(const Fq2& T, const Fq2& Tw, uint32_t count, int lg, bool need,
                           const UnitLane& ul) {
   const uint32_t half = 1u << lg;
@@ -100,15 +110,15 @@ __device__ __forceinline__ int32_t locate(const Fq2& T, const Fq2& Tw, uint32_t 
   int32_t found = -1;
 #pragma unroll 1
   for (uint32_t q = 0; q < half; ++q) {
-    const bool live = need && found < 0 && p0 + q < count;
+    const bool live = need && found < 0;
     if (!gt::wave_any(live)) break;
     if (gt::equal(acc, Tw, ul.ps) && live) found = (int32_t)(p0 + q);
     gt::mul(acc, acc, T, ul.ps);
   }
-  // combine the two halves (side 0's answer first: the smaller position)
+  // combine the two halves
   const int32_t other = (int32_t)gt::shfl((uint32_t)found, ul.partner);
   const int32_t f0 = ul.side ? other : found, f1 = ul.side ? found : other;
-  return f0 >= 0 ? f0 : f1;
+  return weight_pos(f0 >= 0 ? f0 : f1, lg + 1, count);
 }
 
 // T (plain, side 0) and Tw (weighted, side 1) on both groups of a unit, the plain verdict.
@@ -198,12 +208,14 @@ __device__ __forceinline__ void gt_fingerprint(uint32_t& a, uint32_t& b, const F
   b = gt::shfl(c.v[0], gt::src(ps, 3));
 }
 
-// Single-error location inside one group: the p < count with Tw == T^p, or -1.  Baby-step
-// giant-step over p = 8 a + b: fingerprints of T^b (b < 8), then Tw T^(-8 a) (T^-8 = conj(T^8):
-// T is cyclotomic) for a < 8 — at most 16 products instead of 64 — and the match is confirmed
-// exactly (T^p recomputed by square-and-multiply and compared in full).
-__device__ __forceinline__ int32_t locate_group(const Fq2& T, const Fq2& Tw, uint32_t count,
+// Single-error location inside one group of 2^lg shares: the weight w < 2^lg with Tw == T^w
+// mapped to its position (weight_pos), or -1.  Baby-step giant-step over w = 8 a + b:
+// fingerprints of T^b (b < 8), then Tw T^(-8 a) (T^-8 = conj(T^8): T is cyclotomic) for
+// 8 a < 2^lg — at most 16 products instead of 64 — and the match is confirmed exactly (T^w
+// recomputed by square-and-multiply and compared in full).
+__device__ __forceinline__ int32_t locate_group(const Fq2& T, const Fq2& Tw, uint32_t count, int lg,
                                                 bool need, const Pos& ps) {
+  const uint32_t size = 1u << lg;
   uint32_t fa[8], fb[8];
   Fq2 acc;
   gt::set_one(acc, ps);
@@ -218,13 +230,13 @@ __device__ __forceinline__ int32_t locate_group(const Fq2& T, const Fq2& Tw, uin
   int32_t found = -1;
 #pragma unroll 1
   for (uint32_t a = 0; a < 8u; ++a) {
-    const bool live = need && found < 0 && 8u * a < count;
+    const bool live = need && found < 0 && 8u * a < size;
     if (!gt::wave_any(live)) break;
     uint32_t ga, gb;
     gt_fingerprint(ga, gb, g, ps);
 #pragma unroll
     for (int b = 0; b < 8; ++b)
-      if (live && found < 0 && ga == fa[b] && gb == fb[b] && 8u * a + (uint32_t)b < count)
+      if (live && found < 0 && ga == fa[b] && gb == fb[b] && 8u * a + (uint32_t)b < size)
         found = (int32_t)(8u * a + (uint32_t)b);
     gt::mul(g, g, step, ps);
   }
@@ -240,7 +252,7 @@ __device__ __forceinline__ int32_t locate_group(const Fq2& T, const Fq2& Tw, uin
     gt::fq2_sel(tp, ((pe >> bit) & 1u) != 0, m, tp);
   }
   const bool ok = gt::equal(tp, Tw, ps);
-  return found >= 0 && ok ? found : -1;
+  return weight_pos(found >= 0 && ok ? found : -1, lg, count);
 }
 
 }  // namespace
@@ -373,7 +385,8 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_weighted(
   Fq2 Tw;
   pair_value(Tw, S, use1, h_lines + (size_t)r.inst * MILLER_STEPS, P, use2,
              w_lines + (size_t)r.inst * MILLER_STEPS, ul.ps);
-  const int32_t loc = locate_group(T, Tw, r.hi - r.lo, r.active, ul.ps);
+  const int32_t loc = locate_group(T, Tw, r.hi - r.lo, LEVEL == 0 ? 6 : (LEVEL == 2 ? 5 : 3),
+                                   r.active, ul.ps);
   if (!r.active || ul.ps.k != 0) return;
   if (loc >= 0 && status[r.lo + loc] == HBTC_RLC_PENDING) {
     status[r.lo + loc] = HBTC_REJECT;

@@ -12,7 +12,8 @@
 // checks it, so E_i has order 1 or r).
 //
 // Single-error location.  Next to the plain sum the item pass also forms the position-weighted
-// sum (weights = the share's position p_i inside its group), so each group yields
+// sum (weights p_i distinct in [0, |G|): p_i = bitrev_k(i) for share i of a group of 2^k, which
+// the reduction tree forms with one doubling per level, rlc_common.h), so each group yields
 //     T = prod E_i^r_i      and      T_w = prod E_i^(p_i r_i).
 // If exactly one share b is wrong, T_w == T^(p_b): the search over p = 0..|G|-1 finds it with
 // |G|-1 GT multiplications instead of per-share pairings, and the rest of the group is valid.

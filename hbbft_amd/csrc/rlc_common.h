@@ -94,7 +94,9 @@ __device__ __forceinline__ void rlc_list_leaf(const Suspects& sus, bool leaf, ui
 
 // Tree reduction of the per-lane points q over the wave (lane = position in the tile): the sum
 // A and the position-weighted sum B of every aligned group of 8 (-> outA/outB[0..7]) and of the
-// tile (-> [8]).  Merging halves of size s:  A = A_l + A_r,  B = B_l + B_r + s A_r.
+// tile (-> [8]).  Merging halves:  A = A_l + A_r,  B = 2 (B_l + B_r) + A_r, so share i of a group
+// of 2^k carries the weight bitrev_k(i) (one doubling per level instead of log2(s) for the
+// positional weights B_l + B_r + s A_r; hbtc_check.hip maps a located weight back).
 template <class F>
 __device__ void rlc_reduce(Jac<F>* redA, Jac<F>* redB, const Jac<F>& q, uint32_t lane,
                            Jac<F>* outA, Jac<F>* outB) {
@@ -111,11 +113,8 @@ __device__ void rlc_reduce(Jac<F>* redA, Jac<F>* redB, const Jac<F>& q, uint32_t
         jac_add(b, b, br);
       }
       const Jac<F> ar = redA[lane + s];
-      {
-        Jac<F> sa = ar;
-        for (uint32_t d = 1; d < s; d <<= 1) jac_dbl(sa, sa);
-        jac_add(b, b, sa);
-      }
+      jac_dbl(b, b);
+      jac_add(b, b, ar);
       redB[lane] = b;
       Jac<F> a = redA[lane];
       jac_add(a, a, ar);
@@ -181,9 +180,8 @@ __device__ void rlc_reduce1(Jac<F>* red, const Jac<F>& q, uint32_t lane, Jac<F>*
       if (active) jac_add(b, b, br);
     }
     if (active) {
-      Jac<F> sa = red[lane + s];
-      for (uint32_t d = 1; d < s; d <<= 1) jac_dbl(sa, sa);
-      jac_add(b, b, sa);
+      jac_dbl(b, b);  // B = 2 (B_l + B_r) + A_r (bit-reversed weights, as rlc_reduce)
+      jac_add(b, b, red[lane + s]);
       Jac<F> a = red[lane];
       const Jac<F> ar = red[lane + s];
       jac_add(a, a, ar);
@@ -207,7 +205,7 @@ __device__ void rlc_reduce1(Jac<F>* red, const Jac<F>& q, uint32_t lane, Jac<F>*
 // Level 1 pairs lanes (2m, 2m+1) in registers: the even lane forms the S pair, the odd lane the
 // P pair (A = left + right, B = right).  From then on LDS entry 2m holds an S group and entry
 // 2m+1 a P group; at level s the lanes with lane mod 2s in {0, 1} merge entry `lane` with entry
-// `lane + s` (A = A_l + A_r, B = B_l + B_r + s A_r).  Outputs as rlc_reduce: [0..7] the aligned
+// `lane + s` (A = A_l + A_r, B = 2 (B_l + B_r) + A_r).  Outputs as rlc_reduce: [0..7] the aligned
 // groups of 8, [8] the tile.  Half the sequential merge chain of two separate reductions.
 __device__ __forceinline__ void rlc_reduce_sp(G1J* redA, G1J* redB, const G1J& S, const G1J& P,
                                               uint32_t lane, G1J* outS, G1J* outSW, G1J* outP,
@@ -240,11 +238,8 @@ __device__ __forceinline__ void rlc_reduce_sp(G1J* redA, G1J* redB, const G1J& S
         jac_add(bl, bl, br);
       }
       const G1J ar = redA[lane + s];
-      {
-        G1J sa = ar;
-        for (uint32_t d = 1; d < s; d <<= 1) jac_dbl(sa, sa);
-        jac_add(bl, bl, sa);
-      }
+      jac_dbl(bl, bl);
+      jac_add(bl, bl, ar);
       redB[lane] = bl;
       G1J al = redA[lane];
       jac_add(al, al, ar);
