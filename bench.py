@@ -37,6 +37,15 @@ import random
 import sys
 import time
 
+# HIP hardware queues per process, read once at the first HIP call: the library's four lanes x
+# (verification + preparation) streams plus the strong-scaling merge's torch / RCCL streams
+# share HIP's default 4 queues, and a gather stream's wait on every lane then blocks the lane
+# work queued behind it on the same queue: the merge at world size 1 cost 28.0 vs 16.5 ms per
+# 125-ciphertext slice and 101.7 vs 79.6 ms per C3 epoch; with 16 queues 17.7 / 80.0 ms, plain
+# runs unchanged (profiles/r03/hw_queues/).  HBTC_KEEP_HW_QUEUES=1 keeps the environment's value.
+if not os.environ.get("HBTC_KEEP_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -227,13 +236,17 @@ class StrongGather:
                      "cst": torch.empty(tot_cts, dtype=torch.int32, device=dev)} for _ in range(N_OUT)]
 
     def before_step(self, ctx):
-        ctx.ctx_wait_stream(self.streams[(self.ep.cur + 1) % N_OUT].cuda_stream)
+        if "wait" not in DIAG_SKIP:
+            ctx.ctx_wait_stream(self.streams[(self.ep.cur + 1) % N_OUT].cuda_stream)
 
     def after_step(self, ctx):
         from hbbft_amd import shard
         j = self.ep.cur
         s = self.streams[j]
-        ctx.stream_wait_ctx(s.cuda_stream)
+        if "order" not in DIAG_SKIP:
+            ctx.stream_wait_ctx(s.cuda_stream)
+        if "gather" in DIAG_SKIP:
+            return
         out = self.ep.out[j]
         with self.torch.cuda.stream(s):
             shard.gather_slices(self.dist, out["status"][1], self.len_items, out=self.all[j]["status"])
@@ -362,6 +375,9 @@ def rocprof_avg_ms(csv_path, kernel):
 
 
 N_OUT = 6  # output sets rotated per step (Epoch.step): four epochs in flight + two gathers
+# diagnostics of the merge's cost (never set by the driver): HBTC_BENCH_SKIP = comma list of
+# wait (output-set reuse wait), order (gather after the verification), gather (the collectives)
+DIAG_SKIP = set(filter(None, os.environ.get("HBTC_BENCH_SKIP", "").split(",")))
 
 FAMS = ["dec_verify", "rlc_items", "chk_tiles", "chk_tiles_w", "chk_halves", "chk_halves_w", "chk_subs", "chk_subs_w",
         "chk_leaves", "rlc_finalize", "lagrange", "comb_decode", "comb_digits", "combine", "prepare"]
@@ -369,12 +385,21 @@ FAMS = ["dec_verify", "rlc_items", "chk_tiles", "chk_tiles_w", "chk_halves", "ch
 
 def timed(ctx, ep, steps, warmup, dist=None, gather=None, sync_all=None):
     """W untimed steps, then exactly K steps bracketed by barrier + device syncs."""
+    host_t = [0.0, 0.0, 0.0]
+
     def run():
+        t = time.perf_counter()
         if gather:
             gather.before_step(ctx)
+        t1 = time.perf_counter()
         ep.step(ctx)
+        t2 = time.perf_counter()
         if gather:
             gather.after_step(ctx)
+        t3 = time.perf_counter()
+        host_t[0] += t1 - t
+        host_t[1] += t2 - t1
+        host_t[2] += t3 - t2
 
     def fence():
         ctx.sync()
@@ -389,11 +414,16 @@ def timed(ctx, ep, steps, warmup, dist=None, gather=None, sync_all=None):
     if dist:
         dist.barrier()
     fence()
+    host_t[:] = [0.0, 0.0, 0.0]
     t0 = time.perf_counter()
     for _ in range(steps):
         run()
     fence()
-    return time.perf_counter() - t0
+    dt = time.perf_counter() - t0
+    if DIAG_SKIP or os.environ.get("HBTC_BENCH_HOSTT"):
+        print("host ms per step: before %.2f  step %.2f  after %.2f; %.2f ms per step in all"
+              % (tuple(1e3 * x / steps for x in host_t) + (1e3 * dt / steps,)), file=sys.stderr, flush=True)
+    return dt
 
 
 def host_buffer_line(ctx, ep, steps, warmup=2):
@@ -529,7 +559,9 @@ def main():
         ep.step(ctx)
         ctx.sync()
         iso = {f: ctx.timing_read(f) for f in FAMS}
-    if strong:
+    if strong and "gather" in DIAG_SKIP:
+        mism, comb_ok, n_acc = ep.check(ctx)  # diagnostics without the collectives: local check
+    elif strong:
         # the merged whole epoch on every rank, against the whole epoch's construction
         st, g, cst = gather.merged()
         expected = np.concatenate([np.asarray(x) for x in _all_expected(dist, ep, torch, dev, slices)])

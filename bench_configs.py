@@ -43,6 +43,11 @@ import random
 import sys
 import time
 
+# 16 HIP hardware queues per process, as bench.py (the library's lanes and streams, plus the node
+# path's devices, otherwise share HIP's default 4); HBTC_KEEP_HW_QUEUES=1 keeps the environment's
+if not os.environ.get("HBTC_KEEP_HW_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
