@@ -360,7 +360,7 @@ def max_over_ranks(elapsed, dist, device=None):
 
 
 # committed rocprofv3 summaries of this command (kernel trace + PMC passes), newest first
-PROFILE_DIRS = ("profiles/r03/final2", "profiles/r03/headline", "profiles/r03/headline_a", "profiles/r02g/headline")
+PROFILE_DIRS = ("profiles/r03/final4", "profiles/r03/final2", "profiles/r03/headline", "profiles/r03/headline_a", "profiles/r02g/headline")
 
 
 def rocprof_avg_ms(csv_path, kernel):
