@@ -76,6 +76,8 @@ SIGNATURES = {
     "hbtc_skg_check_acks": (_I32, [_P, _U32, _U32, _U32, _P, _P, _P, _U32, _P, _P, _P, _P]),
     "hbtc_set_verify_mode": (_I32, [_P, _I32]),
     "hbtc_set_rlc_bits": (_I32, [_P, _U32]),
+    "hbtc_get_rlc_bits": (_I32, [_P, ctypes.POINTER(_U32)]),
+    "hbtc_check_schedule_for": (_I32, [_P, _U32, ctypes.POINTER(_I32)]),
     "hbtc_sha3_256": (_I32, [_P, _SZ, _P]),
     "hbtc_hash_g2": (_I32, [_P, _SZ, _P]),
     "hbtc_hash_g1_g2": (_I32, [_P, _P, _SZ, _P]),
@@ -83,6 +85,8 @@ SIGNATURES = {
     "hbtc_hash_g1_g2_batch": (_I32, [_U32, _P, _P, _P, _P]),
     "hbtc_hash_g2_batch_gpu": (_I32, [_P, _U32, _P, _P, _P]),
     "hbtc_hash_g1_g2_batch_gpu": (_I32, [_P, _U32, _P, _P, _P, _P]),
+    "hbtc_chacha04_words": (_I32, [_P, _U32, _P]),
+    "hbtc_chacha04_words_gpu": (_I32, [_P, _P, _U32, _P]),
     "hbtc_rlc_last_leaves": (_I32, [_P, ctypes.POINTER(_U32)]),
     "hbtc_timing_enable": (_I32, [_P, _I32]),
     "hbtc_timing_read": (_I32, [_P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
@@ -175,6 +179,18 @@ def sha3_256(msg):
     if load().hbtc_sha3_256(m, len(m), out) != 0:
         raise HbtcError("hbtc_sha3_256 failed")
     return out.raw
+
+
+def chacha04_words(seed, n):
+    """The first n words of rand 0.4's ChaChaRng::from_seed(seed) (8 u32 seed words) from the
+    host hashes' ChaCha code (no GPU): the ChaCha20 known-answer tests' entry point."""
+    s = np.ascontiguousarray(np.asarray(seed, dtype=np.uint32))
+    if s.shape != (8,):
+        raise ValueError("seed must be 8 u32 words")
+    out = np.zeros(n, np.uint32)
+    if load().hbtc_chacha04_words(_ptr(s), n, _ptr(out)) != 0:
+        raise HbtcError("hbtc_chacha04_words failed")
+    return out
 
 
 def hash_g2(msg):
@@ -310,8 +326,9 @@ class Context:
     def close(self):
         if getattr(self, "h", None):
             if not getattr(self, "_borrowed", False):
-                self.lib.hbtc_ctx_destroy(self.h)
+                self.lib.hbtc_ctx_destroy(self.h)  # completes in-flight tickets into their outputs
             self.h = None
+            self._inflight.clear()
 
     def __del__(self):
         try:
@@ -343,6 +360,16 @@ class Context:
         self._check(self.lib.hbtc_hash_g1_g2_batch_gpu(self.h, n, _ptr(u), _ptr(buf), _ptr(off),
                                                        _ptr(out)), "hbtc_hash_g1_g2_batch_gpu")
         return [bytes(out[96 * i:96 * i + 96]) for i in range(n)]
+
+    def chacha04_words(self, seed, n):
+        """chacha04_words on this context's GPU (the ChaCha code of k_hash_cand)."""
+        s = np.ascontiguousarray(np.asarray(seed, dtype=np.uint32))
+        if s.shape != (8,):
+            raise ValueError("seed must be 8 u32 words")
+        out = np.zeros(max(n, 1), np.uint32)
+        self._check(self.lib.hbtc_chacha04_words_gpu(self.h, _ptr(s), n, _ptr(out)),
+                    "hbtc_chacha04_words_gpu")
+        return out[:n]
 
     # ---- key sets
     def keyset_load(self, pk_shares):
@@ -381,14 +408,36 @@ class Context:
 
     # ---- pipelined host-buffer epochs (hbtc_*_epoch_submit / hbtc_wait)
     class Pending:
-        """A submitted epoch: its output arrays (filled by wait()) and the inputs kept alive."""
+        """A submitted epoch: its output arrays (filled by wait()) and the inputs kept alive.
+
+        The C side writes into the output arrays when the ticket completes — at wait(), or
+        unasked when a later submit reuses the ticket's lane, or at hbtc_ctx_destroy — so the
+        Context, not this object, owns them until then (a dropped Pending cannot leave the
+        library writing into freed memory)."""
 
         def __init__(self, ctx, ticket, outs, keep):
             self.ctx, self.ticket, self.outs, self._keep = ctx, ticket, outs, keep
 
         def wait(self):
             self.ctx._check(self.ctx.lib.hbtc_wait(self.ctx.h, self.ticket), "hbtc_wait")
+            self.ctx._inflight.pop(self.ticket, None)
             return self.outs
+
+    # tickets whose buffers the Context holds before it completes the oldest itself
+    MAX_HELD_TICKETS = 16
+
+    def _hold(self, ticket, outs, keep):
+        held = self._inflight
+        held[ticket] = (outs, keep)
+        while len(held) > self.MAX_HELD_TICKETS:  # complete (normally long finished) old epochs
+            old = min(held)
+            self._check(self.lib.hbtc_wait(self.h, old), "hbtc_wait")
+            held.pop(old, None)
+        return Context.Pending(self, ticket, outs, keep)
+
+    @property
+    def _inflight(self):
+        return self.__dict__.setdefault("_inflight_d", {})
 
     def dec_epoch_submit(self, keyset, H, w, offsets, idx, shares, t, outs=None):
         """Submit one epoch of DecryptionShares (verification + combine of the first t verified
@@ -405,7 +454,7 @@ class Context:
         self._check(self.lib.hbtc_dec_epoch_submit(self.h, keyset, n_ct, _ptr(Hb), _ptr(wb), _ptr(off), _ptr(ix),
                                                    _ptr(sb), t, _ptr(outs[0]), _ptr(outs[1]), _ptr(outs[2]),
                                                    ctypes.byref(tk)), "hbtc_dec_epoch_submit")
-        return Context.Pending(self, tk.value, outs, (off,))
+        return self._hold(tk.value, outs, (off,))
 
     def sig_epoch_submit(self, keyset, H, offsets, idx, sigs, t, outs=None):
         """The SignatureShare epoch (coins): wait() gives (status, sig [n, 96], parity, combine status)."""
@@ -420,7 +469,7 @@ class Context:
         self._check(self.lib.hbtc_sig_epoch_submit(self.h, keyset, n_inst, _ptr(Hb), _ptr(off), _ptr(ix), _ptr(sb),
                                                    t, _ptr(outs[0]), _ptr(outs[1]), _ptr(outs[2]),
                                                    _ptr(outs[3]), ctypes.byref(tk)), "hbtc_sig_epoch_submit")
-        return Context.Pending(self, tk.value, outs, (off,))
+        return self._hold(tk.value, outs, (off,))
 
     def verify_sigs(self, pks, H, sigs):
         pk, Hb, sb = _join(pks, 48), _join(H, 96), _join(sigs, 96)
@@ -660,8 +709,20 @@ class Context:
         self._check(self.lib.hbtc_set_verify_mode(self.h, int(mode)), "hbtc_set_verify_mode")
 
     def set_rlc_bits(self, bits):
-        """RLC scalar size: 64 (default, <= 2^-64 per group check) or 128 (<= 2^-128)."""
+        """RLC scalar size: 128 (default, <= 2^-128 per group check) or 64 (<= 2^-64)."""
         self._check(self.lib.hbtc_set_rlc_bits(self.h, int(bits)), "hbtc_set_rlc_bits")
+
+    def rlc_bits(self):
+        b = _U32()
+        self._check(self.lib.hbtc_get_rlc_bits(self.h, ctypes.byref(b)), "hbtc_get_rlc_bits")
+        return b.value
+
+    def check_schedule_for(self, n_tiles):
+        """The group-check schedule (CHECK_*) an RLC call of n_tiles 64-share tiles gets."""
+        s = _I32()
+        self._check(self.lib.hbtc_check_schedule_for(self.h, int(n_tiles), ctypes.byref(s)),
+                    "hbtc_check_schedule_for")
+        return s.value
 
     def set_check_schedule(self, schedule):
         """HBTC_CHECK_* (include/hbtc.h): -1 auto, 0 plain-first, 1 paired + sub-tiles, 2 paired -> leaves."""

@@ -25,6 +25,7 @@ void hash_g2_candidate(const uint8_t* msg, size_t len, G2A& p);
 void hash_g1_g2_c96(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8_t* out96);
 hipError_t launch_hash_cand(hipStream_t s, uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
                             const uint32_t* offsets, G2A* cand);
+hipError_t launch_chacha04_words(hipStream_t s, const uint32_t* seed8, uint32_t n, uint32_t* out);
 hipError_t launch_unframe(hipStream_t s, uint32_t n, uint32_t size, const uint8_t* framed, uint8_t* items);
 hipError_t launch_stage_copy(hipStream_t s, const void* src, void* dst, size_t bytes);
 hipError_t launch_zero_u32(hipStream_t s, uint32_t* p, size_t n);
@@ -124,7 +125,7 @@ struct hbtc_ctx {
   std::map<std::string, DevBuf> bufs;
   int verify_mode = HBTC_MODE_RLC;
   bool track_senders = true;
-  uint32_t rlc_bits = 64;  // hbtc_set_rlc_bits
+  uint32_t rlc_bits = 128;  // hbtc_set_rlc_bits (default: the curve's ~2^-128 level)
   bool probe_cold = true;  // probe pass on a cold key set (HBTC_PROBE=0: off)
   uint64_t probes = 0;     // probe passes run
   const uint32_t* last_leaf_count = nullptr;  // device counter of the last RLC call
@@ -2166,6 +2167,20 @@ int hbtc_set_rlc_bits(hbtc_ctx* c, uint32_t bits) {
   return HBTC_OK;
 }
 
+int hbtc_get_rlc_bits(hbtc_ctx* c, uint32_t* bits) {
+  if (!c || !bits) return HBTC_ERR_ARG;
+  Guard g(c);
+  *bits = c->rlc_bits;
+  return HBTC_OK;
+}
+
+int hbtc_check_schedule_for(hbtc_ctx* c, uint32_t n_tiles, int* schedule) {
+  if (!c || !schedule) return HBTC_ERR_ARG;
+  Guard g(c);
+  *schedule = check_mode(c, n_tiles);
+  return HBTC_OK;
+}
+
 int hbtc_set_verify_mode(hbtc_ctx* c, int mode) {
   if (!c || (mode != HBTC_MODE_PER_SHARE && mode != HBTC_MODE_RLC)) return HBTC_ERR_ARG;
   Guard g(c);
@@ -2253,6 +2268,17 @@ int hbtc_hash_g2_batch_gpu(hbtc_ctx* c, uint32_t n, const uint8_t* msgs, const u
     return HBTC_ERR_ARG;
   Guard g(c);
   return hash_batch_gpu(c, n, nullptr, msgs, offsets, out_c96);
+}
+
+int hbtc_chacha04_words_gpu(hbtc_ctx* c, const uint32_t* seed8, uint32_t n, uint32_t* out) {
+  if (!c || !seed8 || (!out && n)) return HBTC_ERR_ARG;
+  if (n == 0) return HBTC_OK;
+  Guard g(c);
+  uint32_t* d_out;
+  HB_TRY(wst(c, "out0", n, &d_out));
+  HB_TRY(timed(c, "hash", [&] { return launch_chacha04_words(c->stream, seed8, n, d_out); }));
+  HB_CHECK(c, hipMemcpyAsync(out, d_out, (size_t)4 * n, hipMemcpyDeviceToHost, c->stream));
+  return sync(c);
 }
 
 int hbtc_hash_g1_g2_batch_gpu(hbtc_ctx* c, uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,

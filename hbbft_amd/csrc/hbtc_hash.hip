@@ -307,6 +307,25 @@ __global__ void __launch_bounds__(64, HBTC_HASH_CAND_WAVES) k_hash_cand(uint32_t
   cand[i] = p;
 }
 
+// The first n words of rand 0.4's ChaChaRng::from_seed(seed) on the device: the keystream code
+// k_hash_cand runs, exposed for the ChaCha20 known-answer tests (tests/test_chacha_kat.py).
+struct Seed8 {
+  uint32_t w[8];
+};
+__global__ void __launch_bounds__(64) k_chacha04_words(Seed8 seed, uint32_t n, uint32_t* __restrict__ out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  ChaCha04 rng(seed.w);
+  for (uint32_t i = 0; i < n; ++i) out[i] = rng.next_u32();
+}
+
+hipError_t launch_chacha04_words(hipStream_t s, const uint32_t* seed8, uint32_t n, uint32_t* out) {
+  if (n == 0) return hipSuccess;
+  Seed8 sd;
+  for (int i = 0; i < 8; ++i) sd.w[i] = seed8[i];
+  hipLaunchKernelGGL(k_chacha04_words, dim3(1), dim3(64), 0, s, sd, n, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_hash_cand(hipStream_t s, uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
                             const uint32_t* offsets, G2A* cand) {
   if (n == 0) return hipSuccess;
@@ -423,6 +442,13 @@ int hbtc_hash_g2(const uint8_t* msg, size_t len, uint8_t* out_c96) {
 int hbtc_hash_g1_g2(const uint8_t* g1_c48, const uint8_t* msg, size_t len, uint8_t* out_c96) {
   if (!g1_c48 || (!msg && len) || !out_c96) return HBTC_ERR_ARG;
   hbtc::hash_g1_g2_c96(g1_c48, msg, len, out_c96);
+  return HBTC_OK;
+}
+
+int hbtc_chacha04_words(const uint32_t* seed8, uint32_t n, uint32_t* out) {
+  if (!seed8 || (!out && n)) return HBTC_ERR_ARG;
+  hbtc::ChaCha04 rng(seed8);
+  for (uint32_t i = 0; i < n; ++i) out[i] = rng.next_u32();
   return HBTC_OK;
 }
 

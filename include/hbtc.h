@@ -159,12 +159,20 @@ int hbtc_hash_g2_batch(uint32_t n, const uint8_t* msgs, const uint32_t* offsets,
                        uint8_t* out_c96);
 int hbtc_hash_g1_g2_batch(uint32_t n, const uint8_t* g1_c48, const uint8_t* msgs,
                           const uint32_t* offsets, uint8_t* out_c96);
-/* The same batches with the full-cofactor multiplication [h2] P (the dominant cost: a 507-bit G2
- * scalar multiplication per hash) on the context's GPU; the host draws the candidates P. */
+/* The same batches with the whole draw on the context's GPU: one lane per message runs the SHA3
+ * seed, the ChaCha stream and G2::rand's candidate loop (k_hash_cand), then [h2] P by the psi
+ * chain (k_g2_clear_cofactor); the host only redraws in the (never observed) case
+ * [h2] P = O. */
 int hbtc_hash_g2_batch_gpu(hbtc_ctx* ctx, uint32_t n, const uint8_t* msgs, const uint32_t* offsets,
                            uint8_t* out_c96);
 int hbtc_hash_g1_g2_batch_gpu(hbtc_ctx* ctx, uint32_t n, const uint8_t* g1_c48,
                               const uint8_t* msgs, const uint32_t* offsets, uint8_t* out_c96);
+/* Diagnostics for the ChaCha20 known-answer tests: the first n words of rand 0.4's
+ * ChaChaRng::from_seed(seed8) (key = the 8 seed words, 128-bit block counter from 0, output words
+ * in block order), computed by the ChaCha code of the host hashes (hbtc_chacha04_words) and of
+ * the GPU candidate kernel (hbtc_chacha04_words_gpu). */
+int hbtc_chacha04_words(const uint32_t* seed8, uint32_t n, uint32_t* out);
+int hbtc_chacha04_words_gpu(hbtc_ctx* ctx, const uint32_t* seed8, uint32_t n, uint32_t* out);
 
 /* ---- pipelined host-buffer epochs ------------------------------------------------------------ */
 /* The batch queue's epoch call without blocking (hbbft keeps the current epoch and up to
@@ -369,26 +377,28 @@ int hbtc_shard_instances(uint32_t n_dev, uint32_t n_inst, const uint32_t* offset
 
 /* ---- verification strategy ----------------------------------------------------------------- */
 /* HBTC_MODE_RLC (default): shares of one instance are checked together by a random linear
- * combination (fresh ChaCha20 scalars per call, 64-bit by default, 128-bit with
+ * combination (fresh ChaCha20 scalars per call, 128-bit by default, 64-bit with
  * hbtc_set_rlc_bits; prime-order points only) in groups of
- * 64 consecutive shares; failing groups are split 64 -> 8 -> 1 share; a group with exactly one
+ * 64 consecutive shares; failing groups are split 64 -> 32 -> 8 -> 1 share (plain-first) or
+ * 64 -> 8 -> 1 (paired schedules); a group with exactly one
  * wrong share is resolved by a position-weighted second combination (the wrong share located
  * without per-share pairings), the rest get the exact pairing check.  The decisions equal the
- * per-share decisions except with probability <= 2^-64 per group check (<= 2^-58 per located
- * group); <= 2^-128 (2^-122) with 128-bit scalars.
+ * per-share decisions except with probability <= 2^-128 per group check (<= 2^-122 per located
+ * group); <= 2^-64 (2^-58) with 64-bit scalars.
  * HBTC_MODE_PER_SHARE: every share gets its own 2-pair pairing check (the reference's count).
  * Applies to hbtc_verify_dec_shares[_dev]. */
 #define HBTC_MODE_PER_SHARE 0
 #define HBTC_MODE_RLC 1
 int hbtc_set_verify_mode(hbtc_ctx* ctx, int mode);
 /* Size of the RLC scalars r_i = a_i + b_i mu (mu = -x^2 mod r, the GLV eigenvalue; DESIGN.md §4,
- * "Soundness"): 64 (default: 32-bit halves, 2^64 distinct scalars, a wrong share survives a group
- * check with probability <= 2^-64, <= 2^-58 per located group) or 128 (64-bit halves, 2^128
- * distinct scalars: <= 2^-128 per group check, <= 2^-122 per located group, matching BLS12-381's
- * ~2^-128 security level; the item passes do twice the doublings and table additions).  Any
- * other value: HBTC_ERR_ARG.  Applies to the RLC calls of hbtc_verify_dec_shares[_dev] and
- * hbtc_verify_sig_shares[_dev]. */
+ * "Soundness"): 128 (default: 64-bit halves, 2^128 distinct scalars: a wrong share survives a
+ * group check with probability <= 2^-128, <= 2^-122 per located group, matching BLS12-381's
+ * ~2^-128 security level, as SURVEY.md §7 step 5 specifies) or 64 (32-bit halves: <= 2^-64 per
+ * group check, <= 2^-58 per located group; the item passes do half the doublings and table
+ * additions).  Any other value: HBTC_ERR_ARG.  Applies to the RLC calls of
+ * hbtc_verify_dec_shares[_dev] and hbtc_verify_sig_shares[_dev]. */
 int hbtc_set_rlc_bits(hbtc_ctx* ctx, uint32_t bits);
+int hbtc_get_rlc_bits(hbtc_ctx* ctx, uint32_t* bits);
 /* Sender tracking (default on, RLC mode): a sender with many shares REJECTed (at least 1/8 of
  * the call's average shares per sender) by one of the last 16 RLC calls on a key set has its
  * shares checked one by one, outside the group sums, so f Byzantine senders who lie in every
@@ -397,16 +407,19 @@ int hbtc_set_rlc_bits(hbtc_ctx* ctx, uint32_t bits);
 int hbtc_set_sender_tracking(hbtc_ctx* ctx, int enable);
 /* Group-check schedule of RLC calls (DecryptionShares).  HBTC_CHECK_AUTO (default) picks by the
  * call's tile count against the device's SIMDs: the plain-first schedule (plain checks of every
- * group, weighted checks only of failing ones: tiles, tiles_w, sub-tiles, sub-tiles_w, leaves =
- * 5 dependent check levels, the least work) for calls that fill the chip, the paired schedules
- * (plain and weighted value of a group in one check launch: tiles -> sub-tiles -> leaves, or
- * tiles -> leaves) for small calls, which are bound by the chain of check latencies (a rank's
- * slice of an epoch under strong scaling).  Decisions are identical under every schedule. */
+ * tile, weighted checks only of failing ones: tiles, tiles_w, halves, halves_w, sub-tiles,
+ * sub-tiles_w, leaves = 7 dependent check levels, the least work) for calls that fill the chip,
+ * the paired schedules (plain and weighted value of a group in one check launch: tiles ->
+ * sub-tiles -> leaves, or tiles -> leaves) for small calls, which are bound by the chain of check
+ * latencies (a rank's slice of an epoch under strong scaling).  Decisions are identical under
+ * every schedule.  hbtc_check_schedule_for reports the schedule a call of n_tiles 64-share tiles
+ * gets (the forced one, if any). */
 #define HBTC_CHECK_AUTO (-1)
 #define HBTC_CHECK_PLAIN_FIRST 0
 #define HBTC_CHECK_PAIR_SUBS 1
 #define HBTC_CHECK_PAIR_LEAVES 2
 int hbtc_set_check_schedule(hbtc_ctx* ctx, int schedule);
+int hbtc_check_schedule_for(hbtc_ctx* ctx, uint32_t n_tiles, int* schedule);
 /* Number of shares that needed the exact single-share check in the last RLC call (syncs). */
 int hbtc_rlc_last_leaves(hbtc_ctx* ctx, uint32_t* leaves);
 

@@ -102,3 +102,36 @@ def test_sig_epochs_in_flight_equal_blocking_calls(ctx):
         for k in range(m):
             if wcst[k] == N.ACCEPT:
                 assert sig[k].tobytes() == wsig[k] and par[k] == wpar[k]
+
+
+def test_dropped_pending_keeps_outputs_alive(ctx):
+    """A Pending dropped without wait(): the Context holds its output arrays, so the unasked
+    completion of that ticket by a later submit (lane reuse) writes into live memory, and the
+    later epochs still give the blocking calls' results (_native.py:383)."""
+    import gc
+    rng = random.Random(73)
+    n = 40
+    t = (n - 1) // 3 + 1
+    counts = [40, 7, 64]
+    pk, H, w, idx, shares, _, _ = _dec_batch(ctx, rng, n, counts, 0.05)
+    ks, _ = ctx.keyset_load(pk)
+    off = np.zeros(len(counts) + 1, np.uint32)
+    off[1:] = np.cumsum(counts)
+    idx = np.asarray(idx, np.uint32)
+    sh = np.asarray(shares, np.uint8)
+    want = ctx.verify_dec_shares(ks, H, w, None, idx, sh, offsets=off)
+    p = ctx.dec_epoch_submit(ks, H, w, off, idx, sh, t)
+    held, tk = p.outs[0], p.ticket
+    del p
+    gc.collect()
+    assert len(ctx._inflight) >= 1
+    later = [ctx.dec_epoch_submit(ks, H, w, off, idx, sh, t) for _ in range(4)]
+    for q in later:
+        st, _, _ = q.wait()
+        assert (st[:len(want)] == want).all()
+    assert ctx.lib.hbtc_wait(ctx.h, tk) == 0  # completed (normally already, by the lane's reuse)
+    assert (held[:len(want)] == want).all()
+    # the held set stays bounded by MAX_HELD_TICKETS
+    for _ in range(N.Context.MAX_HELD_TICKETS + 3):
+        ctx.dec_epoch_submit(ks, H, w, off, idx, sh, 0)
+    assert len(ctx._inflight) <= N.Context.MAX_HELD_TICKETS
