@@ -63,12 +63,23 @@ SEED = 0x6862626674
 # measured v_mad_u64_u32 lane-op throughput on MI355X (tools/microbench/intmul.hip,
 # profiles/r01_intmul_microbench.txt): the VALU integer-multiply roofline of the Fqm kernels
 MAD_U64_PEAK = 29.51e12
-# timing family -> kernel (hbtc_api.hip timed() families, rocprofv3 names)
-KERNEL_NAME = {"dec_verify": "k_dec_verify", "rlc_items": "k_rlc_items",
-               "chk_tiles": "k_chk_plain<0>", "chk_tiles_w": "k_chk_weighted<0>",
-               "chk_halves": "k_chk_halves", "chk_halves_w": "k_chk_weighted<2>",
-               "chk_subs": "k_chk_plain<3>", "chk_subs_w": "k_chk_weighted<3>",
-               "chk_leaves": "k_chk_leaves"}
+# timing family -> kernel (hbtc_api.hip timed() families, rocprofv3 names), per check schedule
+# (hbtc_check_schedule_for: the plain-first form for calls that fill the chip, the paired forms
+# for small calls such as a rank's slice of the epoch)
+KERNEL_NAME_COMMON = {"dec_verify": "k_dec_verify", "rlc_items": "k_rlc_items", "chk_leaves": "k_chk_leaves"}
+KERNEL_NAME_SCHED = {
+    0: {"chk_tiles": "k_chk_plain<0>", "chk_tiles_w": "k_chk_weighted<0>", "chk_halves": "k_chk_halves",
+        "chk_halves_w": "k_chk_weighted<2>", "chk_subs": "k_chk_plain<3>", "chk_subs_w": "k_chk_weighted<3>"},
+    1: {"chk_tiles": "k_chk_pair<0, false>", "chk_subs": "k_chk_pair<1, true>"},
+    2: {"chk_tiles": "k_chk_pair<0, true>"},
+}
+SCHED_NAME = {0: "plain-first", 1: "paired: tiles -> sub-tiles -> leaves", 2: "paired: tiles -> leaves"}
+
+
+def kernel_names(schedule):
+    k = dict(KERNEL_NAME_COMMON)
+    k.update(KERNEL_NAME_SCHED[schedule])
+    return k
 
 
 def log(*a):
@@ -359,8 +370,14 @@ def max_over_ranks(elapsed, dist, device=None):
     return float(tt.item())
 
 
-# committed rocprofv3 summaries of this command (kernel trace + PMC passes), newest first
-PROFILE_DIRS = ("profiles/r03/final4", "profiles/r03/final2", "profiles/r03/headline", "profiles/r03/headline_a", "profiles/r02g/headline")
+def profile_dir(args, world):
+    """The committed rocprofv3 summaries of this bench command's workload (kernel trace + PMC
+    passes, tools/r04/profile.sh): profiles/r04/bench_<cts>ct_<bits>b[_<world>r], or None."""
+    tag = "bench_%dct_%db" % (args.cts, args.rlc_bits) + ("_%dr" % world if world > 1 else "")
+    if args.corrupt_mode != "uniform" or args.mode != "rlc" or args.n != 1000:
+        return None
+    d = os.path.join("profiles", "r04", tag)
+    return d if os.path.exists(os.path.join(ROOT, d, "kt_kernel_stats.csv")) else None
 
 
 def rocprof_avg_ms(csv_path, kernel):
@@ -428,6 +445,26 @@ def timed(ctx, ep, steps, warmup, dist=None, gather=None, sync_all=None):
     return dt
 
 
+def rlc_width_line(ctx, ep, args, bits):
+    """The headline epoch with the other RLC scalar width (hbtc_set_rlc_bits): 64-bit scalars
+    give <= 2^-64 per group check, 128-bit <= 2^-128 (DESIGN.md §4 "Soundness").  Same epoch,
+    same steps, decisions and combines checked against the construction."""
+    ctx.set_rlc_bits(bits)
+    try:
+        elapsed = timed(ctx, ep, args.steps, args.warmup)
+        per = {f: round(ctx.timing_read(f)[0] / args.steps, 3) for f in FAMS if ctx.timing_read(f)[1]}
+        mism, comb_ok, _ = ep.check(ctx)
+    finally:
+        ctx.set_rlc_bits(args.rlc_bits)
+    if mism or not comb_ok:
+        raise SystemExit("rlc%d: results differ from the construction (%d mismatches, combine %s)"
+                         % (bits, mism, comb_ok))
+    return {"value": round(ep.total * args.steps / elapsed, 1), "unit": "shares/s",
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "steps": args.steps, "rlc_bits": bits,
+            "soundness_per_group_check": "2^-%d" % bits, "results_ok": True,
+            "kernel_event_spans_ms_per_step": per}
+
+
 def host_buffer_line(ctx, ep, steps, warmup=2):
     """The epoch through the pipelined host-buffer entry point (what an FFI caller holding wire
     bytes does, hbtc_dec_epoch_submit / hbtc_wait): per epoch, the compressed shares, indices,
@@ -486,9 +523,9 @@ def main():
     ap.add_argument("--mode", choices=["rlc", "per_share"], default="rlc",
                     help="rlc: batched random-linear-combination checks with exact fallback "
                          "(default); per_share: one pairing check per share")
-    ap.add_argument("--rlc-bits", type=int, choices=[64, 128], default=64,
-                    help="RLC scalar size (hbtc_set_rlc_bits): soundness 2^-64 (default) or 2^-128 "
-                         "per group check")
+    ap.add_argument("--rlc-bits", type=int, choices=[64, 128], default=None,
+                    help="RLC scalar size (hbtc_set_rlc_bits): soundness 2^-128 (the library default, "
+                         "SURVEY.md §7 step 5) or 2^-64 per group check")
     ap.add_argument("--corrupt", type=float, default=0.01, help="fraction of wrong shares")
     ap.add_argument("--corrupt-mode", choices=["uniform", "senders"], default="uniform")
     ap.add_argument("--node", action="store_true",
@@ -527,6 +564,8 @@ def main():
     ctx = N.Context(local)
     t0 = time.time()
     ctx.set_verify_mode(N.MODE_RLC if args.mode == "rlc" else N.MODE_PER_SHARE)
+    if args.rlc_bits is None:
+        args.rlc_bits = ctx.rlc_bits()  # the library default
     ctx.set_rlc_bits(args.rlc_bits)
     gather, slices = None, None
     if strong:
@@ -554,12 +593,14 @@ def main():
     # the same epoch once more with nothing else in flight (after the timed region): the dominant
     # kernel's duration on an otherwise idle chip, beside its pipelined duration above (where
     # the other lanes' check levels and combines share the CUs with it)
-    iso = {}
+    iso, iso_wall = {}, None
     if gather is None:
         ctx.sync()
         ctx.timing_reset()
+        a = time.perf_counter()
         ep.step(ctx)
         ctx.sync()
+        iso_wall = time.perf_counter() - a
         iso = {f: ctx.timing_read(f) for f in FAMS}
     if strong and "gather" in DIAG_SKIP:
         mism, comb_ok, n_acc = ep.check(ctx)  # diagnostics without the collectives: local check
@@ -587,13 +628,17 @@ def main():
     combines = job_cts * args.steps / elapsed
     consts = json.load(open(os.path.join(ROOT, "bench", "roofline_constants.json")))
     n_tiles = ep.m * ((ep.n + 63) // 64)
+    sched = ctx.check_schedule_for(n_tiles)
+    kname = kernel_names(sched)
+    paired = sched != N.CHECK_PLAIN_FIRST
     # algorithmic Fqm per launch of each kernel family (tools/fqm_count.cpp)
     fqm_per_launch = {
         "dec_verify": consts["dec_share"]["total"] * ep.total,
         "rlc_items": consts["rlc_item" if args.rlc_bits == 64 else "rlc_item_128"] * ep.total,
-        # the plain 2-pair check of every tile (serial Fqm count of one check; the cooperative
-        # kernel issues more lane-level work than this)
-        "chk_tiles": consts["rlc_group_check"] * n_tiles,
+        # the tile level: the plain 2-pair check of every tile, plus (paired schedules) its
+        # weighted check in the same launch (serial Fqm count of one check; the location search
+        # and the cooperative form's extra lane work are not counted)
+        "chk_tiles": consts["rlc_group_check"] * n_tiles * (2 if paired else 1),
         "chk_leaves": consts["dec_share"]["total"] * leaves,
         "combine": consts.get("g1_msm_combine", 0) * ep.m,
     }
@@ -605,21 +650,20 @@ def main():
     dom = max((f for f in main_stream if breakdown[f][1]), key=lambda f: breakdown[f][0])
     dom_avg_s = breakdown[dom][0] / breakdown[dom][1] / 1e3
     achieved = fqm_per_launch[dom] / dom_avg_s * consts["mad_u64_u32_per_fqm"] / 1e12
-    # HBM traffic and VALU instruction count of the same kernel from the committed rocprofv3
-    # PMC passes of this command (tools/gpu_configs_pmc.sh -> tools/pmc_summary.py): separate
-    # FETCH_SIZE / WRITE_SIZE / SQ passes, FETCH_SIZE doubled per the gfx950 note.
-    traffic, pmc, prof_dir = None, {}, None
-    for cand in PROFILE_DIRS:
-        if os.path.exists(os.path.join(ROOT, cand, "pmc_summary.json")):
-            prof_dir = cand
-            break
-    rocprof_ms = None
+    # rocprofv3 kernel trace + PMC passes of THIS workload (tools/r04/profile.sh -> tools/
+    # pmc_summary.py), committed under profiles/: separate FETCH_SIZE / WRITE_SIZE / SQ passes,
+    # FETCH_SIZE doubled per the gfx950 note.  A workload without a committed profile reports
+    # null rather than another workload's figures.
+    traffic, pmc, rocprof_ms = None, {}, None
+    prof_dir = profile_dir(args, world)
     if prof_dir:
-        summ = json.load(open(os.path.join(ROOT, prof_dir, "pmc_summary.json")))
-        pmc = summ.get("hbtc::" + KERNEL_NAME[dom]) or summ.get("void hbtc::" + KERNEL_NAME[dom], {})
-        if "hbm_read_bytes" in pmc and "hbm_write_bytes" in pmc:
-            traffic = pmc["hbm_read_bytes"] + pmc["hbm_write_bytes"]
-        rocprof_ms = rocprof_avg_ms(os.path.join(ROOT, prof_dir, "kt_kernel_stats.csv"), KERNEL_NAME[dom])
+        summ_path = os.path.join(ROOT, prof_dir, "pmc_summary.json")
+        if os.path.exists(summ_path):
+            summ = json.load(open(summ_path))
+            pmc = summ.get("hbtc::" + kname[dom]) or summ.get("void hbtc::" + kname[dom], {})
+            if "hbm_read_bytes" in pmc and "hbm_write_bytes" in pmc:
+                traffic = pmc["hbm_read_bytes"] + pmc["hbm_write_bytes"]
+        rocprof_ms = rocprof_avg_ms(os.path.join(ROOT, prof_dir, "kt_kernel_stats.csv"), kname[dom])
     if strong:
         coll = ("RCCL (nccl backend) all-gather over xGMI" if args.backend == "nccl"
                 else "gloo all-gather of host copies (rehearsal, not the product merge)")
@@ -652,15 +696,22 @@ def main():
         "accepted_per_step": n_acc,
         "mode": args.mode,
         "rlc_bits": args.rlc_bits,
+        "check_schedule": SCHED_NAME[sched],
         "exact_single_share_checks_per_step_rank0": leaves,
         "kernel_event_spans_ms_per_step_rank0": per_step,
+        "isolated_epoch": ({"ms": round(iso_wall * 1e3, 3),
+                            "spans_ms": {f: round(v[0], 3) for f, v in iso.items() if v[1]},
+                            "note": "one more epoch after the timed region with nothing else in flight: its "
+                                    "wall time is the lane's chain latency (items -> check levels -> "
+                                    "combine); ms_per_step below it means the four lanes overlap"}
+                           if iso_wall else None),
         "kernel_event_spans_note": ("HIP-event spans per kernel family on the library's streams, summed "
                                     "per step: the four verification lanes and the preparation stream "
                                     "overlap, so the spans add up to more than ms_per_step; kernel "
                                     "durations are roofline.rocprof_avg_ms_per_launch (rocprofv3)"),
         "roofline": {
             "bound": "valu-int (v_mad_u64_u32)",
-            "kernel": KERNEL_NAME[dom],
+            "kernel": kname[dom],
             "achieved": round(achieved, 3),
             "peak": MAD_U64_PEAK / 1e12,
             "unit": "T mad_u64_u32/s",
@@ -687,6 +738,10 @@ def main():
         },
     }
     if world == 1 and not args.no_extra:
+        # the other RLC width on the same epoch (SURVEY.md §7 step 5 specifies 128-bit scalars;
+        # the headline runs the library default)
+        alt = 64 if args.rlc_bits == 128 else 128
+        out["rlc%d" % alt] = rlc_width_line(ctx, ep, args, alt)
         out["host_buffers"] = host_buffer_line(ctx, ep, args.steps, min(args.warmup, 2))
         if args.corrupt_mode == "uniform":
             out["adversarial"] = adversarial_line(ctx, args, ep)

@@ -6,6 +6,12 @@ on).  This script measures the remaining hot-path configurations through the sam
 GPU, synthetic seeded inputs generated on the device (setup outside the timed region), results
 checked against the construction after timing:
 
+  c1  Threshold Coin N=10, f=3 (examples/simulation.rs:43-44, BASELINE config 1), single-call
+      latency: one coin's 10 SignatureShares verified, the first t=4 valid ones combined, the
+      combined signature checked against the master key and its parity taken (src/coin.rs:
+      149-207), from host buffers, each call blocking (the BA epoch waits on its coin,
+      binary_agreement.rs:309-323), hash_g2(nonce) on the host inside the call.  Reported beside
+      the C restatement of the same call on one core and on every usable core.
   c2  Binary Agreement coins N=100: 100 coin instances x 100 SignatureShares verified
       (PublicKeyShare::verify, src/coin.rs:151) + 100 G2 combines of the first t=34 verified
       shares (combine_signatures + parity, src/coin.rs:185-191,173).  Inputs resident in HBM.
@@ -33,7 +39,7 @@ checked against the construction after timing:
       (shard_len = ceil((value + 4) / (N - 2f))).  Inputs resident in HBM; the outputs are
       compared with the proposals after timing.
 
-Usage: python bench_configs.py [--configs c2,c4,c5,bc] [--steps K] [--warmup W]
+Usage: python bench_configs.py [--configs c1,c2,c4,c5,bc] [--steps K] [--warmup W]
 """
 import argparse
 import ctypes
@@ -63,7 +69,7 @@ G2_GEN = bytes.fromhex("93e02b6052719f607dacd3a088274f65596bd0d09920b61ab5da61bb
                        "024aa2b2f08f0a91260805272dc51051c6e47ad4fa403b02b4510b647ae3d1770bac0326a805bbefd48056c8c121bdb8")
 SEED = 0x6862626674
 N_OUT = 6  # output sets rotated per step (bench.py's N_OUT)
-STEPS_DEFAULT = {"c2": 20, "c4": 6, "c5": 1, "bc": 20}
+STEPS_DEFAULT = {"c1": 50, "c2": 20, "c4": 6, "c5": 1, "bc": 20}
 
 
 def log(*a):
@@ -307,7 +313,7 @@ class NodeCoinRunner:
 
 
 def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode="uniform", node=None,
-                keep_arrays=False, cpu_budget=0.0):
+                keep_arrays=False, cpu_budget=0.0, latency_steps=0):
     """c2 / c4: n_inst coin instances x n SignatureShares + n_inst combines (first t verified).
     node: a hbtc Node (one process, several device slots) instead of the single context."""
     t0 = time.time()
@@ -330,10 +336,26 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode=
     per = breakdown(tctx, steps, COIN_FAMS)
     consts = json.load(open(os.path.join(ROOT, "bench", "roofline_constants.json")))
     items0 = (run.slots[0]["hi"] - run.slots[0]["lo"]) if node is not None else total
-    roof = roofline_line(tctx, "sig_items", "k_sig_items", consts["sig_rlc_item"] * items0,
-                         "sig_rlc_item Fqm (G2 decode + subgroup test, [a]s + [b](-psi^2 s), r pk from "
-                         "the fixed-base table, tile-tree share) x %d SignatureShares per launch" % items0)
+    bits = tctx.rlc_bits()
+    key = "sig_rlc_item" if bits == 64 or "sig_rlc_item_128" not in consts else "sig_rlc_item_128"
+    roof = roofline_line(tctx, "sig_items", "k_sig_items", consts[key] * items0,
+                         "%s Fqm (G2 decode + subgroup test, [a]s + [b](-psi^2 s), r pk from "
+                         "the fixed-base table, tile-tree share) x %d SignatureShares per launch" % (key, items0))
     stv, out, par, cst = run.results()
+    lat = None
+    if node is None and latency_steps:
+        # single-call latency: one call at a time (verification + combine, then a sync): what a BA
+        # epoch waiting on its coins feels (binary_agreement.rs:309-323, coin.rs:149-181)
+        lats = []
+        for _ in range(latency_steps):
+            a = time.perf_counter()
+            run.step()
+            run.sync()
+            lats.append(time.perf_counter() - a)
+        lat = {"p10": round(_pct(lats, 0.1) * 1e3, 3), "median": round(_pct(lats, 0.5) * 1e3, 3),
+               "p90": round(_pct(lats, 0.9) * 1e3, 3), "calls": latency_steps,
+               "unit": "ms per call (verification + combines, blocking; inputs resident in HBM)"}
+        stv, out, par, cst = run.results()
     want, _ = ctx.g2_mul(G2_GEN, fr_bytes([inp["master"] * hh % R for hh in inp["hs"]]))
     mism = int((stv != inp["expected"]).sum())
     comb_ok = bool((cst == 0).all() and bytes(out) == bytes(want))
@@ -364,6 +386,8 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode=
         "kernel_event_spans_ms_per_step": per, "mismatches": mism, "combine_ok": comb_ok,
     }
     res["roofline"] = roof
+    if lat:
+        res["single_call_latency"] = lat
     if node is not None:
         res["kernel_event_spans_note"] = "event spans of device slot 0 only"
     if cpu_budget and node is None:
@@ -373,10 +397,104 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode=
             res["cpu_baseline"] = run_sig_share_baseline(inp["sigs"][:96 * n], inp["pk"], nonce, cpu_budget)
             res["cpu_baseline"]["sample"] += (" (a synthetic %d-byte nonce: hash_g2 of it is not the bench's H, "
                                               "so the pairings reject; the work per share is the same)" % len(nonce))
+            if lat:
+                from oracle.cbaseline import run_sig_share_baseline as rsb
+                one = rsb(inp["sigs"][:96 * n], inp["pk"], nonce, cpu_budget / 2, cores=1)
+                res["cpu_baseline"]["single_call_latency_ms"] = {
+                    "all_cores": round(1e3 * total / res["cpu_baseline"]["value"], 1),
+                    "one_core": round(1e3 * total / one["value"], 1),
+                    "note": "projected: the call's %d share checks at the measured per-share rates (the "
+                            "%d combines excluded: a lower bound on the reference's call)" % (total, n_inst)}
         except Exception as e:  # the baseline is reported, never the product path
             res["cpu_baseline"] = {"error": repr(e)}
     if keep_arrays:
         res["_arrays"] = (stv, out, par, cst)
+    return res
+
+
+def _pct(xs, q):
+    s = sorted(xs)
+    return s[min(len(s) - 1, int(q * len(s)))]
+
+
+COIN_NONCE = (b"Nonce for Honey Badger [173, 84, 2, 11, 0, 0, 9, 254, 1, 18, 200, 57, 43, 9, "
+              b"4, 77, 190, 91, 12, 0, 1, 2, 3]@3:2:7")
+
+
+def bench_c1(ctx, steps, warmup, cpu_budget=0.0):
+    """c1: single-call latency of one Threshold Coin at N = 10 (see the docstring)."""
+    n, t = 10, 4
+    rng = random.Random(SEED + 10)
+    master, sks = key_shares(rng, n)
+    pk, st = ctx.g1_mul(G1_GEN, fr_bytes(sks))
+    mpk, _ = ctx.g1_mul(G1_GEN, fr_bytes([master]))
+    H = N.hash_g2(COIN_NONCE)
+    scal = list(sks)
+    scal[2] = (scal[2] + 1) % R  # one faulty node's wrong share
+    sigs, st2 = ctx.g2_mul(H, fr_bytes(scal))
+    assert not st.any() and not st2.any()
+    expected = np.zeros(n, np.int32)
+    expected[2] = N.REJECT
+    want_sig, _ = ctx.g2_mul(H, fr_bytes([master]))
+    ks, bad = ctx.keyset_load(pk)
+    assert bad == 0
+    idx = np.arange(n, dtype=np.uint32)
+    sig_list = [bytes(sigs[96 * i:96 * i + 96]) for i in range(n)]
+    phases = {"hash_g2": [], "verify_shares": [], "combine": [], "verify_master": []}
+    total = []
+
+    def call():
+        a = time.perf_counter()
+        Hc = N.hash_g2(COIN_NONCE)  # host, once per coin instance (north star)
+        b = time.perf_counter()
+        stv = ctx.verify_sig_shares(ks, [Hc], [n], idx, sig_list)
+        c = time.perf_counter()
+        sel = [i for i in range(n) if stv[i] == N.ACCEPT][:t]
+        out, par, cst = ctx.combine_sigs([t], sel, [sig_list[i] for i in sel], t)
+        d = time.perf_counter()
+        ok = ctx.verify_sigs([bytes(mpk)], [Hc], [out[0]])
+        e = time.perf_counter()
+        return (b - a, c - b, d - c, e - d, e - a), stv, out[0], int(par[0]), int(cst[0]), int(ok[0])
+
+    for _ in range(warmup):
+        call()
+    for _ in range(steps):
+        ph, stv, sig, par, cst, ok = call()
+        for k, v in zip(phases, ph[:4]):
+            phases[k].append(v)
+        total.append(ph[4])
+    if (stv != expected).any() or cst != 0 or ok != N.ACCEPT or sig != bytes(want_sig):
+        raise SystemExit("c1: results differ from the construction")
+    ctx.keyset_free(ks)
+    med = _pct(total, 0.5)
+    res = {
+        "metric": "Threshold Coin single-call latency at N=10 (verify 10 SignatureShares + combine 4 + "
+                  "master verify + parity)",
+        "value": round(med * 1e3, 3), "unit": "ms per coin call (median)", "n_gpus": 1, "steps": steps,
+        "warmup": warmup, "higher_is_better": False, "dtype": "u32 (381-bit Montgomery limbs)",
+        "data": "synthetic (seeded key set; shares sk_i * hash_g2(nonce) made on the device; 1 wrong share)",
+        "config": {"workload": "c1: Threshold Coin N=10 f=3 (examples/simulation.rs:43-44): one coin call, "
+                               "host buffers, blocking", "N": n, "f": 3, "t": t},
+        "latency_ms": {"p10": round(_pct(total, 0.1) * 1e3, 3), "median": round(med * 1e3, 3),
+                       "p90": round(_pct(total, 0.9) * 1e3, 3)},
+        "phase_median_ms": {k: round(_pct(v, 0.5) * 1e3, 3) for k, v in phases.items()},
+        "calls_per_s": round(1.0 / med, 1),
+        "mode": "rlc" if ctx_mode[0] == N.MODE_RLC else "per_share", "results_ok": True,
+    }
+    if cpu_budget:
+        try:
+            from oracle.cbaseline import run_coin_call_baseline
+            cpu = run_coin_call_baseline(bytes(sigs), bytes(pk), bytes(mpk), COIN_NONCE, t, cpu_budget)
+            ok_c, sig_c, par_c = cpu.pop("results")
+            cpu["results_equal_gpu"] = bool([not x for x in ok_c] == list(expected == N.REJECT)
+                                            and sig_c == bytes(want_sig) and par_c == par)
+            res["cpu_baseline"] = cpu
+            res["gpu_vs_cpu_latency"] = {
+                "gpu_ms": res["value"], "cpu_1core_ms": cpu["value"], "cpu_all_cores_ms": cpu["value_all_cores_ms"],
+                "note": "a single N = 10 coin is a chain of a few dependent kernel launches (decode, sums, "
+                        "one check level, combine, master check) on an idle GPU; the CPU does 11 pairing checks"}
+        except Exception as e:  # reported, never the product path
+            res["cpu_baseline"] = {"error": repr(e)}
     return res
 
 
@@ -647,7 +765,7 @@ ctx_mode = [None]
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c2,c4,c5")
+    ap.add_argument("--configs", default="c1,c2,c4,c5")
     ap.add_argument("--steps", type=int, default=None,
                     help="timed steps (default per config: c2 20, c4 6, c5 1, bc 20 -- enough "
                          "for the pipelined calls to reach steady state)")
@@ -679,9 +797,12 @@ def main():
         for c in args.configs.split(","):
             steps = args.steps if args.steps is not None else STEPS_DEFAULT.get(c, 2)
             warmup = args.warmup if args.warmup is not None else (1 if c == "c5" else 2)
-            if c == "c2":
+            if c == "c1":
+                out = bench_c1(ctx, steps, warmup, cpu_budget=0.0 if args.no_cpu else 10.0)
+            elif c == "c2":
                 out = bench_coins(ctx, "c2", 100, 100, steps, warmup, args.corrupt,
-                                  args.corrupt_mode, node=node, cpu_budget=0.0 if args.no_cpu else 10.0)
+                                  args.corrupt_mode, node=node, cpu_budget=0.0 if args.no_cpu else 10.0,
+                                  latency_steps=20)
             elif c == "c4":
                 out = bench_coins(ctx, "c4", 10000, args.inst, steps, warmup, args.corrupt,
                                   args.corrupt_mode, node=node, cpu_budget=0.0 if args.no_cpu else 10.0)

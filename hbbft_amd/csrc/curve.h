@@ -419,6 +419,88 @@ HD void glv_mul_uniform(Jac<F>& r, const Aff<F>& d, const F& mx, uint64_t a, uin
   r = acc;
 }
 
+// ---------------------------------------------------------------- x-adic RLC scalars
+// The RLC scalar of an item (DESIGN.md §4 "Soundness") is r = d0 + d1 x + d2 mu + d3 mu x (mod r)
+// with four digits d_j < 2^nbits (nbits = 16 or 32: 2^64 or 2^128 distinct scalars), x the BLS
+// parameter and mu = -x^2 the eigenvalue of the endomorphism m(X, Y) = (c X, Y) (G1: phi, c =
+// beta; G2: -psi^2, c = zeta).  For P in the prime-order group and XP = [x] P (G1: the negated
+// [|x|] P the subgroup test computes anyway; G2: psi(P), free):
+//     [r] P = [d0] P + [d1] XP + [d2] m(P) + [d3] m(XP)
+// one joint double-and-add over nbits bits with TWO mixed additions per bit, T[d0_i, d1_i] and
+// m(T[d2_i, d3_i]) from the affine table T = {P, XP, P + XP}: nbits doublings instead of the
+// 2 nbits of the two-digit form [a] P + [b] m(P), for one Fq product (G1) / two (G2) per bit to
+// apply m to the selected entry.  Every lane runs the same instructions (selects only).
+HD void fmul_by_fq(Fq& r, const Fq& a, const Fq& c) { fq_mul(r, a, c); }
+HD void fmul_by_fq(Fq2& r, const Fq2& a, const Fq& c) {
+  fq_mul(r.c0, a.c0, c);
+  fq_mul(r.c1, a.c1, c);
+}
+
+// acc += (tx, ty) when `take` (acc infinity: the table point itself; no exceptional cases
+// otherwise, as in glv_mul_uniform below)
+template <class F>
+HD void uniform_add(Jac<F>& acc, const F& tx, const F& ty, bool take) {
+  const bool first = jac_is_inf(acc);
+  Jac<F> n;
+  jac_madd_generic(n, acc, tx, ty);
+  F one;
+  fone(one);
+  fsel(n.x, first, tx, n.x);
+  fsel(n.y, first, ty, n.y);
+  fsel(n.z, first, one, n.z);
+  fsel(acc.x, take, n.x, acc.x);
+  fsel(acc.y, take, n.y, acc.y);
+  fsel(acc.z, take, n.z, acc.z);
+}
+
+// The table entries XP and P + XP (affine) from XP in Jacobian coordinates: one inversion for
+// both (P + XP != O and XP != P: x != +-1 mod r).
+template <class F>
+HD void xadic_table(Aff<F>& xp, Aff<F>& pxp, const Aff<F>& p, const Jac<F>& xpj) {
+  Jac<F> sj;
+  jac_madd_generic(sj, xpj, p.x, p.y);
+  F z12, inv, zi1, zi2;
+  fmul(z12, xpj.z, sj.z);
+  finv_fast(inv, z12);
+  fmul(zi1, inv, sj.z);   // 1 / xpj.z
+  fmul(zi2, inv, xpj.z);  // 1 / sj.z
+  F t, t2;
+  fsqr(t, zi1);
+  fmul(xp.x, xpj.x, t);
+  fmul(t2, t, zi1);
+  fmul(xp.y, xpj.y, t2);
+  xp.inf = 0;
+  fsqr(t, zi2);
+  fmul(pxp.x, sj.x, t);
+  fmul(t2, t, zi2);
+  fmul(pxp.y, sj.y, t2);
+  pxp.inf = 0;
+}
+
+template <class F>
+HD void xadic_mul_uniform(Jac<F>& r, const Aff<F>& p, const Aff<F>& xp, const Aff<F>& pxp,
+                          const Fq& c, uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3,
+                          int nbits) {
+  Jac<F> acc;
+  jac_set_inf(acc);
+#pragma unroll 1
+  for (int bit = nbits - 1; bit >= 0; --bit) {
+    jac_dbl(acc, acc);
+    const bool b0 = ((d0 >> bit) & 1u) != 0, b1 = ((d1 >> bit) & 1u) != 0;
+    const bool b2 = ((d2 >> bit) & 1u) != 0, b3 = ((d3 >> bit) & 1u) != 0;
+    F tx, ty;
+    fsel(tx, b1, b0 ? pxp.x : xp.x, p.x);
+    fsel(ty, b1, b0 ? pxp.y : xp.y, p.y);
+    uniform_add(acc, tx, ty, b0 || b1);
+    F ux, uy;
+    fsel(ux, b3, b2 ? pxp.x : xp.x, p.x);
+    fsel(uy, b3, b2 ? pxp.y : xp.y, p.y);
+    fmul_by_fq(ux, ux, c);  // m(T[b2, b3])
+    uniform_add(acc, ux, uy, b2 || b3);
+  }
+  r = acc;
+}
+
 // GLV endomorphism of G1: phi(x, y) = (beta x, y) = [-x^2] (x, y) on the r-order subgroup
 HD void g1_phi(G1A& r, const G1A& p) {
   Fq beta;
@@ -500,6 +582,24 @@ HD bool jac_eq(const Jac<F>& p, const Jac<F>& q) {
 }
 
 // ---------------------------------------------------------------- subgroup tests
+// t1 = [|x|] P, the first half of the test (the RLC item passes reuse it: [x] P = -t1)
+HDN bool g1_in_subgroup_t1(const G1A& p, G1J& t) {
+  if (p.inf) {
+    jac_set_inf(t);
+    return true;
+  }
+  G1J t2;
+  jac_mul_u64(t, p, BLS_X_ABS);
+  jac_mul_u64_jac(t2, t, BLS_X_ABS);  // [x^2] P
+  if (jac_is_inf(t2)) return false;   // phi(P) != O for P != O
+  Fq bx, ny;
+  Fq beta;
+  fq_set(beta, G1_BETA);
+  fq_mul(bx, p.x, beta);
+  fq_neg(ny, p.y);  // phi(P) == -[x^2]P  <=>  (beta x, -y) == [x^2] P
+  return jac_eq_aff(t2, bx, ny);
+}
+
 HDN bool g1_in_subgroup(const G1A& p) {
   if (p.inf) return true;
   G1J t, t2;
@@ -684,6 +784,14 @@ HDN bool g1_decompress(G1A& out, const uint32_t* w_in, bool check_subgroup = tru
   fq_canon(out.y, y);
   fq_canon(out.x, out.x);
   return !check_subgroup || g1_in_subgroup(out);
+}
+
+// G1Compressed::into_affine returning also t1 = [|x|] P from the subgroup test (the x-adic RLC
+// table: [x] P = -t1).  t1 is infinity for the point at infinity.
+HDN bool g1_decompress_t1(G1A& out, G1J& t1, const uint32_t* w_in) {
+  jac_set_inf(t1);
+  if (!g1_decompress(out, w_in, false)) return false;
+  return g1_in_subgroup_t1(out, t1);
 }
 
 HDN bool g2_decompress(G2A& out, const uint32_t* w_in, bool check_subgroup = true) {

@@ -55,17 +55,25 @@ HD void fetch2(Fq2& r, const Fq2& x, uint32_t src) {
   fetch(r.c1, x.c1, src);
 }
 
-// position of the calling lane inside its group
+// Position of the calling lane inside its group.  rep = 1: 6 lanes per group, lane k holds
+// coefficient k.  rep = 3 (the latency form): 18 lanes per group, coefficient k replicated on
+// the three lanes 3k + j (sub-lane j), and every Fq2 product split over them (mul2 below: one
+// Fq product per lane instead of three): a check's chain of dependent instructions shrinks by
+// ~1.7x for ~1.7x the lane-instructions, the trade for check levels too small to fill the chip.
 struct Pos {
   uint32_t k;     // coefficient index 0..5
-  uint32_t base;  // lane holding coefficient 0
+  uint32_t base;  // lane holding coefficient 0 (sub-lane 0)
+  uint32_t sub;   // 0..rep-1
+  uint32_t rep;   // lanes per coefficient: 1 or 3
 };
-HD Pos pos() {
+HD Pos pos(uint32_t rep = 1) {
   const uint32_t l = lane_id();
-  const uint32_t g = l / 6u;
-  return Pos{l - 6u * g, 6u * g};
+  const uint32_t gs = 6u * rep;
+  const uint32_t g = l / gs, w = l - gs * g;
+  return Pos{w / rep, gs * g, w % rep, rep};
 }
-HD uint32_t src(const Pos& ps, uint32_t k) { return ps.base + k; }
+// the lane holding coefficient k of the caller's group, on the caller's sub-lane
+HD uint32_t src(const Pos& ps, uint32_t k) { return ps.base + ps.rep * k + ps.sub; }
 
 HD void fq2_sel(Fq2& r, bool c, const Fq2& a, const Fq2& b) {
   fq_sel(r.c0, c, a.c0, b.c0);
@@ -84,7 +92,7 @@ HD void fq2_xi_if(Fq2& r, bool t, const Fq2& a) {
 // With the product as a shared subroutine (HBTC_FQMUL_SR) a site is a few dozen instructions:
 // straight-line Karatsuba, no operand selects.
 #if defined(__HIP_DEVICE_COMPILE__) && defined(HBTC_FQMUL_SR)
-HD void mul2(Fq2& r, const Fq2& a, const Fq2& b) {
+HD void mul2_one(Fq2& r, const Fq2& a, const Fq2& b) {
   Fq sa, sb, t0, t1, t2;
   fq_add(sa, a.c0, a.c1);
   fq_add(sb, b.c0, b.c1);
@@ -95,12 +103,12 @@ HD void mul2(Fq2& r, const Fq2& a, const Fq2& b) {
   fq_sub(t2, t2, t0);
   fq_sub(r.c1, t2, t1);
 }
-HD void mul2_fq(Fq2& r, const Fq2& a, const Fq& y) {
+HD void mul2_fq_one(Fq2& r, const Fq2& a, const Fq& y) {
   fq_mul(r.c0, a.c0, y);
   fq_mul(r.c1, a.c1, y);
 }
 #else
-HD void mul2(Fq2& r, const Fq2& a, const Fq2& b) {
+HD void mul2_one(Fq2& r, const Fq2& a, const Fq2& b) {
   Fq sa, sb;
   fq_add(sa, a.c0, a.c1);
   fq_add(sb, b.c0, b.c1);
@@ -120,7 +128,7 @@ HD void mul2(Fq2& r, const Fq2& a, const Fq2& b) {
   fq_sub(r.c1, t2, t1);
 }
 // a * (y + 0u): two Fq products through the same single site
-HD void mul2_fq(Fq2& r, const Fq2& a, const Fq& y) {
+HD void mul2_fq_one(Fq2& r, const Fq2& a, const Fq& y) {
   Fq t0;
 #pragma unroll 1
   for (uint32_t t = 0; t < 2; ++t) {
@@ -132,6 +140,46 @@ HD void mul2_fq(Fq2& r, const Fq2& a, const Fq& y) {
   r.c0 = t0;
 }
 #endif
+
+// Fq2 products of the group's lanes.  rep = 1: the whole product on each lane.  rep = 3: the
+// three sub-lanes of a coefficient each form one Karatsuba term (a0 b0, a1 b1, (a0 + a1)(b0 +
+// b1)) and exchange them, so every sub-lane ends with the same product (the operands are
+// replicated, hence so is the result).  ps.rep is uniform over the wave: a uniform branch.
+HD void mul2(Fq2& r, const Fq2& a, const Fq2& b, const Pos& ps) {
+  if (ps.rep == 1) {
+    mul2_one(r, a, b);
+    return;
+  }
+  Fq x, y, t, t0, t1, t2;
+  {
+    Fq sa, sb;
+    fq_add(sa, a.c0, a.c1);
+    fq_add(sb, b.c0, b.c1);
+    fq_sel(x, ps.sub == 0, a.c0, ps.sub == 1 ? a.c1 : sa);
+    fq_sel(y, ps.sub == 0, b.c0, ps.sub == 1 ? b.c1 : sb);
+  }
+  fq_mul(t, x, y);
+  const uint32_t l0 = ps.base + ps.rep * ps.k;  // sub-lane 0 of this coefficient
+  fetch(t0, t, l0);
+  fetch(t1, t, l0 + 1);
+  fetch(t2, t, l0 + 2);
+  fq_sub(r.c0, t0, t1);
+  fq_sub(t2, t2, t0);
+  fq_sub(r.c1, t2, t1);
+}
+// a * (y + 0u): sub-lanes 0 and 1 form the two products (sub-lane 2 repeats sub-lane 1's)
+HD void mul2_fq(Fq2& r, const Fq2& a, const Fq& y, const Pos& ps) {
+  if (ps.rep == 1) {
+    mul2_fq_one(r, a, y);
+    return;
+  }
+  Fq x, t;
+  fq_sel(x, ps.sub == 0, a.c0, a.c1);
+  fq_mul(t, x, y);
+  const uint32_t l0 = ps.base + ps.rep * ps.k;
+  fetch(r.c0, t, l0);
+  fetch(r.c1, t, l0 + 1);
+}
 
 // The short operand-choice loops of the line product, the easy part and the Miller step stay
 // rolled where the product is inlined (code size: instruction cache); with the shared-subroutine
@@ -168,7 +216,7 @@ GTN void mul(Fq2& f, const Fq2& a, const Fq2& b, const Pos& ps) {
     Fq2 ai, bj, z;
     fetch2(ai, a, src(ps, i));
     fetch2(bj, b, src(ps, j));
-    mul2(z, ai, bj);
+    mul2(z, ai, bj, ps);
     fq2_xi_if(z, wrap, z);
     fq2_add(acc, acc, z);
   }
@@ -214,7 +262,7 @@ HD void sqr(Fq2& f, const Fq2& a, const Pos& ps) {
     Fq2 ai, aj, z;
     fetch2(ai, a, src(ps, e & 7u));
     fetch2(aj, a, src(ps, (e >> 3) & 7u));
-    mul2(z, ai, aj);
+    mul2(z, ai, aj, ps);
     fq2_xi_if(z, ((e >> 6) & 1u) && !none, z);
     Fq2 z2;
     fq2_dbl(z2, z);
@@ -256,9 +304,9 @@ HBTC_GT_SMALL_LOOP
       fq_zero(q.c1);
     }
     if (!Y2 && t == 2)  // Y in Fq: two products (t is the same on every lane: a uniform branch)
-      mul2_fq(z, x, q.c0);
+      mul2_fq(z, x, q.c0, ps);
     else
-      mul2(z, x, q);
+      mul2(z, x, q, ps);
     fq2_xi_if(z, (t == 1 && k < 2) || (t == 2 && k < 3), z);
     fq2_add(acc, acc, z);
   }
@@ -296,7 +344,7 @@ GTN void frob(Fq2& f, int j, const Pos& ps) {
     fq2_conj(x, f);
   else
     x = f;
-  mul2(f, x, g);
+  mul2(f, x, g, ps);
 }
 
 // Granger-Scott squaring of a cyclotomic element, Fq12 seen as Fq4^3 over the coefficient
@@ -320,7 +368,7 @@ HD void cyc_sqr(Fq2& f, const Pos& ps) {
     fq2_sel(x, lo, apb, a);
     fq2_sel(y, lo, apxb, b);
   }
-  mul2(r, x, y);  // lo: (a + b)(a + xi b); hi: ab
+  mul2(r, x, y, ps);  // lo: (a + b)(a + xi b); hi: ab
   Fq2 m;
   fetch2(m, r, src(ps, pk));  // lo lanes take ab from their partner
   Fq2 T, t1, xm;
@@ -409,7 +457,7 @@ HBTC_GT_SMALL_LOOP
     fq2_sel(py, k == 2, n1, n2);
     fq2_sel(x, t == 0, sx, px);
     fq2_sel(y, t == 0, sx, py);
-    mul2(q, x, y);
+    mul2(q, x, y, ps);
     fq2_sel(z0, t == 0, q, z0);
     z1 = q;
   }
@@ -421,7 +469,7 @@ HBTC_GT_SMALL_LOOP
   Fq2 m, u;
   fq2_sel(m, k == 2, n2, n0);
   fq2_sel(m, k == 4, n1, m);
-  mul2(u, m, tm);
+  mul2(u, m, tm, ps);
   fq2_xi_if(u, k != 0, u);
   Fq2 d, d2, d4;
   fetch2(d, u, src(ps, 0));
@@ -441,7 +489,7 @@ HBTC_GT_SMALL_LOOP
   fq_mul(t1, d.c1, inv);
   fq_neg(dinv.c1, t1);
   Fq2 ninv, zero;
-  mul2(ninv, tm, dinv);
+  mul2(ninv, tm, dinv, ps);
   fq2_zero(zero);
   fq2_sel(ninv, (k & 1u) == 0, ninv, zero);
   Fq2 c2;

@@ -127,6 +127,16 @@ struct hbtc_ctx {
   bool track_senders = true;
   uint32_t rlc_bits = 128;  // hbtc_set_rlc_bits (default: the curve's ~2^-128 level)
   bool probe_cold = true;  // probe pass on a cold key set (HBTC_PROBE=0: off)
+  // failing tiles go through the split levels (check the left child, derive the right one;
+  // k_chk_split) instead of halves / sub-tiles (HBTC_SPLIT=0: the round-3 levels)
+  bool split_levels = true;
+  // items per pair-batch chunk (pb_verify_dev; HBTC_PB_CHUNK overrides, a multiple of 64): the
+  // chunk's per-item line tables (19.6 KB per item, ~5.1 GB at 2^18) stay cached in the
+  // workspace until hbtc_trim_workspace
+  uint32_t pb_chunk = 1u << 18;
+  // layout of the small check levels (split levels, leaves) of calls on the paired schedules:
+  // 3 = the latency form (gt6.h Pos.rep), 1 = the throughput form; HBTC_GT_REP overrides
+  int small_rep = 3;
   uint64_t probes = 0;     // probe passes run
   const uint32_t* last_leaf_count = nullptr;  // device counter of the last RLC call
   // Device ranges that combines still read, each with the event recorded after that combine:
@@ -666,8 +676,8 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
     c->last_dec = {d_status, d_share, n_items, dec, nullptr};
   }
   // counters: [0] leaves, [1] listed tiles (half / sub-tile pass), [2] failing tiles, [3] failing
-  // subs, [4] failing halves, [5] listed halves
-  HB_TRY(wst(c, "rlc.counters", 6, &counters));
+  // subs, [4] failing halves, [5] listed halves, [6..8] the split levels' lists
+  HB_TRY(wst(c, "rlc.counters", 9, &counters));
   HB_TRY(wst(c, "rlc.sub_list", n_tiles, &sub_list));
   HB_TRY(wst(c, "rlc.tw_list", n_tiles, &tw_list));
   HB_TRY(wst(c, "rlc.sw_list", (size_t)8 * n_tiles, &sw_list));
@@ -683,7 +693,23 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
   uint32_t* sw_count = counters + 3;
   uint32_t* hw_count = counters + 4;
   uint32_t* hl_count = counters + 5;
-  HB_CHECK(c, launch_zero_u32(c->stream, counters, 6));
+  HB_CHECK(c, launch_zero_u32(c->stream, counters, 9));
+  // the split levels' lists: level l lists up to n_tiles 2^(l-1) nodes with their T, U (6 Fq2 each)
+  const int chk_mode = check_mode(c, n_tiles);
+  const bool split = c->split_levels && chk_mode != CHK_PAIR_LEAVES;
+  SplitOut sp[3] = {};
+  if (split) {
+    for (int l = 0; l < 3; ++l) {
+      const size_t cap = (size_t)n_tiles << l;
+      const std::string nm = "rlc.split" + std::to_string(l);
+      sp[l].count = counters + 6 + l;
+      HB_TRY(wst(c, (nm + ".list").c_str(), cap, &sp[l].list));
+      HB_TRY(wst(c, (nm + ".ab").c_str(), cap, &sp[l].ab));
+      HB_TRY(wst(c, (nm + ".T").c_str(), 6 * cap, &sp[l].T));
+      HB_TRY(wst(c, (nm + ".U").c_str(), 6 * cap, &sp[l].U));
+    }
+  }
+  const SplitOut no_split{};
   const Suspects sus = suspects_of(c, ks, leaf_count, leaves);
   HB_TRY(items_gate(c));
   HB_TRY(timed(c, "rlc_items", [&] {
@@ -692,20 +718,20 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
   }));
   HB_TRY(items_mark(c));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
-  const int chk_mode = check_mode(c, n_tiles);
   if (chk_mode != CHK_PLAIN_FIRST) {
     // latency form: paired levels (hbtc_check.hip k_chk_pair)
     const bool two = chk_mode == CHK_PAIR_LEAVES;
     HB_TRY(timed(c, "chk_tiles", [&] {
       return launch_chk_pair(c->stream, 0, two, n_tiles, n_tiles, nullptr, nullptr, tiles, sums,
                              h_aff, h_lines, w_aff, w_lines, h_st, w_st, d_status,
-                             two ? leaf_count : sub_count, two ? leaves : sub_list);
+                             two ? leaf_count : sub_count, two ? leaves : sub_list,
+                             split ? sp[0] : no_split);
     }));
-    if (!two)
+    if (!two && !split)
       HB_TRY(timed(c, "chk_subs", [&] {
         return launch_chk_pair(c->stream, 1, true, 8 * n_tiles, 0, sub_count, sub_list, tiles, sums,
                                h_aff, h_lines, w_aff, w_lines, h_st, w_st, d_status, leaf_count,
-                               leaves);
+                               leaves, no_split);
       }));
   } else {  // throughput form: plain first (k_chk_plain / k_chk_halves / k_chk_weighted)
     HB_TRY(timed(c, "chk_tiles", [&] {
@@ -715,8 +741,24 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
     HB_TRY(timed(c, "chk_tiles_w", [&] {
       return launch_chk_weighted(c->stream, 0, n_tiles, tw_count, tw_list, nullptr, nullptr, tiles,
                                  sums, h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_tiles, d_status,
-                                 sub_count, sub_list);
+                                 sub_count, sub_list, split ? sp[0] : no_split);
     }));
+  }
+  // small calls (the paired schedules): their later levels hold a few hundred checks at most,
+  // a chain of check latencies, so they run in the latency form
+  const int rep = chk_mode == CHK_PLAIN_FIRST ? 1 : c->small_rep;
+  if (split) {
+    // split levels: listed tiles -> halves -> quarters -> eighths (unresolved eighths: leaves)
+    static const char* const fam[3] = {"chk_split1", "chk_split2", "chk_split3"};
+    for (int l = 1; l <= 3; ++l) {
+      const SplitOut& in = sp[l - 1];
+      HB_TRY(timed(c, fam[l - 1], [&] {
+        return launch_chk_split(c->stream, l, rep, n_tiles << (l - 1), in.count, in.list, in.T, in.U,
+                                in.ab, tiles, sums, h_aff, h_lines, w_aff, w_lines, d_status,
+                                leaf_count, leaves, l < 3 ? sp[l] : no_split);
+      }));
+    }
+  } else if (chk_mode == CHK_PLAIN_FIRST) {
     HB_TRY(timed(c, "chk_halves", [&] {
       return launch_chk_halves(c->stream, n_tiles, sub_count, sub_list, tiles, sums, h_aff, h_lines,
                                w_aff, w_lines, t_tiles, t_halves, hw_count, hw_list);
@@ -724,7 +766,7 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
     HB_TRY(timed(c, "chk_halves_w", [&] {
       return launch_chk_weighted(c->stream, 2, 2 * n_tiles, hw_count, hw_list, sub_list, nullptr,
                                  tiles, sums, h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_halves,
-                                 d_status, hl_count, hl_list);
+                                 d_status, hl_count, hl_list, no_split);
     }));
     HB_TRY(timed(c, "chk_subs", [&] {
       return launch_chk_plain(c->stream, 3, 8 * n_tiles, 0, hl_count, sub_list, hl_list, tiles, sums,
@@ -733,12 +775,18 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
     HB_TRY(timed(c, "chk_subs_w", [&] {
       return launch_chk_weighted(c->stream, 3, 8 * n_tiles, sw_count, sw_list, sub_list, hl_list,
                                  tiles, sums, h_aff, h_lines, w_aff, w_lines, h_st, w_st, t_subs,
-                                 d_status, leaf_count, leaves);
+                                 d_status, leaf_count, leaves, no_split);
     }));
   }
   HB_TRY(timed(c, "chk_leaves", [&] {
+    // the latency form for lists of at most two leaves per SIMD (one wave each), the throughput
+    // form for longer ones (tracked senders put one share per liar per ciphertext on the list)
+    const uint32_t lim = rep == 3 ? 8u * (uint32_t)c->n_cu : 0u;
+    const hipError_t e = launch_chk_leaves_rep3(c->stream, n_items, lim, leaf_count, leaves, d_idx, dec,
+                                                ks->pk, h_aff, h_lines, w_aff, w_lines, d_status);
+    if (e != hipSuccess) return e;
     return launch_chk_leaves(c->stream, n_items, leaf_count, leaves, d_idx, dec, ks->pk, h_aff,
-                             h_lines, w_aff, w_lines, d_status);
+                             h_lines, w_aff, w_lines, d_status, lim);
   }));
   if (!probe) c->last_leaf_count = leaf_count;
   return timed(c, "rlc_finalize", [&] {
@@ -820,7 +868,13 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   // paired checks either way (plain and weighted value of a group per unit); a small call goes
   // from the tiles straight to the leaves (check_mode)
   const bool to_leaves = check_mode(c, n_tiles) == CHK_PAIR_LEAVES;
+  // the small calls' levels (tiles -> leaves: fewer tiles than half the SIMDs) are chains of check
+  // latencies: the latency form (gt6.h Pos.rep = 3), unless HBTC_GT_REP=1
+  const bool rep3 = to_leaves && c->small_rep == 3;
   HB_TRY(timed(c, "chk_tiles", [&] {
+    if (rep3)
+      return launch_sigchk_tiles_rep3(c->stream, n_tiles, tiles, sums, tables, inf, h_aff, h_lines,
+                                      h_st, d_status, leaf_count, leaves, true);
     return launch_sigchk_tiles(c->stream, n_tiles, tiles, sums, tables, inf, h_aff, h_lines, h_st,
                                d_status, to_leaves ? leaf_count : sub_count,
                                to_leaves ? leaves : sub_list, to_leaves);
@@ -843,8 +897,13 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
                            inf);
     }));
     HB_TRY(timed(c, "chk_leaves", [&] {
+      // a short list (<= 2 leaves per SIMD, all in the first chunk) in the latency form
+      const uint32_t lim = (rep3 && base == 0) ? std::min(LEAF_CHUNK, 8u * (uint32_t)c->n_cu) : 0u;
+      const hipError_t e = launch_sigchk_leaves_rep3(c->stream, chunk, lim, leaf_count, leaves, d_idx,
+                                                     ks->pk, tables, inf, h_aff, h_lines, d_status);
+      if (e != hipSuccess) return e;
       return launch_sigchk_leaves(c->stream, base, chunk, leaf_count, leaves, d_idx, ks->pk, tables,
-                                  inf, h_aff, h_lines, d_status);
+                                  inf, h_aff, h_lines, d_status, lim);
     }));
   }
   c->last_leaf_count = leaf_count;
@@ -1218,6 +1277,12 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (const char* e = getenv("HBTC_G2_GLS")) c->g2_gls = atoi(e) != 0;
   if (const char* e = getenv("HBTC_G1_GLV")) c->g1_glv = atoi(e) != 0;
   if (const char* e = getenv("HBTC_PROBE")) c->probe_cold = atoi(e) != 0;
+  if (const char* e = getenv("HBTC_SPLIT")) c->split_levels = atoi(e) != 0;
+  if (const char* e = getenv("HBTC_GT_REP")) c->small_rep = atoi(e) == 1 ? 1 : 3;
+  if (const char* e = getenv("HBTC_PB_CHUNK")) {
+    const long v = atol(e);
+    if (v >= 64 && v % 64 == 0 && v <= (1l << 20)) c->pb_chunk = (uint32_t)v;
+  }
   if (const char* e = getenv("HBTC_CHECK_MODE")) {
     const std::string m(e);
     c->check_mode_forced = m == "plain" ? 0 : m == "pair3" ? 1 : m == "pair2" ? 2 : -1;
@@ -1384,10 +1449,10 @@ int hbtc_verify_sig_shares(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, con
 // e(A_i, Q_i) == e(G1, W_i) for n items in device memory (A null: the G1 generator; Q trusted:
 // our own hash output, decoded without the subgroup check; statuses ACCEPT / REJECT /
 // DECODE_ERR as k_pair_verify's).  RLC mode: the pair-batch path of hbtc_pb.hip in chunks of
-// PB_CHUNK items (the per-item line tables are 19.6 KB each): item pass, Q line tables, partial
-// Miller products per 8-item sub-tile, the 64-item tile checks, the 8-item sub-tiles of failing tiles, the exact k_pair_verify of the
-// items of failing sub-tiles.  Per-share mode: k_pair_verify for every item.
-constexpr uint32_t PB_CHUNK = 1u << 18;
+// c->pb_chunk items (the per-item line tables are 19.6 KB each): item pass, Q line tables,
+// partial Miller products per 8-item sub-tile, the 64-item tile checks, the 8-item sub-tiles of
+// failing tiles, the exact k_pair_verify of the items of failing sub-tiles; a fresh RLC key per
+// chunk.  Per-share mode: k_pair_verify for every item.
 int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_q, bool q_trusted,
                   const uint8_t* d_w, int32_t* d_status, G1A* d_adec = nullptr) {
   if (c->verify_mode == HBTC_MODE_PER_SHARE) {
@@ -1395,6 +1460,7 @@ int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_
       return launch_pair_verify(c->stream, n, d_a, d_q, nullptr, d_w, d_status);
     });
   }
+  const uint32_t PB_CHUNK = c->pb_chunk;
   for (uint32_t base = 0; base < n; base += PB_CHUNK) {
     const uint32_t m = std::min(PB_CHUNK, n - base);
     const uint32_t T = (m + 63) / 64;
@@ -2164,6 +2230,18 @@ int hbtc_set_rlc_bits(hbtc_ctx* c, uint32_t bits) {
   if (!c || (bits != 64 && bits != 128)) return HBTC_ERR_ARG;
   Guard g(c);
   c->rlc_bits = bits;
+  return HBTC_OK;
+}
+
+int hbtc_trim_workspace(hbtc_ctx* c) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  HB_TRY(sync(c));
+  for (auto& kv : c->bufs)
+    if (kv.second.p) (void)hipFree(kv.second.p);
+  c->bufs.clear();
+  c->last_dec = {};
+  c->last_leaf_count = nullptr;
   return HBTC_OK;
 }
 

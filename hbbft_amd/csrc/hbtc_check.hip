@@ -22,6 +22,8 @@
 #ifndef HBTC_FQMUL_SR
 #define HBTC_FQMUL_INLINE
 #endif
+#include <algorithm>
+
 #include "gt6.h"
 #include "hbtc_kernels.h"
 
@@ -49,21 +51,28 @@ using gt::Pos;
 namespace {
 
 constexpr uint32_t UNITS_PER_WAVE = 5;
+// units per wave of a layout: 5 of 12 lanes (rep 1), 1 of 36 lanes (rep 3, the latency form:
+// gt6.h Pos.rep; lanes 36..63 idle)
+template <uint32_t REP>
+struct Units {
+  static constexpr uint32_t PER_WAVE = REP == 1 ? UNITS_PER_WAVE : 1u;
+};
 
 struct UnitLane {
-  uint32_t unit;     // 0..4 (5: the idle lanes 60..63)
+  uint32_t unit;     // 0..4 (5: the idle lanes 60..63); rep 3: 0 (1: idle)
   uint32_t side;     // 0: first group of the unit, 1: second
   uint32_t partner;  // the same coefficient's lane in the other group
   Pos ps;
 };
 
-__device__ __forceinline__ UnitLane unit_lane() {
+__device__ __forceinline__ UnitLane unit_lane(uint32_t rep = 1) {
   const uint32_t l = gt::lane_id();
+  const uint32_t gs = 6u * rep;
   UnitLane u;
-  u.unit = l / 12u;
-  u.side = (l / 6u) & 1u;
-  u.partner = u.side ? l - 6u : l + 6u;
-  u.ps = gt::pos();
+  u.unit = l / (2u * gs);
+  u.side = (l / gs) & 1u;
+  u.partner = u.side ? l - gs : l + gs;
+  u.ps = gt::pos(rep);
   return u;
 }
 
@@ -255,6 +264,51 @@ __device__ __forceinline__ int32_t locate_group(const Fq2& T, const Fq2& Tw, uin
   return weight_pos(found >= 0 && ok ? found : -1, lg, count);
 }
 
+// Append a group's node to a split level's list with its GT values (T, U) and weight form
+// (ab = log2 alpha | beta << 8: U = prod E_i^(r_i (alpha w_i + beta)), w_i the node-local
+// bit-reversed weights).  Called by every lane of the group (converged: the slot is broadcast).
+__device__ __forceinline__ void split_list(const SplitOut& o, bool list, uint32_t code, const Fq2& T,
+                                           const Fq2& U, uint32_t ab, const Pos& ps) {
+  uint32_t pos = 0;
+  if (list && ps.k == 0 && ps.sub == 0) pos = atomicAdd(o.count, 1u);
+  pos = gt::shfl(pos, ps.base);
+  if (!list || ps.sub != 0) return;
+  o.T[(size_t)pos * 6u + ps.k] = T;
+  o.U[(size_t)pos * 6u + ps.k] = U;
+  if (ps.k == 0) {
+    o.list[pos] = code;
+    o.ab[pos] = ab;
+  }
+}
+
+// y^e for a small non-negative e < 2^NB (square-and-multiply, uniform over the wave)
+template <int NB>
+__device__ __forceinline__ void gt_pow_small(Fq2& r, const Fq2& y, uint32_t e, const Pos& ps) {
+  Fq2 acc;
+  gt::set_one(acc, ps);
+#pragma unroll 1
+  for (int bit = NB - 1; bit >= 0; --bit) {
+    gt::cyc_sqr(acc, ps);
+    Fq2 m;
+    gt::mul(m, acc, y, ps);
+    gt::fq2_sel(acc, ((e >> bit) & 1u) != 0, m, acc);
+  }
+  r = acc;
+}
+
+// y^(2^k) for k <= KMAX (uniform: KMAX squarings, the extra ones discarded)
+template <int KMAX>
+__device__ __forceinline__ void gt_pow2k(Fq2& r, const Fq2& y, uint32_t k, const Pos& ps) {
+  Fq2 acc = y;
+#pragma unroll 1
+  for (int i = 0; i < KMAX; ++i) {
+    Fq2 sq = acc;
+    gt::cyc_sqr(sq, ps);
+    gt::fq2_sel(acc, (uint32_t)i < k, sq, acc);
+  }
+  r = acc;
+}
+
 }  // namespace
 
 #if HBTC_CHECK_IN(1)
@@ -361,7 +415,8 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_weighted(
     const Line* __restrict__ h_lines, const G2A* __restrict__ w_aff,
     const Line* __restrict__ w_lines, const int32_t* __restrict__ h_status,
     const int32_t* __restrict__ w_status, const Fq2* __restrict__ Tbuf,
-    int32_t* __restrict__ status, uint32_t* __restrict__ out_count, uint32_t* __restrict__ out_list) {
+    int32_t* __restrict__ status, uint32_t* __restrict__ out_count, uint32_t* __restrict__ out_list,
+    SplitOut split) {
   HBTC_LATENCY_PRIO();
   const uint32_t n = *fail_count;
   if (blockIdx.x * 2u * UNITS_PER_WAVE >= n) return;
@@ -387,6 +442,13 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_weighted(
              w_lines + (size_t)r.inst * MILLER_STEPS, ul.ps);
   const int32_t loc = locate_group(T, Tw, r.hi - r.lo, LEVEL == 0 ? 6 : (LEVEL == 2 ? 5 : 3),
                                    r.active, ul.ps);
+  if (LEVEL == 0 && split.list) {
+    // the split levels: an unlocated tile is listed with its values (T, T_w; alpha = 1, beta = 0)
+    const bool located = loc >= 0 && status[r.lo + loc] == HBTC_RLC_PENDING;
+    split_list(split, r.active && !located, r.t << 3, T, Tw, 0u, ul.ps);
+    if (r.active && located && ul.ps.k == 0) status[r.lo + loc] = HBTC_REJECT;
+    return;
+  }
   if (!r.active || ul.ps.k != 0) return;
   if (loc >= 0 && status[r.lo + loc] == HBTC_RLC_PENDING) {
     status[r.lo + loc] = HBTC_REJECT;
@@ -419,7 +481,8 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_pair(
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
     const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
     const int32_t* __restrict__ h_status, const int32_t* __restrict__ w_status,
-    int32_t* __restrict__ status, uint32_t* __restrict__ out_count, uint32_t* __restrict__ out_list) {
+    int32_t* __restrict__ status, uint32_t* __restrict__ out_count, uint32_t* __restrict__ out_list,
+    SplitOut split) {
   HBTC_LATENCY_PRIO();
   const uint32_t n = LEVEL == 0 ? n_direct : *n_listed * 8u;
   if (blockIdx.x * UNITS_PER_WAVE >= n) return;  // wave-uniform: grids are sized for the worst case
@@ -440,6 +503,13 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_pair(
   // undecodable H / w: k_rlc_finalize decides the group's items
   const bool fail = r.active && r.inst_ok && !pass;
   const int32_t loc = locate(T, Tw, r.hi - r.lo, LEVEL == 0 ? 5 : 2, fail, ul);
+  if (LEVEL == 0 && !TO_LEAVES && split.list) {
+    // the split levels: an unlocated tile is listed with its values (side 0 lists)
+    const bool located = loc >= 0 && status[r.lo + loc] == HBTC_RLC_PENDING;
+    split_list(split, fail && !located && ul.side == 0, r.t << 3, T, Tw, 0u, ul.ps);
+    if (fail && located && ul.side == 0 && ul.ps.k == 0) status[r.lo + loc] = HBTC_REJECT;
+    return;
+  }
   if (!fail || ul.side != 0 || ul.ps.k != 0) return;
   if (loc >= 0 && status[r.lo + loc] == HBTC_RLC_PENDING) {
     status[r.lo + loc] = HBTC_REJECT;
@@ -460,23 +530,154 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_pair(
   }
 }
 
+// Split level LVL (1: listed tiles, 2: listed halves, 3: listed quarters).  A listed node X
+// (>= 2 wrong shares, or one its location could not confirm) carries its values T_X and
+// U_X = prod_X E_i^(r_i (alpha w_i + beta)).  A unit checks X's LEFT child L (plain T_L on side
+// 0, weighted W_L on side 1: one paired check) and derives the right child R without pairings:
+//     T_R = T_X / T_L,   U_R = U_X / (W_L^(2 alpha) T_L^beta)   (alpha_R = 2 alpha, beta_R = alpha + beta)
+// since the parent's local weight of a share is 2 w_L in L and 2 w_R + 1 in R (bit-reversed
+// weights).  GT values are cyclotomic: division is multiplication by the conjugate.  Then side 0
+// locates a single wrong share in L (W_L = T_L^w) and side 1 in R (U_R = T_R^(alpha_R w + beta_R):
+// G = T_R^alpha_R, Y = U_R / T_R^beta_R, G^w = Y), both by the baby-step giant-step search.  A
+// child whose value is 1 passes; an unlocated child is listed for level LVL + 1 (LVL 3: its
+// pending shares go to the exact leaf checks).  Two checks per listed node instead of 16 for its
+// eight sub-tiles; soundness as every group check (hbtc_rlc.hip): a derived value is the plain /
+// weighted RLC value of the child itself.
+template <int LVL, uint32_t REP>
+__global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_split(
+    const uint32_t* __restrict__ n_in, const uint32_t* __restrict__ in_list,
+    const Fq2* __restrict__ in_T, const Fq2* __restrict__ in_U, const uint32_t* __restrict__ in_ab,
+    const Tile* __restrict__ tiles, const TileSums* __restrict__ sums,
+    const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
+    const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
+    int32_t* __restrict__ status, uint32_t* __restrict__ leaf_count, uint32_t* __restrict__ leaves,
+    SplitOut split) {
+  HBTC_LATENCY_PRIO();
+  constexpr uint32_t SIZE = 64u >> (LVL - 1), HALF = SIZE / 2;
+  constexpr int LG = 6 - LVL;  // log2(HALF)
+  constexpr uint32_t UPW = Units<REP>::PER_WAVE;
+  const uint32_t n = *n_in;
+  if (blockIdx.x * UPW >= n) return;  // wave-uniform: grids are sized for the worst case
+  const UnitLane ul = unit_lane(REP);
+  const uint32_t u = blockIdx.x * UPW + ul.unit;
+  const bool active = ul.unit < UPW && u < n;
+  const uint32_t code = active ? in_list[u] : 0u;
+  const uint32_t t = code >> 3, j = code & 7u;
+  Tile tile{0, 0, 0, 0};
+  if (active) tile = tiles[t];
+  const uint32_t end = tile.first + tile.count;
+  const uint32_t x_lo = min(end, tile.first + j * SIZE);
+  const uint32_t x_hi = min(end, x_lo + SIZE);
+  const uint32_t l_hi = min(x_hi, x_lo + HALF);  // L = [x_lo, l_hi), R = [l_hi, x_hi)
+  G1J S, P;
+  jac_set_inf(S);
+  jac_set_inf(P);
+  if (active) {
+    const TileSums& ts = sums[t];
+    const bool wt = ul.side != 0;
+    if (LVL == 1) {
+      S = wt ? ts.SHW[0] : ts.SH[0];
+      P = wt ? ts.PHW[0] : ts.PH[0];
+    } else if (LVL == 2) {  // the left quarter of half j
+      S = wt ? ts.SQW[j] : ts.SQ[j];
+      P = wt ? ts.PQW[j] : ts.PQ[j];
+    } else {  // the left eighth of quarter j
+      S = wt ? ts.SW[2 * j] : ts.S[2 * j];
+      P = wt ? ts.PW[2 * j] : ts.P[2 * j];
+    }
+  }
+  const uint32_t inst = tile.inst;
+  const bool use1 = active && !jac_is_inf(S) && !h_aff[inst].inf;
+  const bool use2 = active && !jac_is_inf(P) && !w_aff[inst].inf;
+  Fq2 e, TL, WL;
+  pair_value(e, S, use1, h_lines + (size_t)inst * MILLER_STEPS, P, use2,
+             w_lines + (size_t)inst * MILLER_STEPS, ul.ps);
+  unit_values(TL, WL, e, ul);
+  Fq2 TX, UX;
+  gt::set_one(TX, ul.ps);
+  gt::set_one(UX, ul.ps);
+  uint32_t ab = 0;
+  if (active) {
+    TX = in_T[(size_t)u * 6u + ul.ps.k];
+    UX = in_U[(size_t)u * 6u + ul.ps.k];
+    ab = in_ab[u];
+  }
+  const uint32_t ka = ab & 0xffu, beta = ab >> 8;  // alpha = 2^ka: ka <= LVL - 1, beta < 2^(LVL-1)
+  Fq2 TR, UR;
+  {
+    Fq2 c = TL;
+    gt::conj(c, ul.ps);
+    gt::mul(TR, TX, c, ul.ps);
+    Fq2 m, tb;
+    gt_pow2k<LVL>(m, WL, ka + 1u, ul.ps);              // W_L^(2 alpha)
+    gt_pow_small<(LVL > 1 ? LVL - 1 : 1)>(tb, TL, beta, ul.ps);  // T_L^beta
+    gt::mul(m, m, tb, ul.ps);
+    gt::conj(m, ul.ps);
+    gt::mul(UR, UX, m, ul.ps);
+  }
+  const uint32_t kaR = ka + 1u, betaR = (1u << ka) + beta;
+  const bool passL = gt::is_one(TL, ul.ps), passR = gt::is_one(TR, ul.ps);
+  // location inputs of this side
+  Fq2 G = TL, Y = WL;
+  {
+    Fq2 g, tb;
+    gt_pow2k<LVL>(g, TR, kaR, ul.ps);
+    gt_pow_small<LVL>(tb, TR, betaR, ul.ps);
+    gt::conj(tb, ul.ps);
+    Fq2 y;
+    gt::mul(y, UR, tb, ul.ps);
+    gt::fq2_sel(G, ul.side != 0, g, TL);
+    gt::fq2_sel(Y, ul.side != 0, y, WL);
+  }
+  const uint32_t lo = ul.side ? l_hi : x_lo, hi = ul.side ? x_hi : l_hi;
+  const bool pass = ul.side ? passR : passL;
+  const bool need = active && !pass && lo < hi;
+  const int32_t loc = locate_group(G, Y, hi - lo, LG, need, ul.ps);
+  // decide on every lane of the group before any write (the status reads must not race)
+  const bool located = need && loc >= 0 && status[lo + loc] == HBTC_RLC_PENDING;
+  const bool unresolved = need && !located;
+  if (LVL < 3) {
+    const uint32_t ab_child = ul.side ? (kaR | (betaR << 8)) : 0u;
+    split_list(split, unresolved, (t << 3) | (2u * j + ul.side), ul.side ? TR : TL,
+               ul.side ? UR : WL, ab_child, ul.ps);
+  }
+  if (ul.ps.k != 0 || ul.ps.sub != 0) return;
+  if (located) status[lo + loc] = HBTC_REJECT;
+  if (LVL == 3 && unresolved) {
+    uint32_t m = 0;
+    for (uint32_t i = lo; i < hi; ++i) m += status[i] == HBTC_RLC_PENDING;
+    uint32_t pos = atomicAdd(leaf_count, m);
+    for (uint32_t i = lo; i < hi; ++i)
+      if (status[i] == HBTC_RLC_PENDING) {
+        leaves[2 * pos] = i;
+        leaves[2 * pos + 1] = inst;
+        ++pos;
+      }
+  }
+}
+
 #endif  // part 2
 
-#if HBTC_CHECK_IN(1)
 // ------------------------------------------------------------------------------ level 3: leaves
+// (a template in both parts: <1> is instantiated by part 1's launcher, <3> by part 2's)
 // e(d_i, H_k) e(-pk_i, w_k) == 1 for two listed shares per unit.
-__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_leaves(
+template <uint32_t REP>
+__global__ void __launch_bounds__(64, REP == 1 ? HBTC_GT_WAVES : HBTC_GT_WAVES_SMALL) k_chk_leaves(
     const uint32_t* __restrict__ leaf_count, const uint32_t* __restrict__ leaves,
     const uint32_t* __restrict__ idx, const G1A* __restrict__ dec, const G1A* __restrict__ pk,
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
     const G2A* __restrict__ w_aff, const Line* __restrict__ w_lines,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ status, uint32_t rep3_limit) {
   HBTC_LATENCY_PRIO();
+  constexpr uint32_t UPW = Units<REP>::PER_WAVE;
   const uint32_t n = *leaf_count;
-  if (blockIdx.x * 2 * UNITS_PER_WAVE >= n) return;
-  const UnitLane ul = unit_lane();
-  const uint32_t li = (blockIdx.x * UNITS_PER_WAVE + ul.unit) * 2u + ul.side;
-  const bool active = ul.unit < UNITS_PER_WAVE && li < n;
+  // a list of at most rep3_limit leaves is the latency form's (REP 3), a longer one the
+  // throughput form's: both are launched, one of them exits at once
+  if ((REP == 3) == (n > rep3_limit)) return;
+  if (blockIdx.x * 2 * UPW >= n) return;
+  const UnitLane ul = unit_lane(REP);
+  const uint32_t li = (blockIdx.x * UPW + ul.unit) * 2u + ul.side;
+  const bool active = ul.unit < UPW && li < n;
   uint32_t item = 0, k = 0;
   G1J S, P;
   jac_set_inf(S);
@@ -493,10 +694,11 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_chk_leaves(
   pair_value(e, S, use1, h_lines + (size_t)k * MILLER_STEPS, P, use2,
              w_lines + (size_t)k * MILLER_STEPS, ul.ps);
   const bool ok = gt::is_one(e, ul.ps);
-  if (active && ul.ps.k == 0) status[item] = ok ? HBTC_ACCEPT : HBTC_REJECT;
+  if (active && ul.ps.k == 0 && ul.ps.sub == 0) status[item] = ok ? HBTC_ACCEPT : HBTC_REJECT;
 }
 
 // ------------------------------------------------------------------------------ SignatureShares
+// (templates on the layout: rep 1 instantiated by part 1, the latency form rep 3 by part 2)
 // e(sum r_i pk_i, H) e(-G1, sum r_i sigma_i) == 1: the first pair over H's precomputed lines,
 // the second over the group's projective line table (hbtc_sig.hip k_plines) at the fixed -G1.
 namespace {
@@ -515,16 +717,18 @@ __device__ __forceinline__ void sig_pair_value(Fq2& e, const G1J& P, bool use1, 
 }
 }  // namespace
 
-__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_tiles(
+template <uint32_t REP>
+__global__ void __launch_bounds__(64, REP == 1 ? HBTC_GT_WAVES : HBTC_GT_WAVES_SMALL) k_sigchk_tiles(
     uint32_t n_tiles, const Tile* __restrict__ tiles, const SigTileSums* __restrict__ sums,
     const Fq2* __restrict__ tables, const uint32_t* __restrict__ inf,
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
     const int32_t* __restrict__ h_status, int32_t* __restrict__ status,
     uint32_t* __restrict__ sub_count, uint32_t* __restrict__ sub_list, bool to_leaves) {
   HBTC_LATENCY_PRIO();
-  const UnitLane ul = unit_lane();
-  const uint32_t t = blockIdx.x * UNITS_PER_WAVE + ul.unit;
-  const bool active = ul.unit < UNITS_PER_WAVE && t < n_tiles;
+  constexpr uint32_t UPW = Units<REP>::PER_WAVE;
+  const UnitLane ul = unit_lane(REP);
+  const uint32_t t = blockIdx.x * UPW + ul.unit;
+  const bool active = ul.unit < UPW && t < n_tiles;
   uint32_t k = 0, first = 0, count = 0, g = 0;
   bool inst_ok = false, inf2 = true;
   G1J P;
@@ -547,7 +751,7 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_tiles(
   const bool pass = unit_values(T, Tw, e, ul);
   const bool fail = active && inst_ok && !pass;
   const int32_t loc = locate(T, Tw, count, 5, fail, ul);
-  if (!fail || ul.side != 0 || ul.ps.k != 0) return;
+  if (!fail || ul.side != 0 || ul.ps.k != 0 || ul.ps.sub != 0) return;
   if (loc >= 0 && status[first + loc] == HBTC_RLC_PENDING) {
     status[first + loc] = HBTC_REJECT;
     return;
@@ -569,6 +773,7 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_tiles(
     }
 }
 
+#if HBTC_CHECK_IN(1)
 __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_subs(
     const uint32_t* __restrict__ sub_count, const uint32_t* __restrict__ sub_list,
     const Tile* __restrict__ tiles, const SigTileSums* __restrict__ sums,
@@ -620,21 +825,28 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_subs(
     }
 }
 
-__global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_leaves(
+#endif  // part 1
+
+// rep3_limit: a list of at most rep3_limit leaves is the latency form's (REP 3, first chunk
+// only), a longer one the throughput form's; both are launched, one exits at once
+template <uint32_t REP>
+__global__ void __launch_bounds__(64, REP == 1 ? HBTC_GT_WAVES : HBTC_GT_WAVES_SMALL) k_sigchk_leaves(
     uint32_t base, uint32_t chunk, const uint32_t* __restrict__ leaf_count,
     const uint32_t* __restrict__ leaves,
     const uint32_t* __restrict__ idx, const G1A* __restrict__ pk,
     const Fq2* __restrict__ tables, const uint32_t* __restrict__ inf,
     const G2A* __restrict__ h_aff, const Line* __restrict__ h_lines,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ status, uint32_t rep3_limit) {
   HBTC_LATENCY_PRIO();
+  constexpr uint32_t UPW = Units<REP>::PER_WAVE;
   // leaves [base, base + chunk) of the list; tables are numbered from the chunk start
   const uint32_t c = *leaf_count;
+  if ((REP == 3) == (c > rep3_limit)) return;
   const uint32_t n = c > base ? min(c - base, chunk) : 0u;
-  if (blockIdx.x * 2 * UNITS_PER_WAVE >= n) return;
-  const UnitLane ul = unit_lane();
-  const uint32_t g = (blockIdx.x * UNITS_PER_WAVE + ul.unit) * 2u + ul.side;
-  const bool active = ul.unit < UNITS_PER_WAVE && g < n;
+  if (blockIdx.x * 2 * UPW >= n) return;
+  const UnitLane ul = unit_lane(REP);
+  const uint32_t g = (blockIdx.x * UPW + ul.unit) * 2u + ul.side;
+  const bool active = ul.unit < UPW && g < n;
   uint32_t item = 0, k = 0;
   bool inf2 = true;
   G1J P;
@@ -651,10 +863,8 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES) k_sigchk_leaves(
   sig_pair_value(e, P, use1, h_lines + (size_t)k * MILLER_STEPS,
                  tables + (size_t)(active ? g : 0) * PLINES_FQ2, use2, ul.ps);
   const bool ok = gt::is_one(e, ul.ps);
-  if (active && ul.ps.k == 0) status[item] = ok ? HBTC_ACCEPT : HBTC_REJECT;
+  if (active && ul.ps.k == 0 && ul.ps.sub == 0) status[item] = ok ? HBTC_ACCEPT : HBTC_REJECT;
 }
-
-#endif  // part 1 (leaves, SignatureShare kernels)
 
 // ------------------------------------------------------------------------------ launchers
 static inline uint32_t unit_blocks(uint64_t units) {
@@ -706,12 +916,12 @@ hipError_t launch_chk_weighted(hipStream_t s, int level, uint32_t max_groups,
                                const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
                                const Line* w_lines, const int32_t* h_status,
                                const int32_t* w_status, const Fq2* Tbuf, int32_t* status,
-                               uint32_t* out_count, uint32_t* out_list) {
+                               uint32_t* out_count, uint32_t* out_list, SplitOut split) {
   if (max_groups == 0) return hipSuccess;
   const dim3 grid(unit_blocks(((uint64_t)max_groups + 1) / 2));
 #define HBTC_WEIGHTED_ARGS                                                                     \
   grid, dim3(64), 0, s, fail_count, fail_list, sub_list, list2, tiles, sums, h_aff, h_lines, w_aff, \
-      w_lines, h_status, w_status, Tbuf, status, out_count, out_list
+      w_lines, h_status, w_status, Tbuf, status, out_count, out_list, split
   if (level == 0)
     hipLaunchKernelGGL(k_chk_weighted<0>, HBTC_WEIGHTED_ARGS);
   else if (level == 1)
@@ -729,12 +939,12 @@ hipError_t launch_chk_pair(hipStream_t s, int level, bool to_leaves, uint32_t ma
                            const Tile* tiles, const TileSums* sums, const G2A* h_aff,
                            const Line* h_lines, const G2A* w_aff, const Line* w_lines,
                            const int32_t* h_status, const int32_t* w_status, int32_t* status,
-                           uint32_t* out_count, uint32_t* out_list) {
+                           uint32_t* out_count, uint32_t* out_list, SplitOut split) {
   if (max_groups == 0) return hipSuccess;
   const dim3 grid(unit_blocks(max_groups));
 #define HBTC_PAIR_ARGS                                                                       \
   grid, dim3(64), 0, s, n_direct, n_listed, sub_list, tiles, sums, h_aff, h_lines, w_aff, w_lines, \
-      h_status, w_status, status, out_count, out_list
+      h_status, w_status, status, out_count, out_list, split
   if (level == 0 && to_leaves)
     hipLaunchKernelGGL((k_chk_pair<0, true>), HBTC_PAIR_ARGS);
   else if (level == 0)
@@ -745,16 +955,85 @@ hipError_t launch_chk_pair(hipStream_t s, int level, bool to_leaves, uint32_t ma
   return hipGetLastError();
 }
 
+hipError_t launch_chk_split(hipStream_t s, int level, int rep, uint32_t max_nodes,
+                            const uint32_t* n_in, const uint32_t* in_list, const Fq2* in_T,
+                            const Fq2* in_U, const uint32_t* in_ab, const Tile* tiles,
+                            const TileSums* sums, const G2A* h_aff, const Line* h_lines,
+                            const G2A* w_aff, const Line* w_lines, int32_t* status,
+                            uint32_t* leaf_count, uint32_t* leaves, SplitOut split) {
+  if (max_nodes == 0) return hipSuccess;
+  const dim3 grid(rep == 3 ? max_nodes : unit_blocks(max_nodes));
+#define HBTC_SPLIT_ARGS                                                                       \
+  grid, dim3(64), 0, s, n_in, in_list, in_T, in_U, in_ab, tiles, sums, h_aff, h_lines, w_aff, \
+      w_lines, status, leaf_count, leaves, split
+  if (rep == 3) {
+    if (level == 1)
+      hipLaunchKernelGGL((k_chk_split<1, 3>), HBTC_SPLIT_ARGS);
+    else if (level == 2)
+      hipLaunchKernelGGL((k_chk_split<2, 3>), HBTC_SPLIT_ARGS);
+    else
+      hipLaunchKernelGGL((k_chk_split<3, 3>), HBTC_SPLIT_ARGS);
+  } else {
+    if (level == 1)
+      hipLaunchKernelGGL((k_chk_split<1, 1>), HBTC_SPLIT_ARGS);
+    else if (level == 2)
+      hipLaunchKernelGGL((k_chk_split<2, 1>), HBTC_SPLIT_ARGS);
+    else
+      hipLaunchKernelGGL((k_chk_split<3, 1>), HBTC_SPLIT_ARGS);
+  }
+#undef HBTC_SPLIT_ARGS
+  return hipGetLastError();
+}
+
+// the latency-form leaf checks (one check per 18-lane group, two per wave), compiled with the
+// one-wave kernels of this part
+hipError_t launch_chk_leaves_rep3(hipStream_t s, uint32_t max_leaves, uint32_t rep3_limit,
+                                  const uint32_t* leaf_count, const uint32_t* leaves,
+                                  const uint32_t* idx, const G1A* dec, const G1A* pk,
+                                  const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
+                                  const Line* w_lines, int32_t* status) {
+  if (max_leaves == 0 || rep3_limit == 0) return hipSuccess;
+  const uint32_t m = std::min(max_leaves, rep3_limit);
+  hipLaunchKernelGGL(k_chk_leaves<3>, dim3((m + 1) / 2), dim3(64), 0, s, leaf_count, leaves, idx, dec,
+                     pk, h_aff, h_lines, w_aff, w_lines, status, rep3_limit);
+  return hipGetLastError();
+}
+
+// SignatureShare tiles and leaves in the latency form (one unit per wave)
+hipError_t launch_sigchk_tiles_rep3(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                                    const SigTileSums* sums, const Fq2* tables, const uint32_t* inf,
+                                    const G2A* h_aff, const Line* h_lines, const int32_t* h_status,
+                                    int32_t* status, uint32_t* sub_count, uint32_t* sub_list,
+                                    bool to_leaves) {
+  if (n_tiles == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sigchk_tiles<3>, dim3(n_tiles), dim3(64), 0, s, n_tiles, tiles, sums, tables, inf,
+                     h_aff, h_lines, h_status, status, sub_count, sub_list, to_leaves);
+  return hipGetLastError();
+}
+hipError_t launch_sigchk_leaves_rep3(hipStream_t s, uint32_t chunk, uint32_t rep3_limit,
+                                     const uint32_t* leaf_count, const uint32_t* leaves,
+                                     const uint32_t* idx, const G1A* pk, const Fq2* tables,
+                                     const uint32_t* inf, const G2A* h_aff, const Line* h_lines,
+                                     int32_t* status) {
+  if (chunk == 0 || rep3_limit == 0) return hipSuccess;
+  const uint32_t m = std::min(chunk, rep3_limit);
+  hipLaunchKernelGGL(k_sigchk_leaves<3>, dim3((m + 1) / 2), dim3(64), 0, s, 0u, chunk, leaf_count, leaves,
+                     idx, pk, tables, inf, h_aff, h_lines, status, rep3_limit);
+  return hipGetLastError();
+}
+
 #endif
 
 #if HBTC_CHECK_IN(1)
 hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t* leaf_count,
                              const uint32_t* leaves, const uint32_t* idx, const G1A* dec,
                              const G1A* pk, const G2A* h_aff, const Line* h_lines,
-                             const G2A* w_aff, const Line* w_lines, int32_t* status) {
+                             const G2A* w_aff, const Line* w_lines, int32_t* status,
+                             uint32_t rep3_limit) {
   if (max_leaves == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_chk_leaves, dim3(unit_blocks(((uint64_t)max_leaves + 1) / 2)), dim3(64), 0,
-                     s, leaf_count, leaves, idx, dec, pk, h_aff, h_lines, w_aff, w_lines, status);
+  hipLaunchKernelGGL(k_chk_leaves<1>, dim3(unit_blocks(((uint64_t)max_leaves + 1) / 2)), dim3(64), 0,
+                     s, leaf_count, leaves, idx, dec, pk, h_aff, h_lines, w_aff, w_lines, status,
+                     rep3_limit);
   return hipGetLastError();
 }
 
@@ -764,7 +1043,7 @@ hipError_t launch_sigchk_tiles(hipStream_t s, uint32_t n_tiles, const Tile* tile
                                int32_t* status, uint32_t* sub_count, uint32_t* sub_list,
                                bool to_leaves) {
   if (n_tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_sigchk_tiles, dim3(unit_blocks(n_tiles)), dim3(64), 0, s, n_tiles, tiles, sums,
+  hipLaunchKernelGGL(k_sigchk_tiles<1>, dim3(unit_blocks(n_tiles)), dim3(64), 0, s, n_tiles, tiles, sums,
                      tables, inf, h_aff, h_lines, h_status, status, sub_count, sub_list, to_leaves);
   return hipGetLastError();
 }
@@ -785,10 +1064,11 @@ hipError_t launch_sigchk_leaves(hipStream_t s, uint32_t base, uint32_t chunk,
                                 const uint32_t* leaf_count, const uint32_t* leaves,
                                 const uint32_t* idx, const G1A* pk, const Fq2* tables,
                                 const uint32_t* inf, const G2A* h_aff, const Line* h_lines,
-                                int32_t* status) {
+                                int32_t* status, uint32_t rep3_limit) {
   if (chunk == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_sigchk_leaves, dim3(unit_blocks(((uint64_t)chunk + 1) / 2)), dim3(64), 0, s,
-                     base, chunk, leaf_count, leaves, idx, pk, tables, inf, h_aff, h_lines, status);
+  hipLaunchKernelGGL(k_sigchk_leaves<1>, dim3(unit_blocks(((uint64_t)chunk + 1) / 2)), dim3(64), 0, s,
+                     base, chunk, leaf_count, leaves, idx, pk, tables, inf, h_aff, h_lines, status,
+                     rep3_limit);
   return hipGetLastError();
 }
 

@@ -51,6 +51,9 @@ struct TileSums {
   // the two 32-share halves (weights = position inside the half): the level between a failing
   // tile and its sub-tiles in the plain-first schedule (hbtc_check.hip)
   G1J SH[2], SHW[2], PH[2], PHW[2];
+  // the LEFT 16-share quarter of each half (quarters 0 and 2): the split levels check a listed
+  // node's left child and derive the right one (hbtc_check.hip k_chk_split)
+  G1J SQ[2], SQW[2], PQ[2], PQW[2];
 };
 
 // Partial sums of one tile of SignatureShares (hbtc_sig.hip): S = sum r_i sigma_i in G2 and
@@ -65,9 +68,9 @@ struct SigTileSums {
 constexpr uint32_t PLINES_FQ2 = 3 * MILLER_STEPS;
 
 // Fixed-base table of every public-key share (built once per key set, resident in HBM):
-// tab[(i * PK_TAB_WIN + w) * 256 + v] = v * 2^(8w) * pk_i (affine, v >= 1), so [a] pk_i for a
-// 32-bit a is 4 mixed additions and no doublings (windows 0..3), for a 64-bit a (128-bit RLC
-// scalars, hbtc_set_rlc_bits) 8 (windows 0..7).
+// tab[(i * PK_TAB_WIN + w) * 256 + v] = v * 2^(8w) * pk_i for w < 4 and v * 2^(8(w-4)) * [x] pk_i
+// for w >= 4 (affine, v >= 1), so the x-adic RLC scalar's r_i pk_i (rlc_common.h rlc_pk_mul_x)
+// is 4 nbits / 8 mixed additions and no doublings (16 for 128-bit scalars, 8 for 64-bit).
 constexpr int PK_TAB_WIN = 8;
 // windows the scalar halves of an RLC call use
 __host__ __device__ constexpr int rlc_windows(uint32_t bits) { return bits == 128 ? 8 : 4; }
@@ -104,23 +107,52 @@ hipError_t launch_chk_halves(hipStream_t s, uint32_t max_tiles, const uint32_t* 
                              const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
                              const Line* w_lines, const Fq2* Ttile, Fq2* Thalf,
                              uint32_t* fail_count, uint32_t* fail_list);
+// The list a split level appends to (hbtc_check.hip k_chk_split): node codes (tile << 3 | node
+// index at the node's size), the node's GT values T and U (6 Fq2 each per entry) and its weight
+// form ab = log2(alpha) | beta << 8.  list == nullptr: no split listing (the older levels).
+struct SplitOut {
+  uint32_t* count;
+  uint32_t* list;
+  Fq2* T;
+  Fq2* U;
+  uint32_t* ab;
+};
 hipError_t launch_chk_weighted(hipStream_t s, int level, uint32_t max_groups,
                                const uint32_t* fail_count, const uint32_t* fail_list,
                                const uint32_t* sub_list, const uint32_t* list2, const Tile* tiles,
                                const TileSums* sums, const G2A* h_aff, const Line* h_lines,
                                const G2A* w_aff, const Line* w_lines, const int32_t* h_status,
                                const int32_t* w_status, const Fq2* Tbuf, int32_t* status,
-                               uint32_t* out_count, uint32_t* out_list);
+                               uint32_t* out_count, uint32_t* out_list, SplitOut split);
 hipError_t launch_chk_pair(hipStream_t s, int level, bool to_leaves, uint32_t max_groups,
                            uint32_t n_direct, const uint32_t* n_listed, const uint32_t* sub_list,
                            const Tile* tiles, const TileSums* sums, const G2A* h_aff,
                            const Line* h_lines, const G2A* w_aff, const Line* w_lines,
                            const int32_t* h_status, const int32_t* w_status, int32_t* status,
-                           uint32_t* out_count, uint32_t* out_list);
+                           uint32_t* out_count, uint32_t* out_list, SplitOut split);
+// Split level `level` (1..3) over the *n_in listed nodes: checks each node's left child, derives
+// the right one, locates single wrong shares in both, lists unresolved children into `split`
+// (level 3: their pending shares to the leaf list).
+// rep = 3: the latency form (18-lane groups, one unit per wave: gt6.h Pos.rep) for levels too
+// small to fill the chip; rep = 1: the throughput form.
+hipError_t launch_chk_split(hipStream_t s, int level, int rep, uint32_t max_nodes,
+                            const uint32_t* n_in, const uint32_t* in_list, const Fq2* in_T,
+                            const Fq2* in_U, const uint32_t* in_ab, const Tile* tiles,
+                            const TileSums* sums, const G2A* h_aff, const Line* h_lines,
+                            const G2A* w_aff, const Line* w_lines, int32_t* status,
+                            uint32_t* leaf_count, uint32_t* leaves, SplitOut split);
+// Leaf checks: the latency form takes a list of at most rep3_limit leaves, the throughput form
+// a longer one (both launched; the count is on the device).  rep3_limit = 0: throughput only.
+hipError_t launch_chk_leaves_rep3(hipStream_t s, uint32_t max_leaves, uint32_t rep3_limit,
+                                  const uint32_t* leaf_count, const uint32_t* leaves,
+                                  const uint32_t* idx, const G1A* dec, const G1A* pk,
+                                  const G2A* h_aff, const Line* h_lines, const G2A* w_aff,
+                                  const Line* w_lines, int32_t* status);
 hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t* leaf_count,
                              const uint32_t* leaves, const uint32_t* idx, const G1A* dec,
                              const G1A* pk, const G2A* h_aff, const Line* h_lines,
-                             const G2A* w_aff, const Line* w_lines, int32_t* status);
+                             const G2A* w_aff, const Line* w_lines, int32_t* status,
+                             uint32_t rep3_limit = 0);
 
 // ---- RLC batch verification of SignatureShares (hbtc_sig.hip, checks in hbtc_check.hip)
 hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
@@ -148,7 +180,18 @@ hipError_t launch_sigchk_leaves(hipStream_t s, uint32_t base, uint32_t chunk,
                                 const uint32_t* leaf_count, const uint32_t* leaves,
                                 const uint32_t* idx, const G1A* pk, const Fq2* tables,
                                 const uint32_t* inf, const G2A* h_aff, const Line* h_lines,
-                                int32_t* status);
+                                int32_t* status, uint32_t rep3_limit = 0);
+// the latency form (rep 3) of the SignatureShare tile checks and of a short leaf list
+hipError_t launch_sigchk_tiles_rep3(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
+                                    const SigTileSums* sums, const Fq2* tables, const uint32_t* inf,
+                                    const G2A* h_aff, const Line* h_lines, const int32_t* h_status,
+                                    int32_t* status, uint32_t* sub_count, uint32_t* sub_list,
+                                    bool to_leaves);
+hipError_t launch_sigchk_leaves_rep3(hipStream_t s, uint32_t chunk, uint32_t rep3_limit,
+                                     const uint32_t* leaf_count, const uint32_t* leaves,
+                                     const uint32_t* idx, const G1A* pk, const Fq2* tables,
+                                     const uint32_t* inf, const G2A* h_aff, const Line* h_lines,
+                                     int32_t* status);
 
 hipError_t launch_g1_decode(hipStream_t s, const uint8_t* in, uint32_t n, G1A* out,
                             int32_t* status);

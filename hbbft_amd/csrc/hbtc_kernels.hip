@@ -176,9 +176,15 @@ __global__ void __launch_bounds__(64) k_pk_table(const G1A* __restrict__ pk,
   Fq* zs = ws + (size_t)g * 512;  // [0, 256): Z_v, [256, 512): prefix products
   const G1A p = pk[i];
   if (pk_status[i] != HBTC_ACCEPT || p.inf) return;  // never read (items check pk first)
+  // windows 0..3: multiples of pk; 4..7: of [x] pk = -[|x|] pk (the x-adic RLC digits d1, d3)
   G1J b;
-  jac_from_aff(b, p);
-  for (uint32_t j = 0; j < 8 * win; ++j) jac_dbl(b, b);
+  if (win < 4) {
+    jac_from_aff(b, p);
+  } else {
+    jac_mul_u64(b, p, BLS_X_ABS);
+    jac_neg(b, b);
+  }
+  for (uint32_t j = 0; j < 8 * (win & 3u); ++j) jac_dbl(b, b);
   G1A base;
   jac_to_aff(base, b);
   G1J acc;

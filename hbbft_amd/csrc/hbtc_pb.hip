@@ -45,15 +45,17 @@ __global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n
   if (i < n) {
     uint32_t w[24];
     G1A A;
+    G1J t1;  // [|x|] A (the subgroup test's first half): [x] A = -t1 for the x-adic table
     G2A Q, W;
     bool ok = true;
     if (a_c48) {
       rlc_load_words(w, a_c48, i, 12);
-      ok = g1_decompress(A, w);
+      ok = g1_decompress_t1(A, t1, w);
     } else {
       fq_set(A.x, G1_GEN_X);
       fq_set(A.y, G1_GEN_Y);
       A.inf = 0;
+      jac_mul_u64(t1, A, BLS_X_ABS);
     }
     rlc_load_words(w, q_c96, i, 24);
     ok = g2_decompress(Q, w, !q_trusted) && ok;
@@ -62,15 +64,18 @@ __global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n
     G1A ra;
     ra.inf = 1;
     if (ok) {
-      uint64_t a, b;
-      rlc_scalar(key, i, a, b);
-      const int nbits = (int)key.bits / 2;
+      // the x-adic scalar r_i (rlc_common.h rlc_digits), the same for A_i (G1: [x] A = -t1, m =
+      // phi) and W_i (G2: [x] W = psi(W), m = -psi^2): both endomorphism pairs have the
+      // eigenvalues x and mu = -x^2
+      const XDigits xd = rlc_digits(key, i);
       if (!A.inf && !Q.inf) {  // r A, affine (one binary-Euclid inversion)
-        Fq bx, beta;
+        G1A xp, pxp;
+        jac_neg(t1, t1);
+        xadic_table(xp, pxp, A, t1);
+        Fq beta;
         fq_set(beta, G1_BETA);
-        fq_mul(bx, A.x, beta);
         G1J t;
-        glv_mul_uniform(t, A, bx, a, b, nbits);
+        xadic_mul_uniform(t, A, xp, pxp, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
         if (!jac_is_inf(t)) {
           Fq zi, zi2, zi3;
           finv_fast(zi, t.z);
@@ -81,13 +86,16 @@ __global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n
           ra.inf = 0;
         }
       }
-      if (!W.inf) {  // r W = [a] W + [b] (-psi^2 W), -psi^2 (x, y) = (zeta x, y)
-        Fq2 mx;
+      if (!W.inf) {  // r W, m = -psi^2: (x, y) -> (zeta x, y)
+        G2A xp, pxp;
+        g2_psi(xp.x, xp.y, W);
+        xp.inf = 0;
+        G2J xj;
+        jac_from_aff(xj, xp);
+        xadic_table(xp, pxp, W, xj);
         Fq zeta;
         fq_set(zeta, G2_ZETA);
-        fq_mul(mx.c0, W.x.c0, zeta);
-        fq_mul(mx.c1, W.x.c1, zeta);
-        glv_mul_uniform(S, W, mx, a, b, nbits);
+        xadic_mul_uniform(S, W, xp, pxp, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
       }
     }
     rA[i] = ra;

@@ -6,10 +6,10 @@
 // For a group G of shares of ONE ciphertext (u, v, w), H = hash_g1_g2(u, v), and
 // E_i = e(d_i, H) / e(pk_i, w) (E_i == 1 iff share i is valid):
 //     every share valid  =>  e(sum_G r_i d_i, H) * e(-sum_G r_i pk_i, w) == prod E_i^r_i == 1
-// and, for r_i drawn uniformly from a set of 2^64 scalars AFTER the shares are fixed (a ChaCha20
-// stream under a fresh 256-bit host key per call), an invalid share makes the equation fail
-// except with probability <= 2^-64 per check (every point is in the prime-order subgroup: decode
-// checks it, so E_i has order 1 or r).
+// and, for r_i drawn uniformly from a set of 2^k scalars AFTER the shares are fixed (a ChaCha20
+// stream under a fresh 256-bit host key per call; k = 128 by default, 64 optional), an invalid
+// share makes the equation fail except with probability <= 2^-k per check (every point is in the
+// prime-order subgroup: decode checks it, so E_i has order 1 or r).
 //
 // Single-error location.  Next to the plain sum the item pass also forms the position-weighted
 // sum (weights p_i distinct in [0, |G|): p_i = bitrev_k(i) for share i of a group of 2^k, which
@@ -18,19 +18,20 @@
 // If exactly one share b is wrong, T_w == T^(p_b): the search over p = 0..|G|-1 finds it with
 // |G|-1 GT multiplications instead of per-share pairings, and the rest of the group is valid.
 // With two or more wrong shares, T_w == T^p holds for some p only if prod_i E_i^(r_i (p_i - p))
-// == 1 with a nonzero exponent on a wrong share, i.e. with probability <= 2^-64 per p (the same
-// argument as the plain check), <= |G| 2^-64 <= 2^-58 per located group; such groups are split.
+// == 1 with a nonzero exponent on a wrong share, i.e. with probability <= 2^-k per p (the same
+// argument as the plain check), <= |G| 2^-k per located group; such groups are split.
 //
 // This file holds the per-item pass (k_rlc_items: decode, r_i, the tile and sub-tile sums)
 // and the final decision (k_rlc_finalize); the pairing-product checks of those sums run on
 // the cooperative GT arithmetic in hbtc_check.hip:
-//     k_chk_tiles   (plain, weighted) checks of every 64-share tile; a failing tile with one
-//                   wrong share is located right there, the others are listed
-//     k_chk_subs    the 8-share sub-tiles of listed tiles, located likewise
-//     k_chk_leaves  the exact per-share check for sub-tiles with >= 2 wrong shares
-// Work per share in the honest case: decode + r_i d_i (a joint 32-bit double-and-add through
-// the GLV endomorphism) + r_i pk_i (8 mixed additions from the key set's fixed-base table) + a
-// share of the wave's reduction tree; the pairing work is per group.
+//     k_chk_plain / k_chk_pair   plain (and weighted) checks of every 64-share tile; a failing
+//                   tile with one wrong share is located right there, the others are listed
+//     k_chk_split   listed tiles split in halves, quarters, eighths (left child checked, right
+//                   child derived), single wrong shares located at every level
+//     k_chk_leaves  the exact per-share check for eighths with >= 2 wrong shares
+// Work per share in the honest case: decode + r_i d_i (the x-adic joint double-and-add, curve.h
+// xadic_mul_uniform) + r_i pk_i (mixed additions from the key set's fixed-base table) + a share
+// of the wave's reduction tree; the pairing work is per group.
 #include "rlc_common.h"
 
 #ifndef HBTC_PART
@@ -42,11 +43,11 @@ namespace hbtc {
 
 #if HBTC_IN_PART(6)
 // ------------------------------------------------------------------------------ per item
-// One wave per tile: decode every share, draw r_i = a_i + b_i mu (a_i, b_i the two 32-bit
-// halves of a ChaCha20 word, mu the eigenvalue of the GLV endomorphism phi: 2^64 distinct
-// residues mod r), compute r_i d_i = [a] d + [b] phi(d) (joint 32-bit
-// double-and-add) and r_i pk_i from the fixed-base table, then the plain and weighted group
-// sums.  Items that cannot be checked (decode error, unknown sender) get their final status
+// One wave per tile: decode every share (the subgroup test yields [|x|] d on the way), draw the
+// x-adic scalar r_i = d0 + d1 x + d2 mu + d3 mu x (four ChaCha20 digits of key.bits / 4 bits,
+// mu = -x^2 the eigenvalue of phi: 2^key.bits distinct residues mod r, rlc_common.h), compute
+// r_i d_i by one joint double-and-add over the digits' bits (curve.h xadic_mul_uniform) and
+// r_i pk_i from the fixed-base table, then the plain and weighted group sums.  Items that cannot be checked (decode error, unknown sender) get their final status
 // here and contribute the identity; a ciphertext whose own H / w failed to decode is resolved
 // by k_rlc_finalize.  Needs nothing from the per-ciphertext preparation, so it runs
 // concurrently with k_g2_prepare on another stream.
@@ -85,24 +86,24 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
       uint32_t w[12];
       rlc_load_words(w, shares, item, 12);
       G1A d;
-      if (!g1_decompress(d, w)) {
+      G1J t1;  // [|x|] d from the subgroup test: [x] d = -t1, the x-adic table's second entry
+      if (!g1_decompress_t1(d, t1, w)) {
         st = HBTC_DECODE_ERR;
       } else {
         dec[item] = d;  // for the exact leaf checks and the combine (no second decode)
         if (is_suspect(sus, id)) {
           st = HBTC_RLC_LEAF;  // straight to an exact check, outside the group sums
         } else {
-          uint64_t ra, rb;
-          rlc_scalar(key, item, ra, rb);
-          Fq bx;  // phi(d) = (beta x, y)
-          {
+          const XDigits xd = rlc_digits(key, item);
+          if (!d.inf) {
+            G1A xp, pxp;
+            jac_neg(t1, t1);
+            xadic_table(xp, pxp, d, t1);
             Fq beta;
             fq_set(beta, G1_BETA);
-            fq_mul(bx, d.x, beta);
+            xadic_mul_uniform(S, d, xp, pxp, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
           }
-          if (!d.inf) glv_mul_uniform(S, d, bx, ra, rb, (int)key.bits / 2);
-          if (!pk[id].inf)
-            rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb, rlc_windows(key.bits));
+          if (!pk[id].inf) rlc_pk_mul_x(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, xd);
         }
       }
     }
@@ -112,7 +113,7 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
   rlc_list_leaf(sus, leaf, (uint32_t)item, tile.inst, lane);
   TileSums* ts = sums + blockIdx.x;
   rlc_reduce_sp(redA, redB, S, P, lane, ts->S, ts->SW, ts->P, ts->PW, ts->SH, ts->SHW, ts->PH,
-                ts->PHW);
+                ts->PHW, ts->SQ, ts->SQW, ts->PQ, ts->PQW);
 }
 #endif  // part 6
 

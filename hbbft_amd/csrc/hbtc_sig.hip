@@ -61,19 +61,21 @@ __global__ void __launch_bounds__(64, W) k_sig_items(
         if (is_suspect(sus, id)) {
           st = HBTC_RLC_LEAF;  // straight to an exact check, outside the group sums
         } else {
-          uint64_t ra, rb;
-          rlc_scalar(key, item, ra, rb);
-          // -psi^2(sigma) = (zeta x, y): the G2 GLV map keeps y
-          Fq2 mx;
-          {
+          // the x-adic scalar (rlc_common.h rlc_digits): [x] sigma = psi(sigma) on G2 (free), m =
+          // -psi^2 = (zeta x, y) of eigenvalue mu = -x^2
+          const XDigits xd = rlc_digits(key, item);
+          if (!sg.inf) {
+            G2A xp, pxp;
+            g2_psi(xp.x, xp.y, sg);
+            xp.inf = 0;
+            G2J xj;
+            jac_from_aff(xj, xp);
+            xadic_table(xp, pxp, sg, xj);
             Fq zeta;
             fq_set(zeta, G2_ZETA);
-            fq_mul(mx.c0, sg.x.c0, zeta);
-            fq_mul(mx.c1, sg.x.c1, zeta);
+            xadic_mul_uniform(S, sg, xp, pxp, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
           }
-          if (!sg.inf) glv_mul_uniform(S, sg, mx, ra, rb, (int)key.bits / 2);
-          if (!pk[id].inf)
-            rlc_pk_mul(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, ra, rb, rlc_windows(key.bits));
+          if (!pk[id].inf) rlc_pk_mul_x(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, xd);
         }
       }
     }

@@ -206,11 +206,13 @@ __device__ void rlc_reduce1(Jac<F>* red, const Jac<F>& q, uint32_t lane, Jac<F>*
 // P pair (A = left + right, B = right).  From then on LDS entry 2m holds an S group and entry
 // 2m+1 a P group; at level s the lanes with lane mod 2s in {0, 1} merge entry `lane` with entry
 // `lane + s` (A = A_l + A_r, B = 2 (B_l + B_r) + A_r).  Outputs as rlc_reduce: [0..7] the aligned
-// groups of 8, [8] the tile.  Half the sequential merge chain of two separate reductions.
+// groups of 8, [8] the tile; plus the two halves and the left quarter of each half.  Half the
+// sequential merge chain of two separate reductions.
 __device__ __forceinline__ void rlc_reduce_sp(G1J* redA, G1J* redB, const G1J& S, const G1J& P,
                                               uint32_t lane, G1J* outS, G1J* outSW, G1J* outP,
                                               G1J* outPW, G1J* outSH, G1J* outSHW, G1J* outPH,
-                                              G1J* outPHW) {
+                                              G1J* outPHW, G1J* outSQ, G1J* outSQW, G1J* outPQ,
+                                              G1J* outPQW) {
   const bool odd = (lane & 1u) != 0;
   G1J x = odd ? S : P, y;  // the value the neighbour lane needs
   {
@@ -255,6 +257,15 @@ __device__ __forceinline__ void rlc_reduce_sp(G1J* redA, G1J* redB, const G1J& S
         outPW[lane >> 3] = redB[lane];
       }
     }
+    if (s == 8 && (lane & 31u) < 2) {  // the left 16-share quarter of each half
+      if ((lane & 31u) == 0) {
+        outSQ[lane >> 5] = redA[lane];
+        outSQW[lane >> 5] = redB[lane];
+      } else {
+        outPQ[lane >> 5] = redA[lane];
+        outPQW[lane >> 5] = redB[lane];
+      }
+    }
     if (s == 16 && (lane & 31u) < 2) {  // the 32-share halves
       if ((lane & 31u) == 0) {
         outSH[lane >> 5] = redA[lane];
@@ -273,6 +284,60 @@ __device__ __forceinline__ void rlc_reduce_sp(G1J* redA, G1J* redB, const G1J& S
     outPW[8] = redB[1];
   }
   __syncthreads();
+}
+
+// The four x-adic digits of item i's scalar (curve.h xadic_mul_uniform): the halves (a, b) of
+// rlc_scalar split in two, d = (a_lo, a_hi, b_lo, b_hi), each key.bits / 4 bits.  r = d0 + d1 x +
+// d2 mu + d3 mu x (mod r) is injective on the digit box: for digits below 2^33 < |x| the integer
+// d0 + d1 x - d2 x^2 - d3 x^3 has absolute value < r, and it is 0 only for all-zero digits
+// (reduce mod x digit by digit), so the 2^key.bits digit vectors give 2^key.bits residues.
+struct XDigits {
+  uint32_t d[4];
+  int nbits;
+};
+__device__ __forceinline__ XDigits rlc_digits(const RlcKey& key, uint64_t item) {
+  uint64_t a, b;
+  rlc_scalar(key, item, a, b);
+  XDigits x;
+  if (key.bits == 128) {
+    x.d[0] = (uint32_t)a;
+    x.d[1] = (uint32_t)(a >> 32);
+    x.d[2] = (uint32_t)b;
+    x.d[3] = (uint32_t)(b >> 32);
+    x.nbits = 32;
+  } else {
+    x.d[0] = (uint32_t)a & 0xffffu;
+    x.d[1] = (uint32_t)(a >> 16) & 0xffffu;
+    x.d[2] = (uint32_t)b & 0xffffu;
+    x.d[3] = (uint32_t)(b >> 16) & 0xffffu;
+    x.nbits = 16;
+  }
+  return x;
+}
+
+// [r] pk for the x-adic scalar from the key set's fixed-base table (hbtc_kernels.h PK_TAB_WIN:
+// windows 0..3 multiples of pk, 4..7 of [x] pk): [d0] pk + [d1] xpk + [d2] phi(pk) + [d3]
+// phi(xpk), 4 nbits / 8 mixed additions and no doublings.
+static __device__ void rlc_pk_mul_x(G1J& r, const PtXY* __restrict__ tab, const XDigits& x) {
+  jac_set_inf(r);
+  const int nwin = x.nbits / 8;
+#pragma unroll 1
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t dj = x.d[0] * (j == 0) + x.d[1] * (j == 1) + x.d[2] * (j == 2) + x.d[3] * (j == 3);
+    const int tw = (j & 1) ? 4 : 0;  // d1, d3: the [x] pk windows
+#pragma unroll 1
+    for (int w = 0; w < nwin; ++w) {
+      const uint32_t v = (dj >> (8 * w)) & 0xffu;
+      if (!v) continue;
+      const PtXY e = tab[(tw + w) * 256 + v];
+      G1A q;
+      q.x = e.x;
+      q.y = e.y;
+      q.inf = 0;
+      if (j >= 2) g1_phi(q, q);
+      jac_add_aff(r, r, q);
+    }
+  }
 }
 
 // [a] pk + [b] phi(pk) from the key set's fixed-base table (2 nwin mixed additions, no

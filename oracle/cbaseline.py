@@ -8,6 +8,7 @@ the Python restatement for the baseline.
 import ctypes
 import os
 import random
+import time
 
 _PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "libtcoracle.so")
 if not os.path.exists(_PATH):
@@ -215,3 +216,64 @@ def run_skg_ack_baseline(n, t, budget_s, cores=None):
             "sample": "%d G1 scalar multiplications in %.1fs (%.0f /s); one Ack = (t+1)^2 = %d of them "
                       "(commit.evaluate at N = %d, t = %d), decrypt pairings excluded"
                       % (done, wall.value, rate, per_ack, n, t)}
+
+
+def _median(xs):
+    s = sorted(xs)
+    return s[len(s) // 2]
+
+
+def coin_call(sigs96, pks48, master_pk48, nonce, t, pool=None):
+    """One Coin call as hbbft makes it (src/coin.rs:149-207), by the C restatement: every
+    SignatureShare through PublicKeyShare::verify (serde decode with the subgroup check,
+    hash_g2(nonce) inside each call, two full pairings; coin.rs:151), the first t valid ones
+    through combine_signatures (Lagrange in G2, :185-191), the result through PublicKey::verify
+    against the master key (:192-197) and Signature::parity (:173).  pool: a thread pool for the
+    share checks (ctypes drops the GIL inside the C calls), None = one core.
+    Returns (statuses, combined signature, parity)."""
+    n = len(pks48) // 48
+    g1 = bytes.fromhex("97f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac58"
+                       "6c55e83ff97a1aeffb3af00adb22c6bb")
+
+    def check(i):
+        H = hash_g2(nonce)
+        return pairing_eq(pks48[48 * i:48 * i + 48], H, g1, sigs96[96 * i:96 * i + 96])
+
+    ok = list(pool.map(check, range(n))) if pool else [check(i) for i in range(n)]
+    sel = [i for i in range(n) if ok[i]][:t]
+    st, sig = combine(2, sel, [sigs96[96 * i:96 * i + 96] for i in sel], t)
+    if st != 0:
+        return ok, None, None
+    H = hash_g2(nonce)
+    assert pairing_eq(master_pk48, H, g1, sig)
+    return ok, sig, sig_parity(sig)
+
+
+def run_coin_call_baseline(sigs96, pks48, master_pk48, nonce, t, budget_s=10.0):
+    """Single-call latency of coin_call on one core and on every usable core (a thread pool over
+    the share checks), each repeated for about budget_s / 2."""
+    from concurrent.futures import ThreadPoolExecutor
+    cpus = host_cpus()
+    res = {}
+    for cores in (1, cpus["usable"]):
+        pool = ThreadPoolExecutor(cores) if cores > 1 else None
+        lat = []
+        t_end = time.perf_counter() + budget_s / 2
+        while True:
+            a = time.perf_counter()
+            ok, sig, par = coin_call(sigs96, pks48, master_pk48, nonce, t, pool)
+            lat.append(time.perf_counter() - a)
+            if time.perf_counter() > t_end and len(lat) >= 3:
+                break
+        if pool:
+            pool.shutdown()
+        res[cores] = (lat, ok, sig, par)
+    one, many = res[1], res[cpus["usable"]]
+    return {"value": round(1e3 * _median(one[0]), 3), "unit": "ms per coin call (median, 1 core)",
+            "value_all_cores_ms": round(1e3 * _median(many[0]), 3), "cores": 1,
+            "cores_all": cpus["usable"], "host_cpus": cpus, "kind": "port",
+            "calls": [len(one[0]), len(many[0])], "results": (one[1], one[2], one[3]),
+            "impl": "C restatement of threshold_crypto 0.1 / pairing 0.14 (oracle/c/tc_oracle.c) driven "
+                    "per call; the share checks over a thread pool for the all-cores figure",
+            "sample": "repeated whole coin calls (%d shares: decode + hash_g2 + 2 pairings each; combine of "
+                      "t = %d; master PublicKey::verify; parity)" % (len(pks48) // 48, t)}

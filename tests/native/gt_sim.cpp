@@ -176,6 +176,38 @@ int ht_gt_op(int op, const uint8_t* a576, const uint8_t* b576, uint8_t* out576) 
   return 0;
 }
 
+// The same operations in the replicated layout (gt6.h Pos.rep = 3: 18 lanes, coefficient k on
+// lanes 3k..3k+2, every Fq2 product split over them).  Returns 0 if all three sub-lanes of every
+// coefficient agree (out576 = sub-lane 0's values), 1 otherwise.
+int ht_gt_op_rep(int op, uint32_t rep, const uint8_t* a576, const uint8_t* b576, uint8_t* out576) {
+  Fq12 A, B, R;
+  fq12_load(A, a576);
+  fq12_load(B, b576);
+  std::vector<Fq2> res(6 * rep);
+  run_lanes(6 * rep, [&](uint32_t l) {
+    const gt::Pos ps = gt::pos(rep);
+    Fq2 a = *tower_slot(A, flat_to_tower(ps.k)), b = *tower_slot(B, flat_to_tower(ps.k)), r;
+    switch (op) {
+      case 0: gt::mul(r, a, b, ps); break;
+      case 1: gt::sqr(r, a, ps); break;
+      case 2: r = a; gt::cyc_sqr(r, ps); break;
+      case 3: case 4: case 5: r = a; gt::frob(r, op - 2, ps); break;
+      case 6: r = a; gt::conj(r, ps); break;
+      case 7: gt::final_exp(r, a, ps); break;
+      case 8: gt::easy_part(r, a, ps); break;
+      default: gt::exp_by_x(r, a, ps); break;
+    }
+    res[l] = r;  // distinct slots per lane
+  });
+  int bad = 0;
+  for (uint32_t k = 0; k < 6; ++k) {
+    *tower_slot(R, flat_to_tower(k)) = res[rep * k];
+    for (uint32_t j = 1; j < rep; ++j) bad |= !fq2_eq(res[rep * k], res[rep * k + j]);
+  }
+  fq12_store(out576, R);
+  return bad;
+}
+
 // Binary-GCD Fq inversion (gt6.h) on n values, one simulated lane each: Montgomery in / out,
 // values as 48-byte big-endian canonical integers (converted to / from Montgomery here).
 int ht_fq_inv_binary(uint32_t n, const uint8_t* in48, uint8_t* out48) {
@@ -216,8 +248,17 @@ int ht_tower_op(int op, const uint8_t* a576, const uint8_t* b576, uint8_t* out57
 // z = 1 keeps the serial loop's exact Miller value).  Outputs group 0's Miller value and final
 // value (tower layout).  Returns bit 0: group values equal, bit 1: group 0 result is one,
 // bit 2: group 1 result is one; -1 on a decode error.
+int ht_gt_check_rep(uint32_t rep, const uint8_t* p1, const uint8_t* q1, const uint8_t* p2,
+                    const uint8_t* q2, const uint8_t* z1, const uint8_t* z2, uint8_t* out_f576,
+                    uint8_t* out_e576);
 int ht_gt_check(const uint8_t* p1, const uint8_t* q1, const uint8_t* p2, const uint8_t* q2,
                 const uint8_t* z1, const uint8_t* z2, uint8_t* out_f576, uint8_t* out_e576) {
+  return ht_gt_check_rep(1, p1, q1, p2, q2, z1, z2, out_f576, out_e576);
+}
+// ... on 12 rep simulated lanes (rep = 3: the replicated latency form, two groups of 18)
+int ht_gt_check_rep(uint32_t rep, const uint8_t* p1, const uint8_t* q1, const uint8_t* p2,
+                    const uint8_t* q2, const uint8_t* z1, const uint8_t* z2, uint8_t* out_f576,
+                    uint8_t* out_e576) {
   G1A P1, P2;
   G2A Q1, Q2;
   if (!decode_g1(P1, p1) || !decode_g1(P2, p2) || !decode_g2(Q1, q1) || !decode_g2(Q2, q2))
@@ -244,11 +285,12 @@ int ht_gt_check(const uint8_t* p1, const uint8_t* q1, const uint8_t* p2, const u
   Fq12 F, E, E1;
   bool one0 = false, one1 = false, same = true;
   std::mutex mu;
-  run_lanes(12, [&](uint32_t l) {
-    const gt::Pos ps = gt::pos();
+  const uint32_t gs = 6 * rep;
+  run_lanes(2 * gs, [&](uint32_t l) {
+    const gt::Pos ps = gt::pos(rep);
     gt::MillerArg a{l1, nullptr, J1, use1}, b{l2, nullptr, J2, use2};
     Fq2 f, e;
-    if (l < 6)
+    if (l < gs)
       gt::miller2(f, a, b, ps);
     else
       gt::miller2(f, b, a, ps);
@@ -256,10 +298,14 @@ int ht_gt_check(const uint8_t* p1, const uint8_t* q1, const uint8_t* p2, const u
     const bool one = gt::is_one(e, ps);
     // compare the two groups' final values coefficient by coefficient
     Fq2 other;
-    gt::fetch2(other, e, l < 6 ? l + 6 : l - 6);
+    gt::fetch2(other, e, l < gs ? l + gs : l - gs);
     const bool eq = gt::group_all(fq2_eq(e, other), ps);
     std::lock_guard<std::mutex> lk(mu);
-    if (l < 6) {
+    if (ps.sub != 0) {
+      same &= eq;
+      return;
+    }
+    if (l < gs) {
       *tower_slot(F, flat_to_tower(ps.k)) = f;
       *tower_slot(E, flat_to_tower(ps.k)) = e;
       one0 = one;

@@ -3,7 +3,7 @@ for a batch, as hbtc_verify_ciphertexts (Ciphertext::verify: e(G1, w) == e(u, H)
 (PublicKey::verify: e(pk, H) == e(G1, sigma)) and hbtc_decrypt use it.  The RLC decisions must
 equal the per-share path's (one exact pairing check per item, k_pair_verify) on valid items,
 wrong ones, bad encodings and points at infinity, inside one 64-item tile, across tiles and
-across the 65,536-item chunk boundary."""
+across chunk boundaries (a context with 4096-item chunks)."""
 import json
 import os
 import random
@@ -72,17 +72,46 @@ def _ct_batch(ctx, rng, n, n_distinct=96):
 
 @pytest.mark.parametrize("n", [1, 40, 64, 200, 65536 + 130])
 def test_verify_ciphertexts_rlc_equals_per_share(ctx, n):
+    """Ciphertext::verify by pair-batch RLC equals the per-item check (one chunk: the default
+    chunk is 2^18 items)."""
+    _ct_rlc_equals_per_share(ctx, n)
+
+
+def test_verify_ciphertexts_across_chunks():
+    """The multi-chunk path of pb_verify_dev: a context with 4096-item chunks
+    (HBTC_PB_CHUNK) verifies 3 x 4096 + 130 ciphertexts in four chunks — base offsets into the
+    item and status arrays, a fresh key per chunk, workspace reused across chunks, each chunk's
+    exact-check list — with the same decisions as the per-item path, at 64- and 128-bit scalars;
+    then hbtc_trim_workspace frees the cache and the context still works."""
+    os.environ["HBTC_PB_CHUNK"] = "4096"
+    try:
+        c = N.Context(0)
+    finally:
+        del os.environ["HBTC_PB_CHUNK"]
+    try:
+        _ct_rlc_equals_per_share(c, 3 * 4096 + 130, extra_bad=(4095, 4096, 8191, 12287, 12290))
+        c.trim_workspace()
+        _ct_rlc_equals_per_share(c, 200)
+    finally:
+        c.close()
+
+
+def _ct_rlc_equals_per_share(ctx, n, extra_bad=()):
     rng = random.Random(n + 5)
     us, Hs, ws = _ct_batch(ctx, rng, n)
+    for i in extra_bad:  # wrong w at chunk edges
+        us[i], ws[i] = us[i], ws[(i + 1) % n]
     ctx.set_verify_mode(N.MODE_PER_SHARE)
     ref = ctx.verify_ciphertexts(us, Hs, ws)
+    for i in extra_bad:
+        assert ref[i] == N.REJECT, i
     ctx.set_verify_mode(N.MODE_RLC)
     for bits in (64, 128):
         ctx.set_rlc_bits(bits)
         try:
             st = ctx.verify_ciphertexts(us, Hs, ws)
         finally:
-            ctx.set_rlc_bits(64)
+            ctx.set_rlc_bits(128)  # the library default
         assert (st == ref).all(), (bits, np.nonzero(st != ref)[0][:20])
     if n > 20:
         assert ref[10] == N.REJECT and ref[11] == N.REJECT

@@ -139,3 +139,40 @@ def test_gt_check_projective_second_pair(ht):
         sf, se = ctypes.create_string_buffer(576), ctypes.create_string_buffer(576)
         rs = ht.ht_serial_check(pk, H, g1, s2, sf, se)
         assert rc == want and rs == want and e.raw == se.raw
+
+
+def test_gt_ops_replicated_layout_match_tower(ht):
+    """The latency form of the cooperative arithmetic (gt6.h Pos.rep = 3: 18 lanes per value,
+    every Fq2 product split over a coefficient's three sub-lanes) gives the tower results, and
+    every sub-lane ends with the same value."""
+    rng = random.Random(33)
+    ht.ht_gt_op_rep.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p,
+                                ctypes.c_char_p]
+    a, b = rand12(rng), rand12(rng)
+    c = cyclotomic(ht, rng)
+    for code, x in ((0, a), (1, a), (3, a), (4, a), (5, a), (6, a), (8, a), (2, c), (9, c), (7, a)):
+        got = ctypes.create_string_buffer(576)
+        assert ht.ht_gt_op_rep(code, 3, x, b, got) == 0, code
+        assert got.raw == op(ht, "ht_tower_op", code, x, b), code
+
+
+def test_gt_check_replicated_layout(ht):
+    """A whole pairing-product check on two 18-lane groups equals the 6-lane one (Miller value,
+    final value, verdict) on a valid pair, a wrong pair and a Jacobian-scaled point."""
+    rng = random.Random(34)
+    ht.ht_gt_check_rep.argtypes = [ctypes.c_uint32] + [ctypes.c_char_p] * 8
+    for valid in (True, False):
+        k = rng.randrange(1, B.R)
+        h = rng.randrange(1, B.R)
+        P1 = B.g1_mul(B.G1_GEN, k)
+        Q1 = B.g2_mul(B.G2_GEN, h)
+        P2 = B.g1_mul(B.G1_GEN, k * h % B.R if valid else (k * h + 1) % B.R)
+        Q2 = B.G2_GEN
+        z1 = rng.randrange(1, B.P).to_bytes(48, "big")
+        z2 = (1).to_bytes(48, "big")
+        args = [B.g1_compress(P1), B.g2_compress(Q1), B.g1_compress(P2), B.g2_compress(Q2), z1, z2]
+        f1, e1, f3, e3 = (ctypes.create_string_buffer(576) for _ in range(4))
+        r1 = ht.ht_gt_check(*args, f1, e1)
+        r3 = ht.ht_gt_check_rep(3, *args, f3, e3)
+        assert r1 == r3 and f1.raw == f3.raw and e1.raw == e3.raw
+        assert (r3 & 2 != 0) == valid and (r3 & 1) == 1

@@ -78,6 +78,46 @@ def test_glv_split_scalar_of_rlc_items(ht):
         assert o.raw == B.g1_compress(B.g1_mul(P, (a + b * mu) % B.R)), (a, b)
 
 
+@pytest.mark.parametrize("nbits", [16, 32])
+def test_xadic_scalar_of_rlc_items(ht, nbits):
+    """The x-adic RLC scalar (curve.h xadic_mul_uniform, rlc_common.h rlc_digits): the item passes
+    compute [d0] P + [d1] [x]P + [d2] m(P) + [d3] m([x]P) with m the endomorphism of eigenvalue
+    mu = -x^2 (G1: phi, G2: -psi^2) and [x]P = -[|x|]P from the G1 subgroup test / psi(P) on G2;
+    it must equal [d0 + d1 x + d2 mu + d3 mu x] P, for 16- and 32-bit digits (64- / 128-bit RLC)."""
+    rng = random.Random(nbits)
+    mu = (-(B.X * B.X)) % B.R
+    top = (1 << nbits) - 1
+    cases = [(0, 0, 0, 0), (1, 0, 0, 0), (0, 1, 0, 0), (0, 0, 1, 0), (0, 0, 0, 1), (top,) * 4,
+             (1, top, 0, top)]
+    cases += [tuple(rng.getrandbits(nbits) for _ in range(4)) for _ in range(4)]
+    ht.ht_g1_mul_xadic.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
+    ht.ht_g2_mul_xadic.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
+    for d in cases:
+        r = (d[0] + d[1] * B.X + d[2] * mu + d[3] * mu * B.X) % B.R
+        arr = (ctypes.c_uint32 * 4)(*d)
+        P = B.g1_mul(B.G1_GEN, rng.randrange(1, B.R))
+        o = buf(48)
+        assert ht.ht_g1_mul_xadic(B.g1_compress(P), ctypes.cast(arr, ctypes.c_void_p), nbits, o) == 0
+        assert o.raw == B.g1_compress(B.g1_mul(P, r)), ("g1", d)
+        Q = B.g2_mul(B.G2_GEN, rng.randrange(1, B.R))
+        o2 = buf(96)
+        assert ht.ht_g2_mul_xadic(B.g2_compress(Q), ctypes.cast(arr, ctypes.c_void_p), nbits, o2) == 0
+        assert o2.raw == B.g2_compress(B.g2_mul(Q, r)), ("g2", d)
+
+
+def test_xadic_digit_box_is_injective():
+    """2^(4 nbits) distinct digit vectors give distinct residues: d0 + d1 x - d2 x^2 - d3 x^3 with
+    |d_j| < 2^33 < |x| is below r in absolute value and zero only for zero digits (digit by digit
+    mod x); checked here on the extreme differences."""
+    X = B.X
+    assert abs(X) > 1 << 33
+    worst = (1 << 33) * (1 + abs(X) + X * X + abs(X) ** 3)
+    assert worst < B.R
+    for d in [(1, 0, 0, 0), (0, 1, 0, 0), (-(1 << 32), 1 << 32, -(1 << 32), 1 << 32)]:
+        v = d[0] + d[1] * X - d[2] * X * X - d[3] * X ** 3
+        assert v != 0 and v % B.R != 0
+
+
 def test_miller_loop_value_matches_oracle(ht):
     o = buf(576)
     assert ht.ht_miller(B.g1_compress(B.G1_GEN), B.g2_compress(B.G2_GEN), o) == 0

@@ -113,74 +113,74 @@ int main() {
   jac_add(acc2, qj, m2);
   const unsigned long long comb2 = hbtc_fqm_count;
 
-  // RLC item: decode + r*d = [a] d + [b] phi(d) (joint 32-bit double-and-add, a and b with
-  // 16 of 32 bits set, the mean) + r*pk (8 mixed additions from the fixed-base table + 4 phi)
-  // + the item's share of the plain + position-weighted reduction tree of its tile: per side
-  // 3 * 63 Jacobian additions and 57 doublings (merges of halves of size s cost 3 adds and
-  // log2(s) doublings), two sides, over 64 items
-  hbtc_fqm_count = 0;
-  G1A d2;
-  g1_decompress(d2, w1);
-  const uint32_t ra = 0xa5a55a5au, rb = 0x5a5aa5a5u;  // popcount 16 each
-  G1J rd;
-  G1A pd;
-  g1_phi(pd, d2);
-  jac_mul2_u32(rd, d2, ra, pd, rb);
-  G1J rp = rd;  // a generic accumulator for the 4 + 4 table additions
-  for (int w = 0; w < 4; ++w) {
+  // RLC item (k_rlc_items): decode (the subgroup test yields [|x|] d), the x-adic table {d, [x] d,
+  // d + [x] d} (one batched inversion), r*d by xadic_mul_uniform over nbits = 16 (64-bit RLC) or
+  // 32 (128-bit) digit bits, r*pk from the fixed-base table (4 nbits / 8 mixed additions, half
+  // of them with phi), and the item's share of the plain + position-weighted reduction tree of
+  // its tile: per side 3 * 63 Jacobian additions and 57 doublings, two sides, over 64 items
+  const uint32_t dg[4] = {0xa5a55a5au, 0x5a5aa5a5u, 0x3c3cc3c3u, 0xc3c33c3cu};
+  G1J rd;  // a generic accumulator, for the tree costs below
+  unsigned long long rlc_item = 0, rlc_item_128 = 0, jadd = 0, jdbl = 0;
+  {
+    G1J pj2;
+    jac_dbl(pj2, pj);
+    hbtc_fqm_count = 0;
+    G1J ts;
+    jac_add(ts, pj, pj2);
+    jadd = hbtc_fqm_count;
+    hbtc_fqm_count = 0;
+    jac_dbl(ts, ts);
+    jdbl = hbtc_fqm_count;
+  }
+  const unsigned long long tree1 = (2 * (189 * jadd + 57 * jdbl) + 63) / 64;
+  for (int nb : {16, 32}) {
+    hbtc_fqm_count = 0;
+    G1A d2;
+    G1J t1;
+    g1_decompress_t1(d2, t1, w1);
+    jac_neg(t1, t1);
+    G1A xp, pxp;
+    xadic_table(xp, pxp, d2, t1);
+    Fq beta;
+    fq_set(beta, G1_BETA);
+    const uint32_t m = nb == 32 ? 0xffffffffu : 0xffffu;
+    xadic_mul_uniform(rd, d2, xp, pxp, beta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
+    G1J rp;
+    jac_set_inf(rp);
     jac_add_aff(rp, rp, gen1);
-    G1A pq;
-    g1_phi(pq, gen1);
-    jac_add_aff(rp, rp, pq);
+    for (int a = 1; a < nb / 2; ++a) {  // 4 nb / 8 table additions, half with phi
+      G1A q = gen1;
+      if (a & 1) g1_phi(q, gen1);
+      jac_add_aff(rp, rp, q);
+    }
+    (nb == 16 ? rlc_item : rlc_item_128) = hbtc_fqm_count + tree1;
   }
-  const unsigned long long rlc_item_mults = hbtc_fqm_count;
-  hbtc_fqm_count = 0;
-  G1J ts;
-  jac_add(ts, rd, rp);
-  const unsigned long long jadd = hbtc_fqm_count;
-  hbtc_fqm_count = 0;
-  jac_dbl(ts, ts);
-  const unsigned long long jdbl = hbtc_fqm_count;
-  const unsigned long long rlc_item = rlc_item_mults + (2 * (189 * jadd + 57 * jdbl) + 63) / 64;
-  // 128-bit RLC scalars (hbtc_set_rlc_bits): 64-bit halves, so 32 more doublings and 32 more
-  // mixed additions in the joint double-and-add (half the bits set) and 8 more table additions
-  // (4 with phi)
-  unsigned long long rlc_item_128 = 0;
-  {
-    hbtc_fqm_count = 0;
-    G1J tm = rd;
-    jac_add_aff(tm, tm, gen1);
-    const unsigned long long madd1 = hbtc_fqm_count;
-    hbtc_fqm_count = 0;
-    G1A pq;
-    g1_phi(pq, gen1);
-    const unsigned long long phi1 = hbtc_fqm_count;
-    rlc_item_128 = rlc_item + 32 * jdbl + 32 * madd1 + 8 * madd1 + 4 * phi1;
-  }
-  // SignatureShare RLC item (k_sig_items): G2 decode + subgroup test, -psi^2(sigma) = (zeta x, y)
-  // (2 Fqm), r * sigma = [a] sigma + [b] (-psi^2 sigma) (joint 32-bit double-and-add in G2, 16 of
-  // 32 bits set per half), r * pk from the fixed-base table (8 G1 mixed additions + 4 phi), and
-  // the item's share of the G2 and G1 plain + position-weighted tile trees
-  unsigned long long sig_rlc_item = 0;
-  {
+  // SignatureShare RLC item (k_sig_items): G2 decode + subgroup test, the x-adic G2 table {s,
+  // psi(s), s + psi(s)}, r*sigma by xadic_mul_uniform in G2 (m = -psi^2 = (zeta x, y)), r*pk
+  // from the fixed-base table, and the item's share of the G2 and G1 plain + weighted tile trees
+  unsigned long long sig_rlc_item = 0, sig_rlc_item_128 = 0;
+  for (int nb : {16, 32}) {
     hbtc_fqm_count = 0;
     G2A s2;
     g2_decompress(s2, w2);
-    G2A m2 = s2;
-    {
-      Fq zeta;
-      fq_set(zeta, G2_ZETA);
-      fq_mul(m2.x.c0, s2.x.c0, zeta);
-      fq_mul(m2.x.c1, s2.x.c1, zeta);
-    }
+    G2A xp, pxp;
+    g2_psi(xp.x, xp.y, s2);
+    xp.inf = 0;
+    G2J xj;
+    jac_from_aff(xj, xp);
+    xadic_table(xp, pxp, s2, xj);
+    Fq zeta;
+    fq_set(zeta, G2_ZETA);
+    const uint32_t m = nb == 32 ? 0xffffffffu : 0xffffu;
     G2J r2;
-    jac_mul2_u32(r2, s2, ra, m2, rb);
-    G1J rp1 = rd;
-    for (int w = 0; w < 4; ++w) {
-      jac_add_aff(rp1, rp1, gen1);
-      G1A pq;
-      g1_phi(pq, gen1);
-      jac_add_aff(rp1, rp1, pq);
+    xadic_mul_uniform(r2, s2, xp, pxp, zeta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
+    G1J rp;
+    jac_set_inf(rp);
+    jac_add_aff(rp, rp, gen1);
+    for (int a = 1; a < nb / 2; ++a) {
+      G1A q = gen1;
+      if (a & 1) g1_phi(q, gen1);
+      jac_add_aff(rp, rp, q);
     }
     const unsigned long long mults = hbtc_fqm_count;
     hbtc_fqm_count = 0;
@@ -190,8 +190,10 @@ int main() {
     hbtc_fqm_count = 0;
     jac_dbl(t2, t2);
     const unsigned long long jdbl2 = hbtc_fqm_count;
-    sig_rlc_item = mults + (2 * (189 * jadd2 + 57 * jdbl2) / 2 + 2 * (189 * jadd + 57 * jdbl) / 2 + 63) / 64;
+    (nb == 16 ? sig_rlc_item : sig_rlc_item_128) =
+        mults + (2 * (189 * jadd2 + 57 * jdbl2) / 2 + 2 * (189 * jadd + 57 * jdbl) / 2 + 63) / 64;
   }
+  G1J rp = rd;
   // group check: two normalisations + 2-pair Miller loop + final exponentiation
   hbtc_fqm_count = 0;
   G1A sa, pa;
@@ -259,6 +261,7 @@ int main() {
   printf("  \"g1_combine_item\": %llu,\n  \"g2_combine_item\": %llu,\n", comb1, comb2);
   printf("  \"g1_msm_combine\": %llu,\n", msm_combine);
   printf("  \"rlc_item\": %llu,\n  \"rlc_item_128\": %llu,\n  \"sig_rlc_item\": %llu,\n"
-         "  \"rlc_group_check\": %llu\n}\n", rlc_item, rlc_item_128, sig_rlc_item, rlc_group);
+         "  \"sig_rlc_item_128\": %llu,\n  \"rlc_group_check\": %llu\n}\n", rlc_item, rlc_item_128,
+         sig_rlc_item, sig_rlc_item_128, rlc_group);
   return 0;
 }
