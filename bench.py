@@ -399,7 +399,8 @@ N_OUT = 6  # output sets rotated per step (Epoch.step): four epochs in flight + 
 DIAG_SKIP = set(filter(None, os.environ.get("HBTC_BENCH_SKIP", "").split(",")))
 
 FAMS = ["dec_verify", "rlc_items", "chk_tiles", "chk_tiles_w", "chk_halves", "chk_halves_w", "chk_subs", "chk_subs_w",
-        "chk_leaves", "rlc_finalize", "lagrange", "comb_decode", "comb_digits", "combine", "prepare"]
+        "chk_split1", "chk_split2", "chk_split3", "chk_leaves", "rlc_finalize", "lagrange", "comb_decode",
+        "comb_digits", "combine", "prepare"]
 
 
 def timed(ctx, ep, steps, warmup, dist=None, gather=None, sync_all=None):

@@ -13,6 +13,7 @@
 //!   SyncKeyGen::handle_part / handle_ack                  skg_check_parts / skg_check_acks / decrypt
 #![allow(clippy::too_many_arguments)]
 pub mod ffi;
+#[cfg(feature = "experimental-queues")]
 pub mod queues;
 
 use std::ffi::CStr;
