@@ -311,6 +311,69 @@ HD void fq_mul_ol(Fq& r, const Fq& a, const Fq& b) {
 #endif
 }
 
+// ---------------------------------------------------------------- lazy (double-width) reduction
+// A sum of products of reduced operands (< 2p each) kept unreduced in 25 words and reduced ONCE:
+// fq_acc_mac is the product half of a Montgomery multiplication (144 v_mad_u64_u32), fq_acc_redc
+// the reduction half plus conditional subtractions of 4p and 2p (result < 2p).  At most 12
+// products per accumulator (< 48 p^2, so the Montgomery quotient is < 5.6p).  Device
+// builds with the shared-subroutine product run both as subroutines on fixed registers (the
+// accumulator pinned to v60..v84 across calls: tools/gen_fips_asm.py); elsewhere plain C++ with
+// the same arithmetic (same Montgomery quotient, same subtractions: the same representative).
+struct FqAcc {
+  uint32_t v[25];
+};
+HD void fq_acc_zero(FqAcc& a) {
+#pragma unroll
+  for (int i = 0; i < 25; ++i) a.v[i] = 0;
+}
+#if defined(__HIP_DEVICE_COMPILE__) && defined(HBTC_FQMUL_SR)
+HD void fq_acc_mac(FqAcc& acc, const Fq& a, const Fq& b) { fips::fq_mac_sr(acc.v, a.v, b.v); }
+HD void fq_acc_redc(Fq& r, const FqAcc& acc) { fips::fq_redc_sr(r.v, acc.v); }
+#else
+HD void fq_acc_mac(FqAcc& acc, const Fq& a, const Fq& b) {
+  uint32_t p[24];
+#pragma unroll
+  for (int i = 0; i < 24; ++i) p[i] = 0;
+  for (int i = 0; i < 12; ++i) {
+    uint32_t c = 0;
+    for (int j = 0; j < 12; ++j) {
+      const uint64_t t = (uint64_t)a.v[i] * b.v[j] + p[i + j] + c;
+      p[i + j] = (uint32_t)t;
+      c = (uint32_t)(t >> 32);
+    }
+    p[i + 12] = c;
+  }
+  uint32_t c = 0;
+  for (int i = 0; i < 24; ++i) acc.v[i] = addc32(acc.v[i], p[i], c, &c);
+  acc.v[24] += c;
+}
+HD void fq_acc_redc(Fq& r, const FqAcc& acc) {
+  uint32_t t[26];
+  for (int i = 0; i < 25; ++i) t[i] = acc.v[i];
+  t[25] = 0;
+  for (int i = 0; i < 12; ++i) {
+    const uint32_t q = t[i] * FQ_NP;
+    uint32_t c = 0;
+    for (int j = 0; j < 12; ++j) {
+      const uint64_t s = (uint64_t)q * FQ_P[j] + t[i + j] + c;
+      t[i + j] = (uint32_t)s;
+      c = (uint32_t)(s >> 32);
+    }
+    for (int j = i + 12; j < 26; ++j) t[j] = addc32(t[j], 0, c, &c);
+  }
+  uint32_t x[12];
+  for (int i = 0; i < 12; ++i) x[i] = t[12 + i];  // < 5.6p: words 24, 25 are 0
+  for (int sh = 2; sh >= 1; --sh) {  // subtract 4p, then 2p, where they fit
+    uint32_t m[12], d[12], b = 0;
+    for (int i = 0; i < 12; ++i) m[i] = (FQ_P[i] << sh) | (i > 0 ? FQ_P[i - 1] >> (32 - sh) : 0u);
+    for (int i = 0; i < 12; ++i) d[i] = subb32(x[i], m[i], b, &b);
+    if (!b)
+      for (int i = 0; i < 12; ++i) x[i] = d[i];
+  }
+  for (int i = 0; i < 12; ++i) r.v[i] = x[i];
+}
+#endif
+
 // canonical value in [0, p)
 HD void fq_canon(Fq& r, const Fq& a) {
   Fq t;

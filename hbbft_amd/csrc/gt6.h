@@ -205,8 +205,67 @@ HD void mul2_fq(Fq2& r, const Fq2& a, const Fq& y, const Pos& ps) {
 #define GTN static inline
 #endif
 
+// ------------------------------------------------------------ lazy reduction (rep = 1 layout)
+// Every output coefficient of mul / sqr / the line product is a sum of 3-6 Fq2 products.  With
+// the double-width accumulator (field.h FqAcc) the products stay unreduced and each Fq half of
+// the coefficient is reduced ONCE: Fq2 schoolbook with xi and the sign folded into the operands,
+//     half 0: sum x0 y0 + x1 (-y1),   half 1: sum x0 y1 + x1 y0,
+// -y1 as the reduced negation (< 2p), so every term is a product of two values < 2p and a half
+// sums at most 12 of them (< 48 p^2).  Per lane of a mul: 24 half products (144 MADs each) + 2
+// reductions, instead of 18 full Montgomery products (288 each).  Two passes (half 0, then half
+// 1) over one accumulator: it is pinned to 25 VGPRs, a second one would cost 25 more.
+#ifndef HBTC_GT_LAZY
+#if !defined(__HIP_DEVICE_COMPILE__) || defined(HBTC_FQMUL_SR)
+#define HBTC_GT_LAZY 1
+#else
+#define HBTC_GT_LAZY 0
+#endif
+#endif
+
+#if HBTC_GT_LAZY
+// acc += half h of x * y
+HD void mac2_half(FqAcc& acc, const Fq2& x, const Fq2& y, uint32_t h) {
+  if (h == 0) {
+    Fq ny1;
+    fq_neg(ny1, y.c1);
+    fq_acc_mac(acc, x.c0, y.c0);
+    fq_acc_mac(acc, x.c1, ny1);
+  } else {
+    fq_acc_mac(acc, x.c0, y.c1);
+    fq_acc_mac(acc, x.c1, y.c0);
+  }
+}
+
+GTN void mul_lazy(Fq2& f, const Fq2& a, const Fq2& b, const Pos& ps) {
+  Fq2 r;
+#pragma unroll
+  for (uint32_t h = 0; h < 2; ++h) {
+    FqAcc acc;
+    fq_acc_zero(acc);
+#pragma unroll 1
+    for (uint32_t i = 0; i < 6; ++i) {
+      const bool wrap = i > ps.k;
+      const uint32_t j = wrap ? ps.k + 6 - i : ps.k - i;
+      Fq2 ai, bj;
+      fetch2(ai, a, src(ps, i));
+      fetch2(bj, b, src(ps, j));
+      fq2_xi_if(bj, wrap, bj);
+      mac2_half(acc, ai, bj, h);
+    }
+    fq_acc_redc(h ? r.c1 : r.c0, acc);
+  }
+  f = r;
+}
+#endif
+
 // f = a * b
 GTN void mul(Fq2& f, const Fq2& a, const Fq2& b, const Pos& ps) {
+#if HBTC_GT_LAZY
+  if (ps.rep == 1) {
+    mul_lazy(f, a, b, ps);
+    return;
+  }
+#endif
   Fq2 acc;
   fq2_zero(acc);
 #pragma unroll 1
@@ -253,6 +312,34 @@ HD uint32_t sqr_terms(uint32_t k) {
 
 HD void sqr(Fq2& f, const Fq2& a, const Pos& ps) {
   const uint32_t terms = sqr_terms(ps.k);
+#if HBTC_GT_LAZY
+  if (ps.rep == 1) {
+    // the doubling and xi go on the second operand (reduced: < 2p), a missing term multiplies 0
+    Fq2 r;
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+      FqAcc lacc;
+      fq_acc_zero(lacc);
+#pragma unroll 1
+      for (uint32_t t = 0; t < 4; ++t) {
+        const uint32_t e = (terms >> (8 * t)) & 0xffu;
+        const bool none = e == 0xffu;
+        Fq2 ai, aj, d, z;
+        fetch2(ai, a, src(ps, e & 7u));
+        fetch2(aj, a, src(ps, (e >> 3) & 7u));
+        fq2_xi_if(aj, ((e >> 6) & 1u) && !none, aj);
+        fq2_dbl(d, aj);
+        fq2_sel(aj, ((e >> 7) & 1u) && !none, d, aj);
+        fq2_zero(z);
+        fq2_sel(aj, none, z, aj);
+        mac2_half(lacc, ai, aj, h);
+      }
+      fq_acc_redc(h ? r.c1 : r.c0, lacc);
+    }
+    f = r;
+    return;
+  }
+#endif
   Fq2 acc;
   fq2_zero(acc);
 #pragma unroll 1
@@ -284,6 +371,42 @@ template <bool A_DIRECT, bool Y2>
 HD void mul_line_t(Fq2& f, const Fq& pa, uint32_t a, const Fq2& Ad, const Fq& pb, uint32_t b,
                    const Fq& py, uint32_t y, bool use, const Pos& ps) {
   const uint32_t k = ps.k;
+#if HBTC_GT_LAZY
+  if (ps.rep == 1) {
+    // xi on the f coefficient (the operand every term has), so an Fq Y stays one product a half
+    Fq2 r;
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {
+      FqAcc lacc;
+      fq_acc_zero(lacc);
+HBTC_GT_SMALL_LOOP
+      for (uint32_t t = 0; t < 3; ++t) {
+        const uint32_t fk = t == 0 ? k : (t == 1 ? (k >= 2 ? k - 2 : k + 4) : (k >= 3 ? k - 3 : k + 3));
+        Fq2 x, q;
+        fetch2(x, f, src(ps, fk));
+        Fq o0, o1;
+        fq_sel(o0, t == 0, pa, t == 1 ? pb : py);
+        fq_sel(o1, t == 0, pa, t == 1 ? pb : py);
+        const uint32_t l0 = t == 0 ? a : (t == 1 ? b : y);
+        fetch(q.c0, o0, src(ps, l0));
+        fetch(q.c1, o1, src(ps, l0 + 1));  // unused for an Fq Y
+        if (A_DIRECT && t == 0) q = Ad;
+        if (t == 0 && !use) {
+          fq_one(q.c0);
+          fq_zero(q.c1);
+        }
+        fq2_xi_if(x, (t == 1 && k < 2) || (t == 2 && k < 3), x);
+        if (!Y2 && t == 2)  // uniform branch
+          fq_acc_mac(lacc, h ? x.c1 : x.c0, q.c0);
+        else
+          mac2_half(lacc, x, q, h);
+      }
+      fq_acc_redc(h ? r.c1 : r.c0, lacc);
+    }
+    f = r;
+    return;
+  }
+#endif
   Fq2 acc;
   fq2_zero(acc);
 HBTC_GT_SMALL_LOOP

@@ -266,6 +266,133 @@ def sr_call(name, label, square):
 """ % (name, args, prep, call, outs, ins, ", ".join(clob))
 
 
+# ------------------------------------------------------------------ lazy (double-width) reduction
+# hbtc_fqmac_sr: ACC += a * b, a double-width accumulator of 25 words (v60..v84) that survives
+# between calls, a and b (v8..v19, v20..v31) preserved; product scanning into the column pair of
+# gen_mul with the column digit added into ACC[k] through the carry chain s[66:67].
+# hbtc_fqredc_sr: r (v8..v19) = ACC * 2^-384 mod p, r < 2p, for ACC < 48 p^2 (ACC unchanged):
+# Montgomery digits q0..q11 over ACC's low half, the quotient (ACC + Q p) / 2^384 < 48 p^2 / 2^384
+# + p < 5.6p (12 words), then conditional subtractions of 4p and 2p.  48 p^2 bounds a sum of 12
+# products of reduced operands (< 2p each).
+SR_MACC, SR_CC = 60, 66
+
+
+def mac_body():
+    A = lambda i: "v%d" % (SR_A + i)
+    B = lambda i: "v%d" % (SR_B + i)
+    ACCW = lambda i: "v%d" % (SR_MACC + i)
+    reg = lambda n: "v%d" % (SR_ACC + n)
+    pair = lambda p: "v[%d:%d]" % (SR_ACC + 2 * p, SR_ACC + 2 * p + 1)
+    cc, chain = "vcc", "s[%d:%d]" % (SR_CC, SR_CC + 1)
+    out = ["v_mov_b32 %s, 0" % reg(0), "v_mov_b32 %s, 0" % reg(1)]
+    for k in range(23):
+        p = k % 2
+        acc, lo, hi, c2, nlo = pair(p), reg(2 * p), reg(2 * p + 1), reg(2 * (1 - p) + 1), reg(2 * (1 - p))
+        lo_i, hi_i = (0, k) if k < 12 else (k - 11, 11)
+        for i in range(lo_i, hi_i + 1):
+            out.append("v_mad_u64_u32 %s, %s, %s, %s, %s" % (acc, cc, A(i), B(k - i), acc))
+            out.append("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (c2, cc, "0" if i == lo_i else c2, cc))
+        if k == 0:
+            out.append("v_add_co_u32_e64 %s, %s, %s, %s" % (ACCW(0), chain, ACCW(0), lo))
+        else:
+            out.append("v_addc_co_u32_e64 %s, %s, %s, %s, %s" % (ACCW(k), chain, ACCW(k), lo, chain))
+        if k < 22:
+            out.append("v_mov_b32 %s, %s" % (nlo, hi))
+    # column 22's high word is digit 23 (its overflow word is 0: a * b < 2^768)
+    out.append("v_addc_co_u32_e64 %s, %s, %s, %s, %s" % (ACCW(23), chain, ACCW(23), reg(1), chain))
+    out.append("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (ACCW(24), chain, ACCW(24), chain))
+    return out
+
+
+def redc_body():
+    Q = lambda i: "v%d" % (SR_Q + i)
+    R = lambda i: "v%d" % (SR_A + i)
+    P = lambda i: "s%d" % (SR_P + i)
+    ACCW = lambda i: "v%d" % (SR_MACC + i)
+    reg = lambda n: "v%d" % (SR_ACC + n)
+    pair = lambda p: "v[%d:%d]" % (SR_ACC + 2 * p, SR_ACC + 2 * p + 1)
+    cc = "vcc"
+    out = ["v_mov_b32 %s, 0" % reg(0), "v_mov_b32 %s, 0" % reg(1)]
+    for k in range(24):
+        p = k % 2
+        acc, lo, hi, c2, nlo = pair(p), reg(2 * p), reg(2 * p + 1), reg(2 * (1 - p) + 1), reg(2 * (1 - p))
+        # the accumulator word enters the column as a product by 1
+        out.append("v_mad_u64_u32 %s, %s, %s, 1, %s" % (acc, cc, ACCW(k), acc))
+        out.append("v_addc_co_u32_e64 %s, %s, 0, 0, %s" % (c2, cc, cc))
+        lo_i, hi_i = (0, k - 1) if k < 12 else (k - 11, 11)
+        for i in range(lo_i, hi_i + 1):
+            out.append("v_mad_u64_u32 %s, %s, %s, %s, %s" % (acc, cc, Q(i), P(k - i), acc))
+            out.append("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (c2, cc, c2, cc))
+        if k < 12:
+            out.append("v_mul_lo_u32 %s, %s, s%d" % (Q(k), lo, SR_NP))
+            out.append("v_mad_u64_u32 %s, %s, %s, %s, %s" % (acc, cc, Q(k), P(0), acc))
+            out.append("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (c2, cc, c2, cc))
+        else:
+            out.append("v_mov_b32 %s, %s" % (R(k - 12), lo))
+        out.append("v_mov_b32 %s, %s" % (nlo, hi))
+    # r < 2^384: column 23's high word and ACC[24] are 0 for ACC < 48 p^2 (see above).  r < 5.6p:
+    # subtract 4p, then 2p, where they fit (r - mp into Q, keep r on a borrow).  The multiple's
+    # words go through a VGPR: a literal and the VCC carry-in together exceed the constant bus.
+    for m in (4, 2):
+        mp = m * P_MOD
+        for i in range(12):
+            w = "0x%08x" % ((mp >> (32 * i)) & 0xFFFFFFFF)
+            t = "v%d" % (SR_Q + i)
+            out.append("v_mov_b32 %s, %s" % (t, w))
+            if i == 0:
+                out.append("v_sub_co_u32_e32 %s, vcc, %s, %s" % (t, R(i), t))
+            else:
+                out.append("v_subb_co_u32_e32 %s, vcc, %s, %s, vcc" % (t, R(i), t))
+        for i in range(12):
+            out.append("v_cndmask_b32_e32 %s, %s, %s, vcc" % (R(i), "v%d" % (SR_Q + i), R(i)))
+    return out
+
+
+def lazy_text(label, body):
+    lines = [".p2align 8", "%s:" % label]
+    lines += ["s_mov_b32 s%d, 0x%08x" % (SR_P + i, (P_MOD >> (32 * i)) & 0xFFFFFFFF) for i in range(12)]
+    lines.append("s_mov_b32 s%d, 0x%08x" % (SR_NP, NP_MOD))
+    lines += body
+    lines.append("s_setpc_b64 s[%d:%d]" % (SR_RET, SR_RET + 1))
+    return lines
+
+
+def lazy_calls():
+    call = lambda label: (
+        '      "s_getpc_b64 s[%d:%d]\\n\\t"\n' % (SR_TGT, SR_TGT + 1) +
+        '      "s_add_u32 s%d, s%d, %s@rel32@lo+4\\n\\t"\n' % (SR_TGT, SR_TGT, label) +
+        '      "s_addc_u32 s%d, s%d, %s@rel32@hi+12\\n\\t"\n' % (SR_TGT + 1, SR_TGT + 1, label) +
+        '      "s_swappc_b64 s[%d:%d], s[%d:%d]"' % (SR_RET, SR_RET + 1, SR_TGT, SR_TGT + 1))
+    accio = ", ".join('"+{v%d}"(acc[%d])' % (SR_MACC + i, i) for i in range(25))
+    ins = ", ".join('"{v%d}"(a[%d])' % (SR_A + i, i) for i in range(12))
+    ins += ",\n        " + ", ".join('"{v%d}"(b[%d])' % (SR_B + i, i) for i in range(12))
+    clob = ['"v%d"' % v for v in range(SR_ACC, SR_ACC + 4)]
+    clob += ['"s%d"' % s for s in range(SR_P, SR_CC + 2)]
+    clob += ['"vcc"', '"scc"']
+    mac = """__device__ __forceinline__ void fq_mac_sr(uint32_t* acc, const uint32_t* a, const uint32_t* b) {
+  asm volatile(
+%s
+      : %s
+      : %s
+      : %s);
+}
+""" % (call("hbtc_fqmac_sr"), accio, ins, ", ".join(clob))
+    outs = ", ".join('"={v%d}"(r[%d])' % (SR_A + i, i) for i in range(12))
+    ains = ", ".join('"{v%d}"(acc[%d])' % (SR_MACC + i, i) for i in range(25))
+    rclob = ['"v%d"' % v for v in range(SR_Q, SR_ACC + 4)]
+    rclob += ['"s%d"' % s for s in range(SR_P, SR_RET + 2)]
+    rclob += ['"vcc"', '"scc"']
+    redc = """__device__ __forceinline__ void fq_redc_sr(uint32_t* r, const uint32_t* acc) {
+  asm volatile(
+%s
+      : %s
+      : %s
+      : %s);
+}
+""" % (call("hbtc_fqredc_sr"), outs, ains, ", ".join(rclob))
+    return mac + redc
+
+
 def main_sr():
     print("""// GENERATED by tools/gen_fips_asm.py --sr -- do not edit.
 // The Fq Montgomery product and squaring of fq_fips_asm.h as ONE shared subroutine each, called
@@ -284,6 +411,9 @@ def main_sr():
     for label, square in (("hbtc_fqmul_sr", False), ("hbtc_fqsqr_sr", True)):
         for l in sr_text(label, square):
             print('    "%s\\n"' % l)
+    for label, body in (("hbtc_fqmac_sr", mac_body()), ("hbtc_fqredc_sr", redc_body())):
+        for l in lazy_text(label, body):
+            print('    "%s\\n"' % l)
     print('    ::: "memory");')
     print('}')
     print("""namespace hbtc {
@@ -291,6 +421,7 @@ namespace fips {
 """)
     print(sr_call("mont_mul_sr", "hbtc_fqmul_sr", False))
     print(sr_call("mont_sqr_sr", "hbtc_fqsqr_sr", True))
+    print(lazy_calls())
     print("""}  // namespace fips
 }  // namespace hbtc
 #endif""")
@@ -385,3 +516,113 @@ def selftest(trials=300):
 if __name__ == "__main__" and len(__import__("sys").argv) > 1 and __import__("sys").argv[1] == "--selftest":
     selftest()
     selftest_sr()
+
+
+def run_prog(prog, regs):
+    """Execute a subroutine body on one lane's register file; carry bits by register name."""
+    M32 = (1 << 32) - 1
+    carry = {}
+
+    def val(t):
+        t = t.strip()
+        if t.startswith("0x") or t.isdigit():
+            return int(t, 0)
+        m = re.fullmatch(r"v\[(\d+):(\d+)\]", t)
+        if m:
+            return regs["v" + m.group(1)] | (regs["v" + m.group(2)] << 32)
+        return regs[t]
+
+    def store(t, v):
+        t = t.strip()
+        m = re.fullmatch(r"v\[(\d+):(\d+)\]", t)
+        if m:
+            regs["v" + m.group(1)] = v & M32
+            regs["v" + m.group(2)] = (v >> 32) & M32
+        else:
+            regs[t] = v & M32
+
+    for line in prog:
+        op, rest = line.split(" ", 1)
+        args = [x.strip() for x in re.split(r",(?![^\[]*\])", rest)]
+        if op in ("s_mov_b32", "v_mov_b32"):
+            store(args[0], val(args[1]))
+        elif op == "v_mad_u64_u32":
+            d, c, x, y, z = args
+            s = val(x) * val(y) + val(z)
+            carry[c] = s >> 64
+            store(d, s)
+        elif op == "v_add_co_u32_e64":
+            d, c, x, y = args
+            s = val(x) + val(y)
+            carry[c] = s >> 32
+            store(d, s)
+        elif op == "v_addc_co_u32_e64":
+            d, c, x, y, ci = args
+            s = val(x) + val(y) + carry[ci]
+            carry[c] = s >> 32
+            store(d, s)
+        elif op == "v_add_u32_e32":
+            d, x, y = args
+            store(d, val(x) + val(y))
+        elif op == "v_subrev_co_u32_e32":
+            d, c, x, y = args
+            s = val(y) - val(x)
+            carry[c] = 1 if s < 0 else 0
+            store(d, s)
+        elif op == "v_subbrev_co_u32_e32":
+            d, c, x, y, ci = args
+            s = val(y) - val(x) - carry[ci]
+            carry[c] = 1 if s < 0 else 0
+            store(d, s)
+        elif op == "v_sub_co_u32_e32":
+            d, c, x, y = args
+            s = val(x) - val(y)
+            carry[c] = 1 if s < 0 else 0
+            store(d, s)
+        elif op == "v_subb_co_u32_e32":
+            d, c, x, y, ci = args
+            s = val(x) - val(y) - carry[ci]
+            carry[c] = 1 if s < 0 else 0
+            store(d, s)
+        elif op == "v_cndmask_b32_e32":
+            d, x, y, c = args
+            store(d, val(y) if carry[c] else val(x))
+        elif op == "v_mul_lo_u32":
+            d, x, y = args
+            store(d, val(x) * val(y))
+        else:
+            raise ValueError(op)
+
+
+def selftest_lazy(trials=200):
+    """ACC = sum of up to 12 products of operands < 2p through hbtc_fqmac_sr, then
+    hbtc_fqredc_sr: r < 2p and r = ACC 2^-384 mod p; a and b survive the MAC."""
+    import random
+    M32 = (1 << 32) - 1
+    rng = random.Random(10)
+    mac = lazy_text("x", mac_body())[2:-1]
+    redc = lazy_text("x", redc_body())[2:-1]
+    for t in range(trials):
+        regs = {"v%d" % (SR_MACC + i): 0 for i in range(25)}
+        total = 0
+        n = [1, 2, 12][t % 3] if t >= 3 else 12
+        for _ in range(n):
+            a = rng.randrange(2 * P_MOD) if t else 2 * P_MOD - 1
+            b = rng.randrange(2 * P_MOD) if t else 2 * P_MOD - 1
+            for i in range(12):
+                regs["v%d" % (SR_A + i)] = (a >> (32 * i)) & M32
+                regs["v%d" % (SR_B + i)] = (b >> (32 * i)) & M32
+            run_prog(mac, regs)
+            total += a * b
+            assert sum(regs["v%d" % (SR_A + i)] << (32 * i) for i in range(12)) == a
+            assert sum(regs["v%d" % (SR_B + i)] << (32 * i) for i in range(12)) == b
+        assert sum(regs["v%d" % (SR_MACC + i)] << (32 * i) for i in range(25)) == total
+        run_prog(redc, regs)
+        r = sum(regs["v%d" % (SR_A + i)] << (32 * i) for i in range(12))
+        assert r < 2 * P_MOD and r % P_MOD == total * pow(2, -384, P_MOD) % P_MOD, (t, n)
+        assert sum(regs["v%d" % (SR_MACC + i)] << (32 * i) for i in range(25)) == total
+    print("selftest_lazy ok (%d / %d instructions)" % (len(mac), len(redc)))
+
+
+if __name__ == "__main__" and len(__import__("sys").argv) > 1 and __import__("sys").argv[1] == "--selftest-lazy":
+    selftest_lazy()
