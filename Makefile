@@ -31,7 +31,9 @@ lib: $(LIB)
 .PHONY: gen-fips
 gen-fips:
 	python3 tools/gen_fips_asm.py --selftest
+	python3 tools/gen_fips_asm.py --selftest-lazy
 	python3 tools/gen_fips_asm.py > $(CSRC)/fq_fips_asm.h
+	python3 tools/gen_fips_asm.py --sr > $(CSRC)/fq_fips_sr.h
 
 $(BUILD):
 	mkdir -p $(BUILD)

@@ -137,6 +137,10 @@ struct hbtc_ctx {
   // layout of the small check levels (split levels, leaves) of calls on the paired schedules:
   // 3 = the latency form (gt6.h Pos.rep), 1 = the throughput form; HBTC_GT_REP overrides
   int small_rep = 3;
+  // RLC calls with fewer items than this take the exact per-item checks instead (one dependent
+  // launch rather than item pass + check levels, on a GPU such a call does not fill either way;
+  // hbtc_set_exact_below, HBTC_EXACT_BELOW)
+  uint32_t exact_below = 64;
   uint64_t probes = 0;     // probe passes run
   const uint32_t* last_leaf_count = nullptr;  // device counter of the last RLC call
   // Device ranges that combines still read, each with the event recorded after that combine:
@@ -544,6 +548,12 @@ uint32_t probe_threshold(const Keyset* ks, uint32_t n_items) {
   return t > 2 ? (uint32_t)t : 2u;
 }
 
+// RLC batch or exact per-item checks for a call of n items (hbtc_set_verify_mode,
+// hbtc_set_exact_below)
+bool use_rlc(const hbtc_ctx* c, uint32_t n) {
+  return c->verify_mode == HBTC_MODE_RLC && n >= c->exact_below;
+}
+
 // Group-check schedule of one RLC call.  The plain-first form (5 levels: plain and weighted
 // checks of tiles, then of sub-tiles, then leaves) does the least work and is right when the
 // call fills the chip; a call with few tiles (a rank's slice under strong scaling, a small
@@ -594,7 +604,7 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   Line *h_lines, *w_lines;
   Tile* tiles;
   uint32_t n_tiles;
-  if (c->verify_mode == HBTC_MODE_PER_SHARE) {
+  if (!use_rlc(c, n_items)) {
     HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
     if (c->last_dec.status == d_status) c->last_dec = {};
     HB_TRY(prepare_g2(c, d_H, d_w, n_ct, &h_aff, &h_st, &h_lines));
@@ -817,7 +827,7 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   Line* h_lines;
   Tile* tiles;
   uint32_t n_tiles;
-  if (c->verify_mode == HBTC_MODE_PER_SHARE) {
+  if (!use_rlc(c, n_items)) {
     HB_TRY(prepare_g2(c, d_H, nullptr, n_inst, &h_aff, &h_st, &h_lines));
     HB_TRY(make_tiles(c, n_inst, offsets, &tiles, &n_tiles));
     HB_TRY(timed(c, "sig_verify", [&] {
@@ -1279,6 +1289,7 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (const char* e = getenv("HBTC_PROBE")) c->probe_cold = atoi(e) != 0;
   if (const char* e = getenv("HBTC_SPLIT")) c->split_levels = atoi(e) != 0;
   if (const char* e = getenv("HBTC_GT_REP")) c->small_rep = atoi(e) == 1 ? 1 : 3;
+  if (const char* e = getenv("HBTC_EXACT_BELOW")) c->exact_below = (uint32_t)atol(e);
   if (const char* e = getenv("HBTC_PB_CHUNK")) {
     const long v = atol(e);
     if (v >= 64 && v % 64 == 0 && v <= (1l << 20)) c->pb_chunk = (uint32_t)v;
@@ -1455,7 +1466,7 @@ int hbtc_verify_sig_shares(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, con
 // chunk.  Per-share mode: k_pair_verify for every item.
 int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_q, bool q_trusted,
                   const uint8_t* d_w, int32_t* d_status, G1A* d_adec = nullptr) {
-  if (c->verify_mode == HBTC_MODE_PER_SHARE) {
+  if (!use_rlc(c, n)) {  // d_adec is then not written: callers decide with use_rlc too
     return timed(c, "pair_verify", [&] {
       return launch_pair_verify(c->stream, n, d_a, d_q, nullptr, d_w, d_status);
     });
@@ -2245,6 +2256,13 @@ int hbtc_trim_workspace(hbtc_ctx* c) {
   return HBTC_OK;
 }
 
+int hbtc_set_exact_below(hbtc_ctx* c, uint32_t n_items) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  c->exact_below = n_items;
+  return HBTC_OK;
+}
+
 int hbtc_get_rlc_bits(hbtc_ctx* c, uint32_t* bits) {
   if (!c || !bits) return HBTC_ERR_ARG;
   Guard g(c);
@@ -2427,7 +2445,7 @@ int hbtc_decrypt(hbtc_ctx* c, uint32_t n, const uint8_t* sk_le32, const uint8_t*
   HB_TRY(ws(c, "out1", (size_t)48 * n, &d_g));
   HB_TRY(ws(c, "out2", (size_t)4 * n, &d_gst));
   // H is this call's own hash output (cofactor cleared: in the subgroup by construction)
-  const bool rlc = c->verify_mode == HBTC_MODE_RLC;
+  const bool rlc = use_rlc(c, n);
   G1A* d_adec = nullptr;
   if (rlc) HB_TRY(wst(c, "dec.adec", n, &d_adec));
   HB_TRY(pb_verify_dev(c, n, (const uint8_t*)d_u, (const uint8_t*)d_H, true, (const uint8_t*)d_w,

@@ -39,3 +39,19 @@ def test_one_move_per_column():
         assert ops.count("v_addc_co_u32_e64") == macs
         # 2 zero-inits + 22 next-low-word moves + 12 result limbs
         assert ops.count("v_mov_b32") == 2 + 22 + 12
+
+
+def test_lazy_reduction_subroutines():
+    """hbtc_fqmac_sr / hbtc_fqredc_sr (the double-width accumulator of gt6.h's lazy products) on
+    the simulator: sums of up to 12 products of operands < 2p, the worst case included, reduce
+    to r < 2p congruent to ACC 2^-384; a MAC is the 144 product MADs, a REDC 144 + 24."""
+    assert "selftest_lazy ok" in _run("--selftest-lazy")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import gen_fips_asm as g
+    finally:
+        sys.path.pop(0)
+    mac = [line.split(" ", 1)[0] for line in g.mac_body()]
+    redc = [line.split(" ", 1)[0] for line in g.redc_body()]
+    assert mac.count("v_mad_u64_u32") == 144
+    assert redc.count("v_mad_u64_u32") == 144 + 24  # q_i p_j, and each ACC word entering by 1

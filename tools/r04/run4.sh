@@ -3,7 +3,8 @@
 # Montgomery reduction per output half).  The GPU suite first, then A/B against the same build
 # without it (hbbft_amd/libhbtc_nolazy.so: HBTC_GT_LAZY=0 in the check / sig / pb objects) on
 # C3 and the 125-ciphertext slice, the split / latency-form A/B of run3 on the lazy build, the
-# coin lines, and the 16-queue suite + context churn.
+# coin lines (small calls on the exact per-item checks, and batched as before), and the
+# 16-queue suite + context churn.
 cd "$(dirname "$0")/../.." || exit 1
 O=gpurun_out/r04run4
 mkdir -p $O
@@ -27,5 +28,6 @@ done; done
 HBTC_SPLIT=0 step 200 python -u bench.py --no-cpu --no-extra > $O/c3_s0.json 2> $O/c3_s0.err
 HBTC_GT_REP=1 step 300 python -u bench_configs.py --configs c1,c2 --no-cpu > $O/c1c2_r1.json 2> $O/c1c2_r1.err
 HBTC_GT_REP=3 step 300 python -u bench_configs.py --configs c1,c2 --no-cpu > $O/c1c2_r3.json 2> $O/c1c2_r3.err
+HBTC_EXACT_BELOW=0 step 200 python -u bench_configs.py --configs c1 --no-cpu > $O/c1_batch.json 2> $O/c1_batch.err
 step 600 bash tools/r04/hwq16.sh
 echo all-done >&2
