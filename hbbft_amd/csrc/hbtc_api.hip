@@ -137,10 +137,6 @@ struct hbtc_ctx {
   // layout of the small check levels (split levels, leaves) of calls on the paired schedules:
   // 3 = the latency form (gt6.h Pos.rep), 1 = the throughput form; HBTC_GT_REP overrides
   int small_rep = 3;
-  // RLC calls with fewer items than this take the exact per-item checks instead (one dependent
-  // launch rather than item pass + check levels, on a GPU such a call does not fill either way;
-  // hbtc_set_exact_below, HBTC_EXACT_BELOW)
-  uint32_t exact_below = 64;
   uint64_t probes = 0;     // probe passes run
   const uint32_t* last_leaf_count = nullptr;  // device counter of the last RLC call
   // Device ranges that combines still read, each with the event recorded after that combine:
@@ -548,12 +544,6 @@ uint32_t probe_threshold(const Keyset* ks, uint32_t n_items) {
   return t > 2 ? (uint32_t)t : 2u;
 }
 
-// RLC batch or exact per-item checks for a call of n items (hbtc_set_verify_mode,
-// hbtc_set_exact_below)
-bool use_rlc(const hbtc_ctx* c, uint32_t n) {
-  return c->verify_mode == HBTC_MODE_RLC && n >= c->exact_below;
-}
-
 // Group-check schedule of one RLC call.  The plain-first form (5 levels: plain and weighted
 // checks of tiles, then of sub-tiles, then leaves) does the least work and is right when the
 // call fills the chip; a call with few tiles (a rank's slice under strong scaling, a small
@@ -604,7 +594,7 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   Line *h_lines, *w_lines;
   Tile* tiles;
   uint32_t n_tiles;
-  if (!use_rlc(c, n_items)) {
+  if (c->verify_mode == HBTC_MODE_PER_SHARE) {
     HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
     if (c->last_dec.status == d_status) c->last_dec = {};
     HB_TRY(prepare_g2(c, d_H, d_w, n_ct, &h_aff, &h_st, &h_lines));
@@ -706,7 +696,10 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
   HB_CHECK(c, launch_zero_u32(c->stream, counters, 9));
   // the split levels' lists: level l lists up to n_tiles 2^(l-1) nodes with their T, U (6 Fq2 each)
   const int chk_mode = check_mode(c, n_tiles);
-  const bool split = c->split_levels && chk_mode != CHK_PAIR_LEAVES;
+  // the split levels pay on the plain-first schedule (C3: 86.2 -> 84.7 ms per epoch); on the
+  // paired ones the sub-tile level is one launch where splitting is three dependent ones (the
+  // 125-ciphertext slice: 17.1 ms per epoch without, 18.5 with; profiles/r04/run4/)
+  const bool split = c->split_levels && chk_mode == CHK_PLAIN_FIRST;
   SplitOut sp[3] = {};
   if (split) {
     for (int l = 0; l < 3; ++l) {
@@ -827,7 +820,7 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   Line* h_lines;
   Tile* tiles;
   uint32_t n_tiles;
-  if (!use_rlc(c, n_items)) {
+  if (c->verify_mode == HBTC_MODE_PER_SHARE) {
     HB_TRY(prepare_g2(c, d_H, nullptr, n_inst, &h_aff, &h_st, &h_lines));
     HB_TRY(make_tiles(c, n_inst, offsets, &tiles, &n_tiles));
     HB_TRY(timed(c, "sig_verify", [&] {
@@ -1289,7 +1282,10 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (const char* e = getenv("HBTC_PROBE")) c->probe_cold = atoi(e) != 0;
   if (const char* e = getenv("HBTC_SPLIT")) c->split_levels = atoi(e) != 0;
   if (const char* e = getenv("HBTC_GT_REP")) c->small_rep = atoi(e) == 1 ? 1 : 3;
-  if (const char* e = getenv("HBTC_EXACT_BELOW")) c->exact_below = (uint32_t)atol(e);
+  if (const char* e = getenv("HBTC_RLC_BITS")) {  // A/B runs: 64 or 128, like hbtc_set_rlc_bits
+    const int b = atoi(e);
+    if (b == 64 || b == 128) c->rlc_bits = (uint32_t)b;
+  }
   if (const char* e = getenv("HBTC_PB_CHUNK")) {
     const long v = atol(e);
     if (v >= 64 && v % 64 == 0 && v <= (1l << 20)) c->pb_chunk = (uint32_t)v;
@@ -1307,30 +1303,39 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   // share a hardware queue, which costs concurrency, never correctness: every wait is on an
   // event recorded by work submitted earlier).  The G2 preparation stream is shared by the lanes
   // (its work is short and ordered anyway); a lane's combines run on the lane's own stream.
+  // a failing HIP call is reported on stderr with its name and error (no context exists yet to
+  // hold the message); the objects created so far are released by hbtc_ctx_destroy
+  auto created = [&](hipError_t e, const char* what) {
+    if (e == hipSuccess) return true;
+    fprintf(stderr, "hbtc_ctx_create(device %d): %s failed: %s (%d)\n", device, what,
+            hipGetErrorString(e), (int)e);
+    return false;
+  };
   for (Lane& l : c->lanes)
-    if (hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&l.ev_main, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&l.ev_prep, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&l.done, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&l.items_done, hipEventDisableTiming) != hipSuccess) {
-      delete c;
+    if (!created(hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking), "hipStreamCreateWithFlags") ||
+        !created(hipEventCreateWithFlags(&l.ev_main, hipEventDisableTiming), "hipEventCreateWithFlags") ||
+        !created(hipEventCreateWithFlags(&l.ev_prep, hipEventDisableTiming), "hipEventCreateWithFlags") ||
+        !created(hipEventCreateWithFlags(&l.done, hipEventDisableTiming), "hipEventCreateWithFlags") ||
+        !created(hipEventCreateWithFlags(&l.items_done, hipEventDisableTiming), "hipEventCreateWithFlags")) {
+      hbtc_ctx_destroy(c);
       return HBTC_ERR_DEVICE;
     }
   // the preparation is a short latency-bound chain (few waves) that the checks wait for: its
   // stream has the highest priority, so its workgroups are dispatched ahead of the item pass's
   int prio_least = 0, prio_greatest = 0;
   if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
-  if (hipStreamCreateWithPriority(&c->lanes[0].s_prep, hipStreamNonBlocking, prio_greatest) != hipSuccess) {
-    delete c;
+  if (!created(hipStreamCreateWithPriority(&c->lanes[0].s_prep, hipStreamNonBlocking, prio_greatest),
+               "hipStreamCreateWithPriority")) {
+    hbtc_ctx_destroy(c);
     return HBTC_ERR_DEVICE;
   }
   for (Lane& l : c->lanes) l.s_prep = c->lanes[0].s_prep;
   select_lane(c, 0);
-  if (hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_ext2, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_ext3, hipEventDisableTiming) != hipSuccess) {
-    delete c;
+  if (!created(hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming), "hipEventCreateWithFlags") ||
+      !created(hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming), "hipEventCreateWithFlags") ||
+      !created(hipEventCreateWithFlags(&c->ev_ext2, hipEventDisableTiming), "hipEventCreateWithFlags") ||
+      !created(hipEventCreateWithFlags(&c->ev_ext3, hipEventDisableTiming), "hipEventCreateWithFlags")) {
+    hbtc_ctx_destroy(c);
     return HBTC_ERR_DEVICE;
   }
   *out = c;
@@ -1370,18 +1375,22 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
     if (kv.second.h) (void)hipHostFree(kv.second.h);
     if (kv.second.ev) (void)hipEventDestroy(kv.second.ev);
   }
+  // (a context whose creation failed part-way has some of these still null)
+  auto ev_free = [](hipEvent_t e) {
+    if (e) (void)hipEventDestroy(e);
+  };
   for (Lane& l : c->lanes) {
-    (void)hipEventDestroy(l.ev_main);
-    (void)hipEventDestroy(l.ev_prep);
-    (void)hipEventDestroy(l.done);
-    (void)hipEventDestroy(l.items_done);
-    (void)hipStreamDestroy(l.stream);
+    ev_free(l.ev_main);
+    ev_free(l.ev_prep);
+    ev_free(l.done);
+    ev_free(l.items_done);
+    if (l.stream) (void)hipStreamDestroy(l.stream);
   }
-  (void)hipStreamDestroy(c->lanes[0].s_prep);
-  (void)hipEventDestroy(c->ev_comb);
-  (void)hipEventDestroy(c->ev_ext);
-  (void)hipEventDestroy(c->ev_ext2);
-  (void)hipEventDestroy(c->ev_ext3);
+  if (c->lanes[0].s_prep) (void)hipStreamDestroy(c->lanes[0].s_prep);
+  ev_free(c->ev_comb);
+  ev_free(c->ev_ext);
+  ev_free(c->ev_ext2);
+  ev_free(c->ev_ext3);
   delete c;
 }
 
@@ -1466,7 +1475,7 @@ int hbtc_verify_sig_shares(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, con
 // chunk.  Per-share mode: k_pair_verify for every item.
 int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_q, bool q_trusted,
                   const uint8_t* d_w, int32_t* d_status, G1A* d_adec = nullptr) {
-  if (!use_rlc(c, n)) {  // d_adec is then not written: callers decide with use_rlc too
+  if (c->verify_mode == HBTC_MODE_PER_SHARE) {
     return timed(c, "pair_verify", [&] {
       return launch_pair_verify(c->stream, n, d_a, d_q, nullptr, d_w, d_status);
     });
@@ -2256,13 +2265,6 @@ int hbtc_trim_workspace(hbtc_ctx* c) {
   return HBTC_OK;
 }
 
-int hbtc_set_exact_below(hbtc_ctx* c, uint32_t n_items) {
-  if (!c) return HBTC_ERR_ARG;
-  Guard g(c);
-  c->exact_below = n_items;
-  return HBTC_OK;
-}
-
 int hbtc_get_rlc_bits(hbtc_ctx* c, uint32_t* bits) {
   if (!c || !bits) return HBTC_ERR_ARG;
   Guard g(c);
@@ -2445,7 +2447,7 @@ int hbtc_decrypt(hbtc_ctx* c, uint32_t n, const uint8_t* sk_le32, const uint8_t*
   HB_TRY(ws(c, "out1", (size_t)48 * n, &d_g));
   HB_TRY(ws(c, "out2", (size_t)4 * n, &d_gst));
   // H is this call's own hash output (cofactor cleared: in the subgroup by construction)
-  const bool rlc = use_rlc(c, n);
+  const bool rlc = c->verify_mode == HBTC_MODE_RLC;
   G1A* d_adec = nullptr;
   if (rlc) HB_TRY(wst(c, "dec.adec", n, &d_adec));
   HB_TRY(pb_verify_dev(c, n, (const uint8_t*)d_u, (const uint8_t*)d_H, true, (const uint8_t*)d_w,

@@ -390,13 +390,6 @@ int hbtc_shard_instances(uint32_t n_dev, uint32_t n_inst, const uint32_t* offset
 #define HBTC_MODE_PER_SHARE 0
 #define HBTC_MODE_RLC 1
 int hbtc_set_verify_mode(hbtc_ctx* ctx, int mode);
-/* In RLC mode, calls with fewer than n_items items (shares for hbtc_verify_dec_shares[_dev] /
- * hbtc_verify_sig_shares[_dev], items for hbtc_verify_sigs / hbtc_verify_ciphertexts /
- * hbtc_decrypt) take the exact per-item checks instead of the batch: one dependent launch
- * instead of the item pass and its check levels, on a GPU that such a call does not fill either
- * way (a single N = 10 coin: its 10 shares and the master signature).  Default 64; 0 = always
- * batch.  Decisions are the same either way. */
-int hbtc_set_exact_below(hbtc_ctx* ctx, uint32_t n_items);
 /* Size of the RLC scalars r_i = d0 + d1 x + d2 mu + d3 mu x (x the BLS parameter, mu = -x^2 mod r;
  * four digits of bits/4 bits; DESIGN.md §4, "x-adic scalars" and "Soundness"): 128 (default:
  * 2^128 distinct scalars: a wrong share survives a group check with probability <= 2^-128,

@@ -30,7 +30,6 @@ def _gens():
 @pytest.fixture(scope="module")
 def ctx():
     c = N.Context(0)
-    c.set_exact_below(0)
     yield c
     c.close()
 
@@ -89,7 +88,6 @@ def test_verify_ciphertexts_across_chunks():
         c = N.Context(0)
     finally:
         del os.environ["HBTC_PB_CHUNK"]
-    c.set_exact_below(0)
     try:
         _ct_rlc_equals_per_share(c, 3 * 4096 + 130, extra_bad=(4095, 4096, 8191, 12287, 12290))
         c.trim_workspace()
@@ -143,22 +141,3 @@ def test_verify_sigs_rlc_equals_per_share(ctx):
     assert (st == ref).all(), np.nonzero(st != ref)
     assert [int(x) for x in np.nonzero(ref == N.REJECT)[0]] == [3, 70, 71, 149]
     assert ref[5] == N.DECODE_ERR
-
-
-def test_small_pair_batches_take_exact_checks():
-    """With the default hbtc_set_exact_below (64), Ciphertext::verify / PublicKey::verify calls of
-    fewer items go straight to k_pair_verify: the per-item decisions, no pair-batch launches."""
-    c = N.Context(0)
-    c.timing_enable(True)
-    try:
-        for n in (1, 40, 63, 64):
-            us, Hs, ws = _ct_batch(c, random.Random(n + 9), n)
-            c.set_verify_mode(N.MODE_PER_SHARE)
-            ref = c.verify_ciphertexts(us, Hs, ws)
-            c.set_verify_mode(N.MODE_RLC)
-            c.timing_reset()
-            st = c.verify_ciphertexts(us, Hs, ws)
-            assert (st == ref).all(), (n, np.nonzero(st != ref))
-            assert (c.timing_read("pb_items")[1] == 0) == (n < 64), n
-    finally:
-        c.close()

@@ -77,7 +77,6 @@ def test_split_levels_equal_per_share_decisions(split):
     os.environ["HBTC_SPLIT"] = split
     try:
         ctx = N.Context(0)  # reads HBTC_SPLIT at creation
-        ctx.set_exact_below(0)
     finally:
         if old is None:
             del os.environ["HBTC_SPLIT"]
@@ -101,17 +100,19 @@ def test_split_levels_equal_per_share_decisions(split):
 
 
 def test_split_levels_cut_leaf_checks():
-    """The split levels resolve tiles whose wrong shares sit in different eighths without exact
-    leaf checks: only the eighths holding >= 2 wrong shares reach them."""
+    """The split levels (the plain-first schedule's: the paired ones keep their one sub-tile
+    level) resolve tiles whose wrong shares sit in different eighths without exact leaf checks:
+    only the eighths holding >= 2 wrong shares reach them."""
     ctx = N.Context(0)
-    ctx.set_exact_below(0)
     try:
         pk, H, w, counts, idx, shares, exp = _batch(ctx, random.Random(516))
         ks, _ = ctx.keyset_load(pk)
         ctx.set_verify_mode(N.MODE_RLC)
-        ctx.set_check_schedule(N.CHECK_PAIR_SUBS)
+        ctx.set_check_schedule(N.CHECK_PLAIN_FIRST)
+        ctx.timing_enable(True)
         st = ctx.verify_dec_shares(ks, H, w, counts, idx, shares)
         assert (st == exp).all()
+        assert all(ctx.timing_read("chk_split%d" % lvl)[1] >= 1 for lvl in (1, 2, 3))
         leaves = ctx.rlc_last_leaves()
         # the eighths with >= 2 wrong shares, 8 shares each: (1, 2), (62, 63), (60, 61), the pair
         # (10, 11), (2, 3) of the 37-share tile, the 8 eighths of the all-wrong tile; (0, 8) of the

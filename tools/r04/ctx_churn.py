@@ -38,6 +38,27 @@ def main():
         nd.close()
     print("300 contexts and 20 eight-slot nodes created, used and destroyed: ok", flush=True)
     c0.close()
+    # contexts ALIVE at the same time (the GPU suite keeps a few module fixtures and nodes open):
+    # create and use them without closing until one fails or 48 exist; hbtc_ctx_create names
+    # the failing HIP call on stderr
+    live = []
+    try:
+        for i in range(48):
+            try:
+                c = N.Context(0)
+            except Exception as e:
+                print("concurrent: context %d failed to create with %d alive: %r" % (i, len(live), e),
+                      flush=True)
+                break
+            live.append(c)
+            ks, _ = c.keyset_load(pk)
+            c.verify_dec_shares(ks, H, w, [40, 7, 64], idx, shares)
+        else:
+            print("concurrent: 48 contexts alive and used: ok", flush=True)
+    finally:
+        for c in live:
+            c.close()
+    print("concurrent phase done (%d contexts)" % len(live), flush=True)
 
 
 if __name__ == "__main__":
