@@ -417,6 +417,7 @@ def _pct(xs, q):
     return s[min(len(s) - 1, int(q * len(s)))]
 
 
+C1_SKIP = set(filter(None, os.environ.get("HBTC_C1_SKIP", "").split(",")))
 COIN_NONCE = (b"Nonce for Honey Badger [173, 84, 2, 11, 0, 0, 9, 254, 1, 18, 200, 57, 43, 9, "
               b"4, 77, 190, 91, 12, 0, 1, 2, 3]@3:2:7")
 
@@ -450,9 +451,15 @@ def bench_c1(ctx, steps, warmup, cpu_budget=0.0):
         stv = ctx.verify_sig_shares(ks, [Hc], [n], idx, sig_list)
         c = time.perf_counter()
         sel = [i for i in range(n) if stv[i] == N.ACCEPT][:t]
-        out, par, cst = ctx.combine_sigs([t], sel, [sig_list[i] for i in sel], t)
+        if "combine" in C1_SKIP:  # diagnostics only
+            out, par, cst = [want_sig], np.zeros(1, np.uint8), np.zeros(1, np.int32)
+        else:
+            out, par, cst = ctx.combine_sigs([t], sel, [sig_list[i] for i in sel], t)
         d = time.perf_counter()
-        ok = ctx.verify_sigs([bytes(mpk)], [Hc], [out[0]])
+        if "master" in C1_SKIP:  # diagnostics only (the results check below then fails loudly)
+            ok = np.zeros(1, np.int32)
+        else:
+            ok = ctx.verify_sigs([bytes(mpk)], [Hc], [out[0]])
         e = time.perf_counter()
         return (b - a, c - b, d - c, e - d, e - a), stv, out[0], int(par[0]), int(cst[0]), int(ok[0])
 
@@ -463,6 +470,9 @@ def bench_c1(ctx, steps, warmup, cpu_budget=0.0):
         for k, v in zip(phases, ph[:4]):
             phases[k].append(v)
         total.append(ph[4])
+    if C1_SKIP:
+        log("c1: HBTC_C1_SKIP=%s: diagnostics run, no line" % ",".join(sorted(C1_SKIP)))
+        return None
     if (stv != expected).any() or cst != 0 or ok != N.ACCEPT or sig != bytes(want_sig):
         raise SystemExit("c1: results differ from the construction")
     ctx.keyset_free(ks)
@@ -813,7 +823,8 @@ def main():
                                 cpu_budget=0.0 if args.no_cpu else 10.0)
             else:
                 raise SystemExit("unknown config " + c)
-            print(json.dumps(out), flush=True)
+            if out is not None:
+                print(json.dumps(out), flush=True)
     finally:
         if node is not None:
             node.close()

@@ -116,6 +116,7 @@ struct hbtc_ctx {
   hipStream_t s_comb = nullptr;  // combines: the current lane's stream (after its verification)
   hipEvent_t ev_main = nullptr, ev_prep = nullptr, ev_comb = nullptr;
   hipEvent_t ev_ext = nullptr, ev_ext2 = nullptr, ev_ext3 = nullptr;  // external-stream ordering
+  hipEvent_t ev_x_in = nullptr, ev_x_out = nullptr;  // ordering around the exact-kernel stream
   std::map<std::string, Stage> stages;
   std::map<std::string, unsigned> stage_next;
   std::mutex mu;
@@ -544,6 +545,42 @@ uint32_t probe_threshold(const Keyset* ks, uint32_t n_items) {
   return t > 2 ? (uint32_t)t : 2u;
 }
 
+// The per-item exact kernels (k_dec_verify, k_sig_verify, k_pair_verify: one pairing check per
+// lane, ~6 KB/lane of scratch) run on ONE stream per device for the whole process.  The runtime
+// reserves a kernel's scratch per hardware queue, for the whole device's wave slots; with
+// GPU_MAX_HW_QUEUES=16 a process whose many contexts dispatched them on every queue ran out
+// (HSA_STATUS_ERROR_OUT_OF_RESOURCES: the queue aborts, and every later HIP call of the process
+// fails -- round 3's 16-queue suite).  On one stream they hold one queue's reservation.
+namespace {
+std::mutex g_exact_mu;
+hipStream_t g_exact_stream[64] = {};
+}  // namespace
+
+hipError_t exact_stream(int device, hipStream_t* out) {
+  std::lock_guard<std::mutex> lk(g_exact_mu);
+  if (device < 0 || device >= 64) return hipErrorInvalidDevice;
+  if (!g_exact_stream[device]) {
+    const hipError_t e = hipStreamCreateWithFlags(&g_exact_stream[device], hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
+  }
+  *out = g_exact_stream[device];
+  return hipSuccess;
+}
+
+// launch(stream) on the exact-kernel stream, after everything queued so far on c->stream and
+// before anything queued there later
+template <class L>
+hipError_t on_exact_stream(hbtc_ctx* c, L&& launch) {
+  hipStream_t xs;
+  hipError_t e = exact_stream(c->device, &xs);
+  if (e != hipSuccess) return e;
+  if ((e = hipEventRecord(c->ev_x_in, c->stream)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(xs, c->ev_x_in, 0)) != hipSuccess) return e;
+  if ((e = launch(xs)) != hipSuccess) return e;
+  if ((e = hipEventRecord(c->ev_x_out, xs)) != hipSuccess) return e;
+  return hipStreamWaitEvent(c->stream, c->ev_x_out, 0);
+}
+
 // Group-check schedule of one RLC call.  The plain-first form (5 levels: plain and weighted
 // checks of tiles, then of sub-tiles, then leaves) does the least work and is right when the
 // call fills the chip; a call with few tiles (a rank's slice under strong scaling, a small
@@ -603,8 +640,10 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
     w_lines = h_lines + (size_t)n_ct * MILLER_STEPS;
     HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles));
     HB_TRY(timed(c, "dec_verify", [&] {
-      return launch_dec_verify(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n,
-                               h_aff, h_st, h_lines, w_aff, w_st, w_lines, d_status);
+      return on_exact_stream(c, [&](hipStream_t xs) {
+        return launch_dec_verify(xs, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n, h_aff,
+                                 h_st, h_lines, w_aff, w_st, w_lines, d_status);
+      });
     }));
     return end_verify(c);
   }
@@ -824,8 +863,10 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
     HB_TRY(prepare_g2(c, d_H, nullptr, n_inst, &h_aff, &h_st, &h_lines));
     HB_TRY(make_tiles(c, n_inst, offsets, &tiles, &n_tiles));
     HB_TRY(timed(c, "sig_verify", [&] {
-      return launch_sig_verify(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->n,
-                               h_aff, h_st, h_lines, d_status);
+      return on_exact_stream(c, [&](hipStream_t xs) {
+        return launch_sig_verify(xs, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->n, h_aff,
+                                 h_st, h_lines, d_status);
+      });
     }));
     return end_verify(c);
   }
@@ -1334,7 +1375,9 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (!created(hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming), "hipEventCreateWithFlags") ||
       !created(hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming), "hipEventCreateWithFlags") ||
       !created(hipEventCreateWithFlags(&c->ev_ext2, hipEventDisableTiming), "hipEventCreateWithFlags") ||
-      !created(hipEventCreateWithFlags(&c->ev_ext3, hipEventDisableTiming), "hipEventCreateWithFlags")) {
+      !created(hipEventCreateWithFlags(&c->ev_ext3, hipEventDisableTiming), "hipEventCreateWithFlags") ||
+      !created(hipEventCreateWithFlags(&c->ev_x_in, hipEventDisableTiming), "hipEventCreateWithFlags") ||
+      !created(hipEventCreateWithFlags(&c->ev_x_out, hipEventDisableTiming), "hipEventCreateWithFlags")) {
     hbtc_ctx_destroy(c);
     return HBTC_ERR_DEVICE;
   }
@@ -1391,6 +1434,8 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
   ev_free(c->ev_ext);
   ev_free(c->ev_ext2);
   ev_free(c->ev_ext3);
+  ev_free(c->ev_x_in);
+  ev_free(c->ev_x_out);
   delete c;
 }
 
@@ -1477,7 +1522,9 @@ int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_
                   const uint8_t* d_w, int32_t* d_status, G1A* d_adec = nullptr) {
   if (c->verify_mode == HBTC_MODE_PER_SHARE) {
     return timed(c, "pair_verify", [&] {
-      return launch_pair_verify(c->stream, n, d_a, d_q, nullptr, d_w, d_status);
+      return on_exact_stream(c, [&](hipStream_t xs) {
+        return launch_pair_verify(xs, n, d_a, d_q, nullptr, d_w, d_status);
+      });
     });
   }
   const uint32_t PB_CHUNK = c->pb_chunk;
@@ -1528,7 +1575,9 @@ int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_
                           counters + 1, leaves);
     }));
     HB_TRY(timed(c, "pair_verify", [&] {
-      return launch_pair_verify(c->stream, m, a, q, nullptr, w, st, leaves, counters + 1);
+      return on_exact_stream(c, [&](hipStream_t xs) {
+        return launch_pair_verify(xs, m, a, q, nullptr, w, st, leaves, counters + 1);
+      });
     }));
   }
   return HBTC_OK;
