@@ -43,9 +43,11 @@ import time
 # work queued behind it on the same queue: the merge at world size 1 cost 28.0 vs 16.5 ms per
 # 125-ciphertext slice and 101.7 vs 79.6 ms per C3 epoch; with 16 queues 17.7 / 80.0 ms, plain
 # runs unchanged (profiles/r03/hw_queues/).  HBTC_KEEP_HW_QUEUES=1 keeps the environment's value.
-# Only when run as a program (torchrun runs it as __main__ too): a test process that imports
-# this module keeps HIP's default (its many contexts' streams then share 4 queues).
-if __name__ == "__main__" and not os.environ.get("HBTC_KEEP_HW_QUEUES"):
+# Set on import too (a test process importing this module gets 16 queues for the whole process):
+# round 3's suite failed that way because the per-item exact kernels' ~6 KB/lane of scratch was
+# reserved on every queue they ran on; they now share one stream, and the suite
+# runs green with 16 queues (profiles/r04/run6/).
+if not os.environ.get("HBTC_KEEP_HW_QUEUES"):
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 import numpy as np
