@@ -77,6 +77,7 @@ SIGNATURES = {
     "hbtc_set_verify_mode": (_I32, [_P, _I32]),
     "hbtc_set_rlc_bits": (_I32, [_P, _U32]),
     "hbtc_get_rlc_bits": (_I32, [_P, ctypes.POINTER(_U32)]),
+    "hbtc_set_exact_below": (_I32, [_P, _U32]),
     "hbtc_trim_workspace": (_I32, [_P]),
     "hbtc_check_schedule_for": (_I32, [_P, _U32, ctypes.POINTER(_I32)]),
     "hbtc_sha3_256": (_I32, [_P, _SZ, _P]),
@@ -712,6 +713,11 @@ class Context:
     def set_rlc_bits(self, bits):
         """RLC scalar size: 128 (default, <= 2^-128 per group check) or 64 (<= 2^-64)."""
         self._check(self.lib.hbtc_set_rlc_bits(self.h, int(bits)), "hbtc_set_rlc_bits")
+
+    def set_exact_below(self, n_items):
+        """RLC share calls with fewer than n_items shares get exact cooperative checks of every
+        share instead of the group sums (default 256; 0 = always batch)."""
+        self._check(self.lib.hbtc_set_exact_below(self.h, int(n_items)), "hbtc_set_exact_below")
 
     def trim_workspace(self):
         """Free the context's cached device workspace (hbtc_trim_workspace)."""

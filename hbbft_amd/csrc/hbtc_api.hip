@@ -127,6 +127,7 @@ struct hbtc_ctx {
   // workspace buffers outgrown while work may still use them: freed at the next sync (hipFree
   // would synchronise the whole device in the middle of a pipelined call sequence)
   std::vector<void*> graveyard;
+  std::vector<void*> host_graveyard;  // the same for outgrown pinned host buffers (hipHostFree)
   int verify_mode = HBTC_MODE_RLC;
   bool track_senders = true;
   uint32_t rlc_bits = 128;  // hbtc_set_rlc_bits (default: the curve's ~2^-128 level)
@@ -141,6 +142,10 @@ struct hbtc_ctx {
   // layout of the small check levels (split levels, leaves) of calls on the paired schedules:
   // 3 = the latency form (gt6.h Pos.rep), 1 = the throughput form; HBTC_GT_REP overrides
   int small_rep = 3;
+  // RLC-mode share calls with fewer items than this skip the group sums: the item pass only
+  // decodes and lists every share for the exact cooperative leaf checks (hbtc_set_exact_below;
+  // HBTC_EXACT_BELOW)
+  uint32_t exact_below = 256;
   uint64_t probes = 0;     // probe passes run
   const uint32_t* last_leaf_count = nullptr;  // device counter of the last RLC call
   // Device ranges that combines still read, each with the event recorded after that combine:
@@ -213,21 +218,39 @@ int fail(hbtc_ctx* c, int code, const std::string& msg) {
   return code;
 }
 
-// Grow-only named device workspace.
+// The workspace names of one buffer on every lane: the current suffix is the lane's tag ("" or
+// "#l") followed by what a pass appends (".probe").
+std::string lane_tag(int l) { return l ? "#" + std::to_string(l) : std::string(); }
+std::vector<std::string> lane_keys(const hbtc_ctx* c, const std::string& name) {
+  const std::string tag = lane_tag(c->lane);
+  const std::string extra =
+      c->ws_suffix.compare(0, tag.size(), tag) == 0 ? c->ws_suffix.substr(tag.size()) : c->ws_suffix;
+  std::vector<std::string> keys;
+  for (int l = 0; l < hbtc_ctx::NL; ++l) keys.push_back(name + lane_tag(l) + extra);
+  return keys;
+}
+
+// Grow-only named device workspace, one per lane.  A buffer that grows (a small call followed
+// by a large one) grows on EVERY lane at once, and the old ones are retired until the next sync,
+// not freed: hipFree waits for the whole device, and lanes whose first call of the new size came
+// later used to grow mid-pipeline (c1's blocking calls, then C2's pipelined ones in one process:
+// 17-22 ms per C2 step for the first steps against 13.2).
 int ws(hbtc_ctx* c, const char* name, size_t bytes, void** out) {
-  DevBuf& b = c->bufs[c->ws_suffix.empty() ? std::string(name) : std::string(name) + c->ws_suffix];
+  const std::string key = c->ws_suffix.empty() ? std::string(name) : std::string(name) + c->ws_suffix;
+  DevBuf& b = c->bufs[key];
   if (bytes == 0) bytes = 16;
   if (b.cap < bytes) {
-    // a buffer that grows (a small call followed by a large one) is retired, not freed: the
-    // lanes still in flight may read it, and hipFree would wait for the whole device (c1's
-    // blocking calls and then C2's pipelined ones in one process: 13.2 -> 22.4 ms per C2 step)
-    if (b.p) c->graveyard.push_back(b.p);
-    b.p = nullptr;
-    b.cap = 0;
-    size_t want = bytes + bytes / 4;
-    hipError_t e = hipMalloc(&b.p, want);
-    if (e != hipSuccess) return fail(c, HBTC_ERR_OOM, std::string("hipMalloc ") + name);
-    b.cap = want;
+    const size_t want = bytes + bytes / 4;
+    for (const std::string& k : lane_keys(c, name)) {
+      DevBuf& x = c->bufs[k];
+      if (x.cap >= bytes && k != key) continue;
+      if (x.p) c->graveyard.push_back(x.p);
+      x.p = nullptr;
+      x.cap = 0;
+      hipError_t e = hipMalloc(&x.p, want);
+      if (e != hipSuccess) return fail(c, HBTC_ERR_OOM, std::string("hipMalloc ") + name);
+      x.cap = want;
+    }
   }
   *out = b.p;
   return HBTC_OK;
@@ -260,6 +283,10 @@ int sync(hbtc_ctx* c) {
   if (!c->graveyard.empty()) {  // (exact-stream work is ordered before later lane work)
     for (void* p : c->graveyard) HB_CHECK(c, hipFree(p));
     c->graveyard.clear();
+  }
+  if (!c->host_graveyard.empty()) {
+    for (void* p : c->host_graveyard) HB_CHECK(c, hipHostFree(p));
+    c->host_graveyard.clear();
   }
   return HBTC_OK;
 }
@@ -435,11 +462,20 @@ int stage_upload(hbtc_ctx* c, const char* name, const void* src, size_t bytes, h
   Stage& sg = c->stages[base + "@" + std::to_string(slot)];
   if (sg.used) HB_CHECK(c, hipEventSynchronize(sg.ev));  // the copy out of this slot is done
   if (sg.cap < bytes || !sg.h) {
-    if (sg.h) HB_CHECK(c, hipHostFree(sg.h));
-    sg.h = nullptr;
+    // every slot of every lane grows at once, the old buffers retired, not freed: hipHostFree
+    // waits for the device (slots outgrown one by one by a larger call than the ones before
+    // stalled every lane in flight: C2 after a few small calls)
     const size_t want = bytes + bytes / 4 + 256;
-    HB_CHECK(c, hipHostMalloc(&sg.h, want, hipHostMallocMapped | hipHostMallocPortable));
-    sg.cap = want;
+    for (const std::string& k : lane_keys(c, name))
+      for (unsigned j = 0; j < STAGE_SLOTS; ++j) {
+        Stage& x = c->stages[k + "@" + std::to_string(j)];
+        if (x.h && x.cap >= bytes && &x != &sg) continue;
+        if (x.h) c->host_graveyard.push_back(x.h);
+        x.h = nullptr;
+        x.cap = 0;
+        HB_CHECK(c, hipHostMalloc(&x.h, want, hipHostMallocMapped | hipHostMallocPortable));
+        x.cap = want;
+      }
   }
   if (!sg.ev) HB_CHECK(c, hipEventCreateWithFlags(&sg.ev, hipEventDisableTiming));
   if (bytes) memcpy(sg.h, src, bytes);
@@ -533,7 +569,7 @@ int prepare_g2(hbtc_ctx* c, const uint8_t* d0, const uint8_t* d1, uint32_t n, G2
 
 // Sender tracking view of one RLC call on key set ks (hbtc_kernels.h Suspects).
 Suspects suspects_of(hbtc_ctx* c, Keyset* ks, uint32_t* leaf_count, uint32_t* leaves) {
-  Suspects s{nullptr, 0, leaf_count, leaves};
+  Suspects s{nullptr, 0, leaf_count, leaves, 0};
   if (c->track_senders) {
     s.last_bad = ks->last_bad;
     s.now = ++ks->calls;
@@ -621,7 +657,8 @@ struct G2Prep {
 };
 uint32_t probe_size(const hbtc_ctx* c, const Keyset* ks, uint32_t n_ct);
 int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets,
-                 const uint32_t* d_idx, const uint8_t* d_share, int32_t* d_status, const G2Prep& pp);
+                 const uint32_t* d_idx, const uint8_t* d_share, int32_t* d_status, const G2Prep& pp,
+                 bool exact = false);
 
 int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t* d_H,
                    const uint8_t* d_w, const uint32_t* offsets, const uint32_t* d_idx,
@@ -668,12 +705,13 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   // Cold key set (no RLC call on it yet, sender tracking on): a probe pass over the first
   // ciphertexts finds the senders who lie on all of them before the call proper, so f Byzantine
   // senders do not send most of the first epoch's shares to the exact checks.
-  const uint32_t n_probe = probe_size(c, ks, n_ct);
+  const bool exact = n_items < c->exact_below;  // a small call: exact leaf checks only
+  const uint32_t n_probe = exact ? 0 : probe_size(c, ks, n_ct);
   if (n_probe) {
     HB_TRY(rlc_dec_pass(c, ks, n_probe, offsets, d_idx, d_share, nullptr, prep));
     ++c->probes;
   }
-  HB_TRY(rlc_dec_pass(c, ks, n_ct, offsets, d_idx, d_share, d_status, prep));
+  HB_TRY(rlc_dec_pass(c, ks, n_ct, offsets, d_idx, d_share, d_status, prep, exact));
   return end_verify(c);
 }
 
@@ -685,9 +723,11 @@ uint32_t probe_size(const hbtc_ctx* c, const Keyset* ks, uint32_t n_ct) {
 
 // One RLC pass over instances [0, n_ct) of a call whose G2 preparation is `pp`: tiles, item pass,
 // group-check levels, leaves, final statuses into d_status.  d_status == nullptr: the probe pass
-// (statuses into scratch, its own workspace: only its sender-tracking counts matter).
+// (statuses into scratch, its own workspace: only its sender-tracking counts matter).  exact: a
+// small call -- the item pass decodes and lists every share, no group levels, no tracking.
 int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets,
-                 const uint32_t* d_idx, const uint8_t* d_share, int32_t* d_status, const G2Prep& pp) {
+                 const uint32_t* d_idx, const uint8_t* d_share, int32_t* d_status, const G2Prep& pp,
+                 bool exact) {
   const bool probe = d_status == nullptr;
   const uint32_t n_items = offsets[n_ct];
   const std::string suffix0 = c->ws_suffix;
@@ -748,7 +788,7 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
   // the split levels pay on the plain-first schedule (C3: 86.2 -> 84.7 ms per epoch); on the
   // paired ones the sub-tile level is one launch where splitting is three dependent ones (the
   // 125-ciphertext slice: 17.1 ms per epoch without, 18.5 with; profiles/r04/run4/)
-  const bool split = c->split_levels && chk_mode == CHK_PLAIN_FIRST;
+  const bool split = !exact && c->split_levels && chk_mode == CHK_PLAIN_FIRST;
   SplitOut sp[3] = {};
   if (split) {
     for (int l = 0; l < 3; ++l) {
@@ -762,7 +802,8 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
     }
   }
   const SplitOut no_split{};
-  const Suspects sus = suspects_of(c, ks, leaf_count, leaves);
+  const Suspects sus =
+      exact ? Suspects{nullptr, 0, leaf_count, leaves, 1} : suspects_of(c, ks, leaf_count, leaves);
   HB_TRY(items_gate(c));
   HB_TRY(timed(c, "rlc_items", [&] {
     return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->tab,
@@ -770,7 +811,9 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
   }));
   HB_TRY(items_mark(c));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
-  if (chk_mode != CHK_PLAIN_FIRST) {
+  if (exact) {
+    // no group levels: every decoded share is on the leaf list
+  } else if (chk_mode != CHK_PLAIN_FIRST) {
     // latency form: paired levels (hbtc_check.hip k_chk_pair)
     const bool two = chk_mode == CHK_PAIR_LEAVES;
     HB_TRY(timed(c, "chk_tiles", [&] {
@@ -798,8 +841,9 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
   }
   // small calls (the paired schedules): their later levels hold a few hundred checks at most,
   // a chain of check latencies, so they run in the latency form
-  const int rep = chk_mode == CHK_PLAIN_FIRST ? 1 : c->small_rep;
-  if (split) {
+  const int rep = chk_mode == CHK_PLAIN_FIRST && !exact ? 1 : c->small_rep;
+  if (exact) {
+  } else if (split) {
     // split levels: listed tiles -> halves -> quarters -> eighths (unresolved eighths: leaves)
     static const char* const fam[3] = {"chk_split1", "chk_split2", "chk_split3"};
     for (int l = 1; l <= 3; ++l) {
@@ -907,33 +951,39 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   uint32_t* leaf_count = counters;
   uint32_t* sub_count = counters + 1;
   HB_CHECK(c, launch_zero_u32(c->stream, counters, 2));
-  const Suspects sus = suspects_of(c, ks, leaf_count, leaves);
+  // a small call: the item pass decodes and lists every share for the exact leaf checks
+  const bool exact = n_items < c->exact_below;
+  const Suspects sus =
+      exact ? Suspects{nullptr, 0, leaf_count, leaves, 1} : suspects_of(c, ks, leaf_count, leaves);
   HB_TRY(items_gate(c));
   HB_TRY(timed(c, "sig_items", [&] {
     return launch_sig_items(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->tab,
                             ks->n, key, sus, sums, dec, d_status);
   }));
   HB_TRY(items_mark(c));
-  HB_TRY(timed(c, "sig_lines", [&] {
-    return launch_plines(c->stream, 0, 2 * n_tiles, 0, nullptr, nullptr, tiles, sums, dec, tables,
-                         inf);
-  }));
+  if (!exact)
+    HB_TRY(timed(c, "sig_lines", [&] {
+      return launch_plines(c->stream, 0, 2 * n_tiles, 0, nullptr, nullptr, tiles, sums, dec, tables,
+                           inf);
+    }));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
   // paired checks either way (plain and weighted value of a group per unit); a small call goes
   // from the tiles straight to the leaves (check_mode)
   const bool to_leaves = check_mode(c, n_tiles) == CHK_PAIR_LEAVES;
   // the small calls' levels (tiles -> leaves: fewer tiles than half the SIMDs) are chains of check
   // latencies: the latency form (gt6.h Pos.rep = 3), unless HBTC_GT_REP=1
-  const bool rep3 = to_leaves && c->small_rep == 3;
-  HB_TRY(timed(c, "chk_tiles", [&] {
-    if (rep3)
-      return launch_sigchk_tiles_rep3(c->stream, n_tiles, tiles, sums, tables, inf, h_aff, h_lines,
-                                      h_st, d_status, leaf_count, leaves, true);
-    return launch_sigchk_tiles(c->stream, n_tiles, tiles, sums, tables, inf, h_aff, h_lines, h_st,
-                               d_status, to_leaves ? leaf_count : sub_count,
-                               to_leaves ? leaves : sub_list, to_leaves);
-  }));
-  if (!to_leaves) {
+  const bool rep3 = (to_leaves || exact) && c->small_rep == 3;
+  if (!exact) {
+    HB_TRY(timed(c, "chk_tiles", [&] {
+      if (rep3)
+        return launch_sigchk_tiles_rep3(c->stream, n_tiles, tiles, sums, tables, inf, h_aff,
+                                        h_lines, h_st, d_status, leaf_count, leaves, true);
+      return launch_sigchk_tiles(c->stream, n_tiles, tiles, sums, tables, inf, h_aff, h_lines, h_st,
+                                 d_status, to_leaves ? leaf_count : sub_count,
+                                 to_leaves ? leaves : sub_list, to_leaves);
+    }));
+  }
+  if (!to_leaves && !exact) {
     HB_TRY(timed(c, "sig_lines", [&] {
       return launch_plines(c->stream, 1, 16 * n_tiles, 0, sub_count, sub_list, tiles, sums, dec,
                            tables, inf);
@@ -1193,7 +1243,7 @@ size_t round256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 int pinned_grow(hbtc_ctx* c, void** h, size_t* cap, size_t bytes) {
   if (*cap >= bytes && *h) return HBTC_OK;
-  if (*h) HB_CHECK(c, hipHostFree(*h));
+  if (*h) c->host_graveyard.push_back(*h);  // retired until the next sync (see stage_upload)
   *h = nullptr;
   *cap = 0;
   const size_t want = bytes + bytes / 4 + 256;
@@ -1333,6 +1383,7 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (const char* e = getenv("HBTC_PROBE")) c->probe_cold = atoi(e) != 0;
   if (const char* e = getenv("HBTC_SPLIT")) c->split_levels = atoi(e) != 0;
   if (const char* e = getenv("HBTC_GT_REP")) c->small_rep = atoi(e) == 1 ? 1 : 3;
+  if (const char* e = getenv("HBTC_EXACT_BELOW")) c->exact_below = (uint32_t)atol(e);
   if (const char* e = getenv("HBTC_RLC_BITS")) {  // A/B runs: 64 or 128, like hbtc_set_rlc_bits
     const int b = atoi(e);
     if (b == 64 || b == 128) c->rlc_bits = (uint32_t)b;
@@ -1402,6 +1453,7 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
   for (auto& kv : c->bufs)
     if (kv.second.p) (void)hipFree(kv.second.p);
   for (void* p : c->graveyard) (void)hipFree(p);
+  for (void* p : c->host_graveyard) (void)hipHostFree(p);
   for (auto& kv : c->keysets) {
     (void)hipFree(kv.second.pk);
     (void)hipFree(kv.second.st);
@@ -2303,6 +2355,13 @@ int hbtc_set_sender_tracking(hbtc_ctx* c, int enable) {
   if (!c) return HBTC_ERR_ARG;
   Guard g(c);
   c->track_senders = enable != 0;
+  return HBTC_OK;
+}
+
+int hbtc_set_exact_below(hbtc_ctx* c, uint32_t n_items) {
+  if (!c) return HBTC_ERR_ARG;
+  Guard g(c);
+  c->exact_below = n_items;
   return HBTC_OK;
 }
 

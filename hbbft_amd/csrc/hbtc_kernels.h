@@ -30,8 +30,10 @@ struct Suspects {
   uint32_t now;              // this call's number (>= 1)
   uint32_t* leaf_count;      // the leaf list the item pass appends tracked shares to
   uint32_t* leaves;
+  uint32_t all;              // every share to the leaf list (a small call's exact checks)
 };
 __device__ __forceinline__ bool is_suspect(const Suspects& s, uint32_t id) {
+  if (s.all) return true;
   if (!s.last_bad) return false;
   const uint32_t b = s.last_bad[id];
   return b != 0 && s.now - b <= SUSPECT_WINDOW;

@@ -390,6 +390,12 @@ int hbtc_shard_instances(uint32_t n_dev, uint32_t n_inst, const uint32_t* offset
 #define HBTC_MODE_PER_SHARE 0
 #define HBTC_MODE_RLC 1
 int hbtc_set_verify_mode(hbtc_ctx* ctx, int mode);
+/* In RLC mode, hbtc_verify_dec_shares[_dev] / hbtc_verify_sig_shares[_dev] calls with fewer than
+ * n_items shares skip the group sums: the item pass only decodes, and every share gets the exact
+ * cooperative pairing check of the leaf level.  Two or three dependent launches instead of the
+ * item pass plus its group-check levels, for calls too small to fill the GPU (a single N = 10
+ * coin).  Default 256; 0 = always batch.  The decisions are the same either way. */
+int hbtc_set_exact_below(hbtc_ctx* ctx, uint32_t n_items);
 /* Size of the RLC scalars r_i = d0 + d1 x + d2 mu + d3 mu x (x the BLS parameter, mu = -x^2 mod r;
  * four digits of bits/4 bits; DESIGN.md §4, "x-adic scalars" and "Soundness"): 128 (default:
  * 2^128 distinct scalars: a wrong share survives a group check with probability <= 2^-128,

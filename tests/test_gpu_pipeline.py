@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
 def ctx():
     c = N.Context(0)
     c.set_verify_mode(N.MODE_RLC)
+    c.set_exact_below(0)
     yield c
     c.close()
 

@@ -77,6 +77,7 @@ def test_split_levels_equal_per_share_decisions(split):
     os.environ["HBTC_SPLIT"] = split
     try:
         ctx = N.Context(0)  # reads HBTC_SPLIT at creation
+        ctx.set_exact_below(0)
     finally:
         if old is None:
             del os.environ["HBTC_SPLIT"]
@@ -104,6 +105,7 @@ def test_split_levels_cut_leaf_checks():
     level) resolve tiles whose wrong shares sit in different eighths without exact leaf checks:
     only the eighths holding >= 2 wrong shares reach them."""
     ctx = N.Context(0)
+    ctx.set_exact_below(0)
     try:
         pk, H, w, counts, idx, shares, exp = _batch(ctx, random.Random(516))
         ks, _ = ctx.keyset_load(pk)
