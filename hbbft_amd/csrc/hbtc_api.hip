@@ -1574,6 +1574,71 @@ int hbtc_verify_sig_shares(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, con
   return sync(c);
 }
 
+// A few pair checks e(A_i, Q_i) == e(G1, W_i) (fewer than c->exact_below items): they have the
+// SignatureShare check's form (pk := A, H := Q, sigma := W), so they take its exact small-call
+// path with one instance per item -- A decoded (into d_adec when given), Q's line tables on
+// s_prep, the item pass decoding W with every item on the leaf list, W's projective lines, the
+// cooperative leaf checks.  Four dependent launches for c1's master signature instead of the
+// pair batch's item pass, line tables, Miller partials and final exponentiation.  Statuses as
+// k_pair_verify's: an A, Q or W that fails to decode is the item's DECODE_ERR.
+int pb_small_exact(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_q,
+                   const uint8_t* d_w, int32_t* d_status, G1A* d_adec) {
+  std::vector<uint32_t> offsets(n + 1), idx(n);
+  for (uint32_t i = 0; i <= n; ++i) offsets[i] = i;
+  for (uint32_t i = 0; i < n; ++i) idx[i] = i;
+  G1A* A = d_adec;
+  int32_t* a_st;
+  if (!A) HB_TRY(wst(c, "pbx.a", n, &A));
+  HB_TRY(wst(c, "pbx.ast", n, &a_st));
+  void* p;
+  HB_TRY(stage_upload(c, "pbx.idx", idx.data(), (size_t)4 * n, c->stream, &p));
+  const uint32_t* d_idx = static_cast<const uint32_t*>(p);
+  HB_TRY(stream_after(c, c->s_prep, c->stream, c->ev_main));
+  G2A* h_aff;
+  int32_t* h_st;
+  Line* h_lines;
+  HB_TRY(prepare_g2(c, d_q, nullptr, n, &h_aff, &h_st, &h_lines, c->s_prep));
+  Tile* tiles;
+  uint32_t n_tiles;
+  HB_TRY(make_tiles(c, n, offsets.data(), &tiles, &n_tiles));
+  SigTileSums* sums;
+  G2A* dec;
+  Fq2* tables;
+  uint32_t *inf, *counters, *leaves;
+  HB_TRY(wst(c, "pbx.sums", n_tiles, &sums));
+  HB_TRY(wst(c, "pbx.dec", n, &dec));
+  HB_TRY(wst(c, "pbx.tables", (size_t)n * PLINES_FQ2, &tables));
+  HB_TRY(wst(c, "pbx.inf", n, &inf));
+  HB_TRY(wst(c, "pbx.counters", 2, &counters));
+  HB_TRY(wst(c, "pbx.leaves", (size_t)2 * n, &leaves));
+  HB_CHECK(c, launch_zero_u32(c->stream, counters, 2));
+  HB_TRY(timed(c, "pb_decode", [&] { return launch_g1_decode(c->stream, d_a, n, A, a_st); }));
+  RlcKey key{};  // no group sums: the scalars are never drawn
+  const Suspects sus{nullptr, 0, counters, leaves, 1};
+  HB_TRY(timed(c, "sig_items", [&] {
+    return launch_sig_items(c->stream, n_tiles, tiles, d_idx, d_w, A, a_st,
+                            reinterpret_cast<const PtXY*>(tables), n, key, sus, sums, dec, d_status);
+  }));
+  HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
+  HB_TRY(timed(c, "sig_lines", [&] {
+    return launch_plines(c->stream, 2, n, 0, counters, leaves, tiles, sums, dec, tables, inf);
+  }));
+  HB_TRY(timed(c, "chk_leaves", [&] {
+    const uint32_t lim = c->small_rep == 3 ? std::min(n, 8u * (uint32_t)c->n_cu) : 0u;
+    const hipError_t e = launch_sigchk_leaves_rep3(c->stream, n, lim, counters, leaves, d_idx, A,
+                                                   tables, inf, h_aff, h_lines, d_status);
+    if (e != hipSuccess) return e;
+    return launch_sigchk_leaves(c->stream, 0, n, counters, leaves, d_idx, A, tables, inf, h_aff,
+                                h_lines, d_status, lim);
+  }));
+  return timed(c, "rlc_finalize", [&] {
+    const hipError_t e = launch_rlc_finalize(c->stream, n_tiles, tiles, h_st, h_st, d_status, d_idx,
+                                             n, nullptr, nullptr, 0, 1);
+    if (e != hipSuccess) return e;
+    return launch_status_remap(c->stream, n, d_status, HBTC_INSTANCE_ERR, HBTC_DECODE_ERR);
+  });
+}
+
 // e(A_i, Q_i) == e(G1, W_i) for n items in device memory (A null: the G1 generator; Q trusted:
 // our own hash output, decoded without the subgroup check; statuses ACCEPT / REJECT /
 // DECODE_ERR as k_pair_verify's).  RLC mode: the pair-batch path of hbtc_pb.hip in chunks of
@@ -1590,6 +1655,7 @@ int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_
       });
     });
   }
+  if (d_a && n < c->exact_below) return pb_small_exact(c, n, d_a, d_q, d_w, d_status, d_adec);
   const uint32_t PB_CHUNK = c->pb_chunk;
   for (uint32_t base = 0; base < n; base += PB_CHUNK) {
     const uint32_t m = std::min(PB_CHUNK, n - base);

@@ -40,7 +40,7 @@ __device__ __forceinline__ bool is_suspect(const Suspects& s, uint32_t id) {
 }
 struct RlcKey {
   uint32_t k[8];  // ChaCha20 key, fresh from the host's random source for every call
-  uint32_t bits;  // 64: r_i = a_i + b_i mu with 32-bit halves (default); 128: 64-bit halves
+  uint32_t bits;  // 128 (default): four 32-bit x-adic digits (rlc_common.h); 64: 16-bit digits
 };
 // Partial sums of one tile: [0..7] the 8-share sub-tiles, [8] the whole tile.  The weighted
 // sums carry the position of every share inside its group (0..7 in a sub-tile, 0..63 in the
@@ -88,6 +88,7 @@ hipError_t launch_rlc_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, 
                             TileSums* sums, G1A* dec, int32_t* status);
 // Final decisions; with last_bad != null, counts every sender's REJECTs in `rejects` and stamps
 // last_bad[i] = now for the senders with >= thresh of them (clearing the counts).
+hipError_t launch_status_remap(hipStream_t s, uint32_t n, int32_t* status, int32_t from, int32_t to);
 hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
                                const int32_t* h_status, const int32_t* w_status, int32_t* status,
                                const uint32_t* idx, uint32_t n_pk, uint32_t* rejects,

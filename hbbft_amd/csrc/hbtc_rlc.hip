@@ -143,6 +143,14 @@ __global__ void __launch_bounds__(64) k_rlc_finalize(const Tile* __restrict__ ti
   }
 }
 
+// status `from` -> `to` (the pair checks run through the SignatureShare path: a Q that fails to
+// decode is the item's own DECODE_ERR there, not an instance error)
+__global__ void __launch_bounds__(256) k_status_remap(uint32_t n, int32_t* __restrict__ status,
+                                                      int32_t from, int32_t to) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && status[i] == from) status[i] = to;
+}
+
 // A sender whose REJECTs in this call reach `thresh` (1/8 of the call's average shares per
 // sender: a liar, not a sender hit by a stray corrupted share) is stamped with the call number;
 // the counts are cleared for the next call.
@@ -181,6 +189,11 @@ hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n_tiles, const Tile* tile
   if (last_bad)
     hipLaunchKernelGGL(k_track_update, dim3(rlc_blocks(n_pk, 256)), dim3(256), 0, s, n_pk, rejects,
                        last_bad, now, thresh);
+  return hipGetLastError();
+}
+hipError_t launch_status_remap(hipStream_t s, uint32_t n, int32_t* status, int32_t from, int32_t to) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_status_remap, dim3(rlc_blocks(n, 256)), dim3(256), 0, s, n, status, from, to);
   return hipGetLastError();
 }
 #endif  // part 6

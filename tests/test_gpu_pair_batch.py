@@ -30,6 +30,7 @@ def _gens():
 @pytest.fixture(scope="module")
 def ctx():
     c = N.Context(0)
+    c.set_exact_below(0)  # this module tests the pair-batch path: small calls batch too
     yield c
     c.close()
 
@@ -88,6 +89,7 @@ def test_verify_ciphertexts_across_chunks():
         c = N.Context(0)
     finally:
         del os.environ["HBTC_PB_CHUNK"]
+    c.set_exact_below(0)
     try:
         _ct_rlc_equals_per_share(c, 3 * 4096 + 130, extra_bad=(4095, 4096, 8191, 12287, 12290))
         c.trim_workspace()
@@ -141,3 +143,27 @@ def test_verify_sigs_rlc_equals_per_share(ctx):
     assert (st == ref).all(), np.nonzero(st != ref)
     assert [int(x) for x in np.nonzero(ref == N.REJECT)[0]] == [3, 70, 71, 149]
     assert ref[5] == N.DECODE_ERR
+
+
+@pytest.mark.parametrize("n", [1, 40, 255])
+def test_small_pair_calls_take_exact_leaf_checks(n):
+    """With the default hbtc_set_exact_below (256), Ciphertext::verify calls of fewer items run
+    as exact SignatureShare-form checks (A decoded, Q's line tables, W decoded and checked by the
+    cooperative leaf kernels): the per-item decisions of k_pair_verify on wrong w, bad encodings
+    of u / H / w, u = O, H = O, a cancelling pair; no pair-batch launch."""
+    c = N.Context(0)
+    c.timing_enable(True)
+    try:
+        us, Hs, ws = _ct_batch(c, random.Random(n + 11), n)
+        c.set_verify_mode(N.MODE_PER_SHARE)
+        ref = c.verify_ciphertexts(us, Hs, ws)
+        c.set_verify_mode(N.MODE_RLC)
+        c.timing_reset()
+        st = c.verify_ciphertexts(us, Hs, ws)
+        assert (st == ref).all(), (n, np.nonzero(st != ref))
+        assert c.timing_read("pb_items")[1] == 0 and c.timing_read("chk_leaves")[1] >= 1
+        if n > 20:
+            assert ref[13] == N.DECODE_ERR and ref[15] == N.ACCEPT and ref[16] == N.ACCEPT
+            assert ref[17] == N.REJECT and ref[10] == N.REJECT and ref[11] == N.REJECT
+    finally:
+        c.close()
