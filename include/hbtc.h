@@ -394,7 +394,9 @@ int hbtc_set_verify_mode(hbtc_ctx* ctx, int mode);
  * n_items shares skip the group sums: the item pass only decodes, and every share gets the exact
  * cooperative pairing check of the leaf level.  Two or three dependent launches instead of the
  * item pass plus its group-check levels, for calls too small to fill the GPU (a single N = 10
- * coin).  Default 256; 0 = always batch.  The decisions are the same either way. */
+ * coin).  hbtc_verify_sigs / hbtc_verify_ciphertexts / hbtc_decrypt calls with fewer than n_items
+ * items take the same exact checks in the SignatureShare form (e(A, Q) = e(G1, W)) instead of
+ * the pair batch.  Default 256; 0 = always batch.  The decisions are the same either way. */
 int hbtc_set_exact_below(hbtc_ctx* ctx, uint32_t n_items);
 /* Size of the RLC scalars r_i = d0 + d1 x + d2 mu + d3 mu x (x the BLS parameter, mu = -x^2 mod r;
  * four digits of bits/4 bits; DESIGN.md §4, "x-adic scalars" and "Soundness"): 128 (default:
