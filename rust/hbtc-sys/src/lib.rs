@@ -106,9 +106,15 @@ impl Context {
         self.ok(unsafe { ffi::hbtc_set_verify_mode(self.raw, mode) })
     }
 
-    /// RLC scalar size: 64 (default) or 128 bits (soundness 2^-64 / 2^-128 per group check).
+    /// RLC scalar size: 128 (default) or 64 bits (soundness 2^-128 / 2^-64 per group check).
     pub fn set_rlc_bits(&self, bits: u32) -> Result<()> {
         self.ok(unsafe { ffi::hbtc_set_rlc_bits(self.raw, bits) })
+    }
+
+    /// Calls with fewer than `n_items` items get exact checks only, no RLC batch (default 256;
+    /// 0 = always batch).  The decisions are the same either way.
+    pub fn set_exact_below(&self, n_items: u32) -> Result<()> {
+        self.ok(unsafe { ffi::hbtc_set_exact_below(self.raw, n_items) })
     }
 
     /// PublicKeyShare::verify for every SignatureShare of every coin instance (H = hash_g2(nonce)).
