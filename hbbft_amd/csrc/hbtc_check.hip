@@ -31,8 +31,12 @@ namespace hbtc {
 
 using gt::Pos;
 
+// Minimum waves per SIMD the check kernels' register budget must allow.  Three since round 4
+// (168 VGPRs, ~500 B/lane of scratch against 256 / ~200 at two): C3 11.74 -> 11.94-12.03 M
+// shares/s, adversarial 4.39 -> 4.55 M, C4 4.83 -> 4.96 M on one box; four (128 VGPRs, ~700 B)
+// falls back (profiles/r04/run18/).
 #ifndef HBTC_GT_WAVES
-#define HBTC_GT_WAVES 2  // minimum waves per SIMD the check kernels' register budget must allow
+#define HBTC_GT_WAVES 3
 #endif
 // The weighted passes run few groups (the failing ones: fewer waves than SIMDs): one wave per
 // SIMD, the full register file, no spills (C3: 13.9 -> 11.5 ms; the plain passes, whose grids
