@@ -355,11 +355,15 @@ int end_verify(hbtc_ctx* c) {
   return HBTC_OK;
 }
 
-// An item pass about to start on the current lane waits for the most recent item pass (on
-// another lane): item passes form one chain.
-int items_gate(hbtc_ctx* c) {
+// An item pass of n_tiles waves about to start on the current lane waits for the most recent
+// item pass (on another lane): large item passes form one chain, so each runs alone on the chip
+// beside the other lanes' check levels.  A pass that fits the chip in one round (at most two
+// waves per SIMD: 8 n_cu) is not chained -- the 125-ciphertext slice (2,000 tiles) runs 16.3
+// instead of 17.4 ms per epoch unchained, the 250 one (4,000) 29.3-29.9 chained against 30.6-31.4,
+// C3 (16,000) 84.2-84.5 against 85.1 (profiles/r04/run22/, run23/).
+int items_gate(hbtc_ctx* c, uint32_t n_tiles) {
   const int o = c->last_items_lane;
-  if (c->items_serial && o >= 0 && o != c->lane)
+  if (c->items_serial && n_tiles > 8u * (uint32_t)c->n_cu && o >= 0 && o != c->lane)
     HB_CHECK(c, hipStreamWaitEvent(c->stream, c->lanes[o].items_done, 0));
   return HBTC_OK;
 }
@@ -804,7 +808,7 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
   const SplitOut no_split{};
   const Suspects sus =
       exact ? Suspects{nullptr, 0, leaf_count, leaves, 1} : suspects_of(c, ks, leaf_count, leaves);
-  HB_TRY(items_gate(c));
+  HB_TRY(items_gate(c, n_tiles));
   HB_TRY(timed(c, "rlc_items", [&] {
     return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->tab,
                             ks->n, key, sus, sums, dec, d_status);
@@ -955,7 +959,7 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   const bool exact = n_items < c->exact_below;
   const Suspects sus =
       exact ? Suspects{nullptr, 0, leaf_count, leaves, 1} : suspects_of(c, ks, leaf_count, leaves);
-  HB_TRY(items_gate(c));
+  HB_TRY(items_gate(c, n_tiles));
   HB_TRY(timed(c, "sig_items", [&] {
     return launch_sig_items(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->tab,
                             ks->n, key, sus, sums, dec, d_status);
