@@ -241,7 +241,11 @@ int ws(hbtc_ctx* c, const char* name, size_t bytes, void** out) {
   if (bytes == 0) bytes = 16;
   if (b.cap < bytes) {
     const size_t want = bytes + bytes / 4;
+    // buffers past 256 MB (the pair batches' per-chunk line tables: 5 GB) grow on their own
+    // lane only: the calls that need them are long, and four copies would hold 20 GB
+    const bool all_lanes = want <= ((size_t)256 << 20);
     for (const std::string& k : lane_keys(c, name)) {
+      if (!all_lanes && k != key) continue;
       DevBuf& x = c->bufs[k];
       if (x.cap >= bytes && k != key) continue;
       if (x.p) c->graveyard.push_back(x.p);

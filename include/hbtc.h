@@ -408,12 +408,12 @@ int hbtc_set_exact_below(hbtc_ctx* ctx, uint32_t n_items);
 int hbtc_set_rlc_bits(hbtc_ctx* ctx, uint32_t bits);
 int hbtc_get_rlc_bits(hbtc_ctx* ctx, uint32_t* bits);
 /* Free every cached device workspace buffer of the context (after completing its work; key sets
- * stay loaded).  Calls size their workspace to the largest batch seen and keep it, on all four
- * verification lanes at once (a buffer that grows mid-pipeline would stall every lane in
- * flight): the peak is set by hbtc_verify_ciphertexts / hbtc_verify_sigs / hbtc_decrypt
- * batches, which run in chunks of 2^18 items with 19.6 KB of G2 line tables per item (~5.8 GB
- * per chunk and lane; HBTC_PB_CHUNK = a smaller multiple of 64 lowers it), and by RLC
- * verification of n shares (~0.15 KB per share and lane). */
+ * stay loaded).  Calls size their workspace to the largest batch seen and keep it; buffers up to
+ * 256 MB grow on all four verification lanes at once (one that grew mid-pipeline would stall
+ * every lane in flight).  The peak is set by hbtc_verify_ciphertexts / hbtc_verify_sigs /
+ * hbtc_decrypt batches, which run in chunks of 2^18 items with 19.6 KB of G2 line tables per
+ * item (~5.8 GB per chunk, on the lanes that ran one; HBTC_PB_CHUNK = a smaller multiple of 64
+ * lowers it), and by RLC verification of n shares (~0.15 KB per share and lane). */
 int hbtc_trim_workspace(hbtc_ctx* ctx);
 /* Sender tracking (default on, RLC mode): a sender with many shares REJECTed (at least 1/8 of
  * the call's average shares per sender) by one of the last 16 RLC calls on a key set has its
