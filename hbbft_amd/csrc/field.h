@@ -326,9 +326,26 @@ HD void fq_acc_zero(FqAcc& a) {
 #pragma unroll
   for (int i = 0; i < 25; ++i) a.v[i] = 0;
 }
+// Karatsuba accumulation of an Fq2 sum (fq_acc_kara below): X starts at 24 p^2 (a multiple of p,
+// so the residue is unchanged) and ends at 24 p^2 + sum (a0 b0 - a1 b1) < 48 p^2 for up to 6 terms
+// of operands < 2p; Y ends at sum (a0 b1 + a1 b0) < 48 p^2.  In between both wrap modulo 2^800.
+HBTC_CONST uint32_t FQ_ACC_K24[25] = {
+    0xaaa55558u, 0x9ff00002u, 0x1544600bu, 0xb6420ac3u, 0x319db7c3u, 0x1424d451u, 0xdaa92e4au, 0xa1f5ae3du, 0x8da706e1u, 0xdc5c87cau, 0x9248ab8bu, 0xc1c926acu, 0xe356681au, 0xfc9edcc8u, 0x24cafa66u, 0x8f9437bau, 0xeedd1b87u, 0xa586d6dcu, 0x5a86a0e9u, 0x44ad9579u, 0x346b8dedu, 0x1bbb55ffu, 0x5250faafu, 0x3f653771u, 0x00000000u};
+HD void fq_acc_k24(FqAcc& a) {
+#pragma unroll
+  for (int i = 0; i < 25; ++i) a.v[i] = FQ_ACC_K24[i];
+}
+// a + b without the reduction: < 4p < 2^384 for operands < 2p (a Karatsuba sum operand)
+HD void fq_add_nr(Fq& r, const Fq& a, const Fq& b) { limbs_add<12>(r, a, b); }
 #if defined(__HIP_DEVICE_COMPILE__) && defined(HBTC_FQMUL_SR)
 HD void fq_acc_mac(FqAcc& acc, const Fq& a, const Fq& b) { fips::fq_mac_sr(acc.v, a.v, b.v); }
 HD void fq_acc_redc(Fq& r, const FqAcc& acc) { fips::fq_redc_sr(r.v, acc.v); }
+// the second accumulator's pair (pinned to v85..v109): a sum of two accumulators in one pass
+HD void fq_acc_mac2(FqAcc& acc, const Fq& a, const Fq& b) { fips::fq_mac2_sr(acc.v, a.v, b.v); }
+HD void fq_acc_redc2(Fq& r, const FqAcc& acc) { fips::fq_redc2_sr(r.v, acc.v); }
+// x += a b, y -= a b  /  x -= a b, y -= a b  (both accumulators in one product)
+HD void fq_acc_macsub(FqAcc& x, FqAcc& y, const Fq& a, const Fq& b) { fips::fq_macsub_sr(x.v, y.v, a.v, b.v); }
+HD void fq_acc_subsub(FqAcc& x, FqAcc& y, const Fq& a, const Fq& b) { fips::fq_subsub_sr(x.v, y.v, a.v, b.v); }
 #else
 HD void fq_acc_mac(FqAcc& acc, const Fq& a, const Fq& b) {
   uint32_t p[24];
@@ -372,7 +389,34 @@ HD void fq_acc_redc(Fq& r, const FqAcc& acc) {
   }
   for (int i = 0; i < 12; ++i) r.v[i] = x[i];
 }
+HD void fq_acc_mac2(FqAcc& acc, const Fq& a, const Fq& b) { fq_acc_mac(acc, a, b); }
+HD void fq_acc_redc2(Fq& r, const FqAcc& acc) { fq_acc_redc(r, acc); }
+// acc -= a b modulo 2^800
+HD void fq_acc_msb(FqAcc& acc, const Fq& a, const Fq& b) {
+  FqAcc p;
+  fq_acc_zero(p);
+  fq_acc_mac(p, a, b);
+  uint32_t c = 0;
+  for (int i = 0; i < 25; ++i) acc.v[i] = subb32(acc.v[i], p.v[i], c, &c);
+}
+HD void fq_acc_macsub(FqAcc& x, FqAcc& y, const Fq& a, const Fq& b) {
+  fq_acc_mac(x, a, b);
+  fq_acc_msb(y, a, b);
+}
+HD void fq_acc_subsub(FqAcc& x, FqAcc& y, const Fq& a, const Fq& b) {
+  fq_acc_msb(x, a, b);
+  fq_acc_msb(y, a, b);
+}
 #endif
+// x += a0 b0 - a1 b1, y += a0 b1 + a1 b0 (three half products: Karatsuba)
+HD void fq_acc_kara(FqAcc& x, FqAcc& y, const Fq& a0, const Fq& a1, const Fq& b0, const Fq& b1) {
+  Fq sa, sb;
+  fq_add_nr(sa, a0, a1);
+  fq_add_nr(sb, b0, b1);
+  fq_acc_macsub(x, y, a0, b0);
+  fq_acc_subsub(x, y, a1, b1);
+  fq_acc_mac2(y, sa, sb);
+}
 
 // canonical value in [0, p)
 HD void fq_canon(Fq& r, const Fq& a) {

@@ -222,26 +222,76 @@ HD void mul2_fq(Fq2& r, const Fq2& a, const Fq& y, const Pos& ps) {
 #endif
 #endif
 
+// With HBTC_GT_LAZY2 (default) both halves accumulate in ONE pass over the terms, half 1 in the
+// second accumulator (v85..v109 in the subroutine builds): each term's operands are fetched and
+// xi / the negation applied once instead of once per half.
+#ifndef HBTC_GT_LAZY2
+#define HBTC_GT_LAZY2 1
+#endif
+// With HBTC_GT_KARA (default, one-pass only) a term is Karatsuba on the two accumulators,
+// three half products instead of four (field.h fq_acc_kara): X = c0 + 24 p^2, Y = c1.
+#ifndef HBTC_GT_KARA
+#define HBTC_GT_KARA HBTC_GT_LAZY2
+#endif
 #if HBTC_GT_LAZY
-// acc += half h of x * y
-HD void mac2_half(FqAcc& acc, const Fq2& x, const Fq2& y, uint32_t h) {
-  if (h == 0) {
+#if HBTC_GT_LAZY2
+constexpr uint32_t GT_LAZY_PASSES = 1;
+#else
+constexpr uint32_t GT_LAZY_PASSES = 2;
+#endif
+// pass h: one-pass mode adds half 0 of x * y to a0 and half 1 to a1; two-pass mode adds half h
+// to a0
+HD void acc_init(FqAcc& a0, FqAcc& a1) {
+  if (HBTC_GT_KARA)
+    fq_acc_k24(a0);
+  else
+    fq_acc_zero(a0);
+  fq_acc_zero(a1);
+}
+HD void mac2_pass(FqAcc& a0, FqAcc& a1, const Fq2& x, const Fq2& y, uint32_t h) {
+  if (HBTC_GT_KARA) {
+    fq_acc_kara(a0, a1, x.c0, x.c1, y.c0, y.c1);
+  } else if (GT_LAZY_PASSES == 1) {
     Fq ny1;
     fq_neg(ny1, y.c1);
-    fq_acc_mac(acc, x.c0, y.c0);
-    fq_acc_mac(acc, x.c1, ny1);
+    fq_acc_mac(a0, x.c0, y.c0);
+    fq_acc_mac2(a1, x.c0, y.c1);
+    fq_acc_mac(a0, x.c1, ny1);
+    fq_acc_mac2(a1, x.c1, y.c0);
+  } else if (h == 0) {
+    Fq ny1;
+    fq_neg(ny1, y.c1);
+    fq_acc_mac(a0, x.c0, y.c0);
+    fq_acc_mac(a0, x.c1, ny1);
   } else {
-    fq_acc_mac(acc, x.c0, y.c1);
-    fq_acc_mac(acc, x.c1, y.c0);
+    fq_acc_mac(a0, x.c0, y.c1);
+    fq_acc_mac(a0, x.c1, y.c0);
+  }
+}
+// x * (y + 0u), y in Fq
+HD void mac1_pass(FqAcc& a0, FqAcc& a1, const Fq2& x, const Fq& y, uint32_t h) {
+  if (GT_LAZY_PASSES == 1) {
+    fq_acc_mac(a0, x.c0, y);
+    fq_acc_mac2(a1, x.c1, y);
+  } else {
+    fq_acc_mac(a0, h ? x.c1 : x.c0, y);
+  }
+}
+HD void redc_pass(Fq2& r, const FqAcc& a0, const FqAcc& a1, uint32_t h) {
+  if (GT_LAZY_PASSES == 1) {
+    fq_acc_redc(r.c0, a0);
+    fq_acc_redc2(r.c1, a1);
+  } else {
+    fq_acc_redc(h ? r.c1 : r.c0, a0);
   }
 }
 
 GTN void mul_lazy(Fq2& f, const Fq2& a, const Fq2& b, const Pos& ps) {
   Fq2 r;
 #pragma unroll
-  for (uint32_t h = 0; h < 2; ++h) {
-    FqAcc acc;
-    fq_acc_zero(acc);
+  for (uint32_t h = 0; h < GT_LAZY_PASSES; ++h) {
+    FqAcc a0, a1;
+    acc_init(a0, a1);
 #pragma unroll 1
     for (uint32_t i = 0; i < 6; ++i) {
       const bool wrap = i > ps.k;
@@ -250,9 +300,9 @@ GTN void mul_lazy(Fq2& f, const Fq2& a, const Fq2& b, const Pos& ps) {
       fetch2(ai, a, src(ps, i));
       fetch2(bj, b, src(ps, j));
       fq2_xi_if(bj, wrap, bj);
-      mac2_half(acc, ai, bj, h);
+      mac2_pass(a0, a1, ai, bj, h);
     }
-    fq_acc_redc(h ? r.c1 : r.c0, acc);
+    redc_pass(r, a0, a1, h);
   }
   f = r;
 }
@@ -317,9 +367,9 @@ HD void sqr(Fq2& f, const Fq2& a, const Pos& ps) {
     // the doubling and xi go on the second operand (reduced: < 2p), a missing term multiplies 0
     Fq2 r;
 #pragma unroll
-    for (uint32_t h = 0; h < 2; ++h) {
-      FqAcc lacc;
-      fq_acc_zero(lacc);
+    for (uint32_t h = 0; h < GT_LAZY_PASSES; ++h) {
+      FqAcc lacc, lacc1;
+      acc_init(lacc, lacc1);
 #pragma unroll 1
       for (uint32_t t = 0; t < 4; ++t) {
         const uint32_t e = (terms >> (8 * t)) & 0xffu;
@@ -332,9 +382,9 @@ HD void sqr(Fq2& f, const Fq2& a, const Pos& ps) {
         fq2_sel(aj, ((e >> 7) & 1u) && !none, d, aj);
         fq2_zero(z);
         fq2_sel(aj, none, z, aj);
-        mac2_half(lacc, ai, aj, h);
+        mac2_pass(lacc, lacc1, ai, aj, h);
       }
-      fq_acc_redc(h ? r.c1 : r.c0, lacc);
+      redc_pass(r, lacc, lacc1, h);
     }
     f = r;
     return;
@@ -376,9 +426,9 @@ HD void mul_line_t(Fq2& f, const Fq& pa, uint32_t a, const Fq2& Ad, const Fq& pb
     // xi on the f coefficient (the operand every term has), so an Fq Y stays one product a half
     Fq2 r;
 #pragma unroll
-    for (uint32_t h = 0; h < 2; ++h) {
-      FqAcc lacc;
-      fq_acc_zero(lacc);
+    for (uint32_t h = 0; h < GT_LAZY_PASSES; ++h) {
+      FqAcc lacc, lacc1;
+      acc_init(lacc, lacc1);
 HBTC_GT_SMALL_LOOP
       for (uint32_t t = 0; t < 3; ++t) {
         const uint32_t fk = t == 0 ? k : (t == 1 ? (k >= 2 ? k - 2 : k + 4) : (k >= 3 ? k - 3 : k + 3));
@@ -397,11 +447,11 @@ HBTC_GT_SMALL_LOOP
         }
         fq2_xi_if(x, (t == 1 && k < 2) || (t == 2 && k < 3), x);
         if (!Y2 && t == 2)  // uniform branch
-          fq_acc_mac(lacc, h ? x.c1 : x.c0, q.c0);
+          mac1_pass(lacc, lacc1, x, q.c0, h);
         else
-          mac2_half(lacc, x, q, h);
+          mac2_pass(lacc, lacc1, x, q, h);
       }
-      fq_acc_redc(h ? r.c1 : r.c0, lacc);
+      redc_pass(r, lacc, lacc1, h);
     }
     f = r;
     return;

@@ -275,15 +275,37 @@ def sr_call(name, label, square):
 # + p < 5.6p (12 words), then conditional subtractions of 4p and 2p.  48 p^2 bounds a sum of 12
 # products of reduced operands (< 2p each).
 SR_MACC, SR_CC = 60, 66
+# A second accumulator (v85..v109) with its own pair of subroutines (hbtc_fqmac2_sr,
+# hbtc_fqredc2_sr) lets the two Fq halves of an Fq2 sum accumulate in one pass over the terms.
+SR_MACC2 = 85
 
 
-def mac_body():
+def mac_body(base=SR_MACC, targets=None):
+    """Column digits of a * b added into (sign "+") or subtracted from ("-") each target
+    accumulator, modulo 2^800, one carry / borrow chain per target (s[66:67], s[68:69])."""
+    if targets is None:
+        targets = [(base, "+")]
     A = lambda i: "v%d" % (SR_A + i)
     B = lambda i: "v%d" % (SR_B + i)
-    ACCW = lambda i: "v%d" % (SR_MACC + i)
     reg = lambda n: "v%d" % (SR_ACC + n)
     pair = lambda p: "v[%d:%d]" % (SR_ACC + 2 * p, SR_ACC + 2 * p + 1)
-    cc, chain = "vcc", "s[%d:%d]" % (SR_CC, SR_CC + 1)
+    cc = "vcc"
+    chains = ["s[%d:%d]" % (SR_CC + 2 * t, SR_CC + 2 * t + 1) for t in range(len(targets))]
+
+    def fold(k, word):
+        for (tb, sign), chain in zip(targets, chains):
+            w = "v%d" % (tb + k)
+            if sign == "+":
+                if k == 0:
+                    out.append("v_add_co_u32_e64 %s, %s, %s, %s" % (w, chain, w, word))
+                else:
+                    out.append("v_addc_co_u32_e64 %s, %s, %s, %s, %s" % (w, chain, w, word, chain))
+            else:
+                if k == 0:
+                    out.append("v_sub_co_u32_e64 %s, %s, %s, %s" % (w, chain, w, word))
+                else:
+                    out.append("v_subb_co_u32_e64 %s, %s, %s, %s, %s" % (w, chain, w, word, chain))
+
     out = ["v_mov_b32 %s, 0" % reg(0), "v_mov_b32 %s, 0" % reg(1)]
     for k in range(23):
         p = k % 2
@@ -292,23 +314,20 @@ def mac_body():
         for i in range(lo_i, hi_i + 1):
             out.append("v_mad_u64_u32 %s, %s, %s, %s, %s" % (acc, cc, A(i), B(k - i), acc))
             out.append("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (c2, cc, "0" if i == lo_i else c2, cc))
-        if k == 0:
-            out.append("v_add_co_u32_e64 %s, %s, %s, %s" % (ACCW(0), chain, ACCW(0), lo))
-        else:
-            out.append("v_addc_co_u32_e64 %s, %s, %s, %s, %s" % (ACCW(k), chain, ACCW(k), lo, chain))
+        fold(k, lo)
         if k < 22:
             out.append("v_mov_b32 %s, %s" % (nlo, hi))
     # column 22's high word is digit 23 (its overflow word is 0: a * b < 2^768)
-    out.append("v_addc_co_u32_e64 %s, %s, %s, %s, %s" % (ACCW(23), chain, ACCW(23), reg(1), chain))
-    out.append("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (ACCW(24), chain, ACCW(24), chain))
+    fold(23, reg(1))
+    fold(24, "0")
     return out
 
 
-def redc_body():
+def redc_body(base=SR_MACC):
     Q = lambda i: "v%d" % (SR_Q + i)
     R = lambda i: "v%d" % (SR_A + i)
     P = lambda i: "s%d" % (SR_P + i)
-    ACCW = lambda i: "v%d" % (SR_MACC + i)
+    ACCW = lambda i: "v%d" % (base + i)
     reg = lambda n: "v%d" % (SR_ACC + n)
     pair = lambda p: "v[%d:%d]" % (SR_ACC + 2 * p, SR_ACC + 2 * p + 1)
     cc = "vcc"
@@ -363,34 +382,60 @@ def lazy_calls():
         '      "s_add_u32 s%d, s%d, %s@rel32@lo+4\\n\\t"\n' % (SR_TGT, SR_TGT, label) +
         '      "s_addc_u32 s%d, s%d, %s@rel32@hi+12\\n\\t"\n' % (SR_TGT + 1, SR_TGT + 1, label) +
         '      "s_swappc_b64 s[%d:%d], s[%d:%d]"' % (SR_RET, SR_RET + 1, SR_TGT, SR_TGT + 1))
-    accio = ", ".join('"+{v%d}"(acc[%d])' % (SR_MACC + i, i) for i in range(25))
+    text = ""
+    for sfx, base in (("", SR_MACC), ("2", SR_MACC2)):
+        accio = ", ".join('"+{v%d}"(acc[%d])' % (base + i, i) for i in range(25))
+        ins = ", ".join('"{v%d}"(a[%d])' % (SR_A + i, i) for i in range(12))
+        ins += ",\n        " + ", ".join('"{v%d}"(b[%d])' % (SR_B + i, i) for i in range(12))
+        clob = ['"v%d"' % v for v in range(SR_ACC, SR_ACC + 4)]
+        clob += ['"s%d"' % s for s in range(SR_P, SR_CC + 2)]
+        clob += ['"vcc"', '"scc"']
+        text += """__device__ __forceinline__ void fq_mac%s_sr(uint32_t* acc, const uint32_t* a, const uint32_t* b) {
+  asm volatile(
+%s
+      : %s
+      : %s
+      : %s);
+}
+""" % (sfx, call("hbtc_fqmac%s_sr" % sfx), accio, ins, ", ".join(clob))
+        outs = ", ".join('"={v%d}"(r[%d])' % (SR_A + i, i) for i in range(12))
+        ains = ", ".join('"{v%d}"(acc[%d])' % (base + i, i) for i in range(25))
+        rclob = ['"v%d"' % v for v in range(SR_Q, SR_ACC + 4)]
+        rclob += ['"s%d"' % s for s in range(SR_P, SR_RET + 2)]
+        rclob += ['"vcc"', '"scc"']
+        text += """__device__ __forceinline__ void fq_redc%s_sr(uint32_t* r, const uint32_t* acc) {
+  asm volatile(
+%s
+      : %s
+      : %s
+      : %s);
+}
+""" % (sfx, call("hbtc_fqredc%s_sr" % sfx), outs, ains, ", ".join(rclob))
+    # the Karatsuba pair: both accumulators at once
+    accio = ", ".join('"+{v%d}"(x[%d])' % (SR_MACC + i, i) for i in range(25))
+    accio += ",\n        " + ", ".join('"+{v%d}"(y[%d])' % (SR_MACC2 + i, i) for i in range(25))
     ins = ", ".join('"{v%d}"(a[%d])' % (SR_A + i, i) for i in range(12))
     ins += ",\n        " + ", ".join('"{v%d}"(b[%d])' % (SR_B + i, i) for i in range(12))
     clob = ['"v%d"' % v for v in range(SR_ACC, SR_ACC + 4)]
-    clob += ['"s%d"' % s for s in range(SR_P, SR_CC + 2)]
+    clob += ['"s%d"' % s for s in range(SR_P, SR_CC + 4)]
     clob += ['"vcc"', '"scc"']
-    mac = """__device__ __forceinline__ void fq_mac_sr(uint32_t* acc, const uint32_t* a, const uint32_t* b) {
+    for name in ("macsub", "subsub"):
+        text += """__device__ __forceinline__ void fq_%s_sr(uint32_t* x, uint32_t* y, const uint32_t* a, const uint32_t* b) {
   asm volatile(
 %s
       : %s
       : %s
       : %s);
 }
-""" % (call("hbtc_fqmac_sr"), accio, ins, ", ".join(clob))
-    outs = ", ".join('"={v%d}"(r[%d])' % (SR_A + i, i) for i in range(12))
-    ains = ", ".join('"{v%d}"(acc[%d])' % (SR_MACC + i, i) for i in range(25))
-    rclob = ['"v%d"' % v for v in range(SR_Q, SR_ACC + 4)]
-    rclob += ['"s%d"' % s for s in range(SR_P, SR_RET + 2)]
-    rclob += ['"vcc"', '"scc"']
-    redc = """__device__ __forceinline__ void fq_redc_sr(uint32_t* r, const uint32_t* acc) {
-  asm volatile(
-%s
-      : %s
-      : %s
-      : %s);
-}
-""" % (call("hbtc_fqredc_sr"), outs, ains, ", ".join(rclob))
-    return mac + redc
+""" % (name, call("hbtc_fq%s_sr" % name), accio, ins, ", ".join(clob))
+    return text
+
+
+# hbtc_fqmacsub_sr: X += a b, Y -= a b;  hbtc_fqsubsub_sr: X -= a b, Y -= a b (X = v60.., Y = v85..,
+# modulo 2^800).  With hbtc_fqmac2_sr (Y += a b) they accumulate an Fq2 product by Karatsuba:
+# X += a0 b0 - a1 b1, Y += (a0 + a1)(b0 + b1) - a0 b0 - a1 b1, three half products per term.
+KARA_BODIES = (("hbtc_fqmacsub_sr", ((SR_MACC, "+"), (SR_MACC2, "-"))),
+               ("hbtc_fqsubsub_sr", ((SR_MACC, "-"), (SR_MACC2, "-"))))
 
 
 def main_sr():
@@ -411,7 +456,9 @@ def main_sr():
     for label, square in (("hbtc_fqmul_sr", False), ("hbtc_fqsqr_sr", True)):
         for l in sr_text(label, square):
             print('    "%s\\n"' % l)
-    for label, body in (("hbtc_fqmac_sr", mac_body()), ("hbtc_fqredc_sr", redc_body())):
+    for label, body in (("hbtc_fqmac_sr", mac_body()), ("hbtc_fqredc_sr", redc_body()),
+                        ("hbtc_fqmac2_sr", mac_body(SR_MACC2)), ("hbtc_fqredc2_sr", redc_body(SR_MACC2))) + tuple(
+                            (label, mac_body(targets=list(t))) for label, t in KARA_BODIES):
         for l in lazy_text(label, body):
             print('    "%s\\n"' % l)
     print('    ::: "memory");')
@@ -574,12 +621,12 @@ def run_prog(prog, regs):
             s = val(y) - val(x) - carry[ci]
             carry[c] = 1 if s < 0 else 0
             store(d, s)
-        elif op == "v_sub_co_u32_e32":
+        elif op in ("v_sub_co_u32_e32", "v_sub_co_u32_e64"):
             d, c, x, y = args
             s = val(x) - val(y)
             carry[c] = 1 if s < 0 else 0
             store(d, s)
-        elif op == "v_subb_co_u32_e32":
+        elif op in ("v_subb_co_u32_e32", "v_subb_co_u32_e64"):
             d, c, x, y, ci = args
             s = val(x) - val(y) - carry[ci]
             carry[c] = 1 if s < 0 else 0
@@ -596,32 +643,75 @@ def run_prog(prog, regs):
 
 def selftest_lazy(trials=200):
     """ACC = sum of up to 12 products of operands < 2p through hbtc_fqmac_sr, then
-    hbtc_fqredc_sr: r < 2p and r = ACC 2^-384 mod p; a and b survive the MAC."""
+    hbtc_fqredc_sr: r < 2p and r = ACC 2^-384 mod p; a and b survive the MAC.  The same for the
+    second accumulator's pair, and neither pair touches the other accumulator."""
     import random
     M32 = (1 << 32) - 1
     rng = random.Random(10)
-    mac = lazy_text("x", mac_body())[2:-1]
-    redc = lazy_text("x", redc_body())[2:-1]
+    for base, other in ((SR_MACC, SR_MACC2), (SR_MACC2, SR_MACC)):
+        mac = lazy_text("x", mac_body(base))[2:-1]
+        redc = lazy_text("x", redc_body(base))[2:-1]
+        for t in range(trials):
+            regs = {"v%d" % (base + i): 0 for i in range(25)}
+            guard = [rng.getrandbits(32) for _ in range(25)]
+            regs.update({"v%d" % (other + i): guard[i] for i in range(25)})
+            total = 0
+            n = [1, 2, 12][t % 3] if t >= 3 else 12
+            for _ in range(n):
+                a = rng.randrange(2 * P_MOD) if t else 2 * P_MOD - 1
+                b = rng.randrange(2 * P_MOD) if t else 2 * P_MOD - 1
+                for i in range(12):
+                    regs["v%d" % (SR_A + i)] = (a >> (32 * i)) & M32
+                    regs["v%d" % (SR_B + i)] = (b >> (32 * i)) & M32
+                run_prog(mac, regs)
+                total += a * b
+                assert sum(regs["v%d" % (SR_A + i)] << (32 * i) for i in range(12)) == a
+                assert sum(regs["v%d" % (SR_B + i)] << (32 * i) for i in range(12)) == b
+            assert sum(regs["v%d" % (base + i)] << (32 * i) for i in range(25)) == total
+            run_prog(redc, regs)
+            r = sum(regs["v%d" % (SR_A + i)] << (32 * i) for i in range(12))
+            assert r < 2 * P_MOD and r % P_MOD == total * pow(2, -384, P_MOD) % P_MOD, (t, n)
+            assert sum(regs["v%d" % (base + i)] << (32 * i) for i in range(25)) == total
+            assert [regs["v%d" % (other + i)] for i in range(25)] == guard
+    # Karatsuba accumulation: X starts at K = 24 p^2, up to 6 terms of operands < 2p
+    K = 24 * P_MOD * P_MOD
+    macsub = lazy_text("x", mac_body(targets=list(KARA_BODIES[0][1])))[2:-1]
+    subsub = lazy_text("x", mac_body(targets=list(KARA_BODIES[1][1])))[2:-1]
+    mac2 = lazy_text("x", mac_body(SR_MACC2))[2:-1]
+    redc1 = lazy_text("x", redc_body(SR_MACC))[2:-1]
+    redc2 = lazy_text("x", redc_body(SR_MACC2))[2:-1]
+    M800 = (1 << 800) - 1
+
+    def load(v, base, words):
+        for i in range(words):
+            regs["v%d" % (base + i)] = (v >> (32 * i)) & M32
+
+    def read(base, words):
+        return sum(regs["v%d" % (base + i)] << (32 * i) for i in range(words))
+
     for t in range(trials):
-        regs = {"v%d" % (SR_MACC + i): 0 for i in range(25)}
-        total = 0
-        n = [1, 2, 12][t % 3] if t >= 3 else 12
-        for _ in range(n):
-            a = rng.randrange(2 * P_MOD) if t else 2 * P_MOD - 1
-            b = rng.randrange(2 * P_MOD) if t else 2 * P_MOD - 1
-            for i in range(12):
-                regs["v%d" % (SR_A + i)] = (a >> (32 * i)) & M32
-                regs["v%d" % (SR_B + i)] = (b >> (32 * i)) & M32
-            run_prog(mac, regs)
-            total += a * b
-            assert sum(regs["v%d" % (SR_A + i)] << (32 * i) for i in range(12)) == a
-            assert sum(regs["v%d" % (SR_B + i)] << (32 * i) for i in range(12)) == b
-        assert sum(regs["v%d" % (SR_MACC + i)] << (32 * i) for i in range(25)) == total
-        run_prog(redc, regs)
-        r = sum(regs["v%d" % (SR_A + i)] << (32 * i) for i in range(12))
-        assert r < 2 * P_MOD and r % P_MOD == total * pow(2, -384, P_MOD) % P_MOD, (t, n)
-        assert sum(regs["v%d" % (SR_MACC + i)] << (32 * i) for i in range(25)) == total
-    print("selftest_lazy ok (%d / %d instructions)" % (len(mac), len(redc)))
+        regs = {}
+        load(K, SR_MACC, 25)
+        load(0, SR_MACC2, 25)
+        c0 = c1 = 0
+        for _ in range(1 + t % 6 if t else 6):
+            a0, a1, b0, b1 = (rng.randrange(2 * P_MOD) if t else 2 * P_MOD - 1 for _ in range(4))
+            for f, x, y in ((macsub, a0, b0), (subsub, a1, b1), (mac2, a0 + a1, b0 + b1)):
+                load(x, SR_A, 12)
+                load(y, SR_B, 12)
+                run_prog(f, regs)
+            c0 += a0 * b0 - a1 * b1
+            c1 += a0 * b1 + a1 * b0
+        assert read(SR_MACC, 25) == (K + c0) & M800 and read(SR_MACC2, 25) == c1 & M800
+        assert 0 <= K + c0 < 48 * P_MOD * P_MOD and 0 <= c1 < 48 * P_MOD * P_MOD
+        run_prog(redc1, regs)
+        r0 = read(SR_A, 12)
+        run_prog(redc2, regs)
+        r1 = read(SR_A, 12)
+        Ri = pow(2, -384, P_MOD)
+        assert r0 < 2 * P_MOD and r0 % P_MOD == c0 * Ri % P_MOD, t
+        assert r1 < 2 * P_MOD and r1 % P_MOD == c1 * Ri % P_MOD, t
+    print("selftest_lazy ok (%d / %d instructions; Karatsuba pair %d)" % (len(mac), len(redc), len(macsub)))
 
 
 if __name__ == "__main__" and len(__import__("sys").argv) > 1 and __import__("sys").argv[1] == "--selftest-lazy":
