@@ -501,6 +501,169 @@ HD void xadic_mul_uniform(Jac<F>& r, const Aff<F>& p, const Aff<F>& xp, const Af
   r = acc;
 }
 
+// ---------------------------------------------------- x-adic scalars, one addition per bit
+// The same [r] P with ONE mixed addition per bit: the 15 nonzero sums T[b] = b0 P + b1 XP +
+// b2 m(P) + b3 m(XP), b = b0 + 2 b1 + 4 b2 + 8 b3, from a per-lane table (scratch memory: 15
+// points of 2 coordinates, read once per bit).  No inversion: the entries share ONE Z (Z*),
+// so their (X, Y) are affine points of the isomorphic curve y^2 = x^3 + b Z*^6, and the
+// doubling and mixed-addition formulas (a = 0) do not involve b: the double-and-add runs on
+// that curve and the result's Z is multiplied by Z* at the end.  Building the table:
+//   P at XP's Z1 (P1 = (x Z1^2, y Z1^3)); S = XP + P1 by a co-Z addition, which also returns XP
+//   at S's Z0 = Z1 H; P1 scaled by H -> the bases U = {P, XP, S} share Z0, and so do their
+//   images m(U) = (c X, Y, Z0);
+//   the 9 sums U[i] + m(U[j]) by co-Z additions (Z = Z0 H_k, never formed);
+//   every entry scaled to Z* = Z0 prod H_k (prefix / suffix products of the H_k).
+// 12 + 3 + 9 x 6 + 23 + 52 Fq products against the two-addition loop's 32 additions and
+// products by c, and its inversion (xadic_table).  Exceptional cases: H_k = 0 would need
+// U[i] = +-m(U[j]), i.e. a - mu b = 0 mod r for a, b in {1, x, 1 + x}: a nonzero integer of size
+// < r, so never for P in the prime-order group (items that fail the subgroup test never get
+// here).
+// G1 item passes (k_rlc_items, k_pb_items' A) use xadic_mul_tab16: 1.5 KB/lane of table.  The
+// G2 passes keep the two-addition loop by default: their table (2.9 KB/lane) takes k_sig_items
+// to 6-8 KB/lane of scratch, and the runtime reserves a kernel's scratch per hardware queue for
+// the device's wave slots: a multi-context process then fails with
+// HSA_STATUS_ERROR_OUT_OF_RESOURCES.
+#ifndef HBTC_XADIC16
+#define HBTC_XADIC16 1
+#endif
+#ifndef HBTC_XADIC16_G2
+#define HBTC_XADIC16_G2 0
+#endif
+template <class F>
+struct XY {
+  F x, y;
+};
+// co-Z addition of A and B (same Z): A + B, with A rescaled to the sum's Z (Z * H) in ax, ay;
+// returns H
+template <class F>
+HD void coz_add(XY<F>& s, F& ax, F& ay, F& h, const XY<F>& b) {
+  F r, hh, hhh, v, t;
+  fsub(h, b.x, ax);
+  fsub(r, b.y, ay);
+  fsqr(hh, h);
+  fmul(hhh, hh, h);
+  fmul(v, ax, hh);
+  fmul(ay, ay, hhh);
+  ax = v;
+  fsqr(s.x, r);
+  fsub(s.x, s.x, hhh);
+  fdbl(t, v);
+  fsub(s.x, s.x, t);
+  fsub(t, v, s.x);
+  fmul(s.y, r, t);
+  fsub(s.y, s.y, ay);
+}
+template <class F>
+HD void scale_xy(XY<F>& p, const F& l2, const F& l3) {
+  fmul(p.x, p.x, l2);
+  fmul(p.y, p.y, l3);
+}
+template <class F>
+HD void xadic_table16(XY<F> tab[16], F& zs, const Aff<F>& p, const Jac<F>& xpj, const Fq& c) {
+  XY<F> u[4];  // u[1] = P, u[2] = XP, u[3] = P + XP at the common Z0
+  F h, hh, hhh;
+  {
+    F z2, z3;
+    fsqr(z2, xpj.z);
+    fmul(z3, z2, xpj.z);
+    fmul(u[1].x, p.x, z2);
+    fmul(u[1].y, p.y, z3);
+    F ax = u[1].x, ay = u[1].y;  // P1, rescaled to Z0 below
+    XY<F> s;
+    F bx = xpj.x, by = xpj.y;
+    coz_add(s, bx, by, h, u[1]);  // s = XP + P1, (bx, by) = XP at Z1 H
+    u[3] = s;
+    u[2].x = bx;
+    u[2].y = by;
+    fsqr(hh, h);
+    fmul(hhh, hh, h);
+    XY<F> p1{ax, ay};
+    scale_xy(p1, hh, hhh);
+    u[1] = p1;
+    fmul(zs, xpj.z, h);  // Z0
+  }
+  XY<F> mu[4];
+  for (int j = 1; j < 4; ++j) {
+    fmul_by_fq(mu[j].x, u[j].x, c);
+    mu[j].y = u[j].y;
+  }
+  // the sums straight into the table, then scaled in place: lam_k = prod_{j != k} H_j from the
+  // prefix products and a running suffix product, Lam = prod H_j for the bases
+  F hk[9], pre[9];
+#pragma unroll
+  for (int i = 1; i < 4; ++i)
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      const int k = 3 * (i - 1) + (j - 1);
+      F ax = u[i].x, ay = u[i].y;
+      coz_add(tab[i + 4 * j], ax, ay, hk[k], mu[j]);
+    }
+  pre[0] = hk[0];
+#pragma unroll
+  for (int k = 1; k < 9; ++k) fmul(pre[k], pre[k - 1], hk[k]);
+  F run;
+#pragma unroll
+  for (int k = 8; k >= 0; --k) {
+    const int i = k / 3 + 1, j = k % 3 + 1;
+    F l, l2, l3;
+    if (k == 8)
+      l = pre[7];
+    else if (k == 0)
+      l = run;
+    else
+      fmul(l, pre[k - 1], run);
+    if (k == 8)
+      run = hk[8];
+    else if (k > 0)
+      fmul(run, run, hk[k]);
+    fsqr(l2, l);
+    fmul(l3, l2, l);
+    scale_xy(tab[i + 4 * j], l2, l3);
+  }
+  {
+    F l2, l3;
+    fsqr(l2, pre[8]);
+    fmul(l3, l2, pre[8]);
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      scale_xy(u[j], l2, l3);
+      tab[j] = u[j];
+      fmul_by_fq(tab[4 * j].x, u[j].x, c);
+      tab[4 * j].y = u[j].y;
+    }
+    fmul(zs, zs, pre[8]);  // Z* = Z0 prod H_k
+  }
+  fzero(tab[0].x);
+  fzero(tab[0].y);
+}
+
+template <class F>
+HD void xadic_mul_tab16(Jac<F>& r, const Aff<F>& p, const Jac<F>& xpj, const Fq& c,
+                        uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, int nbits) {
+  XY<F> tab[16];
+  F zs;
+  xadic_table16(tab, zs, p, xpj, c);
+  auto digit = [&](int bit) {
+    return ((d0 >> bit) & 1u) | (((d1 >> bit) & 1u) << 1) | (((d2 >> bit) & 1u) << 2) |
+           (((d3 >> bit) & 1u) << 3);
+  };
+  Jac<F> acc;
+  jac_set_inf(acc);
+  uint32_t b = digit(nbits - 1);
+  XY<F> t = tab[b];
+#pragma unroll 1
+  for (int bit = nbits - 1; bit >= 0; --bit) {
+    const uint32_t nb = bit > 0 ? digit(bit - 1) : 0u;
+    const XY<F> tn = tab[nb];  // the next bit's entry, loaded ahead of this bit's arithmetic
+    jac_dbl(acc, acc);
+    uniform_add(acc, t.x, t.y, b != 0);
+    b = nb;
+    t = tn;
+  }
+  fmul(acc.z, acc.z, zs);  // back from the isomorphic curve (infinity stays Z = 0)
+  r = acc;
+}
+
 // GLV endomorphism of G1: phi(x, y) = (beta x, y) = [-x^2] (x, y) on the r-order subgroup
 HD void g1_phi(G1A& r, const G1A& p) {
   Fq beta;

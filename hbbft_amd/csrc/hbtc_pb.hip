@@ -69,13 +69,17 @@ __global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n
       // eigenvalues x and mu = -x^2
       const XDigits xd = rlc_digits(key, i);
       if (!A.inf && !Q.inf) {  // r A, affine (one binary-Euclid inversion)
-        G1A xp, pxp;
         jac_neg(t1, t1);
-        xadic_table(xp, pxp, A, t1);
         Fq beta;
         fq_set(beta, G1_BETA);
         G1J t;
+#if HBTC_XADIC16
+        xadic_mul_tab16(t, A, t1, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+#else
+        G1A xp, pxp;
+        xadic_table(xp, pxp, A, t1);
         xadic_mul_uniform(t, A, xp, pxp, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+#endif
         if (!jac_is_inf(t)) {
           Fq zi, zi2, zi3;
           finv_fast(zi, t.z);
@@ -87,15 +91,20 @@ __global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n
         }
       }
       if (!W.inf) {  // r W, m = -psi^2: (x, y) -> (zeta x, y)
-        G2A xp, pxp;
+        G2A xp;
         g2_psi(xp.x, xp.y, W);
         xp.inf = 0;
         G2J xj;
         jac_from_aff(xj, xp);
-        xadic_table(xp, pxp, W, xj);
         Fq zeta;
         fq_set(zeta, G2_ZETA);
+#if HBTC_XADIC16_G2
+        xadic_mul_tab16(S, W, xj, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+#else
+        G2A pxp;
+        xadic_table(xp, pxp, W, xj);
         xadic_mul_uniform(S, W, xp, pxp, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+#endif
       }
     }
     rA[i] = ra;

@@ -96,12 +96,16 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
         } else {
           const XDigits xd = rlc_digits(key, item);
           if (!d.inf) {
-            G1A xp, pxp;
             jac_neg(t1, t1);
-            xadic_table(xp, pxp, d, t1);
             Fq beta;
             fq_set(beta, G1_BETA);
+#if HBTC_XADIC16
+            xadic_mul_tab16(S, d, t1, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+#else
+            G1A xp, pxp;
+            xadic_table(xp, pxp, d, t1);
             xadic_mul_uniform(S, d, xp, pxp, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+#endif
           }
           if (!pk[id].inf) rlc_pk_mul_x(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, xd);
         }

@@ -65,15 +65,20 @@ __global__ void __launch_bounds__(64, W) k_sig_items(
           // -psi^2 = (zeta x, y) of eigenvalue mu = -x^2
           const XDigits xd = rlc_digits(key, item);
           if (!sg.inf) {
-            G2A xp, pxp;
+            G2A xp;
             g2_psi(xp.x, xp.y, sg);
             xp.inf = 0;
             G2J xj;
             jac_from_aff(xj, xp);
-            xadic_table(xp, pxp, sg, xj);
             Fq zeta;
             fq_set(zeta, G2_ZETA);
+#if HBTC_XADIC16_G2
+            xadic_mul_tab16(S, sg, xj, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+#else
+            G2A pxp;
+            xadic_table(xp, pxp, sg, xj);
             xadic_mul_uniform(S, sg, xp, pxp, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+#endif
           }
           if (!pk[id].inf) rlc_pk_mul_x(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, xd);
         }

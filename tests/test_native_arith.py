@@ -92,6 +92,8 @@ def test_xadic_scalar_of_rlc_items(ht, nbits):
     cases += [tuple(rng.getrandbits(nbits) for _ in range(4)) for _ in range(4)]
     ht.ht_g1_mul_xadic.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
     ht.ht_g2_mul_xadic.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
+    ht.ht_g1_mul_xadic16.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
+    ht.ht_g2_mul_xadic16.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
     for d in cases:
         r = (d[0] + d[1] * B.X + d[2] * mu + d[3] * mu * B.X) % B.R
         arr = (ctypes.c_uint32 * 4)(*d)
@@ -103,6 +105,11 @@ def test_xadic_scalar_of_rlc_items(ht, nbits):
         o2 = buf(96)
         assert ht.ht_g2_mul_xadic(B.g2_compress(Q), ctypes.cast(arr, ctypes.c_void_p), nbits, o2) == 0
         assert o2.raw == B.g2_compress(B.g2_mul(Q, r)), ("g2", d)
+        # the one-addition-per-bit form (curve.h xadic_mul_tab16: 15-entry common-Z table)
+        assert ht.ht_g1_mul_xadic16(B.g1_compress(P), ctypes.cast(arr, ctypes.c_void_p), nbits, o) == 0
+        assert o.raw == B.g1_compress(B.g1_mul(P, r)), ("g1 tab16", d)
+        assert ht.ht_g2_mul_xadic16(B.g2_compress(Q), ctypes.cast(arr, ctypes.c_void_p), nbits, o2) == 0
+        assert o2.raw == B.g2_compress(B.g2_mul(Q, r)), ("g2 tab16", d)
 
 
 def test_xadic_digit_box_is_injective():

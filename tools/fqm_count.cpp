@@ -113,9 +113,9 @@ int main() {
   jac_add(acc2, qj, m2);
   const unsigned long long comb2 = hbtc_fqm_count;
 
-  // RLC item (k_rlc_items): decode (the subgroup test yields [|x|] d), the x-adic table {d, [x] d,
-  // d + [x] d} (one batched inversion), r*d by xadic_mul_uniform over nbits = 16 (64-bit RLC) or
-  // 32 (128-bit) digit bits, r*pk from the fixed-base table (4 nbits / 8 mixed additions, half
+  // RLC item (k_rlc_items): decode (the subgroup test yields [|x|] d), r*d by xadic_mul_tab16
+  // (the 15-entry common-Z table, one mixed addition per digit bit) over nbits = 16 (64-bit RLC)
+  // or 32 (128-bit) digit bits, r*pk from the fixed-base table (4 nbits / 8 mixed additions, half
   // of them with phi), and the item's share of the plain + position-weighted reduction tree of
   // its tile: per side 3 * 63 Jacobian additions and 57 doublings, two sides, over 64 items
   const uint32_t dg[4] = {0xa5a55a5au, 0x5a5aa5a5u, 0x3c3cc3c3u, 0xc3c33c3cu};
@@ -139,12 +139,16 @@ int main() {
     G1J t1;
     g1_decompress_t1(d2, t1, w1);
     jac_neg(t1, t1);
-    G1A xp, pxp;
-    xadic_table(xp, pxp, d2, t1);
     Fq beta;
     fq_set(beta, G1_BETA);
     const uint32_t m = nb == 32 ? 0xffffffffu : 0xffffu;
+#if HBTC_XADIC16
+    xadic_mul_tab16(rd, d2, t1, beta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
+#else
+    G1A xp, pxp;
+    xadic_table(xp, pxp, d2, t1);
     xadic_mul_uniform(rd, d2, xp, pxp, beta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
+#endif
     G1J rp;
     jac_set_inf(rp);
     jac_add_aff(rp, rp, gen1);
@@ -155,25 +159,30 @@ int main() {
     }
     (nb == 16 ? rlc_item : rlc_item_128) = hbtc_fqm_count + tree1;
   }
-  // SignatureShare RLC item (k_sig_items): G2 decode + subgroup test, the x-adic G2 table {s,
-  // psi(s), s + psi(s)}, r*sigma by xadic_mul_uniform in G2 (m = -psi^2 = (zeta x, y)), r*pk
+  // SignatureShare RLC item (k_sig_items): G2 decode + subgroup test, r*sigma by
+  // xadic_mul_tab16 in G2 ([x] s = psi(s)) (m = -psi^2 = (zeta x, y)), r*pk
   // from the fixed-base table, and the item's share of the G2 and G1 plain + weighted tile trees
   unsigned long long sig_rlc_item = 0, sig_rlc_item_128 = 0;
   for (int nb : {16, 32}) {
     hbtc_fqm_count = 0;
     G2A s2;
     g2_decompress(s2, w2);
-    G2A xp, pxp;
+    G2A xp;
     g2_psi(xp.x, xp.y, s2);
     xp.inf = 0;
     G2J xj;
     jac_from_aff(xj, xp);
-    xadic_table(xp, pxp, s2, xj);
     Fq zeta;
     fq_set(zeta, G2_ZETA);
     const uint32_t m = nb == 32 ? 0xffffffffu : 0xffffu;
     G2J r2;
+#if HBTC_XADIC16_G2
+    xadic_mul_tab16(r2, s2, xj, zeta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
+#else
+    G2A pxp;
+    xadic_table(xp, pxp, s2, xj);
     xadic_mul_uniform(r2, s2, xp, pxp, zeta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
+#endif
     G1J rp;
     jac_set_inf(rp);
     jac_add_aff(rp, rp, gen1);
