@@ -518,16 +518,16 @@ HD void xadic_mul_uniform(Jac<F>& r, const Aff<F>& p, const Aff<F>& xp, const Af
 // U[i] = +-m(U[j]), i.e. a - mu b = 0 mod r for a, b in {1, x, 1 + x}: a nonzero integer of size
 // < r, so never for P in the prime-order group (items that fail the subgroup test never get
 // here).
-// G1 item passes (k_rlc_items, k_pb_items' A) use xadic_mul_tab16: 1.5 KB/lane of table.  The
-// G2 passes keep the two-addition loop by default: their table (2.9 KB/lane) takes k_sig_items
-// to 6-8 KB/lane of scratch, and the runtime reserves a kernel's scratch per hardware queue for
-// the device's wave slots: a multi-context process then fails with
-// HSA_STATUS_ERROR_OUT_OF_RESOURCES.
+// G1 item passes (k_rlc_items, k_pb_items' A) use xadic_mul_tab16: 1.5 KB/lane of table.  On G2
+// the table is 2.9 KB/lane and takes k_sig_items to 6-8 KB/lane of scratch; the runtime reserves
+// a kernel's scratch per hardware queue for the device's wave slots, so only the
+// throughput form of k_sig_items uses it, on the process-wide exact stream (HBTC_XADIC16_G2);
+// k_pb_items' W and the small-call form keep the two-addition loop.
 #ifndef HBTC_XADIC16
 #define HBTC_XADIC16 1
 #endif
 #ifndef HBTC_XADIC16_G2
-#define HBTC_XADIC16_G2 0
+#define HBTC_XADIC16_G2 1
 #endif
 template <class F>
 struct XY {

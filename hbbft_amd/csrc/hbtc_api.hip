@@ -965,8 +965,12 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
       exact ? Suspects{nullptr, 0, leaf_count, leaves, 1} : suspects_of(c, ks, leaf_count, leaves);
   HB_TRY(items_gate(c, n_tiles));
   HB_TRY(timed(c, "sig_items", [&] {
-    return launch_sig_items(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->tab,
-                            ks->n, key, sus, sums, dec, d_status);
+    auto go = [&](hipStream_t s) {
+      return launch_sig_items(s, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->tab, ks->n, key,
+                              sus, sums, dec, d_status);
+    };
+    // the throughput form's scratch (curve.h HBTC_XADIC16_G2) is held by one queue
+    return sig_items_big(n_tiles) ? on_exact_stream(c, go) : go(c->stream);
   }));
   HB_TRY(items_mark(c));
   if (!exact)
@@ -1624,8 +1628,11 @@ int pb_small_exact(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d
   RlcKey key{};  // no group sums: the scalars are never drawn
   const Suspects sus{nullptr, 0, counters, leaves, 1};
   HB_TRY(timed(c, "sig_items", [&] {
-    return launch_sig_items(c->stream, n_tiles, tiles, d_idx, d_w, A, a_st,
-                            reinterpret_cast<const PtXY*>(tables), n, key, sus, sums, dec, d_status);
+    auto go = [&](hipStream_t s) {
+      return launch_sig_items(s, n_tiles, tiles, d_idx, d_w, A, a_st,
+                              reinterpret_cast<const PtXY*>(tables), n, key, sus, sums, dec, d_status);
+    };
+    return sig_items_big(n_tiles) ? on_exact_stream(c, go) : go(c->stream);
   }));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
   HB_TRY(timed(c, "sig_lines", [&] {

@@ -158,6 +158,9 @@ hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t*
                              uint32_t rep3_limit = 0);
 
 // ---- RLC batch verification of SignatureShares (hbtc_sig.hip, checks in hbtc_check.hip)
+// the two-wave throughput form of k_sig_items (with HBTC_XADIC16_G2: the table form, launched on
+// the exact stream)
+bool sig_items_big(uint32_t n_tiles);
 hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* sigs, const G1A* pk, const int32_t* pk_status,
                             const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,

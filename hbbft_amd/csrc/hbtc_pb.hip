@@ -98,13 +98,9 @@ __global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n
         jac_from_aff(xj, xp);
         Fq zeta;
         fq_set(zeta, G2_ZETA);
-#if HBTC_XADIC16_G2
-        xadic_mul_tab16(S, W, xj, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
-#else
-        G2A pxp;
+        G2A pxp;  // the two-addition loop: the G2 table's scratch (curve.h HBTC_XADIC16_G2)
         xadic_table(xp, pxp, W, xj);
         xadic_mul_uniform(S, W, xp, pxp, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
-#endif
       }
     }
     rA[i] = ra;

@@ -26,7 +26,10 @@ namespace hbtc {
 // ms per step with W = 2 against 171 with W = 1 (profiles/r03/sig_waves/).
 // One wave per tile: decode every SignatureShare (zcash compressed G2 + subgroup check), r_i,
 // r_i sigma_i, r_i pk_i, then the plain and weighted tile / sub-tile sums in both groups.
-template <int W>
+// T16: r_i sigma_i by the 15-entry table (curve.h xadic_mul_tab16; 2.9 KB/lane more scratch).
+// Only the two-wave throughput form uses it, and it runs on the process-wide exact stream
+// (hbtc_api.hip on_exact_stream): the runtime reserves a kernel's scratch per hardware queue.
+template <int W, bool T16>
 __global__ void __launch_bounds__(64, W) k_sig_items(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
     const uint8_t* __restrict__ sigs, const G1A* __restrict__ pk,
@@ -72,13 +75,13 @@ __global__ void __launch_bounds__(64, W) k_sig_items(
             jac_from_aff(xj, xp);
             Fq zeta;
             fq_set(zeta, G2_ZETA);
-#if HBTC_XADIC16_G2
-            xadic_mul_tab16(S, sg, xj, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
-#else
-            G2A pxp;
-            xadic_table(xp, pxp, sg, xj);
-            xadic_mul_uniform(S, sg, xp, pxp, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
-#endif
+            if (T16) {
+              xadic_mul_tab16(S, sg, xj, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+            } else {
+              G2A pxp;
+              xadic_table(xp, pxp, sg, xj);
+              xadic_mul_uniform(S, sg, xp, pxp, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+            }
           }
           if (!pk[id].inf) rlc_pk_mul_x(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, xd);
         }
@@ -169,17 +172,19 @@ static inline uint32_t sig_blocks(uint64_t n, uint32_t bs) { return (uint32_t)((
 #define HBTC_SIG_ITEMS_W2_MIN 1024u  // tiles above which the two-wave form runs
 #endif
 
+bool sig_items_big(uint32_t n_tiles) { return n_tiles > HBTC_SIG_ITEMS_W2_MIN; }
+
 hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* sigs, const G1A* pk, const int32_t* pk_status,
                             const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,
                             SigTileSums* sums, G2A* dec, int32_t* status) {
   if (n_tiles == 0) return hipSuccess;
-  if (n_tiles > HBTC_SIG_ITEMS_W2_MIN)  // more tiles than SIMDs: throughput form
-    hipLaunchKernelGGL(k_sig_items<2>, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk, pk_status,
-                       pk_tab, n_pk, key, sus, sums, dec, status);
+  if (sig_items_big(n_tiles))  // more tiles than SIMDs: throughput form
+    hipLaunchKernelGGL((k_sig_items<2, HBTC_XADIC16_G2 != 0>), dim3(n_tiles), dim3(64), 0, s, tiles, idx,
+                       sigs, pk, pk_status, pk_tab, n_pk, key, sus, sums, dec, status);
   else
-    hipLaunchKernelGGL(k_sig_items<1>, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk, pk_status,
-                       pk_tab, n_pk, key, sus, sums, dec, status);
+    hipLaunchKernelGGL((k_sig_items<1, false>), dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk,
+                       pk_status, pk_tab, n_pk, key, sus, sums, dec, status);
   return hipGetLastError();
 }
 

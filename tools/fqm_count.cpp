@@ -162,7 +162,9 @@ int main() {
   // SignatureShare RLC item (k_sig_items): G2 decode + subgroup test, r*sigma by
   // xadic_mul_tab16 in G2 ([x] s = psi(s)) (m = -psi^2 = (zeta x, y)), r*pk
   // from the fixed-base table, and the item's share of the G2 and G1 plain + weighted tile trees
-  unsigned long long sig_rlc_item = 0, sig_rlc_item_128 = 0;
+  // both forms: the throughput kernel's 15-entry table (t16) and the small-call two-addition loop
+  unsigned long long sig_item[2][2] = {};  // [t16][nb == 32]
+  for (int t16 : {1, 0})
   for (int nb : {16, 32}) {
     hbtc_fqm_count = 0;
     G2A s2;
@@ -176,13 +178,13 @@ int main() {
     fq_set(zeta, G2_ZETA);
     const uint32_t m = nb == 32 ? 0xffffffffu : 0xffffu;
     G2J r2;
-#if HBTC_XADIC16_G2
-    xadic_mul_tab16(r2, s2, xj, zeta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
-#else
-    G2A pxp;
-    xadic_table(xp, pxp, s2, xj);
-    xadic_mul_uniform(r2, s2, xp, pxp, zeta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
-#endif
+    if (t16) {
+      xadic_mul_tab16(r2, s2, xj, zeta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
+    } else {
+      G2A pxp;
+      xadic_table(xp, pxp, s2, xj);
+      xadic_mul_uniform(r2, s2, xp, pxp, zeta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
+    }
     G1J rp;
     jac_set_inf(rp);
     jac_add_aff(rp, rp, gen1);
@@ -199,7 +201,7 @@ int main() {
     hbtc_fqm_count = 0;
     jac_dbl(t2, t2);
     const unsigned long long jdbl2 = hbtc_fqm_count;
-    (nb == 16 ? sig_rlc_item : sig_rlc_item_128) =
+    sig_item[t16][nb == 32] =
         mults + (2 * (189 * jadd2 + 57 * jdbl2) / 2 + 2 * (189 * jadd + 57 * jdbl) / 2 + 63) / 64;
   }
   G1J rp = rd;
@@ -270,7 +272,8 @@ int main() {
   printf("  \"g1_combine_item\": %llu,\n  \"g2_combine_item\": %llu,\n", comb1, comb2);
   printf("  \"g1_msm_combine\": %llu,\n", msm_combine);
   printf("  \"rlc_item\": %llu,\n  \"rlc_item_128\": %llu,\n  \"sig_rlc_item\": %llu,\n"
-         "  \"sig_rlc_item_128\": %llu,\n  \"rlc_group_check\": %llu\n}\n", rlc_item, rlc_item_128,
-         sig_rlc_item, sig_rlc_item_128, rlc_group);
+         "  \"sig_rlc_item_128\": %llu,\n  \"sig_rlc_item_loop\": %llu,\n"
+         "  \"sig_rlc_item_128_loop\": %llu,\n  \"rlc_group_check\": %llu\n}\n", rlc_item,
+         rlc_item_128, sig_item[1][0], sig_item[1][1], sig_item[0][0], sig_item[0][1], rlc_group);
   return 0;
 }

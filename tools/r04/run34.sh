@@ -1,8 +1,8 @@
 #!/bin/bash
 # r04 GPU session 34: the 15-entry x-adic table on the G1 item passes (k_rlc_items, k_pb_items'
-# A; default build), G2 on the two-addition loop: the FULL GPU suite at 16 queues first (the
-# per-queue scratch reservation), then C3, and C4 / C2 / C5 against
-# libhbtc_x16off.so (the two-addition loop everywhere), alternating.
+# A) and on the throughput form of k_sig_items (on the exact stream; default build): the FULL
+# GPU suite at 16 queues first (the per-queue scratch reservation), then C3, and
+# C4 / C2 / C5 against libhbtc_x16off.so (the two-addition loop everywhere), alternating.
 cd "$(dirname "$0")/../.." || exit 1
 O=gpurun_out/r04run34
 mkdir -p $O
