@@ -649,6 +649,10 @@ HD void xadic_mul_tab16(Jac<F>& r, const Aff<F>& p, const Jac<F>& xpj, const Fq&
   };
   Jac<F> acc;
   jac_set_inf(acc);
+#ifndef HBTC_TAB16_PREFETCH
+#define HBTC_TAB16_PREFETCH 1
+#endif
+#if HBTC_TAB16_PREFETCH
   uint32_t b = digit(nbits - 1);
   XY<F> t = tab[b];
 #pragma unroll 1
@@ -660,6 +664,15 @@ HD void xadic_mul_tab16(Jac<F>& r, const Aff<F>& p, const Jac<F>& xpj, const Fq&
     b = nb;
     t = tn;
   }
+#else
+#pragma unroll 1
+  for (int bit = nbits - 1; bit >= 0; --bit) {
+    const uint32_t b = digit(bit);
+    jac_dbl(acc, acc);
+    const XY<F> t = tab[b];
+    uniform_add(acc, t.x, t.y, b != 0);
+  }
+#endif
   fmul(acc.z, acc.z, zs);  // back from the isomorphic curve (infinity stays Z = 0)
   r = acc;
 }
