@@ -212,8 +212,8 @@ HD void mul2_fq(Fq2& r, const Fq2& a, const Fq& y, const Pos& ps) {
 //     half 0: sum x0 y0 + x1 (-y1),   half 1: sum x0 y1 + x1 y0,
 // -y1 as the reduced negation (< 2p), so every term is a product of two values < 2p and a half
 // sums at most 12 of them (< 48 p^2).  Per lane of a mul: 24 half products (144 MADs each) + 2
-// reductions, instead of 18 full Montgomery products (288 each).  Two passes (half 0, then half
-// 1) over one accumulator: it is pinned to 25 VGPRs, a second one would cost 25 more.
+// reductions, instead of 18 full Montgomery products (288 each).  HBTC_GT_LAZY2 / HBTC_GT_KARA
+// below: one pass over two accumulators, Karatsuba terms (18 half products).
 #ifndef HBTC_GT_LAZY
 #if !defined(__HIP_DEVICE_COMPILE__) || defined(HBTC_FQMUL_SR)
 #define HBTC_GT_LAZY 1
