@@ -19,7 +19,7 @@ SKG_PARTS := 10
 KOBJS := $(foreach p,$(PARTS),$(BUILD)/hbtc_kernels.p$(p).o) $(foreach p,$(RLC_PARTS),$(BUILD)/hbtc_rlc.p$(p).o) \
          $(foreach p,$(MSM_PARTS),$(BUILD)/hbtc_msm.p$(p).o) $(foreach p,$(SKG_PARTS),$(BUILD)/hbtc_skg.p$(p).o) \
          $(BUILD)/hbtc_check.c1.o $(BUILD)/hbtc_check.c2.o $(BUILD)/hbtc_sig.o $(BUILD)/hbtc_pb.o \
-         $(BUILD)/hbtc_bcast.o
+         $(BUILD)/hbtc_bcast.o $(BUILD)/hbtc_comb.o
 LIB := hbbft_amd/libhbtc.so
 
 .PHONY: all lib hosttest oracle clean resources roofline-constants
@@ -82,6 +82,11 @@ $(BUILD)/hbtc_sig.o: $(CSRC)/hbtc_sig.hip $(HDRS) | $(BUILD)
 # the pair-batch item pass (Ciphertext::verify / PublicKey::verify by RLC), helpers inlined,
 # the product as the shared subroutine
 $(BUILD)/hbtc_pb.o: $(CSRC)/hbtc_pb.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DHBTC_INLINE_ALL -DHBTC_FQMUL_SR -c $< -o $@
+
+# the small combines (t <= 64: one workgroup per instance), helpers inlined, the product as the
+# shared subroutine
+$(BUILD)/hbtc_comb.o: $(CSRC)/hbtc_comb.hip $(HDRS) | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -DHBTC_INLINE_ALL -DHBTC_FQMUL_SR -c $< -o $@
 
 # Reliable Broadcast: Reed-Solomon over GF(2^8), SHA3 Merkle trees and proofs

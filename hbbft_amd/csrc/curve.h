@@ -677,6 +677,300 @@ HD void xadic_mul_tab16(Jac<F>& r, const Aff<F>& p, const Jac<F>& xpj, const Fq&
   r = acc;
 }
 
+// ------------------------------------------- x-adic scalars, sign-aligned 8-entry table (GLV-SAC)
+// The same [r] P with one mixed addition per bit from EIGHT entries instead of fifteen, small
+// enough to stay in registers (AGPRs at one wave per SIMD) and be read by selects, so no per-lane
+// indexed table in scratch.  Sign-aligned recoding (Faz-Hernandez, Longa, Sanchez, "Efficient and
+// secure algorithms for GLV-based scalar multiplication", 2014, Alg. 1) of the digit vector
+// (k0, d1, d2, d3), k0 odd: l = nbits + 1 columns with
+//     k0 = sum_i s_i 2^i,  s_{l-1} = 1,  s_i = 2 bit_{i+1}(k0) - 1 in {+-1};
+//     d_j = sum_i u_j[i] s_i 2^i,  u_j[i] in {0, 1}   (computed LSB first: u_j[i] = d_j mod 2,
+//                                                      d_j = (d_j >> 1) + (u_j[i] && s_i < 0))
+// so [r] P = sum_i 2^i s_i T[u1 + 2 u2 + 4 u3] with T[u] = P + u1 XP + u2 m(P) + u3 m(XP): every
+// column adds +-one entry (the sign is a y negation), none is empty, the first one starts the sum.
+// k0 = d0 | 1; an even d0 is corrected by one final addition of -P (11 Fq products of ~2,500).
+// The entries are the co-Z sums U + m(V), U in {P, S = P + XP}, V in {P, XP, S} (6 co-Z
+// additions instead of 9) brought to one Z* as in xadic_table16.
+// Exceptional cases: none.  Before column i is added the running sum is [c] of a combination whose
+// P coefficient is 2 * (an odd integer) and whose other coefficients are below 2^(nbits+2) < |x|,
+// the entry's P coefficient is +-1, and such integer combinations of {1, x, mu, mu x} are distinct
+// mod r (the digit-box argument): acc != +-T, acc != O.  The final correction meets
+// acc == P only for the all-zero digit vector (r = 0), which is selected to infinity.
+template <class F>
+HD void xadic_table8(XY<F> tab[8], F& zs, const Aff<F>& p, const Jac<F>& xpj, const Fq& c) {
+  XY<F> u[4];  // u[1] = P, u[2] = XP, u[3] = S = P + XP at the common Z0
+  {
+    F h, hh, hhh, z2, z3;
+    fsqr(z2, xpj.z);
+    fmul(z3, z2, xpj.z);
+    fmul(u[1].x, p.x, z2);
+    fmul(u[1].y, p.y, z3);
+    F ax = u[1].x, ay = u[1].y;
+    XY<F> s;
+    F bx = xpj.x, by = xpj.y;
+    coz_add(s, bx, by, h, u[1]);  // s = XP + P1, (bx, by) = XP at Z1 H
+    u[3] = s;
+    u[2].x = bx;
+    u[2].y = by;
+    fsqr(hh, h);
+    fmul(hhh, hh, h);
+    XY<F> p1{ax, ay};
+    scale_xy(p1, hh, hhh);
+    u[1] = p1;
+    fmul(zs, xpj.z, h);  // Z0
+  }
+  // entry k = 0..5: U = (k & 1 ? S : P), V = u[k / 2 + 1]; table slot 2 (k / 2 + 1) + (k & 1)
+  F hk[6], pre[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    XY<F> mv;
+    fmul_by_fq(mv.x, u[k / 2 + 1].x, c);
+    mv.y = u[k / 2 + 1].y;
+    F ax = u[(k & 1) ? 3 : 1].x, ay = u[(k & 1) ? 3 : 1].y;
+    coz_add(tab[2 * (k / 2 + 1) + (k & 1)], ax, ay, hk[k], mv);
+  }
+  pre[0] = hk[0];
+#pragma unroll
+  for (int k = 1; k < 6; ++k) fmul(pre[k], pre[k - 1], hk[k]);
+  F run;
+#pragma unroll
+  for (int k = 5; k >= 0; --k) {
+    F l, l2, l3;
+    if (k == 5)
+      l = pre[4];
+    else if (k == 0)
+      l = run;
+    else
+      fmul(l, pre[k - 1], run);
+    if (k == 5)
+      run = hk[5];
+    else if (k > 0)
+      fmul(run, run, hk[k]);
+    fsqr(l2, l);
+    fmul(l3, l2, l);
+    scale_xy(tab[2 * (k / 2 + 1) + (k & 1)], l2, l3);
+  }
+  {
+    F l2, l3;
+    fsqr(l2, pre[5]);
+    fmul(l3, l2, pre[5]);
+    scale_xy(u[1], l2, l3);
+    scale_xy(u[3], l2, l3);
+    tab[0] = u[1];
+    tab[1] = u[3];
+    fmul(zs, zs, pre[5]);  // Z* = Z0 prod H_k
+  }
+}
+
+// the sign-aligned recoding above: bit i of m[j - 1] = u_j[i] (j = 1..3), for l = nbits + 1 columns
+HD void xadic_sac_recode(uint64_t m[3], uint32_t k0, uint32_t d1, uint32_t d2, uint32_t d3,
+                         int nbits) {
+  const uint32_t d[3] = {d1, d2, d3};
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    uint64_t k = d[j], mk = 0;
+#pragma unroll 1
+    for (int i = 0; i <= nbits; ++i) {
+      const uint64_t odd = k & 1u;
+      const uint64_t neg = (i < nbits) ? ((~(uint64_t)k0 >> (i + 1)) & 1u) : 0u;  // s_i = -1
+      mk |= odd << i;
+      k = (k >> 1) + (odd & neg);
+    }
+    m[j] = mk;
+  }
+}
+
+template <class F>
+HD void xy_sel(XY<F>& r, bool c, const XY<F>& a, const XY<F>& b) {  // r = c ? a : b
+  fsel(r.x, c, a.x, b.x);
+  fsel(r.y, c, a.y, b.y);
+}
+
+template <class F, bool LDS3 = false>
+HD void xadic_mul_sac8(Jac<F>& r, const Aff<F>& p, const Jac<F>& xpj, const Fq& c, uint32_t d0,
+                       uint32_t d1, uint32_t d2, uint32_t d3, int nbits, uint32_t* lds = nullptr,
+                       uint32_t lane = 0) {
+  XY<F> tab[8];
+  F zs;
+  xadic_table8(tab, zs, p, xpj, c);
+  const uint32_t k0 = d0 | 1u;
+  uint64_t m[3];
+  xadic_sac_recode(m, k0, d1, d2, d3, nbits);
+  // LDS3: entries 5..7 live in LDS (lds: 3 x NWD x 64 words, [entry][word][lane]: each lane reads
+  // its own column, conflict-free) and are read by a lane-dependent address, entries 0..4 stay in
+  // registers (k_rlc_items at two waves per SIMD: 256 VGPRs hold five entries beside the loop)
+  constexpr int NWD = (int)(sizeof(XY<F>) / 4);
+  if (LDS3) {
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(&tab[5 + e]);
+#pragma unroll
+      for (int w = 0; w < NWD; ++w) lds[(e * NWD + w) * 64 + lane] = src[w];
+    }
+  }
+  // the entry of column i, negated when s_i = -1: a select tree over the entries (constant
+  // indices only, so the register entries never go to scratch)
+  auto entry = [&](int i, XY<F>& t) {
+    const bool b1 = ((m[0] >> i) & 1u) != 0, b2 = ((m[1] >> i) & 1u) != 0;
+    const bool b3 = ((m[2] >> i) & 1u) != 0;
+    XY<F> e0, e1;
+    {
+      XY<F> a, b;
+      xy_sel(a, b1, tab[1], tab[0]);
+      xy_sel(b, b1, tab[3], tab[2]);
+      xy_sel(e0, b2, b, a);
+    }
+    if (LDS3) {
+      const uint32_t j = (b1 ? 1u : 0u) + (b2 ? 2u : 0u);  // entry 4 + j
+      const uint32_t li = j ? j - 1u : 0u;
+      XY<F> l;
+      uint32_t* dst = reinterpret_cast<uint32_t*>(&l);
+#pragma unroll
+      for (int w = 0; w < NWD; ++w) dst[w] = lds[(li * NWD + w) * 64 + lane];
+      xy_sel(e1, j != 0, l, tab[4]);
+    } else {
+      XY<F> a, b;
+      xy_sel(a, b1, tab[5], tab[4]);
+      xy_sel(b, b1, tab[7], tab[6]);
+      xy_sel(e1, b2, b, a);
+    }
+    xy_sel(t, b3, e1, e0);
+    const bool neg = i < nbits && (((uint64_t)k0 >> (i + 1)) & 1u) == 0;
+    F ny;
+    fneg(ny, t.y);
+    fsel(t.y, neg, ny, t.y);
+  };
+  Jac<F> acc;
+  {
+    XY<F> t;
+    entry(nbits, t);  // s = +1
+    acc.x = t.x;
+    acc.y = t.y;
+    fone(acc.z);
+  }
+#pragma unroll 1
+  for (int i = nbits - 1; i >= 0; --i) {
+    jac_dbl(acc, acc);
+    XY<F> t;
+    entry(i, t);
+    jac_madd_generic(acc, acc, t.x, t.y);
+  }
+  {  // d0 even: acc - P (P = tab[0] on the isomorphic curve)
+    const bool even = (d0 & 1u) == 0;
+    const bool zero = (d0 | d1 | d2 | d3) == 0;
+    F ny;
+    fneg(ny, tab[0].y);
+    Jac<F> n;
+    jac_madd_generic(n, acc, tab[0].x, ny);
+    fsel(acc.x, even, n.x, acc.x);
+    fsel(acc.y, even, n.y, acc.y);
+    fsel(acc.z, even, n.z, acc.z);
+    F z0;
+    fzero(z0);
+    fsel(acc.z, zero, z0, acc.z);
+  }
+  fmul(acc.z, acc.z, zs);  // back from the isomorphic curve
+  r = acc;
+}
+
+// ------------------------------------------ two-digit sign-aligned form (the small combines)
+// [d0] P + [d1] XP for digits below 2^nbits (nbits <= 64) and XP = [u] P, u = |x| (G1: from the
+// subgroup test's double-and-add; G2: -psi(P)), with ONE mixed addition per column from the
+// two-entry table {P, P + XP} at a common Z (the first step of xadic_table8), GLV-SAC recoded
+// like xadic_mul_sac8: nbits + 1 columns, k0 = d0 | 1, every column adds +-T[u1], an even d0 is
+// corrected by a final addition of -P, and d0 = d1 = 0 gives infinity.
+// The digits here are NOT random (base-u digits of Lagrange coefficients), so exceptional cases
+// are excluded by parity instead of probability: before column i the sum is [2A + 2B u] P with
+// A odd (the processed sign digits), the entry is [+-(1 + v u)] P (v in {0, 1}), both below r in
+// absolute value, and 2A -+ 1 + (2B -+ v) u = 0 is impossible (odd + even, u is even); 2A + 2B u
+// = 0 would make A = -B u even.  The correction meets [k0 + d1 u] P = +-P only for d0 = d1 = 0.
+template <class F>
+HD void sac2_mul(Jac<F>& r, const Aff<F>& p, const Jac<F>& xpj, uint64_t d0, uint64_t d1, int nbits) {
+  XY<F> t0, t1;  // P and S = P + XP at the common Z0 (= zs)
+  F zs;
+  {
+    F h, hh, hhh, z2, z3;
+    fsqr(z2, xpj.z);
+    fmul(z3, z2, xpj.z);
+    fmul(t0.x, p.x, z2);
+    fmul(t0.y, p.y, z3);
+    F bx = xpj.x, by = xpj.y;
+    coz_add(t1, bx, by, h, t0);  // t1 = XP + P1 at Z1 H
+    fsqr(hh, h);
+    fmul(hhh, hh, h);
+    scale_xy(t0, hh, hhh);
+    fmul(zs, xpj.z, h);
+  }
+  const uint64_t k0 = d0 | 1u;
+  const uint64_t all = nbits >= 64 ? ~0ull : ((1ull << nbits) - 1ull);
+  const uint64_t negm = ~(k0 >> 1) & all;  // bit i: s_i = -1 (columns below nbits)
+  uint64_t m1 = 0, k = d1;
+#pragma unroll 1
+  for (int i = 0; i < nbits; ++i) {
+    const uint64_t odd = k & 1u;
+    m1 |= odd << i;
+    k = (k >> 1) + (odd & (negm >> i) & 1u);
+  }
+  Jac<F> acc;  // the top column: s = +1, u1 = what is left of d1 (0 or 1)
+  fsel(acc.x, k != 0, t1.x, t0.x);
+  fsel(acc.y, k != 0, t1.y, t0.y);
+  fone(acc.z);
+#pragma unroll 1
+  for (int i = nbits - 1; i >= 0; --i) {
+    jac_dbl(acc, acc);
+    XY<F> t;
+    xy_sel(t, ((m1 >> i) & 1u) != 0, t1, t0);
+    F ny;
+    fneg(ny, t.y);
+    fsel(t.y, ((negm >> i) & 1u) != 0, ny, t.y);
+    jac_madd_generic(acc, acc, t.x, t.y);
+  }
+  {
+    const bool even = (d0 & 1u) == 0, zero = (d0 | d1) == 0;
+    F ny;
+    fneg(ny, t0.y);
+    Jac<F> n;
+    jac_madd_generic(n, acc, t0.x, ny);
+    fsel(acc.x, even, n.x, acc.x);
+    fsel(acc.y, even, n.y, acc.y);
+    fsel(acc.z, even, n.z, acc.z);
+    F z0;
+    fzero(z0);
+    fsel(acc.z, zero, z0, acc.z);
+  }
+  fmul(acc.z, acc.z, zs);
+  r = acc;
+}
+
+// Base-u digits of a canonical scalar k < r < u^4 (u = |x| = 2^16 v): k = sum_j d_j u^j, 0 <= d_j < u,
+// by three exact divisions by u (16-bit long division in 64-bit registers).  The combines' GLS / GLV
+// splits (hbtc_msm.hip, hbtc_comb.hip).
+HD void gls_u_digits(const uint32_t* k, uint64_t d[4]) {
+  constexpr uint64_t V = BLS_X_ABS >> 16;  // 0xd20100000001
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = k[i];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const uint32_t lo16 = w[0] & 0xffffu;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = (w[i] >> 16) | (i < 7 ? w[i + 1] << 16 : 0u);
+    uint64_t rem = 0;  // < V < 2^48, so rem * 2^16 + 16 bits fits 64
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+      uint64_t cur = (rem << 16) | (w[i] >> 16);
+      const uint32_t qh = (uint32_t)(cur / V);
+      rem = cur - (uint64_t)qh * V;
+      cur = (rem << 16) | (w[i] & 0xffffu);
+      const uint32_t ql = (uint32_t)(cur / V);
+      rem = cur - (uint64_t)ql * V;
+      w[i] = (qh << 16) | ql;
+    }
+    d[j] = (rem << 16) | lo16;
+  }
+  d[3] = ((uint64_t)w[1] << 32) | w[0];  // the quotient after three divisions: < u
+}
+
 // GLV endomorphism of G1: phi(x, y) = (beta x, y) = [-x^2] (x, y) on the r-order subgroup
 HD void g1_phi(G1A& r, const G1A& p) {
   Fq beta;

@@ -110,6 +110,9 @@ struct hbtc_ctx {
   int check_mode_forced = -1;  // HBTC_CHECK_MODE
   bool g2_gls = true;          // G2 combines through the ψ split (HBTC_G2_GLS=0: 255-bit terms)
   bool g1_glv = true;          // G1 combines through the φ split (HBTC_G1_GLV=0: 255-bit terms)
+  // combines of t <= COMB_SMALL_T shares in one launch (hbtc_comb.hip; HBTC_COMB_SMALL=0: the
+  // Pippenger chain for every t)
+  bool comb_small = true;
   std::string ws_suffix;
   hipStream_t stream = nullptr;  // main: items, checks, leaves
   hipStream_t s_prep = nullptr;  // per-instance G2 preparation, overlapped with the item pass
@@ -124,10 +127,17 @@ struct hbtc_ctx {
   std::map<uint32_t, Keyset> keysets;
   uint32_t next_keyset = 1;
   std::map<std::string, DevBuf> bufs;
-  // workspace buffers outgrown while work may still use them: freed at the next sync (hipFree
-  // would synchronise the whole device in the middle of a pipelined call sequence)
-  std::vector<void*> graveyard;
-  std::vector<void*> host_graveyard;  // the same for outgrown pinned host buffers (hipHostFree)
+  // Workspace buffers (device, and pinned host stages) outgrown while queued work may still use
+  // them.  Each retirement batch carries a fence: one event recorded on every stream that could
+  // read the old buffers.  A batch is freed once its fence has completed (checked at the next
+  // growth, without waiting) or at the next sync; hipFree / hipHostFree in the middle of a
+  // pipelined sequence would otherwise wait for the whole device on every growth.
+  struct Retired {
+    std::vector<void*> dev, host;
+    std::vector<hipEvent_t> fence;
+  };
+  std::vector<Retired> graveyard;
+  std::vector<void*> retiring_dev, retiring_host;  // collected by the growth in progress
   int verify_mode = HBTC_MODE_RLC;
   bool track_senders = true;
   uint32_t rlc_bits = 128;  // hbtc_set_rlc_bits (default: the curve's ~2^-128 level)
@@ -230,6 +240,70 @@ std::vector<std::string> lane_keys(const hbtc_ctx* c, const std::string& name) {
   return keys;
 }
 
+hipError_t exact_stream(int device, hipStream_t* out);
+bool exact_stream_exists(int device);
+
+// Close the batch of buffers retired by the growth in progress: a fence on every lane stream,
+// every preparation stream and the exact-kernel stream.
+int retire_fence(hbtc_ctx* c) {
+  if (c->retiring_dev.empty() && c->retiring_host.empty()) return HBTC_OK;
+  hbtc_ctx::Retired r;
+  r.dev.swap(c->retiring_dev);
+  r.host.swap(c->retiring_host);
+  std::vector<hipStream_t> streams;
+  for (const Lane& l : c->lanes) {
+    streams.push_back(l.stream);
+    streams.push_back(l.s_prep);
+  }
+  hipStream_t xs;
+  if (exact_stream_exists(c->device) && exact_stream(c->device, &xs) == hipSuccess) streams.push_back(xs);
+  hipError_t e = hipSuccess;
+  for (hipStream_t st : streams) {
+    hipEvent_t ev = nullptr;
+    if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) break;
+    r.fence.push_back(ev);
+    if ((e = hipEventRecord(ev, st)) != hipSuccess) break;
+  }
+  c->graveyard.push_back(std::move(r));  // kept even on error: freed at sync / destroy
+  HB_CHECK(c, e);
+  return HBTC_OK;
+}
+
+// Free the retired batches whose fence has completed (wait = true: every batch, after waiting for
+// its fence).  The list is taken out first, so a failing free cannot lead to a second one.
+int reap_retired(hbtc_ctx* c, bool wait) {
+  if (c->graveyard.empty()) return HBTC_OK;
+  std::vector<hbtc_ctx::Retired> all;
+  all.swap(c->graveyard);
+  hipError_t first = hipSuccess;
+  for (hbtc_ctx::Retired& r : all) {
+    bool done = true;
+    for (hipEvent_t ev : r.fence) {
+      const hipError_t q = wait ? hipEventSynchronize(ev) : hipEventQuery(ev);
+      if (q == hipErrorNotReady) {
+        done = false;
+        break;
+      }
+      if (q != hipSuccess && first == hipSuccess) first = q;
+    }
+    if (!done) {
+      c->graveyard.push_back(std::move(r));
+      continue;
+    }
+    for (void* p : r.dev) {
+      const hipError_t e = hipFree(p);
+      if (e != hipSuccess && first == hipSuccess) first = e;
+    }
+    for (void* p : r.host) {
+      const hipError_t e = hipHostFree(p);
+      if (e != hipSuccess && first == hipSuccess) first = e;
+    }
+    for (hipEvent_t ev : r.fence) (void)hipEventDestroy(ev);
+  }
+  HB_CHECK(c, first);
+  return HBTC_OK;
+}
+
 // Grow-only named device workspace, one per lane.  A buffer that grows (a small call followed
 // by a large one) grows on EVERY lane at once, and the old ones are retired until the next sync,
 // not freed: hipFree waits for the whole device, and lanes whose first call of the new size came
@@ -240,6 +314,7 @@ int ws(hbtc_ctx* c, const char* name, size_t bytes, void** out) {
   DevBuf& b = c->bufs[key];
   if (bytes == 0) bytes = 16;
   if (b.cap < bytes) {
+    HB_TRY(reap_retired(c, false));
     const size_t want = bytes + bytes / 4;
     // buffers past 256 MB (the pair batches' per-chunk line tables: 5 GB) grow on their own
     // lane only: the calls that need them are long, and four copies would hold 20 GB
@@ -248,13 +323,17 @@ int ws(hbtc_ctx* c, const char* name, size_t bytes, void** out) {
       if (!all_lanes && k != key) continue;
       DevBuf& x = c->bufs[k];
       if (x.cap >= bytes && k != key) continue;
-      if (x.p) c->graveyard.push_back(x.p);
+      if (x.p) c->retiring_dev.push_back(x.p);
       x.p = nullptr;
       x.cap = 0;
       hipError_t e = hipMalloc(&x.p, want);
-      if (e != hipSuccess) return fail(c, HBTC_ERR_OOM, std::string("hipMalloc ") + name);
+      if (e != hipSuccess) {
+        (void)retire_fence(c);
+        return fail(c, HBTC_ERR_OOM, std::string("hipMalloc ") + name);
+      }
       x.cap = want;
     }
+    HB_TRY(retire_fence(c));
   }
   *out = b.p;
   return HBTC_OK;
@@ -284,15 +363,7 @@ int sync(hbtc_ctx* c) {
     HB_CHECK(c, hipStreamSynchronize(l.stream));
     HB_CHECK(c, hipStreamSynchronize(l.s_prep));
   }
-  if (!c->graveyard.empty()) {  // (exact-stream work is ordered before later lane work)
-    for (void* p : c->graveyard) HB_CHECK(c, hipFree(p));
-    c->graveyard.clear();
-  }
-  if (!c->host_graveyard.empty()) {
-    for (void* p : c->host_graveyard) HB_CHECK(c, hipHostFree(p));
-    c->host_graveyard.clear();
-  }
-  return HBTC_OK;
+  return reap_retired(c, true);
 }
 
 void select_lane(hbtc_ctx* c, int l) {
@@ -478,12 +549,17 @@ int stage_upload(hbtc_ctx* c, const char* name, const void* src, size_t bytes, h
       for (unsigned j = 0; j < STAGE_SLOTS; ++j) {
         Stage& x = c->stages[k + "@" + std::to_string(j)];
         if (x.h && x.cap >= bytes && &x != &sg) continue;
-        if (x.h) c->host_graveyard.push_back(x.h);
+        if (x.h) c->retiring_host.push_back(x.h);
         x.h = nullptr;
         x.cap = 0;
-        HB_CHECK(c, hipHostMalloc(&x.h, want, hipHostMallocMapped | hipHostMallocPortable));
+        const hipError_t e = hipHostMalloc(&x.h, want, hipHostMallocMapped | hipHostMallocPortable);
+        if (e != hipSuccess) {
+          (void)retire_fence(c);
+          HB_CHECK(c, e);
+        }
         x.cap = want;
       }
+    HB_TRY(retire_fence(c));
   }
   if (!sg.ev) HB_CHECK(c, hipEventCreateWithFlags(&sg.ev, hipEventDisableTiming));
   if (bytes) memcpy(sg.h, src, bytes);
@@ -609,6 +685,11 @@ namespace {
 std::mutex g_exact_mu;
 hipStream_t g_exact_stream[64] = {};
 }  // namespace
+
+bool exact_stream_exists(int device) {
+  std::lock_guard<std::mutex> lk(g_exact_mu);
+  return device >= 0 && device < 64 && g_exact_stream[device] != nullptr;
+}
 
 hipError_t exact_stream(int device, hipStream_t* out) {
   std::lock_guard<std::mutex> lk(g_exact_mu);
@@ -1140,6 +1221,23 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
   void* p;
   HB_TRY(stage_upload(c, "comb.offsets", offsets, ((size_t)n_inst + 1) * 4, sc, &p));
   uint32_t* d_off = static_cast<uint32_t*>(p);
+  const size_t pbytes = group == 1 ? 48 : 96;
+  if (c->comb_small && t <= COMB_SMALL_T) {
+    // one launch per batch (hbtc_comb.hip): selection, Lagrange, per-share double-and-add and the
+    // tree sum in one workgroup per instance, on the decoded shares of the verification when this
+    // combine follows it over the same arrays
+    const auto& ld = c->last_dec;
+    const bool same = d_item_status && ld.status == d_item_status && ld.shares == d_pts &&
+                      ld.n_items == n_items;
+    const void* dec = same ? (group == 1 ? (const void*)ld.dec : (const void*)ld.dec2) : nullptr;
+    HB_TRY(timed_on(c, sc, "combine", [&] {
+      return launch_comb_small(sc, group, n_inst, t, d_off, d_item_status, d_idx, d_pts, dec,
+                               d_inst_status, d_out, group == 2 ? d_parity : nullptr);
+    }));
+    return note_comb_reads(c, {{d_idx, (size_t)n_items * 4}, {d_pts, n_items * pbytes},
+                               {d_item_status, d_item_status ? (size_t)n_items * 4 : 0},
+                               {dec, dec ? n_items * (group == 1 ? sizeof(G1A) : sizeof(G2A)) : 0}});
+  }
   const uint64_t terms = (uint64_t)n_inst * t;
   uint32_t *d_sel_pos, *d_sel_idx, *d_sel_cnt, *d_dup, *d_bad;
   Fr *d_lambda, *d_lws;
@@ -1255,11 +1353,14 @@ size_t round256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 int pinned_grow(hbtc_ctx* c, void** h, size_t* cap, size_t bytes) {
   if (*cap >= bytes && *h) return HBTC_OK;
-  if (*h) c->host_graveyard.push_back(*h);  // retired until the next sync (see stage_upload)
+  HB_TRY(reap_retired(c, false));
+  if (*h) c->retiring_host.push_back(*h);  // retired behind a fence (see retire_fence)
   *h = nullptr;
   *cap = 0;
   const size_t want = bytes + bytes / 4 + 256;
-  HB_CHECK(c, hipHostMalloc(h, want, hipHostMallocDefault));
+  const hipError_t e = hipHostMalloc(h, want, hipHostMallocDefault);
+  HB_TRY(retire_fence(c));
+  HB_CHECK(c, e);
   *cap = want;
   return HBTC_OK;
 }
@@ -1392,6 +1493,7 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (const char* e = getenv("HBTC_ITEMS_SERIAL")) c->items_serial = atoi(e) != 0;
   if (const char* e = getenv("HBTC_G2_GLS")) c->g2_gls = atoi(e) != 0;
   if (const char* e = getenv("HBTC_G1_GLV")) c->g1_glv = atoi(e) != 0;
+  if (const char* e = getenv("HBTC_COMB_SMALL")) c->comb_small = atoi(e) != 0;
   if (const char* e = getenv("HBTC_PROBE")) c->probe_cold = atoi(e) != 0;
   if (const char* e = getenv("HBTC_SPLIT")) c->split_levels = atoi(e) != 0;
   if (const char* e = getenv("HBTC_GT_REP")) c->small_rep = atoi(e) == 1 ? 1 : 3;
@@ -1464,8 +1566,8 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
   (void)hipDeviceSynchronize();
   for (auto& kv : c->bufs)
     if (kv.second.p) (void)hipFree(kv.second.p);
-  for (void* p : c->graveyard) (void)hipFree(p);
-  for (void* p : c->host_graveyard) (void)hipHostFree(p);
+  (void)retire_fence(c);
+  (void)reap_retired(c, true);
   for (auto& kv : c->keysets) {
     (void)hipFree(kv.second.pk);
     (void)hipFree(kv.second.st);

@@ -1,0 +1,208 @@
+// Small Lagrange combines (t <= 64 shares per instance) in ONE launch: PublicKeySet::
+// combine_signatures (src/coin.rs:185-191: a coin instance combines t = f + 1 SignatureShares, 4 at
+// N = 10, 34 at N = 100) and PublicKeySet::decrypt (src/threshold_decryption.rs:181-185) for
+// networks of up to ~190 validators.
+//
+// The Pippenger chain of hbtc_msm.hip (select -> Lagrange x / den / inv -> GLV/GLS split ->
+// decode -> recode -> sort -> buckets -> segment sums -> Horner) is nine dependent launches whose
+// per-lane chains are long for a handful of terms (C2's 100 x 34-share G2 combines: 11.7 ms in the
+// bucket pass alone).  Here one workgroup of 128 lanes takes one instance:
+//   wave 0     the first t ACCEPTed items in item order (hbbft's verified-share map order);
+//   lane pair  (2i, 2i + 1) for selected share i: its Lagrange coefficient at 0,
+//              lambda_i = prod_{j != i} x_j / prod_{j != i} (x_j - x_i) (x = idx + 1, one Fr
+//              inversion per lane), split into base-u digits lambda = d0 + d1 u + d2 u^2 + d3 u^3
+//              (u = |x|); lane h computes [d_2h] P + [d_2h+1] [u] P by the two-digit sign-aligned
+//              double-and-add (curve.h sac2_mul: 64 doublings + 65 mixed additions), and lane 1
+//              applies [u^2] (G1: -phi = (beta X, -Y); G2: psi^2 = (zeta X, -Y)) to its half;
+//   tree       the 128 partial points summed in LDS, then normalised, compressed, the
+//              instance status (NOT_ENOUGH_SHARES > DECODE_ERR > DUPLICATE_ENTRY > ACCEPT, as
+//              k_msm_final) and Signature::parity (G2).
+// [u] P: G2 -psi(P) (free); G1 [|x|] P by 64 doublings (jac_mul_u64).  Shares the verification
+// decoded are gathered, never decoded again (as k_msm_decode); others are decoded with the
+// subgroup check unless their status says the verifier accepted them.
+#include "hbtc_kernels.h"
+
+namespace hbtc {
+
+namespace {
+__device__ __forceinline__ bool comb_decode(G1A& p, const uint32_t* w, bool chk) {
+  return g1_decompress(p, w, chk);
+}
+__device__ __forceinline__ bool comb_decode(G2A& p, const uint32_t* w, bool chk) {
+  return g2_decompress(p, w, chk);
+}
+// [u] P (u = |x|)
+__device__ __forceinline__ void comb_upoint(G1J& r, const G1A& p) { jac_mul_u64(r, p, BLS_X_ABS); }
+__device__ __forceinline__ void comb_upoint(G2J& r, const G2A& p) {
+  G2A q;
+  g2_psi(q.x, q.y, p);  // psi = [x] = [-u] on G2
+  fq2_neg(q.y, q.y);
+  q.inf = 0;
+  jac_from_aff(r, q);
+}
+// r <- [u^2] r (Jacobian): G1 -phi(X, Y, Z) = (beta X, -Y, Z); G2 psi^2 = -(-psi^2) = (zeta X, -Y, Z)
+__device__ __forceinline__ void comb_u2(G1J& r) {
+  Fq c;
+  fq_set(c, G1_BETA);
+  fq_mul(r.x, r.x, c);
+  fq_neg(r.y, r.y);
+}
+__device__ __forceinline__ void comb_u2(G2J& r) {
+  Fq c;
+  fq_set(c, G2_ZETA);
+  fmul_by_fq(r.x, r.x, c);
+  fq2_neg(r.y, r.y);
+}
+__device__ __forceinline__ void comb_store(uint8_t* out, size_t k, const uint32_t* w, int nw) {
+  uint32_t* o = reinterpret_cast<uint32_t*>(out + k * (size_t)(nw * 4));
+  for (int j = 0; j < nw; ++j) o[j] = w[j];
+}
+__device__ __forceinline__ void comb_load(uint32_t* w, const uint8_t* base, size_t item, int nw) {
+  const uint4* q = reinterpret_cast<const uint4*>(base + item * (size_t)(nw * 4));
+  for (int i = 0; i < nw / 4; ++i) {
+    const uint4 v = q[i];
+    w[4 * i] = v.x;
+    w[4 * i + 1] = v.y;
+    w[4 * i + 2] = v.z;
+    w[4 * i + 3] = v.w;
+  }
+}
+__device__ __forceinline__ void comb_compress(uint32_t* w, const G1A& p) { g1_compress(w, p); }
+__device__ __forceinline__ void comb_compress(uint32_t* w, const G2A& p) { g2_compress(w, p); }
+__device__ __forceinline__ uint32_t comb_parity(const G1A&) { return 0; }
+__device__ __forceinline__ uint32_t comb_parity(const G2A& p) { return g2_parity(p); }
+}  // namespace
+
+template <class F, int NW>
+__global__ void __launch_bounds__(COMB_SMALL_BS, 1)
+    k_comb_small(uint32_t t, const uint32_t* __restrict__ offsets,
+                 const int32_t* __restrict__ item_status, const uint32_t* __restrict__ idx,
+                 const uint8_t* __restrict__ pts, const Aff<F>* __restrict__ dec,
+                 int32_t* __restrict__ inst_status, uint8_t* __restrict__ out,
+                 uint8_t* __restrict__ parity) {
+  HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
+  __shared__ uint32_t s_pos[COMB_SMALL_T];
+  __shared__ Fr s_x[COMB_SMALL_T];
+  __shared__ uint32_t s_cnt, s_bad, s_dup;
+  __shared__ Jac<F> s_red[COMB_SMALL_BS];
+  const uint32_t k = blockIdx.x, tid = threadIdx.x;
+  if (tid < 64) {  // wave 0: the first t items whose status is ACCEPT (all items without status)
+    const uint32_t a = offsets[k], b = offsets[k + 1];
+    uint32_t found = 0;
+    for (uint32_t base = a; base < b && found < t; base += 64) {
+      const uint32_t i = base + tid;
+      const bool ok = i < b && (!item_status || item_status[i] == HBTC_ACCEPT);
+      const uint64_t mask = __ballot(ok);
+      const uint32_t slot = found + (uint32_t)__popcll(mask & ((1ull << tid) - 1ull));
+      if (ok && slot < t) s_pos[slot] = i;
+      found += (uint32_t)__popcll(mask);
+    }
+    if (tid == 0) {
+      s_cnt = found < t ? found : t;
+      s_bad = 0;
+      s_dup = 0;
+    }
+  }
+  __syncthreads();
+  const uint32_t cnt = s_cnt;
+  const uint32_t pi = tid >> 1, h = tid & 1u;
+  const bool live = cnt == t && pi < cnt;
+  if (live && h == 0) {
+    Fr x;
+    fr_from_u64(x, (uint64_t)idx[s_pos[pi]] + 1);
+    s_x[pi] = x;
+  }
+  __syncthreads();
+  Jac<F> R;
+  jac_set_inf(R);
+  if (live) {
+    // lambda_i at 0 (Montgomery Fr), then canonical for the digit split
+    const Fr xi = s_x[pi];
+    Fr num, den;
+    limbs_set_const<8>(num, FR_ONE);
+    limbs_set_const<8>(den, FR_ONE);
+    bool dup = false;
+    for (uint32_t j = 0; j < cnt; ++j) {
+      if (j == pi) continue;
+      const Fr xj = s_x[j];
+      dup |= limbs_eq<8>(xj, xi);
+      Fr d;
+      fr_sub(d, xj, xi);
+      fr_mul(den, den, d);
+      fr_mul(num, num, xj);
+    }
+    if (dup) atomicOr(&s_dup, 1u);
+    Fr inv, l, lc;
+    fr_inv(inv, den);  // den = 0 only for a duplicate: the instance fails, the value is unused
+    fr_mul(l, num, inv);
+    fr_from_mont(lc, l);
+    uint64_t d[4];
+    gls_u_digits(lc.v, d);
+    // the share: decoded by the verification, else decoded here
+    const uint32_t pos = s_pos[pi];
+    const bool accepted = item_status && item_status[pos] == HBTC_ACCEPT;
+    Aff<F> P;
+    if (accepted && dec) {
+      P = dec[pos];
+    } else {
+      uint32_t w[NW];
+      comb_load(w, pts, pos, NW);
+      if (!comb_decode(P, w, !accepted)) {
+        atomicOr(&s_bad, 1u);
+        P.inf = 1;
+      }
+    }
+    if (!P.inf) {
+      Jac<F> XP;
+      comb_upoint(XP, P);
+      sac2_mul(R, P, XP, h ? d[2] : d[0], h ? d[3] : d[1], 64);
+      if (h) comb_u2(R);
+    }
+  }
+  s_red[tid] = R;
+  __syncthreads();
+  for (uint32_t s = COMB_SMALL_BS / 2; s >= 1; s >>= 1) {
+    if (tid < s) {
+      Jac<F> a = s_red[tid];
+      const Jac<F> b = s_red[tid + s];
+      jac_add(a, a, b);
+      s_red[tid] = a;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    int32_t st = HBTC_ACCEPT;
+    if (cnt < t)
+      st = HBTC_NOT_ENOUGH_SHARES;
+    else if (s_bad)
+      st = HBTC_DECODE_ERR;
+    else if (s_dup)
+      st = HBTC_DUPLICATE_ENTRY;
+    inst_status[k] = st;
+    Aff<F> a;
+    jac_to_aff(a, s_red[0]);
+    uint32_t w[NW];
+    comb_compress(w, a);
+    if (st != HBTC_ACCEPT)
+      for (int j = 0; j < NW; ++j) w[j] = 0;
+    comb_store(out, k, w, NW);
+    if (parity) parity[k] = (st == HBTC_ACCEPT) ? (uint8_t)comb_parity(a) : 0;
+  }
+}
+
+hipError_t launch_comb_small(hipStream_t s, int group, uint32_t n_inst, uint32_t t,
+                             const uint32_t* offsets, const int32_t* item_status, const uint32_t* idx,
+                             const uint8_t* pts, const void* dec, int32_t* inst_status, uint8_t* out,
+                             uint8_t* parity) {
+  if (n_inst == 0) return hipSuccess;
+  if (t == 0 || t > COMB_SMALL_T) return hipErrorInvalidValue;
+  if (group == 1)
+    hipLaunchKernelGGL((k_comb_small<Fq, 12>), dim3(n_inst), dim3(COMB_SMALL_BS), 0, s, t, offsets,
+                       item_status, idx, pts, static_cast<const G1A*>(dec), inst_status, out, nullptr);
+  else
+    hipLaunchKernelGGL((k_comb_small<Fq2, 24>), dim3(n_inst), dim3(COMB_SMALL_BS), 0, s, t, offsets,
+                       item_status, idx, pts, static_cast<const G2A*>(dec), inst_status, out, parity);
+  return hipGetLastError();
+}
+
+}  // namespace hbtc

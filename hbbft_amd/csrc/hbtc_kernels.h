@@ -288,6 +288,16 @@ hipError_t launch_msm_reduce_g2(hipStream_t s, const MsmPlan& p, const G2A* pts,
                                 const uint32_t* dup, int32_t* status, uint8_t* out,
                                 uint8_t* parity);
 
+// ---- small combines, t <= COMB_SMALL_T shares per instance, one workgroup each (hbtc_comb.hip)
+constexpr uint32_t COMB_SMALL_T = 64;
+constexpr uint32_t COMB_SMALL_BS = 128;  // two lanes per selected share
+// group 1: DecryptionShares (dec: G1A*), 2: SignatureShares (dec: G2A*, parity written); dec may be
+// null (decode everything); item_status null = combine the first t items
+hipError_t launch_comb_small(hipStream_t s, int group, uint32_t n_inst, uint32_t t,
+                             const uint32_t* offsets, const int32_t* item_status, const uint32_t* idx,
+                             const uint8_t* pts, const void* dec, int32_t* inst_status, uint8_t* out,
+                             uint8_t* parity);
+
 // ---- SyncKeyGen (hbtc_skg.hip)
 hipError_t launch_skg_sym_scalars(hipStream_t s, uint32_t n_parts, uint32_t M, const Fr* U,
                                   uint32_t u_stride, const Fr* V, uint32_t v_stride,

@@ -662,32 +662,6 @@ hipError_t launch_msm_gather_g2(hipStream_t s, uint32_t n_inst, uint32_t t, cons
 // over 65-bit windows (a Horner chain of ~64 doublings in k_msm_final instead of ~255) and the
 // result is the same point.  Term k of msm m goes to positions m * 4n + 4k + j; scalars are
 // written in the 8-word canonical layout k_msm_recode reads.
-__device__ __forceinline__ void gls_u_digits(const uint32_t* k, uint64_t d[4]) {
-  constexpr uint64_t V = BLS_X_ABS >> 16;  // 0xd20100000001
-  uint32_t w[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) w[i] = k[i];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const uint32_t lo16 = w[0] & 0xffffu;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = (w[i] >> 16) | (i < 7 ? w[i + 1] << 16 : 0u);
-    uint64_t rem = 0;  // < V < 2^48, so rem * 2^16 + 16 bits fits 64
-#pragma unroll
-    for (int i = 7; i >= 0; --i) {
-      uint64_t cur = (rem << 16) | (w[i] >> 16);
-      const uint32_t qh = (uint32_t)(cur / V);
-      rem = cur - (uint64_t)qh * V;
-      cur = (rem << 16) | (w[i] & 0xffffu);
-      const uint32_t ql = (uint32_t)(cur / V);
-      rem = cur - (uint64_t)ql * V;
-      w[i] = (qh << 16) | ql;
-    }
-    d[j] = (rem << 16) | lo16;
-  }
-  d[3] = ((uint64_t)w[1] << 32) | w[0];  // the quotient after three divisions: < u
-}
-
 __global__ void __launch_bounds__(64) k_msm_gls_g2(uint64_t terms, uint32_t n,
                                                    const uint32_t* __restrict__ lambda,
                                                    const G2A* __restrict__ pts,

@@ -54,8 +54,17 @@ namespace hbtc {
 #ifndef HBTC_ITEMS_PRIO
 #define HBTC_ITEMS_PRIO 0  // wave priority of the item pass (experiments: 3 = above the check levels)
 #endif
+#ifndef HBTC_XADIC8
+#define HBTC_XADIC8 1  // r_i d_i by the sign-aligned 8-entry table (curve.h xadic_mul_sac8)
+#endif
+#ifndef HBTC_SAC8_LDS
+#define HBTC_SAC8_LDS 1  // three of the eight entries in LDS (the reduction's arrays, unused then)
+#endif
 #ifndef HBTC_ITEMS_WAVES
-#define HBTC_ITEMS_WAVES 2  // minimum waves per SIMD the register allocation must allow (1: 153 ms, 2: 86 ms, 3: 161 ms per C3 launch)
+// minimum waves per SIMD the register allocation must allow (round 5, C3 shares/s: one wave with
+// the whole 8-entry table in registers + AGPRs 11.7 M, two waves with the table partly spilled
+// 13.4 M, profiles/r05/run1/)
+#define HBTC_ITEMS_WAVES 2
 #endif
 __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
@@ -66,8 +75,12 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
 #if HBTC_ITEMS_PRIO > 0
   __builtin_amdgcn_s_setprio(HBTC_ITEMS_PRIO);
 #endif
-  __shared__ G1J redA[64];
-  __shared__ G1J redB[64];
+  // the reduction's two arrays, and before them the x-adic table's three LDS entries (18 KB:
+  // 3 x 24 words x 64 lanes, curve.h xadic_mul_sac8<LDS3>): one wave per block, so the table
+  // reads are over before the reduction writes
+  __shared__ G1J red[128];
+  G1J* redA = red;
+  G1J* redB = red + 64;
   const Tile tile = tiles[blockIdx.x];
   const uint32_t lane = threadIdx.x;
   const size_t item = (size_t)tile.first + lane;
@@ -99,7 +112,14 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
             jac_neg(t1, t1);
             Fq beta;
             fq_set(beta, G1_BETA);
-#if HBTC_XADIC16
+#if HBTC_XADIC8
+#if HBTC_ITEMS_WAVES >= 2 && HBTC_SAC8_LDS
+            xadic_mul_sac8<Fq, true>(S, d, t1, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits,
+                                     reinterpret_cast<uint32_t*>(red), lane);
+#else
+            xadic_mul_sac8(S, d, t1, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+#endif
+#elif HBTC_XADIC16
             xadic_mul_tab16(S, d, t1, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
 #else
             G1A xp, pxp;

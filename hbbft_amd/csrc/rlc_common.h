@@ -214,7 +214,11 @@ __device__ __forceinline__ void rlc_reduce_sp(G1J* redA, G1J* redB, const G1J& S
                                               G1J* outPHW, G1J* outSQ, G1J* outSQW, G1J* outPQ,
                                               G1J* outPQW) {
   const bool odd = (lane & 1u) != 0;
-  G1J x = odd ? S : P, y;  // the value the neighbour lane needs
+  // selects by value (a reference chosen between S and P would put both in scratch)
+  G1J x, y;  // x: the value the neighbour lane needs
+  fsel(x.x, odd, S.x, P.x);
+  fsel(x.y, odd, S.y, P.y);
+  fsel(x.z, odd, S.z, P.z);
   {
     const uint32_t* xs = reinterpret_cast<const uint32_t*>(&x);
     uint32_t* ys = reinterpret_cast<uint32_t*>(&y);
@@ -223,9 +227,13 @@ __device__ __forceinline__ void rlc_reduce_sp(G1J* redA, G1J* redB, const G1J& S
     for (int i = 0; i < (int)(sizeof(G1J) / 4); ++i)
       ys[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)xs[i]);
   }
-  G1J a;
-  const G1J& l = odd ? y : S;
-  const G1J& r = odd ? P : y;
+  G1J a, l, r;
+  fsel(l.x, odd, y.x, S.x);
+  fsel(l.y, odd, y.y, S.y);
+  fsel(l.z, odd, y.z, S.z);
+  fsel(r.x, odd, P.x, y.x);
+  fsel(r.y, odd, P.y, y.y);
+  fsel(r.z, odd, P.z, y.z);
   jac_add(a, l, r);
   redA[lane] = a;
   redB[lane] = r;
@@ -331,10 +339,15 @@ static __device__ void rlc_pk_mul_x(G1J& r, const PtXY* __restrict__ tab, const 
       if (!v) continue;
       const PtXY e = tab[(tw + w) * 256 + v];
       G1A q;
-      q.x = e.x;
       q.y = e.y;
       q.inf = 0;
-      if (j >= 2) g1_phi(q, q);
+      if (j >= 2) {  // wave-uniform
+        Fq beta;
+        fq_set(beta, G1_BETA);
+        fq_mul(q.x, e.x, beta);
+      } else {
+        q.x = e.x;
+      }
       jac_add_aff(r, r, q);
     }
   }

@@ -94,6 +94,9 @@ def test_xadic_scalar_of_rlc_items(ht, nbits):
     ht.ht_g2_mul_xadic.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
     ht.ht_g1_mul_xadic16.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
     ht.ht_g2_mul_xadic16.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
+    ht.ht_g1_mul_xadic8.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
+    ht.ht_g2_mul_xadic8.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
+    cases += [(2, 0, 0, 0), (0, top, top, top), (top - 1, 1, 1, 1), (2, 1, 0, 0)]
     for d in cases:
         r = (d[0] + d[1] * B.X + d[2] * mu + d[3] * mu * B.X) % B.R
         arr = (ctypes.c_uint32 * 4)(*d)
@@ -110,6 +113,34 @@ def test_xadic_scalar_of_rlc_items(ht, nbits):
         assert o.raw == B.g1_compress(B.g1_mul(P, r)), ("g1 tab16", d)
         assert ht.ht_g2_mul_xadic16(B.g2_compress(Q), ctypes.cast(arr, ctypes.c_void_p), nbits, o2) == 0
         assert o2.raw == B.g2_compress(B.g2_mul(Q, r)), ("g2 tab16", d)
+        # the sign-aligned 8-entry form (curve.h xadic_mul_sac8), even d0 included
+        assert ht.ht_g1_mul_xadic8(B.g1_compress(P), ctypes.cast(arr, ctypes.c_void_p), nbits, o) == 0
+        assert o.raw == B.g1_compress(B.g1_mul(P, r)), ("g1 sac8", d)
+        assert ht.ht_g2_mul_xadic8(B.g2_compress(Q), ctypes.cast(arr, ctypes.c_void_p), nbits, o2) == 0
+        assert o2.raw == B.g2_compress(B.g2_mul(Q, r)), ("g2 sac8", d)
+
+
+def test_sac2_two_digit_form(ht):
+    """The small combines' scalar multiplication (curve.h sac2_mul): [d0] P + [d1] [u] P, u = |x|,
+    for 64-bit digits (base-u digits of Lagrange coefficients, so the edge digits are covered too:
+    zero, even / odd d0, all-ones, u - 1) on G1 and G2."""
+    rng = random.Random(77)
+    u = abs(B.X)
+    top = (1 << 64) - 1
+    cases = [(0, 0), (1, 0), (0, 1), (2, 0), (2, 1), (top, top), (u - 1, u - 1), (u - 2, 1), (0, u - 1)]
+    cases += [(rng.getrandbits(64), rng.getrandbits(64)) for _ in range(6)]
+    ht.ht_g1_mul_sac2.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p]
+    ht.ht_g2_mul_sac2.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p]
+    for d0, d1 in cases:
+        k = (d0 + d1 * u) % B.R
+        P = B.g1_mul(B.G1_GEN, rng.randrange(1, B.R))
+        o = buf(48)
+        assert ht.ht_g1_mul_sac2(B.g1_compress(P), d0, d1, o) == 0
+        assert o.raw == B.g1_compress(B.g1_mul(P, k)), ("g1", d0, d1)
+        Q = B.g2_mul(B.G2_GEN, rng.randrange(1, B.R))
+        o2 = buf(96)
+        assert ht.ht_g2_mul_sac2(B.g2_compress(Q), d0, d1, o2) == 0
+        assert o2.raw == B.g2_compress(B.g2_mul(Q, k)), ("g2", d0, d1)
 
 
 def test_xadic_digit_box_is_injective():
