@@ -444,42 +444,56 @@ def bench_c1(ctx, steps, warmup, cpu_budget=0.0):
     want_sig, _ = ctx.g2_mul(H, fr_bytes([master]))
     ks, bad = ctx.keyset_load(pk)
     assert bad == 0
+    ctx.keyset_set_master(ks, bytes(mpk))
     idx = np.arange(n, dtype=np.uint32)
     sig_list = [bytes(sigs[96 * i:96 * i + 96]) for i in range(n)]
-    phases = {"hash_g2": [], "verify_shares": [], "combine": [], "verify_master": []}
-    total = []
 
     def call():
+        """The coin round as ONE call (hbtc_coin_decide): hash_g2 on the host, then the share
+        checks, the combine of the first t verified shares, the master check and the parity."""
         a = time.perf_counter()
         Hc = N.hash_g2(COIN_NONCE)  # host, once per coin instance (north star)
+        b = time.perf_counter()
+        stv, out, par, cst = ctx.coin_decide(ks, [Hc], [n], idx, sig_list, t)
+        e = time.perf_counter()
+        return (b - a, e - b, e - a), stv, out[0], int(par[0]), int(cst[0])
+
+    def call_separate():
+        """The same coin through the three per-call entry points (verify, combine, PublicKey::verify)."""
+        a = time.perf_counter()
+        Hc = N.hash_g2(COIN_NONCE)
         b = time.perf_counter()
         stv = ctx.verify_sig_shares(ks, [Hc], [n], idx, sig_list)
         c = time.perf_counter()
         sel = [i for i in range(n) if stv[i] == N.ACCEPT][:t]
-        if "combine" in C1_SKIP:  # diagnostics only
-            out, par, cst = [want_sig], np.zeros(1, np.uint8), np.zeros(1, np.int32)
-        else:
-            out, par, cst = ctx.combine_sigs([t], sel, [sig_list[i] for i in sel], t)
+        out, par, cst = ctx.combine_sigs([t], sel, [sig_list[i] for i in sel], t)
         d = time.perf_counter()
-        if "master" in C1_SKIP:  # diagnostics only (the results check below then fails loudly)
-            ok = np.zeros(1, np.int32)
-        else:
-            ok = ctx.verify_sigs([bytes(mpk)], [Hc], [out[0]])
+        ok = ctx.verify_sigs([bytes(mpk)], [Hc], [out[0]])
         e = time.perf_counter()
         return (b - a, c - b, d - c, e - d, e - a), stv, out[0], int(par[0]), int(cst[0]), int(ok[0])
 
+    phases = {"hash_g2": [], "coin_decide": []}
+    total = []
     for _ in range(warmup):
         call()
     for _ in range(steps):
-        ph, stv, sig, par, cst, ok = call()
-        for k, v in zip(phases, ph[:4]):
-            phases[k].append(v)
-        total.append(ph[4])
-    if C1_SKIP:
-        log("c1: HBTC_C1_SKIP=%s: diagnostics run, no line" % ",".join(sorted(C1_SKIP)))
-        return None
-    if (stv != expected).any() or cst != 0 or ok != N.ACCEPT or sig != bytes(want_sig):
+        ph, stv, sig, par, cst = call()
+        phases["hash_g2"].append(ph[0])
+        phases["coin_decide"].append(ph[1])
+        total.append(ph[2])
+    if (stv != expected).any() or cst != N.ACCEPT or sig != bytes(want_sig):
         raise SystemExit("c1: results differ from the construction")
+    sep_phases = {"hash_g2": [], "verify_shares": [], "combine": [], "verify_master": []}
+    sep_total = []
+    for _ in range(min(warmup, 2)):
+        call_separate()
+    for _ in range(max(steps // 2, 5)):
+        ph, stv2, sig2, par2, cst2, ok2 = call_separate()
+        for k, v in zip(sep_phases, ph[:4]):
+            sep_phases[k].append(v)
+        sep_total.append(ph[4])
+    if (stv2 != expected).any() or cst2 != 0 or ok2 != N.ACCEPT or sig2 != bytes(want_sig) or par2 != par:
+        raise SystemExit("c1: the separate calls differ from the construction")
     ctx.keyset_free(ks)
     med = _pct(total, 0.5)
     res = {
@@ -487,12 +501,16 @@ def bench_c1(ctx, steps, warmup, cpu_budget=0.0):
                   "master verify + parity)",
         "value": round(med * 1e3, 3), "unit": "ms per coin call (median)", "n_gpus": 1, "steps": steps,
         "warmup": warmup, "higher_is_better": False, "dtype": "u32 (381-bit Montgomery limbs)",
-        "data": "synthetic (seeded key set; shares sk_i * hash_g2(nonce) made on the device; 1 wrong share)",
-        "config": {"workload": "c1: Threshold Coin N=10 f=3 (examples/simulation.rs:43-44): one coin call, "
-                               "host buffers, blocking", "N": n, "f": 3, "t": t},
+        "data": "synthetic (seeded key set, master key; shares sk_i * hash_g2(nonce) made on the device; "
+                "node 2's share is wrong)",
+        "config": {"workload": "c1: Threshold Coin N=10 f=3 (examples/simulation.rs:43-44): one coin call "
+                               "(hbtc_coin_decide), host buffers, blocking", "N": n, "f": 3, "t": t},
         "latency_ms": {"p10": round(_pct(total, 0.1) * 1e3, 3), "median": round(med * 1e3, 3),
                        "p90": round(_pct(total, 0.9) * 1e3, 3)},
         "phase_median_ms": {k: round(_pct(v, 0.5) * 1e3, 3) for k, v in phases.items()},
+        "separate_calls": {"median_ms": round(_pct(sep_total, 0.5) * 1e3, 3),
+                           "phase_median_ms": {k: round(_pct(v, 0.5) * 1e3, 3) for k, v in sep_phases.items()},
+                           "note": "hbtc_verify_sig_shares + hbtc_combine_sigs + hbtc_verify_sigs, each blocking"},
         "calls_per_s": round(1.0 / med, 1),
         "mode": "rlc" if ctx_mode[0] == N.MODE_RLC else "per_share", "results_ok": True,
     }

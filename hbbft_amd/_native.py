@@ -52,6 +52,8 @@ SIGNATURES = {
     "hbtc_keyset_load": (_I32, [_P, _P, _U32, ctypes.POINTER(_U32), ctypes.POINTER(_U32)]),
     "hbtc_keyset_free": (_I32, [_P, _U32]),
     "hbtc_verify_sig_shares": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P]),
+    "hbtc_keyset_set_master": (_I32, [_P, _U32, _P]),
+    "hbtc_coin_decide": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _U32, _P, _P, _P, _P]),
     "hbtc_verify_sigs": (_I32, [_P, _U32, _P, _P, _P, _P]),
     "hbtc_combine_sigs": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P, _P]),
     "hbtc_verify_dec_shares": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P, _P]),
@@ -385,7 +387,28 @@ class Context:
     def keyset_free(self, kid):
         self._check(self.lib.hbtc_keyset_free(self.h, kid), "hbtc_keyset_free")
 
+    def keyset_set_master(self, kid, master_pk):
+        mp = _join([master_pk], 48)
+        self._check(self.lib.hbtc_keyset_set_master(self.h, kid, _ptr(mp)), "hbtc_keyset_set_master")
+
     # ---- verification
+    def coin_decide(self, keyset, H, counts, idx, sigs, t, offsets=None):
+        """One Threshold Coin round (hbtc.h hbtc_coin_decide): item statuses, combined signatures,
+        parity bits and coin statuses (ACCEPT = the combined signature passed the master check)."""
+        off = _offsets(offsets if offsets is not None else counts, offsets is not None)
+        n_inst = off.size - 1
+        Hb, sb = _join(H, 96), _join(sigs, 96)
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        st = np.empty(max(int(off[-1]), 1), dtype=np.int32)
+        sig = np.zeros(96 * max(n_inst, 1), np.uint8)
+        par = np.zeros(max(n_inst, 1), np.uint8)
+        cst = np.zeros(max(n_inst, 1), np.int32)
+        self._check(self.lib.hbtc_coin_decide(self.h, keyset, n_inst, _ptr(Hb), _ptr(off), _ptr(ix),
+                                              _ptr(sb), t, _ptr(st), _ptr(sig), _ptr(par), _ptr(cst)),
+                    "hbtc_coin_decide")
+        return (st[:int(off[-1])], [bytes(sig[96 * k:96 * k + 96]) for k in range(n_inst)],
+                par[:n_inst], cst[:n_inst])
+
     def verify_sig_shares(self, keyset, H, counts, idx, sigs, offsets=None):
         off = _offsets(offsets if offsets is not None else counts, offsets is not None)
         n_inst = off.size - 1

@@ -51,6 +51,7 @@ struct Keyset {
   uint32_t* rejects = nullptr;   // per-sender REJECT counts of the running call
   uint32_t calls = 0;            // RLC verification calls on this key set
   uint32_t n = 0;
+  G1A* master = nullptr;         // hbtc_keyset_set_master: the decoded master public key
 };
 
 struct Span {
@@ -113,6 +114,8 @@ struct hbtc_ctx {
   // combines of t <= COMB_SMALL_T shares in one launch (hbtc_comb.hip; HBTC_COMB_SMALL=0: the
   // Pippenger chain for every t)
   bool comb_small = true;
+  // hbtc_coin_decide's speculative combines (HBTC_COIN_SPEC=0: combine after the checks only)
+  bool coin_spec = true;
   std::string ws_suffix;
   hipStream_t stream = nullptr;  // main: items, checks, leaves
   hipStream_t s_prep = nullptr;  // per-instance G2 preparation, overlapped with the item pass
@@ -120,6 +123,9 @@ struct hbtc_ctx {
   hipEvent_t ev_main = nullptr, ev_prep = nullptr, ev_comb = nullptr;
   hipEvent_t ev_ext = nullptr, ev_ext2 = nullptr, ev_ext3 = nullptr;  // external-stream ordering
   hipEvent_t ev_x_in = nullptr, ev_x_out = nullptr;  // ordering around the exact-kernel stream
+  // speculative coin combines (hbtc_coin_decide), created on first use, high priority
+  hipStream_t s_spec = nullptr;
+  hipEvent_t ev_spec_in = nullptr, ev_spec_out = nullptr;
   std::map<std::string, Stage> stages;
   std::map<std::string, unsigned> stage_next;
   std::mutex mu;
@@ -255,6 +261,7 @@ int retire_fence(hbtc_ctx* c) {
     streams.push_back(l.stream);
     streams.push_back(l.s_prep);
   }
+  if (c->s_spec) streams.push_back(c->s_spec);
   hipStream_t xs;
   if (exact_stream_exists(c->device) && exact_stream(c->device, &xs) == hipSuccess) streams.push_back(xs);
   hipError_t e = hipSuccess;
@@ -363,6 +370,7 @@ int sync(hbtc_ctx* c) {
     HB_CHECK(c, hipStreamSynchronize(l.stream));
     HB_CHECK(c, hipStreamSynchronize(l.s_prep));
   }
+  if (c->s_spec) HB_CHECK(c, hipStreamSynchronize(c->s_spec));
   return reap_retired(c, true);
 }
 
@@ -1230,10 +1238,17 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
     const bool same = d_item_status && ld.status == d_item_status && ld.shares == d_pts &&
                       ld.n_items == n_items;
     const void* dec = same ? (group == 1 ? (const void*)ld.dec : (const void*)ld.dec2) : nullptr;
-    HB_TRY(timed_on(c, sc, "combine", [&] {
-      return launch_comb_small(sc, group, n_inst, t, d_off, d_item_status, d_idx, d_pts, dec,
-                               d_inst_status, d_out, group == 2 ? d_parity : nullptr);
-    }));
+    CombSmallArgs a{};
+    a.t = t;
+    a.offsets = d_off;
+    a.item_status = d_item_status;
+    a.idx = d_idx;
+    a.pts = d_pts;
+    a.dec = dec;
+    a.inst_status = d_inst_status;
+    a.out = d_out;
+    a.parity = group == 2 ? d_parity : nullptr;
+    HB_TRY(timed_on(c, sc, "combine", [&] { return launch_comb_small(sc, group, n_inst, 1, a); }));
     return note_comb_reads(c, {{d_idx, (size_t)n_items * 4}, {d_pts, n_items * pbytes},
                                {d_item_status, d_item_status ? (size_t)n_items * 4 : 0},
                                {dec, dec ? n_items * (group == 1 ? sizeof(G1A) : sizeof(G2A)) : 0}});
@@ -1494,6 +1509,7 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (const char* e = getenv("HBTC_G2_GLS")) c->g2_gls = atoi(e) != 0;
   if (const char* e = getenv("HBTC_G1_GLV")) c->g1_glv = atoi(e) != 0;
   if (const char* e = getenv("HBTC_COMB_SMALL")) c->comb_small = atoi(e) != 0;
+  if (const char* e = getenv("HBTC_COIN_SPEC")) c->coin_spec = atoi(e) != 0;
   if (const char* e = getenv("HBTC_PROBE")) c->probe_cold = atoi(e) != 0;
   if (const char* e = getenv("HBTC_SPLIT")) c->split_levels = atoi(e) != 0;
   if (const char* e = getenv("HBTC_GT_REP")) c->small_rep = atoi(e) == 1 ? 1 : 3;
@@ -1574,6 +1590,7 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
     (void)hipFree(kv.second.tab);
     (void)hipFree(kv.second.last_bad);
     (void)hipFree(kv.second.rejects);
+    (void)hipFree(kv.second.master);
   }
   for (Span& sp : c->spans) {
     (void)hipEventDestroy(sp.a);
@@ -1613,6 +1630,9 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
   ev_free(c->ev_ext3);
   ev_free(c->ev_x_in);
   ev_free(c->ev_x_out);
+  ev_free(c->ev_spec_in);
+  ev_free(c->ev_spec_out);
+  if (c->s_spec) (void)hipStreamDestroy(c->s_spec);
   delete c;
 }
 
@@ -1664,6 +1684,7 @@ int hbtc_keyset_free(hbtc_ctx* c, uint32_t keyset_id) {
   (void)hipFree(it->second.tab);
   (void)hipFree(it->second.last_bad);
   (void)hipFree(it->second.rejects);
+  (void)hipFree(it->second.master);
   c->keysets.erase(it);
   return HBTC_OK;
 }
@@ -1686,6 +1707,164 @@ int hbtc_verify_sig_shares(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, con
                         (const uint32_t*)d_idx, (const uint8_t*)d_sig, (int32_t*)d_st));
   HB_TRY(download(c, status, d_st, (size_t)4 * n));
   return sync(c);
+}
+
+int hbtc_keyset_set_master(hbtc_ctx* c, uint32_t keyset_id, const uint8_t* mpk) {
+  if (!c || !mpk) return HBTC_ERR_ARG;
+  Guard g(c);
+  Keyset* ks;
+  HB_TRY(get_keyset(c, keyset_id, &ks));
+  HB_TRY(sync(c));
+  if (ks->master) {
+    (void)hipFree(ks->master);
+    ks->master = nullptr;
+  }
+  G1A* d_m;
+  int32_t* d_st;
+  HB_CHECK(c, hipMalloc(&d_m, sizeof(G1A)));
+  void* d_in;
+  HB_TRY(upload(c, "in0", mpk, 48, &d_in));
+  HB_TRY(wst(c, "out0", 1, &d_st));
+  HB_CHECK(c, launch_g1_decode(c->stream, (const uint8_t*)d_in, 1, d_m, d_st));
+  int32_t st = -1;
+  HB_TRY(download(c, &st, d_st, 4));
+  HB_TRY(sync(c));
+  if (st != HBTC_ACCEPT) {
+    (void)hipFree(d_m);
+    return fail(c, HBTC_ERR_ARG, "master public key fails to decode");
+  }
+  ks->master = d_m;
+  return HBTC_OK;
+}
+
+// hbtc.h hbtc_coin_decide: the share checks on the lane stream (sig_shares_dev), the speculative
+// leave-one-out combines and master checks on s_spec beside them, then the commit and the
+// status-driven combine + master check of the instances the speculation missed.
+int hbtc_coin_decide(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8_t* H,
+                     const uint32_t* offsets, const uint32_t* idx, const uint8_t* sig, uint32_t t,
+                     int32_t* status, uint8_t* sig_out, uint8_t* parity, int32_t* coin_status) {
+  if (!c || (n_inst && (!H || !offsets || !sig_out || !parity || !coin_status))) return HBTC_ERR_ARG;
+  Guard g(c);
+  Keyset* ks;
+  HB_TRY(get_keyset(c, keyset_id, &ks));
+  if (!ks->master) return fail(c, HBTC_ERR_ARG, "key set has no master key (hbtc_keyset_set_master)");
+  if (t == 0 || t > COMB_SMALL_T) return fail(c, HBTC_ERR_ARG, "t must be in 1..64");
+  uint32_t n;
+  HB_TRY(check_offsets(c, n_inst, offsets, &n));
+  if (n_inst == 0) return HBTC_OK;
+  if (n && (!idx || !sig || !status)) return fail(c, HBTC_ERR_ARG, "NULL item array");
+  const size_t n1 = std::max<uint32_t>(n, 1);
+  void *d_H, *d_idx, *d_sig, *d_st;
+  HB_TRY(upload(c, "in0", H, (size_t)96 * n_inst, &d_H));
+  HB_TRY(upload(c, "in1", idx, (size_t)4 * n, &d_idx));
+  HB_TRY(upload(c, "in2", sig, (size_t)96 * n, &d_sig));
+  HB_TRY(ws(c, "out0", (size_t)4 * n1, &d_st));
+  PinLane pin(c);  // the uploads above went to the current lane
+  void* p;
+  HB_TRY(stage_upload(c, "coin.offsets", offsets, ((size_t)n_inst + 1) * 4, c->stream, &p));
+  const uint32_t* d_off = static_cast<const uint32_t*>(p);
+  int32_t *d_cst, *d_master;
+  uint8_t *d_sig_out, *d_par;
+  uint32_t* d_redo;
+  HB_TRY(wst(c, "coin.cst", n_inst, &d_cst));
+  HB_TRY(wst(c, "coin.master", n_inst, &d_master));
+  HB_TRY(wst(c, "coin.sig", (size_t)96 * n_inst, &d_sig_out));
+  HB_TRY(wst(c, "coin.par", n_inst, &d_par));
+  HB_TRY(wst(c, "coin.redo", n_inst, &d_redo));
+  // speculation: the leave-one-out subsets of the first t + 1 items, beside the share checks
+  const uint32_t n_sub = t + 1;
+  const bool spec = c->coin_spec && (uint64_t)n_inst * n_sub <= 256;
+  int32_t *s_cst = nullptr, *s_master = nullptr;
+  uint8_t *s_sig = nullptr, *s_par = nullptr;
+  if (spec) {
+    if (!c->s_spec) {
+      int lo = 0, hi = 0;
+      if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+      HB_CHECK(c, hipStreamCreateWithPriority(&c->s_spec, hipStreamNonBlocking, hi));
+      HB_CHECK(c, hipEventCreateWithFlags(&c->ev_spec_in, hipEventDisableTiming));
+      HB_CHECK(c, hipEventCreateWithFlags(&c->ev_spec_out, hipEventDisableTiming));
+    }
+    const size_t slots = (size_t)n_inst * n_sub;
+    HB_TRY(wst(c, "coin.s_cst", slots, &s_cst));
+    HB_TRY(wst(c, "coin.s_master", slots, &s_master));
+    HB_TRY(wst(c, "coin.s_sig", slots * 96, &s_sig));
+    HB_TRY(wst(c, "coin.s_par", slots, &s_par));
+    HB_CHECK(c, hipEventRecord(c->ev_spec_in, c->stream));  // after the uploads
+    HB_CHECK(c, hipStreamWaitEvent(c->s_spec, c->ev_spec_in, 0));
+    CombSmallArgs a{};
+    a.t = t;
+    a.offsets = d_off;
+    a.idx = (const uint32_t*)d_idx;
+    a.pts = (const uint8_t*)d_sig;
+    a.inst_status = s_cst;
+    a.out = s_sig;
+    a.parity = s_par;
+    CombSmallArgs m{};
+    m.t = t;
+    m.offsets = d_off;
+    m.idx = (const uint32_t*)d_idx;
+    m.dec = ks->pk;
+    m.by_node = 1;
+    m.n_nodes = ks->n;
+    m.inst_status = s_master;
+    m.cmp = ks->master;
+    HB_TRY(timed_on(c, c->s_spec, "coin_spec", [&] {
+      hipError_t e = launch_comb_small(c->s_spec, 2, n_inst, n_sub, a);
+      if (e != hipSuccess) return e;
+      return launch_comb_small(c->s_spec, 1, n_inst, n_sub, m);
+    }));
+    HB_CHECK(c, hipEventRecord(c->ev_spec_out, c->s_spec));
+  }
+  HB_TRY(sig_shares_dev(c, keyset_id, n_inst, (const uint8_t*)d_H, offsets, (const uint32_t*)d_idx,
+                        (const uint8_t*)d_sig, (int32_t*)d_st));
+  const int32_t* d_item = (const int32_t*)d_st;
+  if (spec) {
+    HB_CHECK(c, hipStreamWaitEvent(c->stream, c->ev_spec_out, 0));
+    HB_TRY(timed(c, "coin_commit", [&] {
+      return launch_coin_commit(c->stream, n_inst, t, d_off, d_item, n_sub, s_cst, s_sig, s_par,
+                                s_master, d_cst, d_sig_out, d_par, d_master, d_redo);
+    }));
+  }
+  {  // the status-driven combine and master check (only the instances the speculation missed)
+    const auto& ld = c->last_dec;
+    const bool same = ld.status == d_item && ld.shares == (const uint8_t*)d_sig && ld.n_items == n;
+    CombSmallArgs a{};
+    a.t = t;
+    a.offsets = d_off;
+    a.item_status = d_item;
+    a.idx = (const uint32_t*)d_idx;
+    a.pts = (const uint8_t*)d_sig;
+    a.dec = same ? (const void*)ld.dec2 : nullptr;
+    a.inst_status = d_cst;
+    a.out = d_sig_out;
+    a.parity = d_par;
+    a.only = spec ? d_redo : nullptr;
+    CombSmallArgs m{};
+    m.t = t;
+    m.offsets = d_off;
+    m.item_status = d_item;
+    m.idx = (const uint32_t*)d_idx;
+    m.dec = ks->pk;
+    m.by_node = 1;
+    m.n_nodes = ks->n;
+    m.inst_status = d_master;
+    m.cmp = ks->master;
+    m.only = spec ? d_redo : nullptr;
+    HB_TRY(timed(c, "combine", [&] {
+      hipError_t e = launch_comb_small(c->stream, 2, n_inst, 1, a);
+      if (e != hipSuccess) return e;
+      return launch_comb_small(c->stream, 1, n_inst, 1, m);
+    }));
+  }
+  std::vector<int32_t> cst(n_inst), mst(n_inst);
+  HB_TRY(download(c, status, d_st, (size_t)4 * n));
+  HB_TRY(download(c, sig_out, d_sig_out, (size_t)96 * n_inst));
+  HB_TRY(download(c, parity, d_par, n_inst));
+  HB_TRY(download(c, cst.data(), d_cst, (size_t)4 * n_inst));
+  HB_TRY(download(c, mst.data(), d_master, (size_t)4 * n_inst));
+  HB_TRY(sync(c));
+  for (uint32_t k = 0; k < n_inst; ++k) coin_status[k] = cst[k] != HBTC_ACCEPT ? cst[k] : mst[k];
+  return HBTC_OK;
 }
 
 // A few pair checks e(A_i, Q_i) == e(G1, W_i) (fewer than c->exact_below items): they have the

@@ -74,24 +74,24 @@ __device__ __forceinline__ uint32_t comb_parity(const G2A& p) { return g2_parity
 }  // namespace
 
 template <class F, int NW>
-__global__ void __launch_bounds__(COMB_SMALL_BS, 1)
-    k_comb_small(uint32_t t, const uint32_t* __restrict__ offsets,
-                 const int32_t* __restrict__ item_status, const uint32_t* __restrict__ idx,
-                 const uint8_t* __restrict__ pts, const Aff<F>* __restrict__ dec,
-                 int32_t* __restrict__ inst_status, uint8_t* __restrict__ out,
-                 uint8_t* __restrict__ parity) {
+__global__ void __launch_bounds__(COMB_SMALL_BS, 1) k_comb_small(CombSmallArgs A) {
   HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
   __shared__ uint32_t s_pos[COMB_SMALL_T];
   __shared__ Fr s_x[COMB_SMALL_T];
   __shared__ uint32_t s_cnt, s_bad, s_dup;
   __shared__ Jac<F> s_red[COMB_SMALL_BS];
   const uint32_t k = blockIdx.x, tid = threadIdx.x;
+  if (A.only && !A.only[k]) return;  // block-uniform
+  const uint32_t t = A.t;
+  // speculative subsets (gridDim.y > 1): block j leaves out the instance's j-th item
+  const uint32_t skip = gridDim.y > 1 ? blockIdx.y : 0xffffffffu;
+  const size_t o = (size_t)k * gridDim.y + blockIdx.y;  // output slot
   if (tid < 64) {  // wave 0: the first t items whose status is ACCEPT (all items without status)
-    const uint32_t a = offsets[k], b = offsets[k + 1];
+    const uint32_t a = A.offsets[k], b = A.offsets[k + 1];
     uint32_t found = 0;
     for (uint32_t base = a; base < b && found < t; base += 64) {
       const uint32_t i = base + tid;
-      const bool ok = i < b && (!item_status || item_status[i] == HBTC_ACCEPT);
+      const bool ok = i < b && i - a != skip && (!A.item_status || A.item_status[i] == HBTC_ACCEPT);
       const uint64_t mask = __ballot(ok);
       const uint32_t slot = found + (uint32_t)__popcll(mask & ((1ull << tid) - 1ull));
       if (ok && slot < t) s_pos[slot] = i;
@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(COMB_SMALL_BS, 1)
   const bool live = cnt == t && pi < cnt;
   if (live && h == 0) {
     Fr x;
-    fr_from_u64(x, (uint64_t)idx[s_pos[pi]] + 1);
+    fr_from_u64(x, (uint64_t)A.idx[s_pos[pi]] + 1);
     s_x[pi] = x;
   }
   __syncthreads();
@@ -138,18 +138,29 @@ __global__ void __launch_bounds__(COMB_SMALL_BS, 1)
     fr_from_mont(lc, l);
     uint64_t d[4];
     gls_u_digits(lc.v, d);
-    // the share: decoded by the verification, else decoded here
+    // the point: a key-set entry (by node), the verification's decoded share, or decoded here
     const uint32_t pos = s_pos[pi];
-    const bool accepted = item_status && item_status[pos] == HBTC_ACCEPT;
+    const Aff<F>* dec = static_cast<const Aff<F>*>(A.dec);
     Aff<F> P;
-    if (accepted && dec) {
-      P = dec[pos];
-    } else {
-      uint32_t w[NW];
-      comb_load(w, pts, pos, NW);
-      if (!comb_decode(P, w, !accepted)) {
+    if (A.by_node) {
+      const uint32_t id = A.idx[pos];
+      if (id < A.n_nodes) {
+        P = dec[id];
+      } else {  // an unknown sender (its share is never ACCEPTed: only speculative subsets get here)
         atomicOr(&s_bad, 1u);
         P.inf = 1;
+      }
+    } else {
+      const bool accepted = A.item_status && A.item_status[pos] == HBTC_ACCEPT;
+      if (accepted && dec) {
+        P = dec[pos];
+      } else {
+        uint32_t w[NW];
+        comb_load(w, A.pts, pos, NW);
+        if (!comb_decode(P, w, !accepted)) {
+          atomicOr(&s_bad, 1u);
+          P.inf = 1;
+        }
       }
     }
     if (!P.inf) {
@@ -178,30 +189,93 @@ __global__ void __launch_bounds__(COMB_SMALL_BS, 1)
       st = HBTC_DECODE_ERR;
     else if (s_dup)
       st = HBTC_DUPLICATE_ENTRY;
-    inst_status[k] = st;
+    const Jac<F> sum = s_red[0];
+    if (A.cmp) {  // compare with a point instead of encoding the sum
+      const Aff<F> q = *static_cast<const Aff<F>*>(A.cmp);
+      const bool si = jac_is_inf(sum);
+      const bool eq = (si || q.inf) ? (si && q.inf) : jac_eq_aff(sum, q.x, q.y);
+      A.inst_status[o] = st != HBTC_ACCEPT ? st : (eq ? HBTC_ACCEPT : HBTC_REJECT);
+      return;
+    }
+    A.inst_status[o] = st;
     Aff<F> a;
-    jac_to_aff(a, s_red[0]);
+    jac_to_aff(a, sum);
     uint32_t w[NW];
     comb_compress(w, a);
     if (st != HBTC_ACCEPT)
       for (int j = 0; j < NW; ++j) w[j] = 0;
-    comb_store(out, k, w, NW);
-    if (parity) parity[k] = (st == HBTC_ACCEPT) ? (uint8_t)comb_parity(a) : 0;
+    comb_store(A.out, o, w, NW);
+    if (A.parity) A.parity[o] = (st == HBTC_ACCEPT) ? (uint8_t)comb_parity(a) : 0;
   }
 }
 
-hipError_t launch_comb_small(hipStream_t s, int group, uint32_t n_inst, uint32_t t,
-                             const uint32_t* offsets, const int32_t* item_status, const uint32_t* idx,
-                             const uint8_t* pts, const void* dec, int32_t* inst_status, uint8_t* out,
-                             uint8_t* parity) {
+hipError_t launch_comb_small(hipStream_t s, int group, uint32_t n_inst, uint32_t n_sub,
+                             const CombSmallArgs& a) {
   if (n_inst == 0) return hipSuccess;
-  if (t == 0 || t > COMB_SMALL_T) return hipErrorInvalidValue;
+  if (a.t == 0 || a.t > COMB_SMALL_T || n_sub == 0) return hipErrorInvalidValue;
   if (group == 1)
-    hipLaunchKernelGGL((k_comb_small<Fq, 12>), dim3(n_inst), dim3(COMB_SMALL_BS), 0, s, t, offsets,
-                       item_status, idx, pts, static_cast<const G1A*>(dec), inst_status, out, nullptr);
+    hipLaunchKernelGGL((k_comb_small<Fq, 12>), dim3(n_inst, n_sub), dim3(COMB_SMALL_BS), 0, s, a);
   else
-    hipLaunchKernelGGL((k_comb_small<Fq2, 24>), dim3(n_inst), dim3(COMB_SMALL_BS), 0, s, t, offsets,
-                       item_status, idx, pts, static_cast<const G2A*>(dec), inst_status, out, parity);
+    hipLaunchKernelGGL((k_comb_small<Fq2, 24>), dim3(n_inst, n_sub), dim3(COMB_SMALL_BS), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- coin calls: commit
+// One thread per coin instance, after its shares' verification: the speculative subset whose
+// selection equals the verified one -- the first t items when they are all ACCEPTed (subset t,
+// which leaves out item t), or the first t + 1 minus the one non-ACCEPTed item j < t (subset j)
+// -- has its signature, parity, combine status and master check copied to the outputs; any
+// other pattern (two or more rejected among the first t + 1, fewer than t + 1 items with a
+// rejection, fewer than t items) is flagged for the status-driven combine (redo).
+__global__ void __launch_bounds__(64) k_coin_commit(uint32_t n_inst, uint32_t t, const uint32_t* __restrict__ offsets,
+                                                    const int32_t* __restrict__ item_status, uint32_t n_sub,
+                                                    const int32_t* __restrict__ spec_cst,
+                                                    const uint8_t* __restrict__ spec_sig,
+                                                    const uint8_t* __restrict__ spec_par,
+                                                    const int32_t* __restrict__ spec_master,
+                                                    int32_t* __restrict__ cst, uint8_t* __restrict__ sig,
+                                                    uint8_t* __restrict__ par, int32_t* __restrict__ master,
+                                                    uint32_t* __restrict__ redo) {
+  const uint32_t k = blockIdx.x * 64 + threadIdx.x;
+  if (k >= n_inst) return;
+  const uint32_t a = offsets[k], c = offsets[k + 1] - a;
+  uint32_t choice = 0xffffffffu;
+  if (c >= t) {
+    const uint32_t m = c < t + 1 ? c : t + 1;
+    uint32_t nrej = 0, rej = 0;
+    for (uint32_t i = 0; i < m; ++i)
+      if (item_status[a + i] != HBTC_ACCEPT) {
+        ++nrej;
+        rej = i;
+      }
+    if (nrej == 0 || (nrej == 1 && rej == t))
+      choice = t;  // the first t are ACCEPTed
+    else if (nrej == 1 && c >= t + 1)
+      choice = rej;
+  }
+  if (choice == 0xffffffffu) {
+    redo[k] = 1;
+    return;
+  }
+  redo[k] = 0;
+  const size_t o = (size_t)k * n_sub + choice;
+  cst[k] = spec_cst[o];
+  master[k] = spec_master[o];
+  par[k] = spec_par[o];
+  const uint4* src = reinterpret_cast<const uint4*>(spec_sig + o * 96);
+  uint4* dst = reinterpret_cast<uint4*>(sig + (size_t)k * 96);
+  for (int j = 0; j < 6; ++j) dst[j] = src[j];
+}
+
+hipError_t launch_coin_commit(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* offsets,
+                              const int32_t* item_status, uint32_t n_sub, const int32_t* spec_cst,
+                              const uint8_t* spec_sig, const uint8_t* spec_par,
+                              const int32_t* spec_master, int32_t* cst, uint8_t* sig, uint8_t* par,
+                              int32_t* master, uint32_t* redo) {
+  if (n_inst == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_coin_commit, dim3((n_inst + 63) / 64), dim3(64), 0, s, n_inst, t, offsets,
+                     item_status, n_sub, spec_cst, spec_sig, spec_par, spec_master, cst, sig, par,
+                     master, redo);
   return hipGetLastError();
 }
 

@@ -291,12 +291,30 @@ hipError_t launch_msm_reduce_g2(hipStream_t s, const MsmPlan& p, const G2A* pts,
 // ---- small combines, t <= COMB_SMALL_T shares per instance, one workgroup each (hbtc_comb.hip)
 constexpr uint32_t COMB_SMALL_T = 64;
 constexpr uint32_t COMB_SMALL_BS = 128;  // two lanes per selected share
-// group 1: DecryptionShares (dec: G1A*), 2: SignatureShares (dec: G2A*, parity written); dec may be
-// null (decode everything); item_status null = combine the first t items
-hipError_t launch_comb_small(hipStream_t s, int group, uint32_t n_inst, uint32_t t,
-                             const uint32_t* offsets, const int32_t* item_status, const uint32_t* idx,
-                             const uint8_t* pts, const void* dec, int32_t* inst_status, uint8_t* out,
-                             uint8_t* parity);
+struct CombSmallArgs {
+  uint32_t t;
+  const uint32_t* offsets;     // CSR instances over the items
+  const int32_t* item_status;  // null: the first t items; else the first t ACCEPTed ones
+  const uint32_t* idx;         // node index per item (x = idx + 1)
+  const uint8_t* pts;          // compressed items (48 / 96 B)
+  const void* dec;             // decoded items (Aff<F>*, used for ACCEPTed items) or null; by_node: per node
+  uint32_t by_node;            // points are dec[idx[item]] (a key set's resident pk), never decoded
+  uint32_t n_nodes;            // by_node: entries of dec (an idx past it counts as a decode error)
+  int32_t* inst_status;        // per output slot (instance k, subset j: k * n_sub + j)
+  uint8_t* out;                // compressed sums per slot (unused with cmp)
+  uint8_t* parity;             // G2 Signature::parity per slot, or null
+  const void* cmp;             // Aff<F>*: compare the sum with it (status ACCEPT / REJECT) instead of encoding
+  const uint32_t* only;        // per instance: run only where only[k] != 0 (null: all)
+};
+// group 1: G1 (DecryptionShares, key-set pk), 2: G2 (SignatureShares).  n_sub > 1: speculative
+// subsets, block (k, j) leaves out instance k's j-th item
+hipError_t launch_comb_small(hipStream_t s, int group, uint32_t n_inst, uint32_t n_sub,
+                             const CombSmallArgs& a);
+hipError_t launch_coin_commit(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* offsets,
+                              const int32_t* item_status, uint32_t n_sub, const int32_t* spec_cst,
+                              const uint8_t* spec_sig, const uint8_t* spec_par,
+                              const int32_t* spec_master, int32_t* cst, uint8_t* sig, uint8_t* par,
+                              int32_t* master, uint32_t* redo);
 
 // ---- SyncKeyGen (hbtc_skg.hip)
 hipError_t launch_skg_sym_scalars(hipStream_t s, uint32_t n_parts, uint32_t M, const Fr* U,

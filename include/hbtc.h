@@ -102,6 +102,30 @@ int hbtc_verify_sig_shares(hbtc_ctx* ctx, uint32_t keyset_id, uint32_t n_inst,
 int hbtc_verify_sigs(hbtc_ctx* ctx, uint32_t n, const uint8_t* pk_c48, const uint8_t* H_c96,
                      const uint8_t* sig_c96, int32_t* status);
 
+/* The key set's master public key (NetworkInfo::public_key, src/messaging.rs:253; compressed
+ * G1), decoded once with the subgroup check and kept resident for hbtc_coin_decide.  Returns
+ * HBTC_OK, or HBTC_ERR_ARG when it fails to decode (the key set keeps no master key then). */
+int hbtc_keyset_set_master(hbtc_ctx* ctx, uint32_t keyset_id, const uint8_t* master_pk_c48);
+
+/* A Threshold Coin round of n_inst coin instances in ONE call (the batch queue of src/coin.rs:
+ * 149-207): every SignatureShare verified as hbtc_verify_sig_shares (status[i], coin.rs:151),
+ * the first t ACCEPTed shares of each instance combined (combine_signatures, coin.rs:185-191:
+ * sig_c96[k], parity[k] = Signature::parity, coin.rs:173), and the combined signature checked
+ * against the master key (PublicKey::verify, coin.rs:192-197).  coin_status[k]: HBTC_ACCEPT (the
+ * coin value is parity[k]), the combine's failure (NOT_ENOUGH_SHARES, DUPLICATE_ENTRY,
+ * DECODE_ERR), or HBTC_REJECT when the combined signature fails the master check.
+ * The master check is exact without a pairing: every combined share passed e(pk_i, H) ==
+ * e(G1, sig_i), so e(G1, sum l_i sig_i) == e(sum l_i pk_i, H), and PublicKey::verify holds iff
+ * sum l_i pk_i == master pk in G1 (H != O, e non-degenerate) -- a G1 combine of the key set's
+ * resident shares.  Small calls (n_inst * (t + 1) <= 256, t < 64) combine speculatively while the
+ * shares are checked: every leave-one-out subset of each instance's first t + 1 items, committed
+ * when the verified selection is one of them (at most one of the first t + 1 rejected), else
+ * combined again from the statuses.  Needs hbtc_keyset_set_master; t in 1..64. */
+int hbtc_coin_decide(hbtc_ctx* ctx, uint32_t keyset_id, uint32_t n_inst, const uint8_t* H_c96,
+                     const uint32_t* offsets, const uint32_t* idx, const uint8_t* sig_items_c96,
+                     uint32_t t, int32_t* status, uint8_t* sig_c96, uint8_t* parity,
+                     int32_t* coin_status);
+
 /* Lagrange combine of the first t items of each instance (x = idx + 1) in G2: the compressed
  * signature, Signature::parity() (0/1) and an instance status (ACCEPT, NOT_ENOUGH_SHARES,
  * DUPLICATE_ENTRY, DECODE_ERR). */
