@@ -526,6 +526,9 @@ HD void xadic_mul_uniform(Jac<F>& r, const Aff<F>& p, const Aff<F>& xp, const Af
 #ifndef HBTC_XADIC16
 #define HBTC_XADIC16 1
 #endif
+#ifndef HBTC_XADIC8
+#define HBTC_XADIC8 1  // G1 item passes: the sign-aligned 8-entry table (xadic_mul_sac8) instead
+#endif
 #ifndef HBTC_XADIC16_G2
 #define HBTC_XADIC16_G2 1
 #endif

@@ -122,7 +122,6 @@ struct hbtc_ctx {
   hipStream_t s_comb = nullptr;  // combines: the current lane's stream (after its verification)
   hipEvent_t ev_main = nullptr, ev_prep = nullptr, ev_comb = nullptr;
   hipEvent_t ev_ext = nullptr, ev_ext2 = nullptr, ev_ext3 = nullptr;  // external-stream ordering
-  hipEvent_t ev_x_in = nullptr, ev_x_out = nullptr;  // ordering around the exact-kernel stream
   // speculative coin combines (hbtc_coin_decide), created on first use, high priority
   hipStream_t s_spec = nullptr;
   hipEvent_t ev_spec_in = nullptr, ev_spec_out = nullptr;
@@ -246,11 +245,8 @@ std::vector<std::string> lane_keys(const hbtc_ctx* c, const std::string& name) {
   return keys;
 }
 
-hipError_t exact_stream(int device, hipStream_t* out);
-bool exact_stream_exists(int device);
-
 // Close the batch of buffers retired by the growth in progress: a fence on every lane stream,
-// every preparation stream and the exact-kernel stream.
+// the preparation stream and the speculation stream.
 int retire_fence(hbtc_ctx* c) {
   if (c->retiring_dev.empty() && c->retiring_host.empty()) return HBTC_OK;
   hbtc_ctx::Retired r;
@@ -262,8 +258,6 @@ int retire_fence(hbtc_ctx* c) {
     streams.push_back(l.s_prep);
   }
   if (c->s_spec) streams.push_back(c->s_spec);
-  hipStream_t xs;
-  if (exact_stream_exists(c->device) && exact_stream(c->device, &xs) == hipSuccess) streams.push_back(xs);
   hipError_t e = hipSuccess;
   for (hipStream_t st : streams) {
     hipEvent_t ev = nullptr;
@@ -683,47 +677,6 @@ uint32_t probe_threshold(const Keyset* ks, uint32_t n_items) {
   return t > 2 ? (uint32_t)t : 2u;
 }
 
-// The per-item exact kernels (k_dec_verify, k_sig_verify, k_pair_verify: one pairing check per
-// lane, ~6 KB/lane of scratch) run on ONE stream per device for the whole process.  The runtime
-// reserves a kernel's scratch per hardware queue, for the whole device's wave slots; with
-// GPU_MAX_HW_QUEUES=16 a process whose many contexts dispatched them on every queue ran out
-// (HSA_STATUS_ERROR_OUT_OF_RESOURCES: the queue aborts, and every later HIP call of the process
-// fails -- round 3's 16-queue suite).  On one stream they hold one queue's reservation.
-namespace {
-std::mutex g_exact_mu;
-hipStream_t g_exact_stream[64] = {};
-}  // namespace
-
-bool exact_stream_exists(int device) {
-  std::lock_guard<std::mutex> lk(g_exact_mu);
-  return device >= 0 && device < 64 && g_exact_stream[device] != nullptr;
-}
-
-hipError_t exact_stream(int device, hipStream_t* out) {
-  std::lock_guard<std::mutex> lk(g_exact_mu);
-  if (device < 0 || device >= 64) return hipErrorInvalidDevice;
-  if (!g_exact_stream[device]) {
-    const hipError_t e = hipStreamCreateWithFlags(&g_exact_stream[device], hipStreamNonBlocking);
-    if (e != hipSuccess) return e;
-  }
-  *out = g_exact_stream[device];
-  return hipSuccess;
-}
-
-// launch(stream) on the exact-kernel stream, after everything queued so far on c->stream and
-// before anything queued there later
-template <class L>
-hipError_t on_exact_stream(hbtc_ctx* c, L&& launch) {
-  hipStream_t xs;
-  hipError_t e = exact_stream(c->device, &xs);
-  if (e != hipSuccess) return e;
-  if ((e = hipEventRecord(c->ev_x_in, c->stream)) != hipSuccess) return e;
-  if ((e = hipStreamWaitEvent(xs, c->ev_x_in, 0)) != hipSuccess) return e;
-  if ((e = launch(xs)) != hipSuccess) return e;
-  if ((e = hipEventRecord(c->ev_x_out, xs)) != hipSuccess) return e;
-  return hipStreamWaitEvent(c->stream, c->ev_x_out, 0);
-}
-
 // Group-check schedule of one RLC call.  The plain-first form (5 levels: plain and weighted
 // checks of tiles, then of sub-tiles, then leaves) does the least work and is right when the
 // call fills the chip; a call with few tiles (a rank's slice under strong scaling, a small
@@ -775,22 +728,6 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   Line *h_lines, *w_lines;
   Tile* tiles;
   uint32_t n_tiles;
-  if (c->verify_mode == HBTC_MODE_PER_SHARE) {
-    HB_TRY(guard_write(c, d_status, (size_t)n_items * 4));
-    if (c->last_dec.status == d_status) c->last_dec = {};
-    HB_TRY(prepare_g2(c, d_H, d_w, n_ct, &h_aff, &h_st, &h_lines));
-    w_aff = h_aff + n_ct;
-    w_st = h_st + n_ct;
-    w_lines = h_lines + (size_t)n_ct * MILLER_STEPS;
-    HB_TRY(make_tiles(c, n_ct, offsets, &tiles, &n_tiles));
-    HB_TRY(timed(c, "dec_verify", [&] {
-      return on_exact_stream(c, [&](hipStream_t xs) {
-        return launch_dec_verify(xs, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->n, h_aff,
-                                 h_st, h_lines, w_aff, w_st, w_lines, d_status);
-      });
-    }));
-    return end_verify(c);
-  }
   // RLC batch verification with hierarchical fallback (hbtc_rlc.hip).  The per-ciphertext G2
   // preparation runs on s_prep concurrently with the item pass; the checks wait for both.
   HB_TRY(stream_after(c, c->s_prep, c->stream, c->ev_main));
@@ -802,7 +739,9 @@ int dec_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const uint8_t
   // Cold key set (no RLC call on it yet, sender tracking on): a probe pass over the first
   // ciphertexts finds the senders who lie on all of them before the call proper, so f Byzantine
   // senders do not send most of the first epoch's shares to the exact checks.
-  const bool exact = n_items < c->exact_below;  // a small call: exact leaf checks only
+  // per-share mode, or a small call: no group sums, every share gets the exact cooperative leaf
+  // check (the per-share mode's count of pairing checks, on the leaf kernels' layout)
+  const bool exact = c->verify_mode == HBTC_MODE_PER_SHARE || n_items < c->exact_below;
   const uint32_t n_probe = exact ? 0 : probe_size(c, ks, n_ct);
   if (n_probe) {
     HB_TRY(rlc_dec_pass(c, ks, n_probe, offsets, d_idx, d_share, nullptr, prep));
@@ -1010,17 +949,6 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   Line* h_lines;
   Tile* tiles;
   uint32_t n_tiles;
-  if (c->verify_mode == HBTC_MODE_PER_SHARE) {
-    HB_TRY(prepare_g2(c, d_H, nullptr, n_inst, &h_aff, &h_st, &h_lines));
-    HB_TRY(make_tiles(c, n_inst, offsets, &tiles, &n_tiles));
-    HB_TRY(timed(c, "sig_verify", [&] {
-      return on_exact_stream(c, [&](hipStream_t xs) {
-        return launch_sig_verify(xs, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->n, h_aff,
-                                 h_st, h_lines, d_status);
-      });
-    }));
-    return end_verify(c);
-  }
   // RLC batch verification (hbtc_sig.hip): H's line tables on s_prep beside the item pass; the
   // G2 sums' projective line tables before each check level.
   HB_TRY(stream_after(c, c->s_prep, c->stream, c->ev_main));
@@ -1048,18 +976,15 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   uint32_t* leaf_count = counters;
   uint32_t* sub_count = counters + 1;
   HB_CHECK(c, launch_zero_u32(c->stream, counters, 2));
-  // a small call: the item pass decodes and lists every share for the exact leaf checks
-  const bool exact = n_items < c->exact_below;
+  // per-share mode, or a small call: the item pass decodes and lists every share for the exact
+  // leaf checks
+  const bool exact = c->verify_mode == HBTC_MODE_PER_SHARE || n_items < c->exact_below;
   const Suspects sus =
       exact ? Suspects{nullptr, 0, leaf_count, leaves, 1} : suspects_of(c, ks, leaf_count, leaves);
   HB_TRY(items_gate(c, n_tiles));
   HB_TRY(timed(c, "sig_items", [&] {
-    auto go = [&](hipStream_t s) {
-      return launch_sig_items(s, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->tab, ks->n, key,
-                              sus, sums, dec, d_status);
-    };
-    // the throughput form's scratch (curve.h HBTC_XADIC16_G2) is held by one queue
-    return sig_items_big(n_tiles) ? on_exact_stream(c, go) : go(c->stream);
+    return launch_sig_items(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->tab, ks->n,
+                            key, sus, sums, dec, d_status);
   }));
   HB_TRY(items_mark(c));
   if (!exact)
@@ -1566,9 +1491,7 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (!created(hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming), "hipEventCreateWithFlags") ||
       !created(hipEventCreateWithFlags(&c->ev_ext, hipEventDisableTiming), "hipEventCreateWithFlags") ||
       !created(hipEventCreateWithFlags(&c->ev_ext2, hipEventDisableTiming), "hipEventCreateWithFlags") ||
-      !created(hipEventCreateWithFlags(&c->ev_ext3, hipEventDisableTiming), "hipEventCreateWithFlags") ||
-      !created(hipEventCreateWithFlags(&c->ev_x_in, hipEventDisableTiming), "hipEventCreateWithFlags") ||
-      !created(hipEventCreateWithFlags(&c->ev_x_out, hipEventDisableTiming), "hipEventCreateWithFlags")) {
+      !created(hipEventCreateWithFlags(&c->ev_ext3, hipEventDisableTiming), "hipEventCreateWithFlags")) {
     hbtc_ctx_destroy(c);
     return HBTC_ERR_DEVICE;
   }
@@ -1628,8 +1551,6 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
   ev_free(c->ev_ext);
   ev_free(c->ev_ext2);
   ev_free(c->ev_ext3);
-  ev_free(c->ev_x_in);
-  ev_free(c->ev_x_out);
   ev_free(c->ev_spec_in);
   ev_free(c->ev_spec_out);
   if (c->s_spec) (void)hipStreamDestroy(c->s_spec);
@@ -1873,9 +1794,9 @@ int hbtc_coin_decide(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uin
 // s_prep, the item pass decoding W with every item on the leaf list, W's projective lines, the
 // cooperative leaf checks.  Four dependent launches for c1's master signature instead of the
 // pair batch's item pass, line tables, Miller partials and final exponentiation.  Statuses as
-// k_pair_verify's: an A, Q or W that fails to decode is the item's DECODE_ERR.
-int pb_small_exact(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_q,
-                   const uint8_t* d_w, int32_t* d_status, G1A* d_adec) {
+// the pair check's: an A, Q or W that fails to decode is the item's DECODE_ERR.
+int pb_small_exact_chunk(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_q,
+                         const uint8_t* d_w, int32_t* d_status, G1A* d_adec) {
   std::vector<uint32_t> offsets(n + 1), idx(n);
   for (uint32_t i = 0; i <= n; ++i) offsets[i] = i;
   for (uint32_t i = 0; i < n; ++i) idx[i] = i;
@@ -1906,14 +1827,12 @@ int pb_small_exact(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d
   HB_TRY(wst(c, "pbx.leaves", (size_t)2 * n, &leaves));
   HB_CHECK(c, launch_zero_u32(c->stream, counters, 2));
   HB_TRY(timed(c, "pb_decode", [&] { return launch_g1_decode(c->stream, d_a, n, A, a_st); }));
-  RlcKey key{};  // no group sums: the scalars are never drawn
+  RlcKey key{};  // no group sums (Suspects.all): the scalars and the pk table are never read
+  key.bits = c->rlc_bits;
   const Suspects sus{nullptr, 0, counters, leaves, 1};
   HB_TRY(timed(c, "sig_items", [&] {
-    auto go = [&](hipStream_t s) {
-      return launch_sig_items(s, n_tiles, tiles, d_idx, d_w, A, a_st,
-                              reinterpret_cast<const PtXY*>(tables), n, key, sus, sums, dec, d_status);
-    };
-    return sig_items_big(n_tiles) ? on_exact_stream(c, go) : go(c->stream);
+    return launch_sig_items(c->stream, n_tiles, tiles, d_idx, d_w, A, a_st, nullptr, n, key, sus, sums,
+                            dec, d_status);
   }));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
   HB_TRY(timed(c, "sig_lines", [&] {
@@ -1935,23 +1854,52 @@ int pb_small_exact(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d
   });
 }
 
+// pb_small_exact over any n: chunks of PBX_CHUNK items (19.6 KB of line tables per item).
+constexpr uint32_t PBX_CHUNK = 1u << 15;
+int pb_small_exact(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_q,
+                   const uint8_t* d_w, int32_t* d_status, G1A* d_adec) {
+  if (!d_a) return fail(c, HBTC_ERR_ARG, "pair checks need their G1 arguments");
+  for (uint32_t base = 0; base < n; base += PBX_CHUNK) {
+    const uint32_t m = std::min(PBX_CHUNK, n - base);
+    HB_TRY(pb_small_exact_chunk(c, m, d_a + (size_t)48 * base, d_q + (size_t)96 * base,
+                                d_w + (size_t)96 * base, d_status + base, d_adec ? d_adec + base : nullptr));
+  }
+  return HBTC_OK;
+}
+
+// The exact checks of the items a pair batch's failing sub-tiles listed (`count` on the device):
+// gathered into a compact batch, checked by pb_small_exact, statuses scattered back.  The count
+// is read back first (a failing sub-tile is rare; pair batches run inside blocking host calls).
+int pb_exact_list(hbtc_ctx* c, uint32_t m, const uint8_t* a, const uint8_t* q, const uint8_t* w,
+                  int32_t* st, const uint32_t* d_count, const uint32_t* d_list) {
+  uint32_t cnt = 0;
+  HB_TRY(download(c, &cnt, d_count, 4));
+  HB_CHECK(c, hipStreamSynchronize(c->stream));
+  if (cnt == 0) return HBTC_OK;
+  if (cnt > m) return fail(c, HBTC_ERR_DEVICE, "pair batch: leaf count past the chunk");
+  uint8_t *ga, *gq, *gw;
+  int32_t* gst;
+  HB_TRY(wst(c, "pbl.a", (size_t)48 * cnt, &ga));
+  HB_TRY(wst(c, "pbl.q", (size_t)96 * cnt, &gq));
+  HB_TRY(wst(c, "pbl.w", (size_t)96 * cnt, &gw));
+  HB_TRY(wst(c, "pbl.st", cnt, &gst));
+  HB_CHECK(c, launch_pb_gather(c->stream, cnt, d_list, a, q, w, ga, gq, gw));
+  HB_TRY(pb_small_exact(c, cnt, ga, gq, gw, gst, nullptr));
+  HB_CHECK(c, launch_pb_scatter(c->stream, cnt, d_list, gst, st));
+  return HBTC_OK;
+}
+
 // e(A_i, Q_i) == e(G1, W_i) for n items in device memory (A null: the G1 generator; Q trusted:
 // our own hash output, decoded without the subgroup check; statuses ACCEPT / REJECT /
-// DECODE_ERR as k_pair_verify's).  RLC mode: the pair-batch path of hbtc_pb.hip in chunks of
+// DECODE_ERR).  RLC mode: the pair-batch path of hbtc_pb.hip in chunks of
 // c->pb_chunk items (the per-item line tables are 19.6 KB each): item pass, Q line tables,
 // partial Miller products per 8-item sub-tile, the 64-item tile checks, the 8-item sub-tiles of
-// failing tiles, the exact k_pair_verify of the items of failing sub-tiles; a fresh RLC key per
-// chunk.  Per-share mode: k_pair_verify for every item.
+// failing tiles, the exact cooperative checks of the items of failing sub-tiles (pb_exact_list); a
+// fresh RLC key per chunk.  Per-share mode and small calls: the exact checks for every item.
 int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_q, bool q_trusted,
                   const uint8_t* d_w, int32_t* d_status, G1A* d_adec = nullptr) {
-  if (c->verify_mode == HBTC_MODE_PER_SHARE) {
-    return timed(c, "pair_verify", [&] {
-      return on_exact_stream(c, [&](hipStream_t xs) {
-        return launch_pair_verify(xs, n, d_a, d_q, nullptr, d_w, d_status);
-      });
-    });
-  }
-  if (d_a && n < c->exact_below) return pb_small_exact(c, n, d_a, d_q, d_w, d_status, d_adec);
+  if (c->verify_mode == HBTC_MODE_PER_SHARE || n < c->exact_below)
+    return pb_small_exact(c, n, d_a, d_q, d_w, d_status, d_adec);
   const uint32_t PB_CHUNK = c->pb_chunk;
   for (uint32_t base = 0; base < n; base += PB_CHUNK) {
     const uint32_t m = std::min(PB_CHUNK, n - base);
@@ -1999,11 +1947,7 @@ int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_
       return launch_pb_fe(c->stream, 1, 8 * T, m, 0, counters, tlist, fbuf, wtab, winf, st,
                           counters + 1, leaves);
     }));
-    HB_TRY(timed(c, "pair_verify", [&] {
-      return on_exact_stream(c, [&](hipStream_t xs) {
-        return launch_pair_verify(xs, m, a, q, nullptr, w, st, leaves, counters + 1);
-      });
-    }));
+    HB_TRY(pb_exact_list(c, m, a, q, w, st, counters + 1, leaves));
   }
   return HBTC_OK;
 }

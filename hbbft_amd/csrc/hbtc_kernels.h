@@ -158,9 +158,6 @@ hipError_t launch_chk_leaves(hipStream_t s, uint32_t max_leaves, const uint32_t*
                              uint32_t rep3_limit = 0);
 
 // ---- RLC batch verification of SignatureShares (hbtc_sig.hip, checks in hbtc_check.hip)
-// the two-wave throughput form of k_sig_items (with HBTC_XADIC16_G2: the table form, launched on
-// the exact stream)
-bool sig_items_big(uint32_t n_tiles);
 hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* sigs, const G1A* pk, const int32_t* pk_status,
                             const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,
@@ -205,22 +202,14 @@ hipError_t launch_g1_decode(hipStream_t s, const uint8_t* in, uint32_t n, G1A* o
 // contiguous); ws holds 3 * MILLER_STEPS Fq2 per argument.
 hipError_t launch_g2_prepare(hipStream_t s, const uint8_t* in0, uint32_t n0, const uint8_t* in1,
                              uint32_t n1, G2A* aff, Line* lines, Fq2* ws, int32_t* status);
-hipError_t launch_dec_verify(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
-                             const uint32_t* idx, const uint8_t* shares, const G1A* pk,
-                             const int32_t* pk_status, uint32_t n_pk, const G2A* h_aff,
-                             const int32_t* h_status, const Line* h_lines, const G2A* w_aff,
-                             const int32_t* w_status, const Line* w_lines, int32_t* status);
-hipError_t launch_sig_verify(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
-                             const uint32_t* idx, const uint8_t* sigs, const G1A* pk,
-                             const int32_t* pk_status, uint32_t n_pk, const G2A* h_aff,
-                             const int32_t* h_status, const Line* h_lines, int32_t* status);
-hipError_t launch_pair_verify(hipStream_t s, uint32_t n, const uint8_t* a1, const uint8_t* a2,
-                              const uint8_t* b1, const uint8_t* b2, int32_t* status,
-                              const uint32_t* list = nullptr, const uint32_t* count = nullptr);
 // ---- pair batches e(A_i, Q_i) == e(G1, W_i) by RLC (hbtc_pb.hip, checks in hbtc_check.hip)
 // items: decode A (null: the G1 generator), Q (q_trusted: no subgroup check), W; r_i A_i (affine)
 // -> rA, decoded Q -> Qdec, the plain sums of r_i W_i per 64-item tile and 8-item sub-tile (S[]
 // of SigTileSums), statuses PENDING / DECODE_ERR
+hipError_t launch_pb_gather(hipStream_t s, uint32_t n, const uint32_t* list, const uint8_t* a,
+                            const uint8_t* q, const uint8_t* w, uint8_t* ga, uint8_t* gq, uint8_t* gw);
+hipError_t launch_pb_scatter(hipStream_t s, uint32_t n, const uint32_t* list, const int32_t* gst,
+                             int32_t* st);
 hipError_t launch_pb_items(hipStream_t s, uint32_t n, const uint8_t* a_c48, const uint8_t* q_c96,
                            bool q_trusted, const uint8_t* w_c96, RlcKey key, G1A* rA, G2A* Qdec,
                            SigTileSums* sums, int32_t* status, G1A* adec = nullptr);

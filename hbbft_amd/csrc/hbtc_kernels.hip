@@ -18,8 +18,9 @@
 //     SGPRs, which the multiplies consume directly as operands.
 #include "hbtc_kernels.h"
 
-// The file is compiled once per kernel group (Makefile: -DHBTC_PART=1..5) so the groups,
-// each minutes of register allocation, build in parallel; HBTC_PART=0 builds all of them.
+// Kernel groups are selected by -DHBTC_PART (one group left since round 5: the per-item exact
+// kernels k_dec_verify / k_sig_verify / k_pair_verify, a whole Fq12 tower per lane and ~6 KB of
+// scratch per lane, are gone -- the per-share modes take the cooperative exact leaf checks).
 #ifndef HBTC_PART
 #define HBTC_PART 0
 #endif
@@ -223,151 +224,6 @@ __global__ void __launch_bounds__(64) k_pk_table(const G1A* __restrict__ pk,
 
 #endif  // part 1
 
-// ------------------------------------------------------------------------------ share checks
-#if HBTC_IN_PART(2)
-// DecryptionShare: e(share_i, H_k) == e(pk_idx, w_k)  <=>  e(share_i, H_k) e(-pk_idx, w_k) == 1.
-// Both G2 arguments are per-ciphertext constants: two precomputed line tables, one Fq12
-// squaring chain, one final exponentiation per item.
-__global__ void __launch_bounds__(64) k_dec_verify(
-    const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
-    const uint8_t* __restrict__ shares, const G1A* __restrict__ pk,
-    const int32_t* __restrict__ pk_status, uint32_t n_pk, const G2A* __restrict__ h_aff,
-    const int32_t* __restrict__ h_status, const Line* __restrict__ h_lines,
-    const G2A* __restrict__ w_aff, const int32_t* __restrict__ w_status,
-    const Line* __restrict__ w_lines, int32_t* __restrict__ status) {
-  const Tile tile = tiles[blockIdx.x];
-  const uint32_t lane = threadIdx.x;
-  if (lane >= tile.count) return;
-  const size_t item = (size_t)tile.first + lane;
-  const uint32_t k = tile.inst;
-  if (h_status[k] != HBTC_ACCEPT || w_status[k] != HBTC_ACCEPT) {
-    status[item] = HBTC_INSTANCE_ERR;
-    return;
-  }
-  const uint32_t id = idx[item];
-  if (id >= n_pk) {
-    status[item] = HBTC_UNKNOWN_SENDER;
-    return;
-  }
-  if (pk_status[id] != HBTC_ACCEPT) {
-    status[item] = HBTC_DECODE_ERR;
-    return;
-  }
-  uint32_t w[12];
-  load_words(w, shares, item, 12);
-  G1A s;
-  if (!g1_decompress(s, w)) {
-    status[item] = HBTC_DECODE_ERR;
-    return;
-  }
-  G1A npk;
-  aff_neg(npk, pk[id]);
-  const bool h_inf = h_aff[k].inf != 0, w_inf = w_aff[k].inf != 0;
-  Fq12 f, e;
-  miller_loop_2(f, TableLines{h_lines + (size_t)k * MILLER_STEPS}, s, !s.inf && !h_inf,
-                TableLines{w_lines + (size_t)k * MILLER_STEPS}, npk, !npk.inf && !w_inf);
-  final_exponentiation(e, f);
-  status[item] = fq12_is_one(e) ? HBTC_ACCEPT : HBTC_REJECT;
-}
-
-#endif  // part 2
-
-#if HBTC_IN_PART(3)
-// SignatureShare: e(pk_idx, H_k) == e(G1, sig_i)  <=>  e(pk_idx, H_k) e(-G1, sig_i) == 1.
-// H_k's lines are precomputed per instance; sig_i's lines are computed on the fly.
-__global__ void __launch_bounds__(64) k_sig_verify(
-    const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
-    const uint8_t* __restrict__ sigs, const G1A* __restrict__ pk,
-    const int32_t* __restrict__ pk_status, uint32_t n_pk, const G2A* __restrict__ h_aff,
-    const int32_t* __restrict__ h_status, const Line* __restrict__ h_lines,
-    int32_t* __restrict__ status) {
-  const Tile tile = tiles[blockIdx.x];
-  const uint32_t lane = threadIdx.x;
-  if (lane >= tile.count) return;
-  const size_t item = (size_t)tile.first + lane;
-  const uint32_t k = tile.inst;
-  if (h_status[k] != HBTC_ACCEPT) {
-    status[item] = HBTC_INSTANCE_ERR;
-    return;
-  }
-  const uint32_t id = idx[item];
-  if (id >= n_pk) {
-    status[item] = HBTC_UNKNOWN_SENDER;
-    return;
-  }
-  if (pk_status[id] != HBTC_ACCEPT) {
-    status[item] = HBTC_DECODE_ERR;
-    return;
-  }
-  uint32_t w[24];
-  load_words(w, sigs, item, 24);
-  G2A sg;
-  if (!g2_decompress(sg, w)) {
-    status[item] = HBTC_DECODE_ERR;
-    return;
-  }
-  const G1A P = pk[id];
-  G1A ng;
-  neg_g1_generator(ng);
-  const bool h_inf = h_aff[k].inf != 0;
-  Fq12 f, e;
-  miller_loop_fixed_var(f, TableLines{h_lines + (size_t)k * MILLER_STEPS}, P,
-                        !P.inf && !h_inf, ng, sg, !sg.inf);
-  final_exponentiation(e, f);
-  status[item] = fq12_is_one(e) ? HBTC_ACCEPT : HBTC_REJECT;
-}
-
-#endif  // part 3
-
-#if HBTC_IN_PART(4)
-// Generic e(a1, a2) == e(b1, b2) with every argument per item; a null G1 pointer means the
-// G1 generator.  verify_sigs: (pk, H) vs (G1, sig).  verify_ciphertexts: (G1, w) vs (u, H).
-// With `count` non-null: only the *count items list[0 ..) (the exact checks behind a failing
-// pair-batch group, hbtc_pb.hip).
-__global__ void __launch_bounds__(64) k_pair_verify(uint32_t n, const uint8_t* __restrict__ a1,
-                                                    const uint8_t* __restrict__ a2,
-                                                    const uint8_t* __restrict__ b1,
-                                                    const uint8_t* __restrict__ b2,
-                                                    int32_t* __restrict__ status,
-                                                    const uint32_t* __restrict__ list,
-                                                    const uint32_t* __restrict__ count) {
-  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
-  if (count) n = *count;
-  if (g >= n) return;
-  const uint32_t i = count ? list[g] : g;
-  uint32_t w[24];
-  G1A A1, B1;
-  G2A A2, B2;
-  bool ok = true;
-  if (a1) {
-    load_words(w, a1, i, 12);
-    ok &= g1_decompress(A1, w);
-  } else {
-    g1_generator(A1);
-  }
-  if (b1) {
-    load_words(w, b1, i, 12);
-    ok &= g1_decompress(B1, w);
-  } else {
-    g1_generator(B1);
-  }
-  load_words(w, a2, i, 24);
-  ok &= g2_decompress(A2, w);
-  load_words(w, b2, i, 24);
-  ok &= g2_decompress(B2, w);
-  if (!ok) {
-    status[i] = HBTC_DECODE_ERR;
-    return;
-  }
-  G1A nB1;
-  aff_neg(nB1, B1);
-  Fq12 f, e;
-  miller_loop_var_var(f, A1, A2, !A1.inf && !A2.inf, nB1, B2, !nB1.inf && !B2.inf);
-  final_exponentiation(e, f);
-  status[i] = fq12_is_one(e) ? HBTC_ACCEPT : HBTC_REJECT;
-}
-
-#endif  // part 4
 
 #if HBTC_IN_PART(1)
 // ------------------------------------------------------------------------------ scalar mult
@@ -442,44 +298,6 @@ hipError_t launch_g2_prepare(hipStream_t s, const uint8_t* in0, uint32_t n0, con
 
 #endif  // part 1
 
-#if HBTC_IN_PART(2)
-hipError_t launch_dec_verify(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
-                             const uint32_t* idx, const uint8_t* shares, const G1A* pk,
-                             const int32_t* pk_status, uint32_t n_pk, const G2A* h_aff,
-                             const int32_t* h_status, const Line* h_lines, const G2A* w_aff,
-                             const int32_t* w_status, const Line* w_lines, int32_t* status) {
-  if (n_tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_dec_verify, dim3(n_tiles), dim3(64), 0, s, tiles, idx, shares, pk,
-                     pk_status, n_pk, h_aff, h_status, h_lines, w_aff, w_status, w_lines, status);
-  return hipGetLastError();
-}
-
-#endif  // part 2
-
-#if HBTC_IN_PART(3)
-hipError_t launch_sig_verify(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
-                             const uint32_t* idx, const uint8_t* sigs, const G1A* pk,
-                             const int32_t* pk_status, uint32_t n_pk, const G2A* h_aff,
-                             const int32_t* h_status, const Line* h_lines, int32_t* status) {
-  if (n_tiles == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_sig_verify, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk,
-                     pk_status, n_pk, h_aff, h_status, h_lines, status);
-  return hipGetLastError();
-}
-
-#endif  // part 3
-
-#if HBTC_IN_PART(4)
-hipError_t launch_pair_verify(hipStream_t s, uint32_t n, const uint8_t* a1, const uint8_t* a2,
-                              const uint8_t* b1, const uint8_t* b2, int32_t* status,
-                              const uint32_t* list, const uint32_t* count) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_pair_verify, dim3(blocks_for(n, 64)), dim3(64), 0, s, n, a1, a2, b1, b2,
-                     status, list, count);
-  return hipGetLastError();
-}
-
-#endif  // part 4
 
 #if HBTC_IN_PART(1)
 hipError_t launch_point_mul(hipStream_t s, int group, uint32_t n, const uint8_t* base,

@@ -22,7 +22,7 @@
 namespace hbtc {
 
 #ifndef HBTC_PB_ITEMS_WAVES
-#define HBTC_PB_ITEMS_WAVES 2
+#define HBTC_PB_ITEMS_WAVES 1  // one wave per SIMD: 740 B/lane of scratch (two: 1.5 KB)
 #endif
 
 // One wave per tile of 64 consecutive items: decode A (G1, subgroup check; null = the G1
@@ -73,7 +73,9 @@ __global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n
         Fq beta;
         fq_set(beta, G1_BETA);
         G1J t;
-#if HBTC_XADIC16
+#if HBTC_XADIC8
+        xadic_mul_sac8(t, A, t1, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+#elif HBTC_XADIC16
         xadic_mul_tab16(t, A, t1, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
 #else
         G1A xp, pxp;
@@ -120,6 +122,44 @@ __global__ void __launch_bounds__(64) k_pb_lines(uint32_t n, const G2A* __restri
   const G2A Q = Qdec[i];
   if (Q.inf) return;  // the pair is unused (e(A, O) = 1)
   g2_proj_lines(tables + (size_t)i * PLINES_FQ2, Q);
+}
+
+// The items of a failing sub-tile, gathered for the exact checks (pb_exact_list): list[0, n).
+__global__ void __launch_bounds__(64) k_pb_gather(uint32_t n, const uint32_t* __restrict__ list,
+                                                  const uint8_t* __restrict__ a, const uint8_t* __restrict__ q,
+                                                  const uint8_t* __restrict__ w, uint8_t* __restrict__ ga,
+                                                  uint8_t* __restrict__ gq, uint8_t* __restrict__ gw) {
+  const uint32_t g = blockIdx.x * 64u + threadIdx.x;
+  if (g >= n) return;
+  const size_t i = list[g];
+  const uint4* sa = reinterpret_cast<const uint4*>(a + 48 * i);
+  const uint4* sq = reinterpret_cast<const uint4*>(q + 96 * i);
+  const uint4* sw = reinterpret_cast<const uint4*>(w + 96 * i);
+  uint4* da = reinterpret_cast<uint4*>(ga + (size_t)48 * g);
+  uint4* dq = reinterpret_cast<uint4*>(gq + (size_t)96 * g);
+  uint4* dw = reinterpret_cast<uint4*>(gw + (size_t)96 * g);
+  for (int j = 0; j < 3; ++j) da[j] = sa[j];
+  for (int j = 0; j < 6; ++j) {
+    dq[j] = sq[j];
+    dw[j] = sw[j];
+  }
+}
+__global__ void __launch_bounds__(64) k_pb_scatter(uint32_t n, const uint32_t* __restrict__ list,
+                                                   const int32_t* __restrict__ gst, int32_t* __restrict__ st) {
+  const uint32_t g = blockIdx.x * 64u + threadIdx.x;
+  if (g < n) st[list[g]] = gst[g];
+}
+hipError_t launch_pb_gather(hipStream_t s, uint32_t n, const uint32_t* list, const uint8_t* a,
+                            const uint8_t* q, const uint8_t* w, uint8_t* ga, uint8_t* gq, uint8_t* gw) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pb_gather, dim3((n + 63) / 64), dim3(64), 0, s, n, list, a, q, w, ga, gq, gw);
+  return hipGetLastError();
+}
+hipError_t launch_pb_scatter(hipStream_t s, uint32_t n, const uint32_t* list, const int32_t* gst,
+                             int32_t* st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pb_scatter, dim3((n + 63) / 64), dim3(64), 0, s, n, list, gst, st);
+  return hipGetLastError();
 }
 
 hipError_t launch_pb_items(hipStream_t s, uint32_t n, const uint8_t* a_c48, const uint8_t* q_c96,

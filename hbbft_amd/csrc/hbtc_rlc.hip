@@ -54,9 +54,6 @@ namespace hbtc {
 #ifndef HBTC_ITEMS_PRIO
 #define HBTC_ITEMS_PRIO 0  // wave priority of the item pass (experiments: 3 = above the check levels)
 #endif
-#ifndef HBTC_XADIC8
-#define HBTC_XADIC8 1  // r_i d_i by the sign-aligned 8-entry table (curve.h xadic_mul_sac8)
-#endif
 #ifndef HBTC_SAC8_LDS
 #define HBTC_SAC8_LDS 1  // three of the eight entries in LDS (the reduction's arrays, unused then)
 #endif

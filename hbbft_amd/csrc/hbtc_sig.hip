@@ -19,24 +19,19 @@
 
 namespace hbtc {
 
-// Two instances (launch_sig_items picks by the call's size): W = 2, two waves per SIMD with one
-// LDS array (rlc_reduce1; more VGPR spills per wave, C4's 10^4 tiles: k_sig_items 106 -> 80 ms)
-// and W = 1, one wave per SIMD with two arrays (shorter waves: C2's 200 tiles, 13.3 -> 10.2 ms).
-// Re-measured with the shared-subroutine product (2.5 KB / 0.7 KB of scratch per lane): C4 161
-// ms per step with W = 2 against 171 with W = 1 (profiles/r03/sig_waves/).
 // One wave per tile: decode every SignatureShare (zcash compressed G2 + subgroup check), r_i,
-// r_i sigma_i, r_i pk_i, then the plain and weighted tile / sub-tile sums in both groups.
-// T16: r_i sigma_i by the 15-entry table (curve.h xadic_mul_tab16; 2.9 KB/lane more scratch).
-// Only the two-wave throughput form uses it, and it runs on the process-wide exact stream
-// (hbtc_api.hip on_exact_stream): the runtime reserves a kernel's scratch per hardware queue.
-template <int W, bool T16>
-__global__ void __launch_bounds__(64, W) k_sig_items(
+// r_i sigma_i, r_i pk_i, then the plain and weighted tile / sub-tile sums in both groups.  One
+// wave per SIMD (256 VGPRs + 256 AGPRs: 736 B/lane of scratch).  Round 5 dropped the two-wave
+// form (2.7 KB/lane) and its 15-entry G2 table (8.2 KB/lane), which had to run on one
+// process-wide stream: the runtime reserves a kernel's scratch per hardware queue, and with 16
+// queues those private segments aborted queues (HSA_STATUS_ERROR_OUT_OF_RESOURCES).
+__global__ void __launch_bounds__(64, 1) k_sig_items(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
     const uint8_t* __restrict__ sigs, const G1A* __restrict__ pk,
     const int32_t* __restrict__ pk_status, const PtXY* __restrict__ pk_tab, uint32_t n_pk,
     RlcKey key, Suspects sus, SigTileSums* __restrict__ sums, G2A* __restrict__ dec,
     int32_t* __restrict__ status) {
-  __shared__ G2J red2[W == 2 ? 1 : 2][64];  // reused for the G1 reduction (W = 2: 13.8 KB)
+  __shared__ G2J red2[2][64];  // reused for the G1 reduction
   G1J* red1 = reinterpret_cast<G1J*>(&red2[0][0]);
   const Tile tile = tiles[blockIdx.x];
   const uint32_t lane = threadIdx.x;
@@ -75,13 +70,9 @@ __global__ void __launch_bounds__(64, W) k_sig_items(
             jac_from_aff(xj, xp);
             Fq zeta;
             fq_set(zeta, G2_ZETA);
-            if (T16) {
-              xadic_mul_tab16(S, sg, xj, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
-            } else {
-              G2A pxp;
-              xadic_table(xp, pxp, sg, xj);
-              xadic_mul_uniform(S, sg, xp, pxp, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
-            }
+            G2A pxp;
+            xadic_table(xp, pxp, sg, xj);
+            xadic_mul_uniform(S, sg, xp, pxp, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
           }
           if (!pk[id].inf) rlc_pk_mul_x(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, xd);
         }
@@ -92,13 +83,8 @@ __global__ void __launch_bounds__(64, W) k_sig_items(
   }
   rlc_list_leaf(sus, leaf, (uint32_t)item, tile.inst, lane);
   SigTileSums* ts = sums + blockIdx.x;
-  if (W == 2) {
-    rlc_reduce1<Fq2>(red2[0], S, lane, ts->S, ts->SW);
-    rlc_reduce1<Fq>(red1, P, lane, ts->P, ts->PW);
-  } else {
-    rlc_reduce<Fq2>(red2[0], red2[W == 2 ? 0 : 1], S, lane, ts->S, ts->SW);
-    rlc_reduce<Fq>(red1, red1 + 64, P, lane, ts->P, ts->PW);
-  }
+  rlc_reduce<Fq2>(red2[0], red2[1], S, lane, ts->S, ts->SW);
+  rlc_reduce<Fq>(red1, red1 + 64, P, lane, ts->P, ts->PW);
 }
 
 // Projective line table of one G2 sum: affine (one Fq2 inversion) then the 68 steps.
@@ -168,23 +154,13 @@ __global__ void __launch_bounds__(64) k_plines(int mode, uint32_t max_groups, ui
 
 static inline uint32_t sig_blocks(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
 
-#ifndef HBTC_SIG_ITEMS_W2_MIN
-#define HBTC_SIG_ITEMS_W2_MIN 1024u  // tiles above which the two-wave form runs
-#endif
-
-bool sig_items_big(uint32_t n_tiles) { return n_tiles > HBTC_SIG_ITEMS_W2_MIN; }
-
 hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* sigs, const G1A* pk, const int32_t* pk_status,
                             const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,
                             SigTileSums* sums, G2A* dec, int32_t* status) {
   if (n_tiles == 0) return hipSuccess;
-  if (sig_items_big(n_tiles))  // more tiles than SIMDs: throughput form
-    hipLaunchKernelGGL((k_sig_items<2, HBTC_XADIC16_G2 != 0>), dim3(n_tiles), dim3(64), 0, s, tiles, idx,
-                       sigs, pk, pk_status, pk_tab, n_pk, key, sus, sums, dec, status);
-  else
-    hipLaunchKernelGGL((k_sig_items<1, false>), dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk,
-                       pk_status, pk_tab, n_pk, key, sus, sums, dec, status);
+  hipLaunchKernelGGL(k_sig_items, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk, pk_status,
+                     pk_tab, n_pk, key, sus, sums, dec, status);
   return hipGetLastError();
 }
 

@@ -24,7 +24,7 @@ for o in build/*.o; do
     if [[ $stem == *.p* ]]; then part="-DHBTC_PART=${stem##*.p}"; fi
     if [[ $stem == hbtc_check.c* ]]; then src=hbtc_check; part="-DHBTC_CHECK_PART=${stem##*.c} -DHBTC_GT_INLINE ${CHKFQ:--DHBTC_FQMUL_SR}"; fi
     base=""
-    case $stem in hbtc_rlc.p6|hbtc_msm.p8) base="-DHBTC_INLINE_ALL ${FQMUL:--DHBTC_FQMUL_INLINE}";; hbtc_sig|hbtc_pb|hbtc_comb) base="-DHBTC_INLINE_ALL ${G2FQ:--DHBTC_FQMUL_SR}";; esac
+    case $stem in hbtc_rlc.p6|hbtc_msm.p8) base="-DHBTC_INLINE_ALL ${FQMUL:--DHBTC_FQMUL_INLINE}";; hbtc_sig|hbtc_pb|hbtc_comb) base="-DHBTC_INLINE_ALL ${G2FQ:--DHBTC_FQMUL_SR}";; hbtc_kernels.p*|hbtc_hash|hbtc_msm.p9) base="-DHBTC_INLINE_ALL -DHBTC_FQMUL_SR";; esac
     $HIPCC $FLAGS $part $base ${extra[$stem]} -c "hbbft_amd/csrc/$src.hip" -o "$out/$stem.o" &
     objs+=("$out/$stem.o")
   else
