@@ -372,27 +372,41 @@ def max_over_ranks(elapsed, dist, device=None):
     return float(tt.item())
 
 
+PROFILE_ROUND = "r05"
+
+
 def profile_dir(args, world):
     """The committed rocprofv3 summaries of this bench command's workload (kernel trace + PMC
-    passes, tools/r04/profile.sh): profiles/r04/bench_<cts>ct_<bits>b[_<world>r], or None."""
+    passes, tools/profile.sh): profiles/<round>/bench_<cts>ct_<bits>b[_<world>r], or None."""
     tag = "bench_%dct_%db" % (args.cts, args.rlc_bits) + ("_%dr" % world if world > 1 else "")
     if args.corrupt_mode != "uniform" or args.mode != "rlc" or args.n != 1000:
         return None
-    d = os.path.join("profiles", "r04", tag)
+    d = os.path.join("profiles", PROFILE_ROUND, tag)
     return d if os.path.exists(os.path.join(ROOT, d, "kt_kernel_stats.csv")) else None
 
 
-def rocprof_avg_ms(csv_path, kernel):
-    """Average duration (ms) of `kernel` in a committed rocprofv3 --stats kernel table."""
+def rocprof_avg_ms(prof_dir, kernel):
+    """Average duration (ms) of `kernel`'s FULL-SIZE launches in the committed kernel trace
+    (kt_launches.csv: the largest grid only -- a cold key set's probe pass is a smaller launch of
+    the same kernel), with the launch count; else the --stats table's average over all launches."""
     import csv
-    if not os.path.exists(csv_path):
-        return None
-    with open(csv_path, newline="") as fh:
+    p = os.path.join(ROOT, prof_dir, "kt_launches.csv")
+    if os.path.exists(p):
+        with open(p, newline="") as fh:
+            rows = [r for r in csv.DictReader(fh) if r["kernel"].endswith("hbtc::" + kernel)]
+        if rows:
+            g = max(int(r["grid_x"]) for r in rows)
+            d = [int(r["duration_ns"]) for r in rows if int(r["grid_x"]) == g]
+            return round(sum(d) / len(d) / 1e6, 3), len(d), "kt_launches.csv (full-size launches, grid %d)" % g
+    p = os.path.join(ROOT, prof_dir, "kt_kernel_stats.csv")
+    if not os.path.exists(p):
+        return None, 0, None
+    with open(p, newline="") as fh:
         for row in csv.DictReader(fh):
             name = row["Name"].split("(")[0]
             if name.endswith("hbtc::" + kernel):
-                return round(float(row["AverageNs"]) / 1e6, 3)
-    return None
+                return round(float(row["AverageNs"]) / 1e6, 3), int(row["Calls"]), "kt_kernel_stats.csv (all launches)"
+    return None, 0, None
 
 
 N_OUT = 6  # output sets rotated per step (Epoch.step): four epochs in flight + two gathers
@@ -653,11 +667,11 @@ def main():
     dom = max((f for f in main_stream if breakdown[f][1]), key=lambda f: breakdown[f][0])
     dom_avg_s = breakdown[dom][0] / breakdown[dom][1] / 1e3
     achieved = fqm_per_launch[dom] / dom_avg_s * consts["mad_u64_u32_per_fqm"] / 1e12
-    # rocprofv3 kernel trace + PMC passes of THIS workload (tools/r04/profile.sh -> tools/
+    # rocprofv3 kernel trace + PMC passes of THIS workload (tools/profile.sh -> tools/
     # pmc_summary.py), committed under profiles/: separate FETCH_SIZE / WRITE_SIZE / SQ passes,
     # FETCH_SIZE doubled per the gfx950 note.  A workload without a committed profile reports
     # null rather than another workload's figures.
-    traffic, pmc, rocprof_ms = None, {}, None
+    traffic, pmc, rocprof_ms, rocprof_n, rocprof_src = None, {}, None, 0, None
     prof_dir = profile_dir(args, world)
     if prof_dir:
         summ_path = os.path.join(ROOT, prof_dir, "pmc_summary.json")
@@ -666,7 +680,7 @@ def main():
             pmc = summ.get("hbtc::" + kname[dom]) or summ.get("void hbtc::" + kname[dom], {})
             if "hbm_read_bytes" in pmc and "hbm_write_bytes" in pmc:
                 traffic = pmc["hbm_read_bytes"] + pmc["hbm_write_bytes"]
-        rocprof_ms = rocprof_avg_ms(os.path.join(ROOT, prof_dir, "kt_kernel_stats.csv"), kname[dom])
+        rocprof_ms, rocprof_n, rocprof_src = rocprof_avg_ms(prof_dir, kname[dom])
     if strong:
         coll = ("RCCL (nccl backend) all-gather over xGMI" if args.backend == "nccl"
                 else "gloo all-gather of host copies (rehearsal, not the product merge)")
@@ -726,6 +740,8 @@ def main():
             "kernel_ms_per_launch_source": "HIP events on the kernel's stream, this run (the span can "
                                            "include time the kernel shares the CUs with other lanes)",
             "rocprof_avg_ms_per_launch": rocprof_ms,
+            "rocprof_launches_averaged": rocprof_n,
+            "rocprof_source": rocprof_src,
             "frac_at_rocprof_duration": (round(fqm_per_launch[dom] * consts["mad_u64_u32_per_fqm"]
                                                / (rocprof_ms * 1e-3) / MAD_U64_PEAK, 4) if rocprof_ms else None),
             "profile_dir": prof_dir,

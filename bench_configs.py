@@ -338,11 +338,7 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode=
     items0 = (run.slots[0]["hi"] - run.slots[0]["lo"]) if node is not None else total
     bits = tctx.rlc_bits()
     key = "sig_rlc_item" if bits == 64 or "sig_rlc_item_128" not in consts else "sig_rlc_item_128"
-    # the launch's form (hbtc_sig.hip sig_items_big: > 1024 tiles): the throughput form builds
-    # r_i sigma_i from the 15-entry table, the small-call form by the two-addition loop
-    tiles0 = (items0 // n) * ((n + 63) // 64)
-    if tiles0 <= 1024 and key + "_loop" in consts:
-        key += "_loop"
+    # (one form since round 5: r_i sigma_i by the two-addition x-adic loop at one wave per SIMD)
     roof = roofline_line(tctx, "sig_items", "k_sig_items", consts[key] * items0,
                          "%s Fqm (G2 decode + subgroup test, [a]s + [b](-psi^2 s), r pk from "
                          "the fixed-base table, tile-tree share) x %d SignatureShares per launch" % (key, items0))

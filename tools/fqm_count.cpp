@@ -113,8 +113,9 @@ int main() {
   jac_add(acc2, qj, m2);
   const unsigned long long comb2 = hbtc_fqm_count;
 
-  // RLC item (k_rlc_items): decode (the subgroup test yields [|x|] d), r*d by xadic_mul_tab16
-  // (the 15-entry common-Z table, one mixed addition per digit bit) over nbits = 16 (64-bit RLC)
+  // RLC item (k_rlc_items): decode (the subgroup test yields [|x|] d), r*d by xadic_mul_sac8
+  // (the sign-aligned 8-entry common-Z table, one mixed addition per digit bit, plus the even-d0
+  // correction, computed by every lane) over nbits = 16 (64-bit RLC)
   // or 32 (128-bit) digit bits, r*pk from the fixed-base table (4 nbits / 8 mixed additions, half
   // of them with phi), and the item's share of the plain + position-weighted reduction tree of
   // its tile: per side 3 * 63 Jacobian additions and 57 doublings, two sides, over 64 items
@@ -142,7 +143,9 @@ int main() {
     Fq beta;
     fq_set(beta, G1_BETA);
     const uint32_t m = nb == 32 ? 0xffffffffu : 0xffffu;
-#if HBTC_XADIC16
+#if HBTC_XADIC8
+    xadic_mul_sac8(rd, d2, t1, beta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
+#elif HBTC_XADIC16
     xadic_mul_tab16(rd, d2, t1, beta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
 #else
     G1A xp, pxp;
@@ -164,7 +167,7 @@ int main() {
   // from the fixed-base table, and the item's share of the G2 and G1 plain + weighted tile trees
   // both forms: the throughput kernel's 15-entry table (t16) and the small-call two-addition loop
   unsigned long long sig_item[2][2] = {};  // [t16][nb == 32]
-  for (int t16 : {1, 0})
+  for (int t16 : {0})
   for (int nb : {16, 32}) {
     hbtc_fqm_count = 0;
     G2A s2;
@@ -271,9 +274,9 @@ int main() {
          sig_decode, mlfv, fe, sig_decode + mlfv + fe);
   printf("  \"g1_combine_item\": %llu,\n  \"g2_combine_item\": %llu,\n", comb1, comb2);
   printf("  \"g1_msm_combine\": %llu,\n", msm_combine);
+  // k_sig_items runs the two-addition loop only since round 5 (the G2 table is gone)
   printf("  \"rlc_item\": %llu,\n  \"rlc_item_128\": %llu,\n  \"sig_rlc_item\": %llu,\n"
-         "  \"sig_rlc_item_128\": %llu,\n  \"sig_rlc_item_loop\": %llu,\n"
-         "  \"sig_rlc_item_128_loop\": %llu,\n  \"rlc_group_check\": %llu\n}\n", rlc_item,
-         rlc_item_128, sig_item[1][0], sig_item[1][1], sig_item[0][0], sig_item[0][1], rlc_group);
+         "  \"sig_rlc_item_128\": %llu,\n  \"rlc_group_check\": %llu\n}\n", rlc_item,
+         rlc_item_128, sig_item[0][0], sig_item[0][1], rlc_group);
   return 0;
 }
