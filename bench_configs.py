@@ -334,6 +334,7 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode=
     run.sync()
     elapsed = time.perf_counter() - t1
     per = breakdown(tctx, steps, COIN_FAMS)
+    leaves = tctx.rlc_last_leaves() if ctx_mode[0] == N.MODE_RLC else None
     consts = json.load(open(os.path.join(ROOT, "bench", "roofline_constants.json")))
     items0 = (run.slots[0]["hi"] - run.slots[0]["lo"]) if node is not None else total
     bits = tctx.rlc_bits()
@@ -385,6 +386,7 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode=
                    "parallelism": par_s},
         "combines_per_s": round(n_inst * steps / elapsed, 2),
         "kernel_event_spans_ms_per_step": per, "mismatches": mism, "combine_ok": comb_ok,
+        "exact_single_share_checks_last_call": leaves,
     }
     res["roofline"] = roof
     if lat:

@@ -54,6 +54,8 @@ struct Keyset {
   G1A* master = nullptr;         // hbtc_keyset_set_master: the decoded master public key
 };
 
+constexpr uint32_t FACT_N = 65535;  // factorial tables of the Lagrange coefficients (node indices < FACT_N)
+
 struct Span {
   std::string family;
   hipEvent_t a, b;
@@ -116,6 +118,10 @@ struct hbtc_ctx {
   bool comb_small = true;
   // hbtc_coin_decide's speculative combines (HBTC_COIN_SPEC=0: combine after the checks only)
   bool coin_spec = true;
+  // factorial tables of the Lagrange coefficients (k_lagrange_fact): 0..FACT_N, built at the first
+  // Pippenger combine (HBTC_LAGRANGE_FACT=0: the O(t) per term kernels)
+  bool lagrange_fact = true;
+  Fr *fact = nullptr, *inv_fact = nullptr;
   std::string ws_suffix;
   hipStream_t stream = nullptr;  // main: items, checks, leaves
   hipStream_t s_prep = nullptr;  // per-instance G2 preparation, overlapped with the item pass
@@ -1019,16 +1025,20 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
                                 h_aff, h_lines, d_status, leaf_count, leaves);
     }));
   }
-  // leaves in chunks: launches past the device-side count exit at once
-  for (uint32_t base = 0; base < n_items; base += LEAF_CHUNK) {
-    const uint32_t chunk = std::min(LEAF_CHUNK, n_items - base);
+  // leaves in chunks: launches past the device-side count exit at once.  A chunk as large as the
+  // table buffer already is (16 tables per tile for the sub-tile level), so a large call issues a
+  // few launch pairs rather than n_items / LEAF_CHUNK (C4: 4 instead of 20 -- the empty ones wait
+  // for free CU slots behind the other lanes' item passes)
+  const uint32_t leaf_chunk = (uint32_t)n_tables;
+  for (uint32_t base = 0; base < n_items; base += leaf_chunk) {
+    const uint32_t chunk = std::min(leaf_chunk, n_items - base);
     HB_TRY(timed(c, "sig_lines", [&] {
       return launch_plines(c->stream, 2, chunk, base, leaf_count, leaves, tiles, sums, dec, tables,
                            inf);
     }));
     HB_TRY(timed(c, "chk_leaves", [&] {
       // a short list (<= 2 leaves per SIMD, all in the first chunk) in the latency form
-      const uint32_t lim = (rep3 && base == 0) ? std::min(LEAF_CHUNK, 8u * (uint32_t)c->n_cu) : 0u;
+      const uint32_t lim = (rep3 && base == 0) ? std::min(chunk, 8u * (uint32_t)c->n_cu) : 0u;
       const hipError_t e = launch_sigchk_leaves_rep3(c->stream, chunk, lim, leaf_count, leaves, d_idx,
                                                      ks->pk, tables, inf, h_aff, h_lines, d_status);
       if (e != hipSuccess) return e;
@@ -1190,11 +1200,27 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
   HB_TRY(wst(c, "comb.lambda", terms, &d_lambda));
   HB_CHECK(c, launch_zero_u32(sc, d_dup, n_inst));
   HB_CHECK(c, launch_zero_u32(sc, d_bad, n_inst));
+  LagrangeFact lf{};
+  if (c->lagrange_fact) {
+    if (!c->fact) {  // once per context: 0! .. FACT_N! and their inverses (then every stream may read them)
+      Fr* part;
+      HB_CHECK(c, hipMalloc(&c->fact, sizeof(Fr) * (FACT_N + 1)));
+      HB_CHECK(c, hipMalloc(&c->inv_fact, sizeof(Fr) * (FACT_N + 1)));
+      HB_CHECK(c, hipMalloc(&part, sizeof(Fr) * (FACT_N / 256 + 1)));
+      HB_CHECK(c, launch_fact_tables(sc, FACT_N, part, c->fact, c->inv_fact));
+      HB_CHECK(c, hipStreamSynchronize(sc));
+      HB_CHECK(c, hipFree(part));
+    }
+    uint32_t* d_done;
+    HB_TRY(wst(c, "comb.fact_done", n_inst, &d_done));
+    lf = LagrangeFact{c->fact, c->inv_fact, FACT_N, d_sel_cnt, d_done};
+  }
   HB_TRY(timed_on(c, sc, "lagrange", [&] {
     hipError_t e = launch_select(sc, n_inst, d_off, t, d_item_status, d_idx, d_sel_pos, d_sel_idx,
                                  d_sel_cnt);
     if (e != hipSuccess) return e;
-    return launch_lagrange_sel(sc, n_inst, t, d_sel_idx, d_lambda, d_lws, d_dup);
+    return launch_lagrange_sel(sc, n_inst, t, d_sel_idx, d_lambda, d_lws, d_dup,
+                               c->lagrange_fact ? &lf : nullptr);
   }));
   const MsmPlan plan = msm_plan(n_inst, t);
   const size_t pb = group == 1 ? 48 : 96;
@@ -1435,6 +1461,8 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (const char* e = getenv("HBTC_G1_GLV")) c->g1_glv = atoi(e) != 0;
   if (const char* e = getenv("HBTC_COMB_SMALL")) c->comb_small = atoi(e) != 0;
   if (const char* e = getenv("HBTC_COIN_SPEC")) c->coin_spec = atoi(e) != 0;
+  if (const char* e = getenv("HBTC_TRACK")) c->track_senders = atoi(e) != 0;
+  if (const char* e = getenv("HBTC_LAGRANGE_FACT")) c->lagrange_fact = atoi(e) != 0;
   if (const char* e = getenv("HBTC_PROBE")) c->probe_cold = atoi(e) != 0;
   if (const char* e = getenv("HBTC_SPLIT")) c->split_levels = atoi(e) != 0;
   if (const char* e = getenv("HBTC_GT_REP")) c->small_rep = atoi(e) == 1 ? 1 : 3;
@@ -1507,6 +1535,8 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
     if (kv.second.p) (void)hipFree(kv.second.p);
   (void)retire_fence(c);
   (void)reap_retired(c, true);
+  if (c->fact) (void)hipFree(c->fact);
+  if (c->inv_fact) (void)hipFree(c->inv_fact);
   for (auto& kv : c->keysets) {
     (void)hipFree(kv.second.pk);
     (void)hipFree(kv.second.st);

@@ -243,9 +243,20 @@ struct MsmPlan {
 hipError_t launch_select(hipStream_t s, uint32_t n_inst, const uint32_t* offsets, uint32_t t,
                          const int32_t* status, const uint32_t* idx, uint32_t* sel_pos,
                          uint32_t* sel_idx, uint32_t* sel_cnt);
-// lambda: n_inst * t canonical coefficients; ws: n_inst * t Fr of workspace
+// Lagrange through factorial tables (hbtc_msm.hip k_lagrange_fact): fact / inv_fact of 0..n
+// (Montgomery), the selection counts, and a per-instance flag the fallback kernels skip
+struct LagrangeFact {
+  const Fr* fact;
+  const Fr* inv_fact;
+  uint32_t n;
+  const uint32_t* sel_cnt;
+  uint32_t* done;
+};
+hipError_t launch_fact_tables(hipStream_t s, uint32_t n, Fr* part, Fr* fact, Fr* inv_fact);
+// lambda: n_inst * t canonical coefficients; ws: n_inst * t Fr of workspace; lf: null = the O(t)
+// per term kernels for every instance
 hipError_t launch_lagrange_sel(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_idx,
-                               Fr* lambda, Fr* ws, uint32_t* dup);
+                               Fr* lambda, Fr* ws, uint32_t* dup, const LagrangeFact* lf = nullptr);
 hipError_t launch_msm_digits(hipStream_t s, const MsmPlan& p, const uint32_t* scalars,
                              int16_t* digits, uint32_t* list, uint32_t* roff);
 hipError_t launch_msm_gather_g1(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_pos,

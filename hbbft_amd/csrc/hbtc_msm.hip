@@ -139,11 +139,13 @@ __global__ void __launch_bounds__(256) k_lagrange_x(uint64_t n, const uint32_t* 
 __global__ void __launch_bounds__(256) k_lagrange_den(uint32_t n_inst, uint32_t t,
                                                       const Fr* __restrict__ x,
                                                       Fr* __restrict__ q,
-                                                      uint32_t* __restrict__ dup) {
+                                                      uint32_t* __restrict__ dup,
+                                                      const uint32_t* __restrict__ done) {
   HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
   const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (g >= (uint64_t)n_inst * t) return;
   const uint32_t k = (uint32_t)(g / t), i = (uint32_t)(g % t);
+  if (done && done[k]) return;  // k_lagrange_fact has the coefficients
   const Fr* xk = x + (size_t)k * t;
   const Fr xi = xk[i];
   Fr den;
@@ -165,8 +167,10 @@ __global__ void __launch_bounds__(256) k_lagrange_den(uint32_t n_inst, uint32_t 
 
 constexpr uint32_t LG_BS = 256;
 __global__ void __launch_bounds__(LG_BS) k_lagrange_inv(uint32_t t, Fr* __restrict__ x,
-                                                        Fr* __restrict__ q_lambda) {
+                                                        Fr* __restrict__ q_lambda,
+                                                        const uint32_t* __restrict__ done) {
   HBTC_LATENCY_PRIO();  // a latency chain beside the item passes: win the issue arbitration
+  if (done && done[blockIdx.x]) return;  // block-uniform: k_lagrange_fact has the coefficients
   __shared__ Fr C[LG_BS];   // product of q over chunk u
   __shared__ Fr E[LG_BS];   // product of q over the chunks before u
   __shared__ Fr IE[LG_BS];  // (E[u] * C[u])^-1
@@ -236,6 +240,125 @@ __global__ void __launch_bounds__(LG_BS) k_lagrange_inv(uint32_t t, Fr* __restri
     fr_from_mont(lc, l);
     q[i] = lc;
   }
+}
+
+// ---------------------------------------------------- Lagrange through factorials (round 5)
+// The selected abscissae of a combine are the first t ACCEPTed shares in node order, so they are
+// strictly increasing and fill [1, M] but for the few rejected / missing nodes R = [1, M] \ S
+// (|R| = M - t).  Then
+//   prod_{j in S, j != i} x_j          = M! / (prod_R r * x_i)
+//   prod_{j in S, j != i} (x_j - x_i)  = (-1)^(x_i - 1) (x_i - 1)! (M - x_i)! / prod_R (r - x_i)
+// so lambda_i = (-1)^(x_i - 1) M! Q_i / (prod_R r) / x_i! / (M - x_i)!,  Q_i = prod_R (r - x_i):
+// |R| + 5 products per term and no inversion (1/r = (r - 1)! / r! from the tables), against
+// O(t) products per term and a batched inversion (k_lagrange_den / k_lagrange_inv).  Instances
+// whose x are not strictly increasing (a duplicate: DUPLICATE_ENTRY), with M past the tables or
+// with |R| > LG_FACT_RMAX are left to those kernels (done[k] = 0).
+__global__ void __launch_bounds__(256) k_fact_chunks(uint32_t n, Fr* __restrict__ part) {
+  // part[c] = prod_{i in chunk c} i, chunks of 256 of [1, n]
+  const uint32_t c = blockIdx.x * 256 + threadIdx.x;
+  if (c * 256u >= n + 1) return;
+  Fr acc, v;
+  limbs_set_const<8>(acc, FR_ONE);
+  for (uint32_t i = c * 256u; i < min(n + 1, c * 256u + 256u); ++i) {
+    if (i == 0) continue;
+    fr_from_u64(v, i);
+    fr_mul(acc, acc, v);
+  }
+  part[c] = acc;
+}
+__global__ void __launch_bounds__(256) k_fact_fill(uint32_t n, const Fr* __restrict__ part,
+                                                   Fr* __restrict__ fact, Fr* __restrict__ inv_fact) {
+  // fact[i] = i! (Montgomery), inv_fact[i] = 1 / i!
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i > n) return;
+  Fr acc, v;
+  limbs_set_const<8>(acc, FR_ONE);
+  for (uint32_t c = 0; c < i / 256u; ++c) fr_mul(acc, acc, part[c]);
+  for (uint32_t j = (i / 256u) * 256u; j <= i; ++j) {
+    if (j == 0) continue;
+    fr_from_u64(v, j);
+    fr_mul(acc, acc, v);
+  }
+  fact[i] = acc;
+  Fr inv;
+  fr_inv(inv, acc);
+  inv_fact[i] = inv;
+}
+
+constexpr uint32_t LG_FACT_RMAX = 256;
+constexpr uint32_t LG_FACT_TMAX = 4096;
+__global__ void __launch_bounds__(256) k_lagrange_fact(uint32_t t, const uint32_t* __restrict__ sel_idx,
+                                                       const uint32_t* __restrict__ sel_cnt,
+                                                       uint32_t n_fact, const Fr* __restrict__ fact,
+                                                       const Fr* __restrict__ inv_fact,
+                                                       Fr* __restrict__ lambda, uint32_t* __restrict__ done) {
+  HBTC_LATENCY_PRIO();
+  __shared__ uint32_t xs[LG_FACT_TMAX];
+  __shared__ uint32_t rs[LG_FACT_RMAX];
+  __shared__ uint32_t s_ok, s_nr;
+  __shared__ Fr s_c;  // M! / prod_R r
+  const uint32_t k = blockIdx.x, tid = threadIdx.x;
+  const uint32_t* sx = sel_idx + (size_t)k * t;
+  if (tid == 0) s_ok = sel_cnt[k] == t ? 1u : 0u;
+  __syncthreads();
+  if (!s_ok) {  // NOT_ENOUGH_SHARES: the coefficients are never used
+    if (tid == 0) done[k] = 1;
+    return;
+  }
+  for (uint32_t j = tid; j < t; j += 256) xs[j] = sx[j] + 1u;
+  __syncthreads();
+  for (uint32_t j = tid; j + 1 < t; j += 256)
+    if (xs[j + 1] <= xs[j] || xs[j] == 0) s_ok = 0;  // not strictly increasing (x = 0: idx wrap)
+  __syncthreads();
+  const uint32_t M = xs[t - 1];
+  if (tid == 0 && (xs[0] == 0 || M > n_fact || M - t > LG_FACT_RMAX)) s_ok = 0;
+  __syncthreads();
+  if (!s_ok) {
+    if (tid == 0) done[k] = 0;
+    return;
+  }
+  if (tid == 0) {  // R: the gaps of S in [1, M]
+    uint32_t nr = 0, prev = 0;
+    for (uint32_t j = 0; j < t; ++j) {
+      for (uint32_t r = prev + 1; r < xs[j]; ++r) rs[nr++] = r;
+      prev = xs[j];
+    }
+    s_nr = nr;
+    Fr c = fact[M], q;
+    for (uint32_t j = 0; j < nr; ++j) {  // 1 / r = (r - 1)! / r!
+      fr_mul(q, fact[rs[j] - 1], inv_fact[rs[j]]);
+      fr_mul(c, c, q);
+    }
+    s_c = c;
+  }
+  __syncthreads();
+  const uint32_t nr = s_nr;
+  const Fr c = s_c;
+  for (uint32_t i = tid; i < t; i += 256) {
+    const uint32_t x = xs[i];
+    Fr q, d, l, lc;
+    fr_mul(q, inv_fact[x], inv_fact[M - x]);
+    fr_mul(q, q, c);
+    for (uint32_t j = 0; j < nr; ++j) {
+      const uint32_t r = rs[j];
+      fr_from_u64(d, r > x ? r - x : x - r);
+      if (r < x) {
+        Fr z;
+        limbs_zero<8>(z);
+        fr_sub(d, z, d);
+      }
+      fr_mul(q, q, d);
+    }
+    if (!(x & 1u)) {  // (-1)^(x - 1)
+      Fr z;
+      limbs_zero<8>(z);
+      fr_sub(q, z, q);
+    }
+    l = q;
+    fr_from_mont(lc, l);
+    lambda[(size_t)k * t + i] = lc;
+  }
+  if (tid == 0) done[k] = 1;
 }
 
 // ------------------------------------------------------------------ digits and buckets
@@ -582,18 +705,33 @@ hipError_t launch_select(hipStream_t s, uint32_t n_inst, const uint32_t* offsets
   return hipGetLastError();
 }
 
-hipError_t launch_lagrange_sel(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_idx,
-                               Fr* lambda, Fr* ws, uint32_t* dup) {
-  const uint64_t n = (uint64_t)n_inst * t;
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_lagrange_x, dim3(msm_blocks(n, 256)), dim3(256), 0, s, n, sel_idx, ws);
+hipError_t launch_fact_tables(hipStream_t s, uint32_t n, Fr* part, Fr* fact, Fr* inv_fact) {
+  hipLaunchKernelGGL(k_fact_chunks, dim3(msm_blocks(n / 256 + 1, 256)), dim3(256), 0, s, n, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_fact_fill, dim3(msm_blocks((uint64_t)n + 1, 256)), dim3(256), 0, s, n, part, fact,
+                     inv_fact);
+  return hipGetLastError();
+}
+
+hipError_t launch_lagrange_sel(hipStream_t s, uint32_t n_inst, uint32_t t, const uint32_t* sel_idx,
+                               Fr* lambda, Fr* ws, uint32_t* dup, const LagrangeFact* lf) {
+  const uint64_t n = (uint64_t)n_inst * t;
+  if (n == 0) return hipSuccess;
+  hipError_t e;
+  const uint32_t* done = nullptr;
+  if (lf && lf->fact && t <= LG_FACT_TMAX) {
+    hipLaunchKernelGGL(k_lagrange_fact, dim3(n_inst), dim3(256), 0, s, t, sel_idx, lf->sel_cnt, lf->n,
+                       lf->fact, lf->inv_fact, lambda, lf->done);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    done = lf->done;
+  }
+  hipLaunchKernelGGL(k_lagrange_x, dim3(msm_blocks(n, 256)), dim3(256), 0, s, n, sel_idx, ws);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_lagrange_den, dim3(msm_blocks(n, 256)), dim3(256), 0, s, n_inst, t, ws, lambda,
-                     dup);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_lagrange_inv, dim3(n_inst), dim3(LG_BS), 0, s, t, ws, lambda);
+                     dup, done);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_lagrange_inv, dim3(n_inst), dim3(LG_BS), 0, s, t, ws, lambda, done);
   return hipGetLastError();
 }
 
