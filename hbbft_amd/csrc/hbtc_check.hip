@@ -507,13 +507,7 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_pair(
   // undecodable H / w: k_rlc_finalize decides the group's items
   const bool fail = r.active && r.inst_ok && !pass;
   const int32_t loc = locate(T, Tw, r.hi - r.lo, LEVEL == 0 ? 5 : 2, fail, ul);
-  if (LEVEL == 0 && !TO_LEAVES && split.list) {
-    // the split levels: an unlocated tile is listed with its values (side 0 lists)
-    const bool located = loc >= 0 && status[r.lo + loc] == HBTC_RLC_PENDING;
-    split_list(split, fail && !located && ul.side == 0, r.t << 3, T, Tw, 0u, ul.ps);
-    if (fail && located && ul.side == 0 && ul.ps.k == 0) status[r.lo + loc] = HBTC_REJECT;
-    return;
-  }
+  // (the split levels follow the plain-first tile level only: `split` is unused here)
   if (!fail || ul.side != 0 || ul.ps.k != 0) return;
   if (loc >= 0 && status[r.lo + loc] == HBTC_RLC_PENDING) {
     status[r.lo + loc] = HBTC_REJECT;
@@ -966,25 +960,19 @@ hipError_t launch_chk_split(hipStream_t s, int level, int rep, uint32_t max_node
                             const G2A* w_aff, const Line* w_lines, int32_t* status,
                             uint32_t* leaf_count, uint32_t* leaves, SplitOut split) {
   if (max_nodes == 0) return hipSuccess;
-  const dim3 grid(rep == 3 ? max_nodes : unit_blocks(max_nodes));
+  // the split levels run on the plain-first schedule only, which keeps the throughput layout
+  // (rep 1): the latency-form instantiations were never launched and are gone (round 5)
+  if (rep != 1) return hipErrorInvalidValue;
+  const dim3 grid(unit_blocks(max_nodes));
 #define HBTC_SPLIT_ARGS                                                                       \
   grid, dim3(64), 0, s, n_in, in_list, in_T, in_U, in_ab, tiles, sums, h_aff, h_lines, w_aff, \
       w_lines, status, leaf_count, leaves, split
-  if (rep == 3) {
-    if (level == 1)
-      hipLaunchKernelGGL((k_chk_split<1, 3>), HBTC_SPLIT_ARGS);
-    else if (level == 2)
-      hipLaunchKernelGGL((k_chk_split<2, 3>), HBTC_SPLIT_ARGS);
-    else
-      hipLaunchKernelGGL((k_chk_split<3, 3>), HBTC_SPLIT_ARGS);
-  } else {
-    if (level == 1)
-      hipLaunchKernelGGL((k_chk_split<1, 1>), HBTC_SPLIT_ARGS);
-    else if (level == 2)
-      hipLaunchKernelGGL((k_chk_split<2, 1>), HBTC_SPLIT_ARGS);
-    else
-      hipLaunchKernelGGL((k_chk_split<3, 1>), HBTC_SPLIT_ARGS);
-  }
+  if (level == 1)
+    hipLaunchKernelGGL((k_chk_split<1, 1>), HBTC_SPLIT_ARGS);
+  else if (level == 2)
+    hipLaunchKernelGGL((k_chk_split<2, 1>), HBTC_SPLIT_ARGS);
+  else
+    hipLaunchKernelGGL((k_chk_split<3, 1>), HBTC_SPLIT_ARGS);
 #undef HBTC_SPLIT_ARGS
   return hipGetLastError();
 }
