@@ -19,6 +19,37 @@
 
 namespace hbtc {
 
+#ifndef HBTC_SIG_SPLIT
+#define HBTC_SIG_SPLIT 1
+#endif
+#if HBTC_SIG_SPLIT
+// The decode half of the SignatureShare item pass, a kernel of its own so it runs at two waves per
+// SIMD (772 B/lane of scratch; in one kernel with the scalar half the G2 state needs one wave per
+// SIMD): zcash G2 decode with the psi subgroup test into dec, DECODE_ERR into status (every other
+// item: RLC_PENDING, decided by k_sig_items).
+__global__ void __launch_bounds__(64, 2) k_sig_decode(
+    const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ sigs,
+    const int32_t* __restrict__ pk_status, uint32_t n_pk, G2A* __restrict__ dec,
+    int32_t* __restrict__ status) {
+  const Tile tile = tiles[blockIdx.x];
+  const uint32_t lane = threadIdx.x;
+  if (lane >= tile.count) return;
+  const size_t item = (size_t)tile.first + lane;
+  const uint32_t id = idx[item];
+  int32_t st = HBTC_RLC_PENDING;
+  if (id < n_pk && pk_status[id] == HBTC_ACCEPT) {
+    uint32_t w[24];
+    rlc_load_words(w, sigs, item, 24);
+    G2A sg;
+    if (g2_decompress(sg, w))
+      dec[item] = sg;  // for the scalar half, the exact leaf checks and the combine
+    else
+      st = HBTC_DECODE_ERR;
+  }
+  status[item] = st;
+}
+#endif
+
 // One wave per tile: decode every SignatureShare (zcash compressed G2 + subgroup check), r_i,
 // r_i sigma_i, r_i pk_i, then the plain and weighted tile / sub-tile sums in both groups.  One
 // wave per SIMD (256 VGPRs + 256 AGPRs: 736 B/lane of scratch).  Round 5 dropped the two-wave
@@ -49,13 +80,21 @@ __global__ void __launch_bounds__(64, 1) k_sig_items(
     } else if (pk_status[id] != HBTC_ACCEPT) {
       st = HBTC_DECODE_ERR;
     } else {
+      G2A sg;
+#if HBTC_SIG_SPLIT
+      const bool dec_ok = status[item] != HBTC_DECODE_ERR;  // k_sig_decode ran first
+      if (dec_ok) sg = dec[item];
+#else
       uint32_t w[24];
       rlc_load_words(w, sigs, item, 24);
-      G2A sg;
-      if (!g2_decompress(sg, w)) {
+      const bool dec_ok = g2_decompress(sg, w);
+#endif
+      if (!dec_ok) {
         st = HBTC_DECODE_ERR;
       } else {
+#if !HBTC_SIG_SPLIT
         dec[item] = sg;  // for the exact leaf checks and the combine (no second decode)
+#endif
         if (is_suspect(sus, id)) {
           st = HBTC_RLC_LEAF;  // straight to an exact check, outside the group sums
         } else {
@@ -159,6 +198,12 @@ hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, 
                             const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,
                             SigTileSums* sums, G2A* dec, int32_t* status) {
   if (n_tiles == 0) return hipSuccess;
+#if HBTC_SIG_SPLIT
+  hipLaunchKernelGGL(k_sig_decode, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk_status, n_pk, dec,
+                     status);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+#endif
   hipLaunchKernelGGL(k_sig_items, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk, pk_status,
                      pk_tab, n_pk, key, sus, sums, dec, status);
   return hipGetLastError();
