@@ -75,6 +75,9 @@ KERNEL_NAME_SCHED = {
     1: {"chk_tiles": "k_chk_pair<0, false>", "chk_subs": "k_chk_pair<1, true>"},
     2: {"chk_tiles": "k_chk_pair<0, true>"},
 }
+# families launched as more than one kernel (hbtc_rlc.hip HBTC_RLC_SPLIT: k_rlc_decode at three waves
+# per SIMD, then the scalar half k_rlc_items)
+KERNEL_PARTS = {"rlc_items": ("k_rlc_decode", "k_rlc_items")}
 SCHED_NAME = {0: "plain-first", 1: "paired: tiles -> sub-tiles -> leaves", 2: "paired: tiles -> leaves"}
 
 
@@ -675,12 +678,22 @@ def main():
     prof_dir = profile_dir(args, world)
     if prof_dir:
         summ_path = os.path.join(ROOT, prof_dir, "pmc_summary.json")
+        # a family launched as two kernels (the item pass: decode, then the scalar half) is priced
+        # by the sum of its kernels' launches, like the HIP-event span that covers both
+        parts = KERNEL_PARTS.get(dom, (kname[dom],))
         if os.path.exists(summ_path):
             summ = json.load(open(summ_path))
-            pmc = summ.get("hbtc::" + kname[dom]) or summ.get("void hbtc::" + kname[dom], {})
-            if "hbm_read_bytes" in pmc and "hbm_write_bytes" in pmc:
-                traffic = pmc["hbm_read_bytes"] + pmc["hbm_write_bytes"]
-        rocprof_ms, rocprof_n, rocprof_src = rocprof_avg_ms(prof_dir, kname[dom])
+            found = [summ.get("hbtc::" + k) or summ.get("void hbtc::" + k) for k in parts]
+            found = [f for f in found if f]
+            pmc = found[-1] if found else {}
+            if found and all("hbm_read_bytes" in f and "hbm_write_bytes" in f for f in found):
+                traffic = sum(f["hbm_read_bytes"] + f["hbm_write_bytes"] for f in found)
+        avgs = [rocprof_avg_ms(prof_dir, k) for k in parts]
+        avgs = [a for a in avgs if a[0] is not None]
+        if avgs:
+            rocprof_ms = round(sum(a[0] for a in avgs), 3)
+            rocprof_n = min(a[1] for a in avgs)
+            rocprof_src = "; ".join("%s: %s" % (k, a[2]) for k, a in zip(parts, avgs))
     if strong:
         coll = ("RCCL (nccl backend) all-gather over xGMI" if args.backend == "nccl"
                 else "gloo all-gather of host copies (rehearsal, not the product merge)")
@@ -728,7 +741,7 @@ def main():
                                     "durations are roofline.rocprof_avg_ms_per_launch (rocprofv3)"),
         "roofline": {
             "bound": "valu-int (v_mad_u64_u32)",
-            "kernel": kname[dom],
+            "kernel": " + ".join(KERNEL_PARTS.get(dom, (kname[dom],))),
             "achieved": round(achieved, 3),
             "peak": MAD_U64_PEAK / 1e12,
             "unit": "T mad_u64_u32/s",

@@ -847,9 +847,11 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
   const Suspects sus =
       exact ? Suspects{nullptr, 0, leaf_count, leaves, 1} : suspects_of(c, ks, leaf_count, leaves);
   HB_TRY(items_gate(c, n_tiles));
+  G1J* t1s = nullptr;
+  if (rlc_items_split()) HB_TRY(wst(c, "rlc.t1", n_items, &t1s));
   HB_TRY(timed(c, "rlc_items", [&] {
     return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->tab,
-                            ks->n, key, sus, sums, dec, d_status);
+                            ks->n, key, sus, sums, dec, d_status, t1s);
   }));
   HB_TRY(items_mark(c));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));

@@ -63,12 +63,51 @@ namespace hbtc {
 // 13.4 M, profiles/r05/run1/)
 #define HBTC_ITEMS_WAVES 2
 #endif
+// The item pass as two kernels: the decode half at three waves per SIMD (332 B/lane), the scalar
+// half at two (its x-adic table) -- C3 13.6 -> 14.1 M shares/s against the single two-wave kernel
+// (profiles/r05/run12/)
+#ifndef HBTC_RLC_SPLIT
+#define HBTC_RLC_SPLIT 1
+#endif
+#ifndef HBTC_RLC_DEC_WAVES
+#define HBTC_RLC_DEC_WAVES 3
+#endif
+#if HBTC_RLC_SPLIT
+// The decode half (HBTC_RLC_SPLIT): zcash G1 decode with the endomorphism subgroup test, whose
+// first half [|x|] d is kept (t1) for the x-adic table; DECODE_ERR into status, everything else
+// RLC_PENDING for k_rlc_items.
+__global__ void __launch_bounds__(64, HBTC_RLC_DEC_WAVES) k_rlc_decode(
+    const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ shares,
+    const int32_t* __restrict__ pk_status, uint32_t n_pk, G1A* __restrict__ dec, G1J* __restrict__ t1s,
+    int32_t* __restrict__ status) {
+  const Tile tile = tiles[blockIdx.x];
+  const uint32_t lane = threadIdx.x;
+  if (lane >= tile.count) return;
+  const size_t item = (size_t)tile.first + lane;
+  const uint32_t id = idx[item];
+  int32_t st = HBTC_RLC_PENDING;
+  if (id < n_pk && pk_status[id] == HBTC_ACCEPT) {
+    uint32_t w[12];
+    rlc_load_words(w, shares, item, 12);
+    G1A d;
+    G1J t1;
+    if (g1_decompress_t1(d, t1, w)) {
+      dec[item] = d;
+      t1s[item] = t1;
+    } else {
+      st = HBTC_DECODE_ERR;
+    }
+  }
+  status[item] = st;
+}
+#endif
+
 __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
     const uint8_t* __restrict__ shares, const G1A* __restrict__ pk,
     const int32_t* __restrict__ pk_status, const PtXY* __restrict__ pk_tab, uint32_t n_pk,
     RlcKey key, Suspects sus, TileSums* __restrict__ sums, G1A* __restrict__ dec,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ status, const G1J* __restrict__ t1s) {
 #if HBTC_ITEMS_PRIO > 0
   __builtin_amdgcn_s_setprio(HBTC_ITEMS_PRIO);
 #endif
@@ -93,14 +132,25 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
     } else if (pk_status[id] != HBTC_ACCEPT) {
       st = HBTC_DECODE_ERR;
     } else {
-      uint32_t w[12];
-      rlc_load_words(w, shares, item, 12);
       G1A d;
       G1J t1;  // [|x|] d from the subgroup test: [x] d = -t1, the x-adic table's second entry
-      if (!g1_decompress_t1(d, t1, w)) {
+#if HBTC_RLC_SPLIT
+      const bool dec_ok = status[item] != HBTC_DECODE_ERR;  // k_rlc_decode ran first
+      if (dec_ok) {
+        d = dec[item];
+        t1 = t1s[item];
+      }
+#else
+      uint32_t w[12];
+      rlc_load_words(w, shares, item, 12);
+      const bool dec_ok = g1_decompress_t1(d, t1, w);
+#endif
+      if (!dec_ok) {
         st = HBTC_DECODE_ERR;
       } else {
+#if !HBTC_RLC_SPLIT
         dec[item] = d;  // for the exact leaf checks and the combine (no second decode)
+#endif
         if (is_suspect(sus, id)) {
           st = HBTC_RLC_LEAF;  // straight to an exact check, outside the group sums
         } else {
@@ -191,13 +241,20 @@ __global__ void __launch_bounds__(256) k_track_update(uint32_t n_pk, uint32_t* _
 static inline uint32_t rlc_blocks(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
 
 #if HBTC_IN_PART(6)
+bool rlc_items_split() { return HBTC_RLC_SPLIT != 0; }
 hipError_t launch_rlc_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* shares, const G1A* pk, const int32_t* pk_status,
                             const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,
-                            TileSums* sums, G1A* dec, int32_t* status) {
+                            TileSums* sums, G1A* dec, int32_t* status, G1J* t1s) {
   if (n_tiles == 0) return hipSuccess;
+#if HBTC_RLC_SPLIT
+  hipLaunchKernelGGL(k_rlc_decode, dim3(n_tiles), dim3(64), 0, s, tiles, idx, shares, pk_status, n_pk,
+                     dec, t1s, status);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+#endif
   hipLaunchKernelGGL(k_rlc_items, dim3(n_tiles), dim3(64), 0, s, tiles, idx, shares, pk, pk_status,
-                     pk_tab, n_pk, key, sus, sums, dec, status);
+                     pk_tab, n_pk, key, sus, sums, dec, status, t1s);
   return hipGetLastError();
 }
 hipError_t launch_rlc_finalize(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
