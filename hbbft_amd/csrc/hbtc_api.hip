@@ -97,6 +97,9 @@ struct hbtc_ctx {
   // runs on the same stream, after it).  Measured (C3 / 125-ciphertext slice / C2, ms per epoch):
   // 2 lanes + a combine stream 107 / 24.4 / 45.3, 3 lanes 100.3 / 22.5 / 36.0, 4 lanes
   // 97.5 / 20.7 / 35.8, 4 lanes with the preparation on the lane stream 98.0 / 22.2 / 38.9.
+  // Round 5 (C3 / 125 / 250-ciphertext slices): 4 lanes 71.5 / 14.1 / 24.3, 6 lanes
+  // 71.0 / 12.7 / 23.1, 8 lanes 71.2 / 13.3 / 23.0 (profiles/r05/run15/) -- the slices gain only
+  // from more epochs in flight than hbbft ever has (current + max_future_epochs = 3), so 4.
 #ifndef HBTC_LANES
 #define HBTC_LANES 4
 #endif
