@@ -789,28 +789,132 @@ HD void xy_sel(XY<F>& r, bool c, const XY<F>& a, const XY<F>& b) {  // r = c ? a
   fsel(r.y, c, a.y, b.y);
 }
 
+// The same eight entries for xadic_mul_sac8<LDS3>, built as a co-Z chain at a running Z instead
+// of six separate co-Z sums brought to one Z by prefix / suffix products: each sum U + m(V)
+// updates U to the new Z (coz_add), and every other live entry is rescaled by (h^2, h^3) at once,
+// so no arrays of H_k and prefix products are live beside the table (k_rlc_items: the build's
+// spills were most of its scratch).  tab[0..4] stay in registers; tab[5..7] are written to LDS
+// ([entry][word][lane], as xadic_mul_sac8 reads them) when formed and rescaled there.  ~16 more
+// Fq products than xadic_table8 (22 rescaled entries), the same additions (the same exceptional-
+// case argument).
+template <class F>
+HD void xy_rescale(XY<F>& p, const F& h2, const F& h3) {
+  fmul(p.x, p.x, h2);
+  fmul(p.y, p.y, h3);
+}
+template <class F>
+HD void xy_lds_put(uint32_t* lds, uint32_t lane, int e, const XY<F>& v) {
+  constexpr int NWD = (int)(sizeof(XY<F>) / 4);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&v);
+#pragma unroll
+  for (int w = 0; w < NWD; ++w) lds[(e * NWD + w) * 64 + lane] = src[w];
+}
+template <class F>
+HD void xy_lds_get(XY<F>& v, const uint32_t* lds, uint32_t lane, int e) {
+  constexpr int NWD = (int)(sizeof(XY<F>) / 4);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+  for (int w = 0; w < NWD; ++w) dst[w] = lds[(e * NWD + w) * 64 + lane];
+}
+template <class F>
+HD void xy_lds_rescale(uint32_t* lds, uint32_t lane, int e, const F& h2, const F& h3) {
+  XY<F> v;
+  xy_lds_get(v, lds, lane, e);
+  xy_rescale(v, h2, h3);
+  xy_lds_put(lds, lane, e, v);
+}
+template <class F>
+HD void xadic_table8_chain(XY<F> tab[5], F& zs, const Aff<F>& p, const Jac<F>& xpj, const Fq& c,
+                           uint32_t* lds, uint32_t lane) {
+  XY<F>& P = tab[0];
+  XY<F>& S = tab[1];
+  XY<F> X;
+  F h, h2, h3;
+  {  // P at XP's Z; S = XP + P (co-Z), XP updated; P rescaled: all three at Z0
+    F z2, z3;
+    fsqr(z2, xpj.z);
+    fmul(z3, z2, xpj.z);
+    fmul(P.x, p.x, z2);
+    fmul(P.y, p.y, z3);
+    X.x = xpj.x;
+    X.y = xpj.y;
+    coz_add(S, X.x, X.y, h, P);
+    fsqr(h2, h);
+    fmul(h3, h2, h);
+    xy_rescale(P, h2, h3);
+    fmul(zs, xpj.z, h);
+  }
+  // out = U + m(V), U updated to the new Z; h2, h3 for the other entries
+  auto sum = [&](XY<F>& out, XY<F>& U, const XY<F>& V) {
+    XY<F> mv;
+    fmul_by_fq(mv.x, V.x, c);
+    mv.y = V.y;
+    coz_add(out, U.x, U.y, h, mv);
+    fsqr(h2, h);
+    fmul(h3, h2, h);
+    fmul(zs, zs, h);
+  };
+  // the two sums over m(XP) first, so XP is dropped after two steps: 22 rescaled entries
+  sum(tab[4], P, X);  // P + m(XP)
+  xy_rescale(X, h2, h3);
+  xy_rescale(S, h2, h3);
+  {
+    XY<F> t5;
+    sum(t5, S, X);  // S + m(XP); XP is not needed past here
+    xy_lds_put(lds, lane, 0, t5);
+  }
+  xy_rescale(P, h2, h3);
+  xy_rescale(tab[4], h2, h3);
+  sum(tab[2], P, P);  // P + m(P)
+  xy_rescale(S, h2, h3);
+  xy_rescale(tab[4], h2, h3);
+  xy_lds_rescale(lds, lane, 0, h2, h3);
+  sum(tab[3], S, P);  // S + m(P)
+  xy_rescale(P, h2, h3);
+  xy_rescale(tab[2], h2, h3);
+  xy_rescale(tab[4], h2, h3);
+  xy_lds_rescale(lds, lane, 0, h2, h3);
+  {
+    XY<F> t6;
+    sum(t6, P, S);  // P + m(S)
+    xy_lds_put(lds, lane, 1, t6);
+  }
+  xy_rescale(S, h2, h3);
+  xy_rescale(tab[2], h2, h3);
+  xy_rescale(tab[3], h2, h3);
+  xy_rescale(tab[4], h2, h3);
+  xy_lds_rescale(lds, lane, 0, h2, h3);
+  {
+    XY<F> t7;
+    const XY<F> s0 = S;
+    sum(t7, S, s0);  // S + m(S)
+    xy_lds_put(lds, lane, 2, t7);
+  }
+  xy_rescale(P, h2, h3);
+  xy_rescale(tab[2], h2, h3);
+  xy_rescale(tab[3], h2, h3);
+  xy_rescale(tab[4], h2, h3);
+  xy_lds_rescale(lds, lane, 0, h2, h3);
+  xy_lds_rescale(lds, lane, 1, h2, h3);
+}
+
 template <class F, bool LDS3 = false>
 HD void xadic_mul_sac8(Jac<F>& r, const Aff<F>& p, const Jac<F>& xpj, const Fq& c, uint32_t d0,
                        uint32_t d1, uint32_t d2, uint32_t d3, int nbits, uint32_t* lds = nullptr,
                        uint32_t lane = 0) {
-  XY<F> tab[8];
-  F zs;
-  xadic_table8(tab, zs, p, xpj, c);
-  const uint32_t k0 = d0 | 1u;
-  uint64_t m[3];
-  xadic_sac_recode(m, k0, d1, d2, d3, nbits);
   // LDS3: entries 5..7 live in LDS (lds: 3 x NWD x 64 words, [entry][word][lane]: each lane reads
   // its own column, conflict-free) and are read by a lane-dependent address, entries 0..4 stay in
   // registers (k_rlc_items at two waves per SIMD: 256 VGPRs hold five entries beside the loop)
   constexpr int NWD = (int)(sizeof(XY<F>) / 4);
-  if (LDS3) {
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(&tab[5 + e]);
-#pragma unroll
-      for (int w = 0; w < NWD; ++w) lds[(e * NWD + w) * 64 + lane] = src[w];
-    }
-  }
+  XY<F> tab[LDS3 ? 5 : 8];
+  F zs;
+  if constexpr (LDS3)
+    xadic_table8_chain(tab, zs, p, xpj, c, lds, lane);
+  else
+    xadic_table8(tab, zs, p, xpj, c);
+  const uint32_t k0 = d0 | 1u;
+  uint64_t m[3];
+  xadic_sac_recode(m, k0, d1, d2, d3, nbits);
   // the entry of column i, negated when s_i = -1: a select tree over the entries (constant
   // indices only, so the register entries never go to scratch)
   auto entry = [&](int i, XY<F>& t) {
@@ -823,7 +927,7 @@ HD void xadic_mul_sac8(Jac<F>& r, const Aff<F>& p, const Jac<F>& xpj, const Fq& 
       xy_sel(b, b1, tab[3], tab[2]);
       xy_sel(e0, b2, b, a);
     }
-    if (LDS3) {
+    if constexpr (LDS3) {
       const uint32_t j = (b1 ? 1u : 0u) + (b2 ? 2u : 0u);  // entry 4 + j
       const uint32_t li = j ? j - 1u : 0u;
       XY<F> l;

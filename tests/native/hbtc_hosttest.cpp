@@ -224,6 +224,47 @@ int ht_g1_mul_xadic8(const uint8_t* in48, const uint32_t* d, int nbits, uint8_t*
   store_words(out48, w, 12);
   return 0;
 }
+// the same with entries 5..7 in an LDS-layout buffer ([entry][word][lane], lane 5 of 64) and the
+// co-Z chain build (curve.h xadic_table8_chain: k_rlc_items' form)
+int ht_g1_mul_xadic8_lds(const uint8_t* in48, const uint32_t* d, int nbits, uint8_t* out48) {
+  uint32_t w[12];
+  load_words(w, in48, 12);
+  G1A p;
+  G1J t1;
+  if (!g1_decompress_t1(p, t1, w)) return -1;
+  jac_neg(t1, t1);
+  Fq beta;
+  fq_set(beta, G1_BETA);
+  static uint32_t lds[3 * 24 * 64];
+  G1J r;
+  xadic_mul_sac8<Fq, true>(r, p, t1, beta, d[0], d[1], d[2], d[3], nbits, lds, 5);
+  G1A o;
+  jac_to_aff(o, r);
+  g1_compress(w, o);
+  store_words(out48, w, 12);
+  return 0;
+}
+int ht_g2_mul_xadic8_lds(const uint8_t* in96, const uint32_t* d, int nbits, uint8_t* out96) {
+  uint32_t w[24];
+  load_words(w, in96, 24);
+  G2A p;
+  if (!g2_decompress(p, w)) return -1;
+  G2A xp;
+  g2_psi(xp.x, xp.y, p);
+  xp.inf = 0;
+  G2J xj;
+  jac_from_aff(xj, xp);
+  Fq zeta;
+  fq_set(zeta, G2_ZETA);
+  static uint32_t lds[3 * 48 * 64];
+  G2J r;
+  xadic_mul_sac8<Fq2, true>(r, p, xj, zeta, d[0], d[1], d[2], d[3], nbits, lds, 5);
+  G2A o;
+  jac_to_aff(o, r);
+  g2_compress(w, o);
+  store_words(out96, w, 24);
+  return 0;
+}
 int ht_g2_mul_xadic8(const uint8_t* in96, const uint32_t* d, int nbits, uint8_t* out96) {
   uint32_t w[24];
   load_words(w, in96, 24);

@@ -96,6 +96,8 @@ def test_xadic_scalar_of_rlc_items(ht, nbits):
     ht.ht_g2_mul_xadic16.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
     ht.ht_g1_mul_xadic8.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
     ht.ht_g2_mul_xadic8.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
+    ht.ht_g1_mul_xadic8_lds.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
+    ht.ht_g2_mul_xadic8_lds.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
     cases += [(2, 0, 0, 0), (0, top, top, top), (top - 1, 1, 1, 1), (2, 1, 0, 0)]
     for d in cases:
         r = (d[0] + d[1] * B.X + d[2] * mu + d[3] * mu * B.X) % B.R
@@ -118,6 +120,11 @@ def test_xadic_scalar_of_rlc_items(ht, nbits):
         assert o.raw == B.g1_compress(B.g1_mul(P, r)), ("g1 sac8", d)
         assert ht.ht_g2_mul_xadic8(B.g2_compress(Q), ctypes.cast(arr, ctypes.c_void_p), nbits, o2) == 0
         assert o2.raw == B.g2_compress(B.g2_mul(Q, r)), ("g2 sac8", d)
+        # k_rlc_items' form: three entries in an LDS-layout buffer, the co-Z chain build
+        assert ht.ht_g1_mul_xadic8_lds(B.g1_compress(P), ctypes.cast(arr, ctypes.c_void_p), nbits, o) == 0
+        assert o.raw == B.g1_compress(B.g1_mul(P, r)), ("g1 sac8 lds", d)
+        assert ht.ht_g2_mul_xadic8_lds(B.g2_compress(Q), ctypes.cast(arr, ctypes.c_void_p), nbits, o2) == 0
+        assert o2.raw == B.g2_compress(B.g2_mul(Q, r)), ("g2 sac8 lds", d)
 
 
 def test_sac2_two_digit_form(ht):

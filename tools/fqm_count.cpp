@@ -144,7 +144,9 @@ int main() {
     fq_set(beta, G1_BETA);
     const uint32_t m = nb == 32 ? 0xffffffffu : 0xffffu;
 #if HBTC_XADIC8
-    xadic_mul_sac8(rd, d2, t1, beta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
+    // k_rlc_items' form: the co-Z chain table build, three entries in LDS (xadic_table8_chain)
+    static uint32_t lds[3 * 24 * 64];
+    xadic_mul_sac8<Fq, true>(rd, d2, t1, beta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb, lds, 0);
 #elif HBTC_XADIC16
     xadic_mul_tab16(rd, d2, t1, beta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
 #else
