@@ -22,12 +22,15 @@ namespace hbtc {
 #ifndef HBTC_SIG_SPLIT
 #define HBTC_SIG_SPLIT 1
 #endif
+#ifndef HBTC_SIG_DEC_WAVES
+#define HBTC_SIG_DEC_WAVES 2
+#endif
 #if HBTC_SIG_SPLIT
 // The decode half of the SignatureShare item pass, a kernel of its own so it runs at two waves per
-// SIMD (772 B/lane of scratch; in one kernel with the scalar half the G2 state needs one wave per
+// SIMD (588 B/lane of scratch; in one kernel with the scalar half the G2 state needs one wave per
 // SIMD): zcash G2 decode with the psi subgroup test into dec, DECODE_ERR into status (every other
 // item: RLC_PENDING, decided by k_sig_items).
-__global__ void __launch_bounds__(64, 2) k_sig_decode(
+__global__ void __launch_bounds__(64, HBTC_SIG_DEC_WAVES) k_sig_decode(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ sigs,
     const int32_t* __restrict__ pk_status, uint32_t n_pk, G2A* __restrict__ dec,
     int32_t* __restrict__ status) {
@@ -41,10 +44,36 @@ __global__ void __launch_bounds__(64, 2) k_sig_decode(
     uint32_t w[24];
     rlc_load_words(w, sigs, item, 24);
     G2A sg;
-    if (g2_decompress(sg, w))
-      dec[item] = sg;  // for the scalar half, the exact leaf checks and the combine
-    else
+    if (!g2_decompress(sg, w, false)) {
       st = HBTC_DECODE_ERR;
+    } else {
+      // for the scalar half, the exact leaf checks and the combine; then the psi subgroup test
+      // (curve.h g2_in_subgroup: psi(P) == -[|x|] P) with P parked there: the double-and-add
+      // re-reads it for each of its five additions and for the final comparison, so the
+      // doublings run with only the accumulator live beside the shared-subroutine product's
+      // fixed registers (772 -> 588 B/lane at two waves; one wave, 0 B/lane, loses: C4 126 vs 131 ms,
+      // profiles/r05/run21/)
+      dec[item] = sg;
+      if (!sg.inf) {
+        G2J t;
+        jac_from_aff(t, sg);  // bit 63 of |x|
+#pragma unroll 1
+        for (int b = 62; b >= 0; --b) {
+          jac_dbl(t, t);
+          if ((BLS_X_ABS >> b) & 1ull) {
+            __asm__ volatile("" ::: "memory");  // P is re-read, not kept in registers
+            const G2A q = dec[item];
+            jac_add_aff(t, t, q);
+          }
+        }
+        __asm__ volatile("" ::: "memory");
+        const G2A q = dec[item];
+        Fq2 px, py, npy;
+        g2_psi(px, py, q);
+        fq2_neg(npy, py);
+        if (jac_is_inf(t) || !jac_eq_aff(t, px, npy)) st = HBTC_DECODE_ERR;
+      }
+    }
   }
   status[item] = st;
 }
