@@ -501,6 +501,51 @@ HD void xadic_mul_uniform(Jac<F>& r, const Aff<F>& p, const Aff<F>& xp, const Af
   r = acc;
 }
 
+// The same loop with the three table points in LDS ([entry][word][lane]: each lane reads its own
+// column, conflict-free; entry 0 = P, 1 = XP, 2 = P + XP), read by a lane-dependent entry index
+// instead of selects over registers: the G2 item pass (k_sig_items, one wave per SIMD) holds
+// 144 dwords of table beside its accumulator and the shared product's fixed registers otherwise,
+// and re-read ~53 spilled dwords per bit from scratch.
+template <class F>
+HD void xy_lds_get_aff(F& x, F& y, const uint32_t* lds, uint32_t lane, uint32_t e) {
+  constexpr int NW = (int)(sizeof(F) / 4);
+  uint32_t* dx = reinterpret_cast<uint32_t*>(&x);
+  uint32_t* dy = reinterpret_cast<uint32_t*>(&y);
+#pragma unroll
+  for (int w = 0; w < NW; ++w) dx[w] = lds[(e * 2 * NW + w) * 64 + lane];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) dy[w] = lds[(e * 2 * NW + NW + w) * 64 + lane];
+}
+template <class F>
+HD void xy_lds_put_aff(uint32_t* lds, uint32_t lane, uint32_t e, const Aff<F>& p) {
+  constexpr int NW = (int)(sizeof(F) / 4);
+  const uint32_t* sx = reinterpret_cast<const uint32_t*>(&p.x);
+  const uint32_t* sy = reinterpret_cast<const uint32_t*>(&p.y);
+#pragma unroll
+  for (int w = 0; w < NW; ++w) lds[(e * 2 * NW + w) * 64 + lane] = sx[w];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) lds[(e * 2 * NW + NW + w) * 64 + lane] = sy[w];
+}
+template <class F>
+HD void xadic_mul_uniform_lds(Jac<F>& r, const uint32_t* lds, uint32_t lane, const Fq& c, uint32_t d0,
+                              uint32_t d1, uint32_t d2, uint32_t d3, int nbits) {
+  Jac<F> acc;
+  jac_set_inf(acc);
+#pragma unroll 1
+  for (int bit = nbits - 1; bit >= 0; --bit) {
+    jac_dbl(acc, acc);
+    const bool b0 = ((d0 >> bit) & 1u) != 0, b1 = ((d1 >> bit) & 1u) != 0;
+    const bool b2 = ((d2 >> bit) & 1u) != 0, b3 = ((d3 >> bit) & 1u) != 0;
+    F tx, ty;
+    xy_lds_get_aff(tx, ty, lds, lane, b1 ? (b0 ? 2u : 1u) : 0u);
+    uniform_add(acc, tx, ty, b0 || b1);
+    xy_lds_get_aff(tx, ty, lds, lane, b3 ? (b2 ? 2u : 1u) : 0u);
+    fmul_by_fq(tx, tx, c);  // m(T[b2, b3])
+    uniform_add(acc, tx, ty, b2 || b3);
+  }
+  r = acc;
+}
+
 // ---------------------------------------------------- x-adic scalars, one addition per bit
 // The same [r] P with ONE mixed addition per bit: the 15 nonzero sums T[b] = b0 P + b1 XP +
 // b2 m(P) + b3 m(XP), b = b0 + 2 b1 + 4 b2 + 8 b3, from a per-lane table (scratch memory: 15

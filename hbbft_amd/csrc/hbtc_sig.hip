@@ -22,6 +22,9 @@ namespace hbtc {
 #ifndef HBTC_SIG_SPLIT
 #define HBTC_SIG_SPLIT 1
 #endif
+#ifndef HBTC_SIG_TAB_LDS
+#define HBTC_SIG_TAB_LDS 1  // k_sig_items: the x-adic table's three points in LDS
+#endif
 #ifndef HBTC_SIG_DEC_WAVES
 #define HBTC_SIG_DEC_WAVES 2
 #endif
@@ -140,7 +143,17 @@ __global__ void __launch_bounds__(64, 1) k_sig_items(
             fq_set(zeta, G2_ZETA);
             G2A pxp;
             xadic_table(xp, pxp, sg, xj);
+#if HBTC_SIG_TAB_LDS
+            // the three table points in the reduction's LDS (idle until the loop is over: one
+            // wave per block)
+            uint32_t* tl = reinterpret_cast<uint32_t*>(&red2[0][0]);
+            xy_lds_put_aff(tl, lane, 0, sg);
+            xy_lds_put_aff(tl, lane, 1, xp);
+            xy_lds_put_aff(tl, lane, 2, pxp);
+            xadic_mul_uniform_lds(S, tl, lane, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+#else
             xadic_mul_uniform(S, sg, xp, pxp, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+#endif
           }
           if (!pk[id].inf) rlc_pk_mul_x(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, xd);
         }
