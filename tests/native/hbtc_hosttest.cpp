@@ -168,6 +168,33 @@ int ht_g2_mul_xadic(const uint8_t* in96, const uint32_t* d, int nbits, uint8_t* 
   store_words(out96, w, 24);
   return 0;
 }
+// the same loop over the table held in an LDS-layout buffer (curve.h xadic_mul_uniform_lds:
+// k_sig_items' form), lane 7 of 64
+int ht_g2_mul_xadic_lds(const uint8_t* in96, const uint32_t* d, int nbits, uint8_t* out96) {
+  uint32_t w[24];
+  load_words(w, in96, 24);
+  G2A p;
+  if (!g2_decompress(p, w)) return -1;
+  G2A xp, pxp;
+  g2_psi(xp.x, xp.y, p);
+  xp.inf = 0;
+  G2J xj;
+  jac_from_aff(xj, xp);
+  xadic_table(xp, pxp, p, xj);
+  Fq zeta;
+  fq_set(zeta, G2_ZETA);
+  static uint32_t lds[3 * 48 * 64];
+  xy_lds_put_aff(lds, 7, 0, p);
+  xy_lds_put_aff(lds, 7, 1, xp);
+  xy_lds_put_aff(lds, 7, 2, pxp);
+  G2J r;
+  xadic_mul_uniform_lds(r, lds, 7, zeta, d[0], d[1], d[2], d[3], nbits);
+  G2A o;
+  jac_to_aff(o, r);
+  g2_compress(w, o);
+  store_words(out96, w, 24);
+  return 0;
+}
 // the one-addition-per-bit form (curve.h xadic_mul_tab16) of the same scalar
 int ht_g1_mul_xadic16(const uint8_t* in48, const uint32_t* d, int nbits, uint8_t* out48) {
   uint32_t w[12];
