@@ -18,7 +18,7 @@ MSM_PARTS := 8 9
 SKG_PARTS := 10
 KOBJS := $(foreach p,$(PARTS),$(BUILD)/hbtc_kernels.p$(p).o) $(foreach p,$(RLC_PARTS),$(BUILD)/hbtc_rlc.p$(p).o) \
          $(foreach p,$(MSM_PARTS),$(BUILD)/hbtc_msm.p$(p).o) $(foreach p,$(SKG_PARTS),$(BUILD)/hbtc_skg.p$(p).o) \
-         $(BUILD)/hbtc_check.c1.o $(BUILD)/hbtc_check.c2.o $(BUILD)/hbtc_sig.o $(BUILD)/hbtc_pb.o \
+         $(BUILD)/hbtc_check.c1.o $(BUILD)/hbtc_check.c2.o $(BUILD)/hbtc_sig.s1.o $(BUILD)/hbtc_sig.s2.o $(BUILD)/hbtc_pb.o \
          $(BUILD)/hbtc_bcast.o $(BUILD)/hbtc_comb.o
 LIB := hbbft_amd/libhbtc.so
 
@@ -83,8 +83,13 @@ $(BUILD)/hbtc_check.c%.o: $(CSRC)/hbtc_check.hip $(HDRS) | $(BUILD)
 
 # the G2 item pass, all helpers inlined, the product as the shared subroutine (no ABI calls:
 # C2 658k -> 696k, C4 3.67M -> 3.93M shares/s with the check kernels, profiles/r03/fq_sr/)
-$(BUILD)/hbtc_sig.o: $(CSRC)/hbtc_sig.hip $(HDRS) | $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -DHBTC_INLINE_ALL -DHBTC_FQMUL_SR -c $< -o $@
+$(BUILD)/hbtc_sig.s2.o: $(CSRC)/hbtc_sig.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DHBTC_SIG_PART=2 -DHBTC_INLINE_ALL -DHBTC_FQMUL_SR -c $< -o $@
+
+# the G2 decode half (k_sig_decode) with the product inlined: no scratch in its loops
+# (588 -> 432 B/lane, the doubling loop's ~150 spilled dwords per bit gone)
+$(BUILD)/hbtc_sig.s1.o: $(CSRC)/hbtc_sig.hip $(HDRS) | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -DHBTC_SIG_PART=1 -DHBTC_INLINE_ALL -DHBTC_FQMUL_INLINE -c $< -o $@
 
 # the pair-batch item pass (Ciphertext::verify / PublicKey::verify by RLC), helpers inlined,
 # the product as the shared subroutine

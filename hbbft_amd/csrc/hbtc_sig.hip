@@ -28,9 +28,17 @@ namespace hbtc {
 #ifndef HBTC_SIG_DEC_WAVES
 #define HBTC_SIG_DEC_WAVES 2
 #endif
-#if HBTC_SIG_SPLIT
+// The file is compiled twice (Makefile): part 1 = the decode half with the Fq product inlined
+// (its loops then run without scratch: the shared subroutine's 102 fixed VGPRs left the G2
+// doubling loop re-reading ~150 spilled dwords per bit at two waves), part 2 = the rest with the
+// product as the shared subroutine.
+#ifndef HBTC_SIG_PART
+#define HBTC_SIG_PART 0
+#endif
+#define HBTC_SIG_IN(n) (HBTC_SIG_PART == 0 || HBTC_SIG_PART == (n))
+#if HBTC_SIG_SPLIT && HBTC_SIG_IN(1)
 // The decode half of the SignatureShare item pass, a kernel of its own so it runs at two waves per
-// SIMD (588 B/lane of scratch; in one kernel with the scalar half the G2 state needs one wave per
+// SIMD (432 B/lane of scratch; in one kernel with the scalar half the G2 state needs one wave per
 // SIMD): zcash G2 decode with the psi subgroup test into dec, DECODE_ERR into status (every other
 // item: RLC_PENDING, decided by k_sig_items).
 __global__ void __launch_bounds__(64, HBTC_SIG_DEC_WAVES) k_sig_decode(
@@ -53,8 +61,9 @@ __global__ void __launch_bounds__(64, HBTC_SIG_DEC_WAVES) k_sig_decode(
       // for the scalar half, the exact leaf checks and the combine; then the psi subgroup test
       // (curve.h g2_in_subgroup: psi(P) == -[|x|] P) with P parked there: the double-and-add
       // re-reads it for each of its five additions and for the final comparison, so the
-      // doublings run with only the accumulator live beside the shared-subroutine product's
-      // fixed registers (772 -> 588 B/lane at two waves; one wave, 0 B/lane, loses: C4 126 vs 131 ms,
+      // doublings run with only the accumulator live (772 -> 588 B/lane with the shared-
+      // subroutine product, 432 with it inlined -- this part's build -- and no scratch access in
+      // any loop; one wave per SIMD instead, 0 B/lane, loses: C4 126 vs 131 ms,
       // profiles/r05/run21/)
       dec[item] = sg;
       if (!sg.inf) {
@@ -80,8 +89,19 @@ __global__ void __launch_bounds__(64, HBTC_SIG_DEC_WAVES) k_sig_decode(
   }
   status[item] = st;
 }
+hipError_t launch_sig_decode(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
+                             const uint8_t* sigs, const int32_t* pk_status, uint32_t n_pk, G2A* dec,
+                             int32_t* status) {
+  hipLaunchKernelGGL(k_sig_decode, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk_status, n_pk, dec,
+                     status);
+  return hipGetLastError();
+}
 #endif
 
+#if HBTC_SIG_IN(2)
+hipError_t launch_sig_decode(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
+                             const uint8_t* sigs, const int32_t* pk_status, uint32_t n_pk, G2A* dec,
+                             int32_t* status);
 // One wave per tile: decode every SignatureShare (zcash compressed G2 + subgroup check), r_i,
 // r_i sigma_i, r_i pk_i, then the plain and weighted tile / sub-tile sums in both groups.  One
 // wave per SIMD (256 VGPRs + 256 AGPRs: 736 B/lane of scratch).  Round 5 dropped the two-wave
@@ -241,9 +261,7 @@ hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, 
                             SigTileSums* sums, G2A* dec, int32_t* status) {
   if (n_tiles == 0) return hipSuccess;
 #if HBTC_SIG_SPLIT
-  hipLaunchKernelGGL(k_sig_decode, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk_status, n_pk, dec,
-                     status);
-  const hipError_t e = hipGetLastError();
+  const hipError_t e = launch_sig_decode(s, n_tiles, tiles, idx, sigs, pk_status, n_pk, dec, status);
   if (e != hipSuccess) return e;
 #endif
   hipLaunchKernelGGL(k_sig_items, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk, pk_status,
@@ -259,5 +277,6 @@ hipError_t launch_plines(hipStream_t s, int mode, uint32_t max_groups, uint32_t 
                      base, count, list, tiles, sums, dec, tables, inf);
   return hipGetLastError();
 }
+#endif  // part 2
 
 }  // namespace hbtc

@@ -21,7 +21,8 @@ BASE = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I" + os.path.jo
 # object -> (source, flags), as the Makefile builds them
 OBJECTS = {
     "hbtc_rlc.p6": ("hbtc_rlc.hip", ["-DHBTC_PART=6", "-DHBTC_INLINE_ALL", "-DHBTC_FQMUL_INLINE"]),
-    "hbtc_sig": ("hbtc_sig.hip", ["-DHBTC_INLINE_ALL", "-DHBTC_FQMUL_SR"]),
+    "hbtc_sig.s1": ("hbtc_sig.hip", ["-DHBTC_SIG_PART=1", "-DHBTC_INLINE_ALL", "-DHBTC_FQMUL_INLINE"]),
+    "hbtc_sig.s2": ("hbtc_sig.hip", ["-DHBTC_SIG_PART=2", "-DHBTC_INLINE_ALL", "-DHBTC_FQMUL_SR"]),
     "hbtc_check.c1": ("hbtc_check.hip", ["-DHBTC_CHECK_PART=1", "-DHBTC_GT_INLINE", "-DHBTC_FQMUL_SR"]),
     "hbtc_check.c2": ("hbtc_check.hip", ["-DHBTC_CHECK_PART=2", "-DHBTC_GT_INLINE", "-DHBTC_FQMUL_SR"]),
 }

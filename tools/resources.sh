@@ -16,7 +16,8 @@ run -DHBTC_PART=9 -DHBTC_INLINE_ALL -DHBTC_FQMUL_SR -c hbbft_amd/csrc/hbtc_msm.h
 run -DHBTC_PART=10 -c hbbft_amd/csrc/hbtc_skg.hip &
 wait
 for p in 1 2; do run -DHBTC_CHECK_PART=$p -DHBTC_GT_INLINE -DHBTC_FQMUL_SR -c hbbft_amd/csrc/hbtc_check.hip & done
-run -DHBTC_INLINE_ALL -DHBTC_FQMUL_SR -c hbbft_amd/csrc/hbtc_sig.hip &
+run -DHBTC_SIG_PART=1 -DHBTC_INLINE_ALL -DHBTC_FQMUL_INLINE -c hbbft_amd/csrc/hbtc_sig.hip &
+run -DHBTC_SIG_PART=2 -DHBTC_INLINE_ALL -DHBTC_FQMUL_SR -c hbbft_amd/csrc/hbtc_sig.hip &
 run -DHBTC_INLINE_ALL -DHBTC_FQMUL_SR -c hbbft_amd/csrc/hbtc_pb.hip &
 run -DHBTC_INLINE_ALL -DHBTC_FQMUL_SR -c hbbft_amd/csrc/hbtc_comb.hip &
 run -DHBTC_INLINE_ALL -DHBTC_FQMUL_SR -c hbbft_amd/csrc/hbtc_hash.hip &
