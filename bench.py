@@ -62,9 +62,19 @@ G1_GEN = bytes.fromhex("97f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f
 G2_GEN = bytes.fromhex("93e02b6052719f607dacd3a088274f65596bd0d09920b61ab5da61bbdc7f5049334cf11213945d57e5ac7d055d042b7e"
                        "024aa2b2f08f0a91260805272dc51051c6e47ad4fa403b02b4510b647ae3d1770bac0326a805bbefd48056c8c121bdb8")
 SEED = 0x6862626674
-# measured v_mad_u64_u32 lane-op throughput on MI355X (tools/microbench/intmul.hip,
-# profiles/r01_intmul_microbench.txt): the VALU integer-multiply roofline of the Fqm kernels
-MAD_U64_PEAK = 29.51e12
+# The VALU integer-multiply roofline of the Fqm kernels: v_mad_u64_u32 issues at 4 cycles per
+# wave-instruction per SIMD (16 lane-ops / cycle; tools/microbench/intmul.hip measures 4.15-4.2
+# including its loop, at 2 to 8 waves per SIMD), so at the 2.4 GHz spec clock the chip's peak is
+# 256 CUs x 4 SIMDs x 16 x 2.4e9 = 39.32 T lane-ops/s.  The harness that measures it reaches 72.1 T
+# packed-FMA lane-ops/s = 0.92 of the 78.6 T behind the 157.3 TFLOP/s FP32 spec (its sanity line);
+# under an integer-multiply load the chip holds 2.15-2.28 GHz, where the same harness delivers
+# 35.6 T v_mad_u64_u32/s.  profiles/r06/intmul_peak.txt.  (Rounds 1-5 divided by the round-1
+# harness's 29.51 T, which under-drove the instruction: every earlier frac reads ~1.33x high.)
+MAD_U64_PEAK = 39.32e12
+MAD_U64_PEAK_NOTE = ("v_mad_u64_u32 at 4 cycles per wave-instruction per SIMD x 1024 SIMDs x 64 lanes x 2.4 GHz "
+                     "spec clock; tools/microbench/intmul.hip: 4.15-4.2 cyc/insn measured (35.6 T at the 2.28 GHz "
+                     "the chip holds under load), sanity line v_pk_fma_f32 72.1 T lane-FMA/s = 0.92 of the FP32 "
+                     "spec; profiles/r06/intmul_peak.txt")
 # timing family -> kernel (hbtc_api.hip timed() families, rocprofv3 names), per check schedule
 # (hbtc_check_schedule_for: the plain-first form for calls that fill the chip, the paired forms
 # for small calls such as a rank's slice of the epoch)
@@ -375,7 +385,7 @@ def max_over_ranks(elapsed, dist, device=None):
     return float(tt.item())
 
 
-PROFILE_ROUND = "r05"
+PROFILE_ROUND = "r06"
 
 
 def profile_dir(args, world):
@@ -675,6 +685,7 @@ def main():
     # FETCH_SIZE doubled per the gfx950 note.  A workload without a committed profile reports
     # null rather than another workload's figures.
     traffic, pmc, rocprof_ms, rocprof_n, rocprof_src = None, {}, None, 0, None
+    valu_insts, pmc_parts = None, None
     prof_dir = profile_dir(args, world)
     if prof_dir:
         summ_path = os.path.join(ROOT, prof_dir, "pmc_summary.json")
@@ -688,6 +699,13 @@ def main():
             pmc = found[-1] if found else {}
             if found and all("hbm_read_bytes" in f and "hbm_write_bytes" in f for f in found):
                 traffic = sum(f["hbm_read_bytes"] + f["hbm_write_bytes"] for f in found)
+            vi = [f.get("counters_mean_per_dispatch", {}).get("SQ_INSTS_VALU") for f in found]
+            if found and all(v is not None for v in vi):
+                valu_insts = sum(vi)
+            pmc_parts = {k: {x: f.get(x) for x in ("grid", "full_size_dispatches", "dispatches", "vgpr",
+                                                    "scratch_bytes_per_lane", "valu_busy", "hbm_read_bytes",
+                                                    "hbm_write_bytes")}
+                         for k, f in zip(parts, found)}
         avgs = [rocprof_avg_ms(prof_dir, k) for k in parts]
         avgs = [a for a in avgs if a[0] is not None]
         if avgs:
@@ -744,10 +762,12 @@ def main():
             "kernel": " + ".join(KERNEL_PARTS.get(dom, (kname[dom],))),
             "achieved": round(achieved, 3),
             "peak": MAD_U64_PEAK / 1e12,
+            "peak_source": MAD_U64_PEAK_NOTE,
             "unit": "T mad_u64_u32/s",
             "frac": round(achieved / (MAD_U64_PEAK / 1e12), 4),
             "traffic": traffic,
-            "traffic_unit": "bytes per launch (HBM read + write, rocprofv3 PMC)",
+            "traffic_unit": "bytes per full-size launch (HBM read + write, rocprofv3 PMC; FETCH_SIZE x2 per "
+                            "the gfx950 note), summed over the family's kernels",
             "fqm_per_launch": fqm_per_launch[dom],
             "kernel_ms_per_launch": round(dom_avg_s * 1e3, 3),
             "kernel_ms_per_launch_source": "HIP events on the kernel's stream, this run (the span can "
@@ -764,9 +784,13 @@ def main():
                                     / (iso[dom][0] / iso[dom][1] * 1e-3) / MAD_U64_PEAK, 4)
                               if iso.get(dom, (0, 0))[1] else None),
             "isolated_note": "one extra epoch after the timed region with no other epoch in flight",
-            "pmc": {k: pmc[k] for k in ("vgpr", "scratch_bytes_per_lane", "valu_busy",
-                                        "hbm_read_bytes", "hbm_write_bytes") if k in pmc} or None,
-            "valu_insts_per_launch": pmc.get("counters_mean_per_dispatch", {}).get("SQ_INSTS_VALU"),
+            "pmc": pmc_parts,
+            "pmc_note": ("per kernel: means over the full-size dispatches only (grid = the kernel's "
+                         "largest in the pass; a key set's probe pass is excluded), tools/pmc_summary.py"),
+            "valu_wave_insts_per_launch": valu_insts,
+            "valu_wave_insts_per_wave_mad": (round(valu_insts / (fqm_per_launch[dom]
+                                                                * consts["mad_u64_u32_per_fqm"] / 64), 3)
+                                             if valu_insts else None),
         },
     }
     if world == 1 and not args.no_extra:

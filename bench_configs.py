@@ -115,7 +115,7 @@ def breakdown(ctx, steps, fams):
     return out
 
 
-MAD_U64_PEAK = 29.51e12  # measured v_mad_u64_u32 lane-ops/s (bench.py MAD_U64_PEAK)
+MAD_U64_PEAK = 39.32e12  # v_mad_u64_u32 peak at the spec clock (bench.py MAD_U64_PEAK, profiles/r06/intmul_peak.txt)
 
 
 def roofline_line(ctx, family, kernel, fqm_per_launch, note):

@@ -506,27 +506,29 @@ HD void xadic_mul_uniform(Jac<F>& r, const Aff<F>& p, const Aff<F>& xp, const Af
 // instead of selects over registers: the G2 item pass (k_sig_items, one wave per SIMD) holds
 // 144 dwords of table beside its accumulator and the shared product's fixed registers otherwise,
 // and re-read ~53 spilled dwords per bit from scratch.
-template <class F>
+// (LANES: the lane stride of the layout -- 64 for one lane per item, 128 for a two-wave
+// workgroup of lane pairs, pair.h)
+template <class F, int LANES = 64>
 HD void xy_lds_get_aff(F& x, F& y, const uint32_t* lds, uint32_t lane, uint32_t e) {
   constexpr int NW = (int)(sizeof(F) / 4);
   uint32_t* dx = reinterpret_cast<uint32_t*>(&x);
   uint32_t* dy = reinterpret_cast<uint32_t*>(&y);
 #pragma unroll
-  for (int w = 0; w < NW; ++w) dx[w] = lds[(e * 2 * NW + w) * 64 + lane];
+  for (int w = 0; w < NW; ++w) dx[w] = lds[(e * 2 * NW + w) * LANES + lane];
 #pragma unroll
-  for (int w = 0; w < NW; ++w) dy[w] = lds[(e * 2 * NW + NW + w) * 64 + lane];
+  for (int w = 0; w < NW; ++w) dy[w] = lds[(e * 2 * NW + NW + w) * LANES + lane];
 }
-template <class F>
+template <class F, int LANES = 64>
 HD void xy_lds_put_aff(uint32_t* lds, uint32_t lane, uint32_t e, const Aff<F>& p) {
   constexpr int NW = (int)(sizeof(F) / 4);
   const uint32_t* sx = reinterpret_cast<const uint32_t*>(&p.x);
   const uint32_t* sy = reinterpret_cast<const uint32_t*>(&p.y);
 #pragma unroll
-  for (int w = 0; w < NW; ++w) lds[(e * 2 * NW + w) * 64 + lane] = sx[w];
+  for (int w = 0; w < NW; ++w) lds[(e * 2 * NW + w) * LANES + lane] = sx[w];
 #pragma unroll
-  for (int w = 0; w < NW; ++w) lds[(e * 2 * NW + NW + w) * 64 + lane] = sy[w];
+  for (int w = 0; w < NW; ++w) lds[(e * 2 * NW + NW + w) * LANES + lane] = sy[w];
 }
-template <class F>
+template <class F, int LANES = 64>
 HD void xadic_mul_uniform_lds(Jac<F>& r, const uint32_t* lds, uint32_t lane, const Fq& c, uint32_t d0,
                               uint32_t d1, uint32_t d2, uint32_t d3, int nbits) {
   Jac<F> acc;
@@ -537,45 +539,18 @@ HD void xadic_mul_uniform_lds(Jac<F>& r, const uint32_t* lds, uint32_t lane, con
     const bool b0 = ((d0 >> bit) & 1u) != 0, b1 = ((d1 >> bit) & 1u) != 0;
     const bool b2 = ((d2 >> bit) & 1u) != 0, b3 = ((d3 >> bit) & 1u) != 0;
     F tx, ty;
-    xy_lds_get_aff(tx, ty, lds, lane, b1 ? (b0 ? 2u : 1u) : 0u);
+    xy_lds_get_aff<F, LANES>(tx, ty, lds, lane, b1 ? (b0 ? 2u : 1u) : 0u);
     uniform_add(acc, tx, ty, b0 || b1);
-    xy_lds_get_aff(tx, ty, lds, lane, b3 ? (b2 ? 2u : 1u) : 0u);
+    xy_lds_get_aff<F, LANES>(tx, ty, lds, lane, b3 ? (b2 ? 2u : 1u) : 0u);
     fmul_by_fq(tx, tx, c);  // m(T[b2, b3])
     uniform_add(acc, tx, ty, b2 || b3);
   }
   r = acc;
 }
 
-// ---------------------------------------------------- x-adic scalars, one addition per bit
-// The same [r] P with ONE mixed addition per bit: the 15 nonzero sums T[b] = b0 P + b1 XP +
-// b2 m(P) + b3 m(XP), b = b0 + 2 b1 + 4 b2 + 8 b3, from a per-lane table (scratch memory: 15
-// points of 2 coordinates, read once per bit).  No inversion: the entries share ONE Z (Z*),
-// so their (X, Y) are affine points of the isomorphic curve y^2 = x^3 + b Z*^6, and the
-// doubling and mixed-addition formulas (a = 0) do not involve b: the double-and-add runs on
-// that curve and the result's Z is multiplied by Z* at the end.  Building the table:
-//   P at XP's Z1 (P1 = (x Z1^2, y Z1^3)); S = XP + P1 by a co-Z addition, which also returns XP
-//   at S's Z0 = Z1 H; P1 scaled by H -> the bases U = {P, XP, S} share Z0, and so do their
-//   images m(U) = (c X, Y, Z0);
-//   the 9 sums U[i] + m(U[j]) by co-Z additions (Z = Z0 H_k, never formed);
-//   every entry scaled to Z* = Z0 prod H_k (prefix / suffix products of the H_k).
-// 12 + 3 + 9 x 6 + 23 + 52 Fq products against the two-addition loop's 32 additions and
-// products by c, and its inversion (xadic_table).  Exceptional cases: H_k = 0 would need
-// U[i] = +-m(U[j]), i.e. a - mu b = 0 mod r for a, b in {1, x, 1 + x}: a nonzero integer of size
-// < r, so never for P in the prime-order group (items that fail the subgroup test never get
-// here).
-// G1 item passes (k_rlc_items, k_pb_items' A) use xadic_mul_tab16: 1.5 KB/lane of table.  On G2
-// the table is 2.9 KB/lane and takes k_sig_items to 6-8 KB/lane of scratch; the runtime reserves
-// a kernel's scratch per hardware queue for the device's wave slots, so only the
-// throughput form of k_sig_items uses it, on the process-wide exact stream (HBTC_XADIC16_G2);
-// k_pb_items' W and the small-call form keep the two-addition loop.
-#ifndef HBTC_XADIC16
-#define HBTC_XADIC16 1
-#endif
+// ------------------------------------------------------------ x-adic scalars: shared pieces
 #ifndef HBTC_XADIC8
-#define HBTC_XADIC8 1  // G1 item passes: the sign-aligned 8-entry table (xadic_mul_sac8) instead
-#endif
-#ifndef HBTC_XADIC16_G2
-#define HBTC_XADIC16_G2 1
+#define HBTC_XADIC8 1  // G1 item passes: the sign-aligned 8-entry table (xadic_mul_sac8)
 #endif
 template <class F>
 struct XY {
@@ -606,129 +581,11 @@ HD void scale_xy(XY<F>& p, const F& l2, const F& l3) {
   fmul(p.x, p.x, l2);
   fmul(p.y, p.y, l3);
 }
-template <class F>
-HD void xadic_table16(XY<F> tab[16], F& zs, const Aff<F>& p, const Jac<F>& xpj, const Fq& c) {
-  XY<F> u[4];  // u[1] = P, u[2] = XP, u[3] = P + XP at the common Z0
-  F h, hh, hhh;
-  {
-    F z2, z3;
-    fsqr(z2, xpj.z);
-    fmul(z3, z2, xpj.z);
-    fmul(u[1].x, p.x, z2);
-    fmul(u[1].y, p.y, z3);
-    F ax = u[1].x, ay = u[1].y;  // P1, rescaled to Z0 below
-    XY<F> s;
-    F bx = xpj.x, by = xpj.y;
-    coz_add(s, bx, by, h, u[1]);  // s = XP + P1, (bx, by) = XP at Z1 H
-    u[3] = s;
-    u[2].x = bx;
-    u[2].y = by;
-    fsqr(hh, h);
-    fmul(hhh, hh, h);
-    XY<F> p1{ax, ay};
-    scale_xy(p1, hh, hhh);
-    u[1] = p1;
-    fmul(zs, xpj.z, h);  // Z0
-  }
-  XY<F> mu[4];
-  for (int j = 1; j < 4; ++j) {
-    fmul_by_fq(mu[j].x, u[j].x, c);
-    mu[j].y = u[j].y;
-  }
-  // the sums straight into the table, then scaled in place: lam_k = prod_{j != k} H_j from the
-  // prefix products and a running suffix product, Lam = prod H_j for the bases
-  F hk[9], pre[9];
-#pragma unroll
-  for (int i = 1; i < 4; ++i)
-#pragma unroll
-    for (int j = 1; j < 4; ++j) {
-      const int k = 3 * (i - 1) + (j - 1);
-      F ax = u[i].x, ay = u[i].y;
-      coz_add(tab[i + 4 * j], ax, ay, hk[k], mu[j]);
-    }
-  pre[0] = hk[0];
-#pragma unroll
-  for (int k = 1; k < 9; ++k) fmul(pre[k], pre[k - 1], hk[k]);
-  F run;
-#pragma unroll
-  for (int k = 8; k >= 0; --k) {
-    const int i = k / 3 + 1, j = k % 3 + 1;
-    F l, l2, l3;
-    if (k == 8)
-      l = pre[7];
-    else if (k == 0)
-      l = run;
-    else
-      fmul(l, pre[k - 1], run);
-    if (k == 8)
-      run = hk[8];
-    else if (k > 0)
-      fmul(run, run, hk[k]);
-    fsqr(l2, l);
-    fmul(l3, l2, l);
-    scale_xy(tab[i + 4 * j], l2, l3);
-  }
-  {
-    F l2, l3;
-    fsqr(l2, pre[8]);
-    fmul(l3, l2, pre[8]);
-#pragma unroll
-    for (int j = 1; j < 4; ++j) {
-      scale_xy(u[j], l2, l3);
-      tab[j] = u[j];
-      fmul_by_fq(tab[4 * j].x, u[j].x, c);
-      tab[4 * j].y = u[j].y;
-    }
-    fmul(zs, zs, pre[8]);  // Z* = Z0 prod H_k
-  }
-  fzero(tab[0].x);
-  fzero(tab[0].y);
-}
-
-template <class F>
-HD void xadic_mul_tab16(Jac<F>& r, const Aff<F>& p, const Jac<F>& xpj, const Fq& c,
-                        uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, int nbits) {
-  XY<F> tab[16];
-  F zs;
-  xadic_table16(tab, zs, p, xpj, c);
-  auto digit = [&](int bit) {
-    return ((d0 >> bit) & 1u) | (((d1 >> bit) & 1u) << 1) | (((d2 >> bit) & 1u) << 2) |
-           (((d3 >> bit) & 1u) << 3);
-  };
-  Jac<F> acc;
-  jac_set_inf(acc);
-#ifndef HBTC_TAB16_PREFETCH
-#define HBTC_TAB16_PREFETCH 1
-#endif
-#if HBTC_TAB16_PREFETCH
-  uint32_t b = digit(nbits - 1);
-  XY<F> t = tab[b];
-#pragma unroll 1
-  for (int bit = nbits - 1; bit >= 0; --bit) {
-    const uint32_t nb = bit > 0 ? digit(bit - 1) : 0u;
-    const XY<F> tn = tab[nb];  // the next bit's entry, loaded ahead of this bit's arithmetic
-    jac_dbl(acc, acc);
-    uniform_add(acc, t.x, t.y, b != 0);
-    b = nb;
-    t = tn;
-  }
-#else
-#pragma unroll 1
-  for (int bit = nbits - 1; bit >= 0; --bit) {
-    const uint32_t b = digit(bit);
-    jac_dbl(acc, acc);
-    const XY<F> t = tab[b];
-    uniform_add(acc, t.x, t.y, b != 0);
-  }
-#endif
-  fmul(acc.z, acc.z, zs);  // back from the isomorphic curve (infinity stays Z = 0)
-  r = acc;
-}
-
 // ------------------------------------------- x-adic scalars, sign-aligned 8-entry table (GLV-SAC)
-// The same [r] P with one mixed addition per bit from EIGHT entries instead of fifteen, small
-// enough to stay in registers (AGPRs at one wave per SIMD) and be read by selects, so no per-lane
-// indexed table in scratch.  Sign-aligned recoding (Faz-Hernandez, Longa, Sanchez, "Efficient and
+// [r] P with one mixed addition per bit from EIGHT entries, small enough to stay in registers
+// (AGPRs at one wave per SIMD) and be read by selects, so no per-lane indexed table in scratch.
+// (Round 4's table of all fifteen digit-bit sums was indexed per lane and lived in scratch:
+// 3 KB/lane; it is gone.)  Sign-aligned recoding (Faz-Hernandez, Longa, Sanchez, "Efficient and
 // secure algorithms for GLV-based scalar multiplication", 2014, Alg. 1) of the digit vector
 // (k0, d1, d2, d3), k0 odd: l = nbits + 1 columns with
 //     k0 = sum_i s_i 2^i,  s_{l-1} = 1,  s_i = 2 bit_{i+1}(k0) - 1 in {+-1};
@@ -738,7 +595,9 @@ HD void xadic_mul_tab16(Jac<F>& r, const Aff<F>& p, const Jac<F>& xpj, const Fq&
 // column adds +-one entry (the sign is a y negation), none is empty, the first one starts the sum.
 // k0 = d0 | 1; an even d0 is corrected by one final addition of -P (11 Fq products of ~2,500).
 // The entries are the co-Z sums U + m(V), U in {P, S = P + XP}, V in {P, XP, S} (6 co-Z
-// additions instead of 9) brought to one Z* as in xadic_table16.
+// additions) brought to one Z*: no inversion, since points sharing one Z are affine points of the
+// isomorphic curve y^2 = x^3 + b Z*^6 and the a = 0 doubling / mixed-addition formulas do not
+// involve b; the double-and-add runs there and the result's Z is multiplied by Z* at the end.
 // Exceptional cases: none.  Before column i is added the running sum is [c] of a combination whose
 // P coefficient is 2 * (an odd integer) and whose other coefficients are below 2^(nbits+2) < |x|,
 // the entry's P coefficient is +-1, and such integer combinations of {1, x, mu, mu x} are distinct

@@ -1206,16 +1206,27 @@ int combine_dev(hbtc_ctx* c, int group, uint32_t n_inst, const uint32_t* offsets
   HB_CHECK(c, launch_zero_u32(sc, d_dup, n_inst));
   HB_CHECK(c, launch_zero_u32(sc, d_bad, n_inst));
   LagrangeFact lf{};
-  if (c->lagrange_fact) {
-    if (!c->fact) {  // once per context: 0! .. FACT_N! and their inverses (then every stream may read them)
-      Fr* part;
-      HB_CHECK(c, hipMalloc(&c->fact, sizeof(Fr) * (FACT_N + 1)));
-      HB_CHECK(c, hipMalloc(&c->inv_fact, sizeof(Fr) * (FACT_N + 1)));
-      HB_CHECK(c, hipMalloc(&part, sizeof(Fr) * (FACT_N / 256 + 1)));
-      HB_CHECK(c, launch_fact_tables(sc, FACT_N, part, c->fact, c->inv_fact));
-      HB_CHECK(c, hipStreamSynchronize(sc));
-      HB_CHECK(c, hipFree(part));
+  if (c->lagrange_fact && !c->fact) {
+    // once per context: 0! .. FACT_N! and their inverses, then every stream may read them.  One
+    // allocation holds both tables and the build's partial products (nothing is freed in the
+    // middle of the pipeline: hipFree synchronises the device), and the tables are published
+    // only once built; if any step fails the context keeps the O(t) coefficients instead
+    // (a half-built table would give wrong coefficients under an ACCEPT status).
+    const size_t n = FACT_N + 1;
+    Fr* tab = nullptr;
+    hipError_t e = hipMalloc(&tab, sizeof(Fr) * (2 * n + FACT_N / 256 + 1));
+    if (e == hipSuccess) e = launch_fact_tables(sc, FACT_N, tab + 2 * n, tab, tab + n);
+    if (e == hipSuccess) e = hipStreamSynchronize(sc);
+    if (e == hipSuccess) {
+      c->fact = tab;
+      c->inv_fact = tab + n;
+    } else {
+      if (tab) (void)hipFree(tab);
+      c->lagrange_fact = false;
+      HB_CHECK(c, e);
     }
+  }
+  if (c->lagrange_fact) {
     uint32_t* d_done;
     HB_TRY(wst(c, "comb.fact_done", n_inst, &d_done));
     lf = LagrangeFact{c->fact, c->inv_fact, FACT_N, d_sel_cnt, d_done};
@@ -1540,8 +1551,7 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
     if (kv.second.p) (void)hipFree(kv.second.p);
   (void)retire_fence(c);
   (void)reap_retired(c, true);
-  if (c->fact) (void)hipFree(c->fact);
-  if (c->inv_fact) (void)hipFree(c->inv_fact);
+  if (c->fact) (void)hipFree(c->fact);  // inv_fact lives in the same allocation
   for (auto& kv : c->keysets) {
     (void)hipFree(kv.second.pk);
     (void)hipFree(kv.second.st);
@@ -1676,18 +1686,21 @@ int hbtc_keyset_set_master(hbtc_ctx* c, uint32_t keyset_id, const uint8_t* mpk) 
     ks->master = nullptr;
   }
   G1A* d_m;
-  int32_t* d_st;
   HB_CHECK(c, hipMalloc(&d_m, sizeof(G1A)));
-  void* d_in;
-  HB_TRY(upload(c, "in0", mpk, 48, &d_in));
-  HB_TRY(wst(c, "out0", 1, &d_st));
-  HB_CHECK(c, launch_g1_decode(c->stream, (const uint8_t*)d_in, 1, d_m, d_st));
   int32_t st = -1;
-  HB_TRY(download(c, &st, d_st, 4));
-  HB_TRY(sync(c));
-  if (st != HBTC_ACCEPT) {
+  // every step after the allocation frees d_m on failure (the error paths leaked it)
+  const int rc = [&]() -> int {
+    int32_t* d_st;
+    void* d_in;
+    HB_TRY(upload(c, "in0", mpk, 48, &d_in));
+    HB_TRY(wst(c, "out0", 1, &d_st));
+    HB_CHECK(c, launch_g1_decode(c->stream, (const uint8_t*)d_in, 1, d_m, d_st));
+    HB_TRY(download(c, &st, d_st, 4));
+    return sync(c);
+  }();
+  if (rc != HBTC_OK || st != HBTC_ACCEPT) {
     (void)hipFree(d_m);
-    return fail(c, HBTC_ERR_ARG, "master public key fails to decode");
+    return rc != HBTC_OK ? rc : fail(c, HBTC_ERR_ARG, "master public key fails to decode");
   }
   ks->master = d_m;
   return HBTC_OK;
@@ -1924,8 +1937,9 @@ int pb_exact_list(hbtc_ctx* c, uint32_t m, const uint8_t* a, const uint8_t* q, c
   return HBTC_OK;
 }
 
-// e(A_i, Q_i) == e(G1, W_i) for n items in device memory (A null: the G1 generator; Q trusted:
-// our own hash output, decoded without the subgroup check; statuses ACCEPT / REJECT /
+// e(A_i, Q_i) == e(G1, W_i) for n items in device memory (A required: every caller passes its
+// G1 arguments, and the exact fallbacks gather them; Q trusted: our own hash output, decoded
+// without the subgroup check; statuses ACCEPT / REJECT /
 // DECODE_ERR).  RLC mode: the pair-batch path of hbtc_pb.hip in chunks of
 // c->pb_chunk items (the per-item line tables are 19.6 KB each): item pass, Q line tables,
 // partial Miller products per 8-item sub-tile, the 64-item tile checks, the 8-item sub-tiles of
@@ -1933,6 +1947,7 @@ int pb_exact_list(hbtc_ctx* c, uint32_t m, const uint8_t* a, const uint8_t* q, c
 // fresh RLC key per chunk.  Per-share mode and small calls: the exact checks for every item.
 int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_q, bool q_trusted,
                   const uint8_t* d_w, int32_t* d_status, G1A* d_adec = nullptr) {
+  if (n && !d_a) return fail(c, HBTC_ERR_ARG, "pair checks need their G1 arguments");
   if (c->verify_mode == HBTC_MODE_PER_SHARE || n < c->exact_below)
     return pb_small_exact(c, n, d_a, d_q, d_w, d_status, d_adec);
   const uint32_t PB_CHUNK = c->pb_chunk;
@@ -1954,7 +1969,7 @@ int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_
     HB_TRY(wst(c, "pb.counters", 2, &counters));
     HB_TRY(wst(c, "pb.tlist", T, &tlist));
     HB_TRY(wst(c, "pb.leaves", m, &leaves));
-    const uint8_t* a = d_a ? d_a + (size_t)48 * base : nullptr;
+    const uint8_t* a = d_a + (size_t)48 * base;
     const uint8_t* q = d_q + (size_t)96 * base;
     const uint8_t* w = d_w + (size_t)96 * base;
     int32_t* st = d_status + base;

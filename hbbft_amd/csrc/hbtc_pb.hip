@@ -75,8 +75,6 @@ __global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n
         G1J t;
 #if HBTC_XADIC8
         xadic_mul_sac8(t, A, t1, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
-#elif HBTC_XADIC16
-        xadic_mul_tab16(t, A, t1, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
 #else
         G1A xp, pxp;
         xadic_table(xp, pxp, A, t1);
@@ -100,7 +98,7 @@ __global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n
         jac_from_aff(xj, xp);
         Fq zeta;
         fq_set(zeta, G2_ZETA);
-        G2A pxp;  // the two-addition loop: the G2 table's scratch (curve.h HBTC_XADIC16_G2)
+        G2A pxp;  // the two-addition loop (the 8-entry table is 384 dwords per lane on G2)
         xadic_table(xp, pxp, W, xj);
         xadic_mul_uniform(S, W, xp, pxp, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
       }

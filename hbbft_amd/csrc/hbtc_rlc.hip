@@ -184,8 +184,6 @@ __global__ void __launch_bounds__(64, HBTC_ITEMS_WAVES) k_rlc_items(
 #else
             xadic_mul_sac8(S, d, t1, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
 #endif
-#elif HBTC_XADIC16
-            xadic_mul_tab16(S, d, t1, beta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
 #else
             G1A xp, pxp;
             xadic_table(xp, pxp, d, t1);

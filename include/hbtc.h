@@ -117,7 +117,11 @@ int hbtc_keyset_set_master(hbtc_ctx* ctx, uint32_t keyset_id, const uint8_t* mas
  * The master check is exact without a pairing: every combined share passed e(pk_i, H) ==
  * e(G1, sig_i), so e(G1, sum l_i sig_i) == e(sum l_i pk_i, H), and PublicKey::verify holds iff
  * sum l_i pk_i == master pk in G1 (H != O, e non-degenerate) -- a G1 combine of the key set's
- * resident shares.  Small calls (n_inst * (t + 1) <= 256, t < 64) combine speculatively while the
+ * resident shares.  So the master check is exactly as sound as the share checks under it: exact
+ * in HBTC_MODE_PER_SHARE and for calls below hbtc_set_exact_below (256 shares: every coin of up
+ * to N = 255), and otherwise wrong with probability <= 2^-k per RLC group for k-bit scalars
+ * (hbtc_set_rlc_bits: 2^-128 by default, the curve's level; 2^-64 when set to 64), where the
+ * reference's separate pairing check (coin.rs:192-197) would be exact.  Small calls (n_inst * (t + 1) <= 256, t < 64) combine speculatively while the
  * shares are checked: every leave-one-out subset of each instance's first t + 1 items, committed
  * when the verified selection is one of them (at most one of the first t + 1 rejected), else
  * combined again from the statuses.  Needs hbtc_keyset_set_master; t in 1..64. */

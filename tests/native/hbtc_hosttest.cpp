@@ -195,44 +195,6 @@ int ht_g2_mul_xadic_lds(const uint8_t* in96, const uint32_t* d, int nbits, uint8
   store_words(out96, w, 24);
   return 0;
 }
-// the one-addition-per-bit form (curve.h xadic_mul_tab16) of the same scalar
-int ht_g1_mul_xadic16(const uint8_t* in48, const uint32_t* d, int nbits, uint8_t* out48) {
-  uint32_t w[12];
-  load_words(w, in48, 12);
-  G1A p;
-  G1J t1;
-  if (!g1_decompress_t1(p, t1, w)) return -1;
-  jac_neg(t1, t1);
-  Fq beta;
-  fq_set(beta, G1_BETA);
-  G1J r;
-  xadic_mul_tab16(r, p, t1, beta, d[0], d[1], d[2], d[3], nbits);
-  G1A o;
-  jac_to_aff(o, r);
-  g1_compress(w, o);
-  store_words(out48, w, 12);
-  return 0;
-}
-int ht_g2_mul_xadic16(const uint8_t* in96, const uint32_t* d, int nbits, uint8_t* out96) {
-  uint32_t w[24];
-  load_words(w, in96, 24);
-  G2A p;
-  if (!g2_decompress(p, w)) return -1;
-  G2A xp;
-  g2_psi(xp.x, xp.y, p);
-  xp.inf = 0;
-  G2J xj;
-  jac_from_aff(xj, xp);
-  Fq zeta;
-  fq_set(zeta, G2_ZETA);
-  G2J r;
-  xadic_mul_tab16(r, p, xj, zeta, d[0], d[1], d[2], d[3], nbits);
-  G2A o;
-  jac_to_aff(o, r);
-  g2_compress(w, o);
-  store_words(out96, w, 24);
-  return 0;
-}
 // the sign-aligned 8-entry form (curve.h xadic_mul_sac8) of the same scalar
 int ht_g1_mul_xadic8(const uint8_t* in48, const uint32_t* d, int nbits, uint8_t* out48) {
   uint32_t w[12];

@@ -164,3 +164,69 @@ def test_coin_decide_needs_master(ctx):
     finally:
         ctx.keyset_free(ks)
     assert np.int32(N.ACCEPT) == 0
+
+
+def _golden_c1_instances(c):
+    """hbtc_coin_decide instances built from the C1 coin fixture (tests/golden/c1_coin.json, the
+    threshold_crypto restatement's vectors): per instance the items, and the expected item
+    statuses, coin status, combined signature and parity."""
+    it = {i["name"]: i for i in c["items"]}
+    comb = {x["name"]: x for x in c["combines"]}
+    rejects = [n for n in it if it[n]["expected"] != "ACCEPT"]
+    insts = [
+        # every fixture item in fixture order: the first t ACCEPTed are nodes 0..3
+        ("all", list(it), "ACCEPT", comb["first_t"]),
+        # every rejected / undecodable item first, then nodes 6..9: the combine skips them all
+        ("rejects_then_last_t", rejects + ["valid_%d" % i for i in range(6, 10)], "ACCEPT", comb["last_t"]),
+        # a wrong share in the middle of the first t + 1 (the speculation's leave-one-out subset)
+        ("one_wrong_first", ["valid_0", "valid_1", "wrong_message", "valid_2", "valid_3", "valid_4"],
+         "ACCEPT", comb["first_t"]),
+        ("not_enough", ["valid_0", "wrong_key", "valid_1", "identity", "valid_2", "enc_not_in_subgroup"],
+         "NOT_ENOUGH_SHARES", comb["not_enough"]),
+        ("duplicate", ["valid_0", "valid_0", "valid_1", "valid_2", "valid_3"], "DUPLICATE_ENTRY",
+         comb["duplicate"]),
+    ]
+    return it, insts
+
+
+def test_coin_decide_golden_c1():
+    """hbtc_coin_decide against the C1 coin fixture: item statuses, the coin status, the combined
+    signature's bytes and its parity bit equal the threshold_crypto restatement's vectors
+    (coin.rs:151 / :185-191 / :173 / :192-197), with the speculation on and off."""
+    c = json.load(open(os.path.join(HERE, "golden", "c1_coin.json")))
+    assert c["master_verify"] is True
+    b = bytes.fromhex
+    it, insts = _golden_c1_instances(c)
+    counts = [len(names) for _, names, _, _ in insts]
+    idx = [it[n]["idx"] for _, names, _, _ in insts for n in names]
+    sigs = [b(it[n]["sig"]) for _, names, _, _ in insts for n in names]
+    H = [b(c["H"])] * len(insts)
+    want_st = [it[n]["expected"] for _, names, _, _ in insts for n in names]
+    for spec in ("1", "0"):
+        old = os.environ.get("HBTC_COIN_SPEC")
+        os.environ["HBTC_COIN_SPEC"] = spec
+        try:
+            cx = N.Context(0)
+            try:
+                ks, nbad = cx.keyset_load([b(p) for p in c["pk_shares"]])
+                assert nbad == 0
+                cx.keyset_set_master(ks, b(c["master_pk"]))
+                st, out, par, cst = cx.coin_decide(ks, H, counts, idx, sigs, c["t"])
+                # the single-coin form hbbft calls once per coin (c1: one instance per call)
+                one = cx.coin_decide(ks, H[:1], counts[:1], idx[:counts[0]], sigs[:counts[0]], c["t"])
+            finally:
+                cx.close()
+        finally:
+            if old is None:
+                os.environ.pop("HBTC_COIN_SPEC", None)
+            else:
+                os.environ["HBTC_COIN_SPEC"] = old
+        assert [N.STATUS_NAMES[int(s)] for s in st] == want_st, spec
+        for k, (name, _, want_coin, cmb) in enumerate(insts):
+            assert N.STATUS_NAMES[int(cst[k])] == want_coin == cmb["expected"], (spec, name)
+            if want_coin == "ACCEPT":
+                assert out[k].hex() == cmb["sig"], (spec, name)
+                assert int(par[k]) == cmb["parity"], (spec, name)
+        assert [N.STATUS_NAMES[int(s)] for s in one[0]] == want_st[:counts[0]], spec
+        assert one[1][0].hex() == insts[0][3]["sig"] and int(one[2][0]) == insts[0][3]["parity"], spec
+        assert int(one[3][0]) == N.ACCEPT, spec

@@ -37,7 +37,7 @@ def test_c3_full_epoch_against_construction(ctx):
     mism, comb_ok, n_acc = ep.check(ctx)
     assert mism == 0 and comb_ok
     assert n_acc == int((ep.expected == N.ACCEPT).sum()) >= 1000 * 1000 - 10 * 1000 - 8
-    # the group sums themselves are right (curve.h xadic_mul_tab16 in k_rlc_items): only the
+    # the group sums themselves are right (curve.h xadic_mul_sac8 in k_rlc_items): only the
     # tiles holding wrong shares fall back, about 2.3 k exact checks, not every share
     assert ctx.rlc_last_leaves() < 10000, ctx.rlc_last_leaves()
     # a second epoch through the same buffers (pipelined: combine k overlaps verification k+1)
@@ -109,8 +109,8 @@ def test_c4_full_64_instances_single_context_and_node(ctx):
     bench_configs.ctx_mode[0] = N.MODE_RLC
     a = bench_configs.bench_coins(ctx, "c4", 10000, 64, 1, 0, 0.01, keep_arrays=True)
     assert a["mismatches"] == 0 and a["combine_ok"]
-    # 10^4 tiles: the throughput form of k_sig_items (the 15-entry G2 table, on the exact stream);
-    # its group sums are right, so only tiles holding wrong shares reach exact checks
+    # 10^4 tiles: the throughput form of k_sig_items (the two-addition x-adic loop, its table in
+    # LDS); its group sums are right, so only tiles holding wrong shares reach exact checks
     assert ctx.rlc_last_leaves() < 64000, ctx.rlc_last_leaves()
     assert a["config"]["instances"] == 64 and a["config"]["t"] == 3334
     node = N.Node([0, 0])

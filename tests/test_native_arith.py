@@ -92,8 +92,6 @@ def test_xadic_scalar_of_rlc_items(ht, nbits):
     cases += [tuple(rng.getrandbits(nbits) for _ in range(4)) for _ in range(4)]
     ht.ht_g1_mul_xadic.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
     ht.ht_g2_mul_xadic.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
-    ht.ht_g1_mul_xadic16.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
-    ht.ht_g2_mul_xadic16.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
     ht.ht_g1_mul_xadic8.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
     ht.ht_g2_mul_xadic8.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
     ht.ht_g2_mul_xadic_lds.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]
@@ -114,11 +112,6 @@ def test_xadic_scalar_of_rlc_items(ht, nbits):
         # k_sig_items' form: the same loop over the table in an LDS-layout buffer
         assert ht.ht_g2_mul_xadic_lds(B.g2_compress(Q), ctypes.cast(arr, ctypes.c_void_p), nbits, o2) == 0
         assert o2.raw == B.g2_compress(B.g2_mul(Q, r)), ("g2 lds", d)
-        # the one-addition-per-bit form (curve.h xadic_mul_tab16: 15-entry common-Z table)
-        assert ht.ht_g1_mul_xadic16(B.g1_compress(P), ctypes.cast(arr, ctypes.c_void_p), nbits, o) == 0
-        assert o.raw == B.g1_compress(B.g1_mul(P, r)), ("g1 tab16", d)
-        assert ht.ht_g2_mul_xadic16(B.g2_compress(Q), ctypes.cast(arr, ctypes.c_void_p), nbits, o2) == 0
-        assert o2.raw == B.g2_compress(B.g2_mul(Q, r)), ("g2 tab16", d)
         # the sign-aligned 8-entry form (curve.h xadic_mul_sac8), even d0 included
         assert ht.ht_g1_mul_xadic8(B.g1_compress(P), ctypes.cast(arr, ctypes.c_void_p), nbits, o) == 0
         assert o.raw == B.g1_compress(B.g1_mul(P, r)), ("g1 sac8", d)

@@ -147,8 +147,6 @@ int main() {
     // k_rlc_items' form: the co-Z chain table build, three entries in LDS (xadic_table8_chain)
     static uint32_t lds[3 * 24 * 64];
     xadic_mul_sac8<Fq, true>(rd, d2, t1, beta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb, lds, 0);
-#elif HBTC_XADIC16
-    xadic_mul_tab16(rd, d2, t1, beta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
 #else
     G1A xp, pxp;
     xadic_table(xp, pxp, d2, t1);
@@ -164,12 +162,10 @@ int main() {
     }
     (nb == 16 ? rlc_item : rlc_item_128) = hbtc_fqm_count + tree1;
   }
-  // SignatureShare RLC item (k_sig_items): G2 decode + subgroup test, r*sigma by
-  // xadic_mul_tab16 in G2 ([x] s = psi(s)) (m = -psi^2 = (zeta x, y)), r*pk
-  // from the fixed-base table, and the item's share of the G2 and G1 plain + weighted tile trees
-  // both forms: the throughput kernel's 15-entry table (t16) and the small-call two-addition loop
-  unsigned long long sig_item[2][2] = {};  // [t16][nb == 32]
-  for (int t16 : {0})
+  // SignatureShare RLC item (k_sig_items): G2 decode + subgroup test, r*sigma by the
+  // two-addition x-adic loop in G2 ([x] s = psi(s), m = -psi^2 = (zeta x, y)), r*pk from the
+  // fixed-base table, and the item's share of the G2 and G1 plain + weighted tile trees
+  unsigned long long sig_item[2] = {};  // [nb == 32]
   for (int nb : {16, 32}) {
     hbtc_fqm_count = 0;
     G2A s2;
@@ -183,13 +179,9 @@ int main() {
     fq_set(zeta, G2_ZETA);
     const uint32_t m = nb == 32 ? 0xffffffffu : 0xffffu;
     G2J r2;
-    if (t16) {
-      xadic_mul_tab16(r2, s2, xj, zeta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
-    } else {
-      G2A pxp;
-      xadic_table(xp, pxp, s2, xj);
-      xadic_mul_uniform(r2, s2, xp, pxp, zeta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
-    }
+    G2A pxp;
+    xadic_table(xp, pxp, s2, xj);
+    xadic_mul_uniform(r2, s2, xp, pxp, zeta, dg[0] & m, dg[1] & m, dg[2] & m, dg[3] & m, nb);
     G1J rp;
     jac_set_inf(rp);
     jac_add_aff(rp, rp, gen1);
@@ -206,7 +198,7 @@ int main() {
     hbtc_fqm_count = 0;
     jac_dbl(t2, t2);
     const unsigned long long jdbl2 = hbtc_fqm_count;
-    sig_item[t16][nb == 32] =
+    sig_item[nb == 32] =
         mults + (2 * (189 * jadd2 + 57 * jdbl2) / 2 + 2 * (189 * jadd + 57 * jdbl) / 2 + 63) / 64;
   }
   G1J rp = rd;
@@ -279,6 +271,6 @@ int main() {
   // k_sig_items runs the two-addition loop only since round 5 (the G2 table is gone)
   printf("  \"rlc_item\": %llu,\n  \"rlc_item_128\": %llu,\n  \"sig_rlc_item\": %llu,\n"
          "  \"sig_rlc_item_128\": %llu,\n  \"rlc_group_check\": %llu\n}\n", rlc_item,
-         rlc_item_128, sig_item[0][0], sig_item[0][1], rlc_group);
+         rlc_item_128, sig_item[0], sig_item[1], rlc_group);
   return 0;
 }

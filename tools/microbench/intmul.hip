@@ -1,137 +1,226 @@
-// Integer-multiply throughput microbenchmark for gfx950 (MI355X).
-// Decides the Fq limb scheme (SURVEY.md §7 "Hard parts"): measures per-instruction
-// throughput of the candidate 32x32 / 24x24 multiply forms and the carry adds.
+// VALU issue-rate microbenchmark for gfx950 (MI355X): the denominator of every roofline `frac`
+// in this repository.  Round 6 rewrite (VERDICT r05 "Weak 3"): the round-1
+// harness read v_fma_f32 at 46.4 T lane-ops/s against the 78.6 T of the 157.3 TFLOP/s FP32 spec,
+// so its v_mad_u64_u32 figure could not be trusted as a peak.  This version
+//   * measures the in-kernel shader clock (s_memtime ticks / s_memrealtime at 100 MHz, median
+//     over workgroups) beside the wall time, so a low figure from DVFS is told apart from a
+//     harness that does not saturate the issue;
+//   * reports CYCLES PER WAVE-INSTRUCTION PER SIMD, the hardware's issue cost, and the peak that
+//     issue cost gives at the 2.4 GHz spec clock (the figure a roofline should divide by);
+//   * sweeps waves per SIMD and operand forms (every source a VGPR vs one source an SGPR: a VGPR
+//     operand read from the same register bank as another costs an extra cycle), so the best
+//     form of each instruction is found rather than assumed.
+// Build: hipcc --offload-arch=gfx950 -O3 tools/microbench/intmul.hip -o tools/microbench/intmul
 #include <hip/hip_runtime.h>
-#include <cstdio>
+#include <algorithm>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
 
-constexpr int NACC = 8;
-constexpr int INNER = 64;
+constexpr int NACC = 8;    // independent accumulation chains per lane
+constexpr int INNER = 32;  // unrolled groups of NACC instructions per loop trip
 
-__global__ void __launch_bounds__(256) k_mad_u64(uint64_t* out, uint32_t seed, int iters) {
-  uint32_t a = threadIdx.x * 2654435761u + seed, b = seed ^ 0x9e3779b9u;
+// one timing record per workgroup: shader-clock ticks and 100 MHz real-time ticks over the loop
+struct Stamp { uint64_t t0, t1, r0, r1; };
+
+__device__ __forceinline__ uint64_t clk() { return __builtin_amdgcn_s_memtime(); }
+__device__ __forceinline__ uint64_t rclk() { return __builtin_amdgcn_s_memrealtime(); }
+
+#define STAMP_BEGIN                                                   \
+  uint64_t t0_ = 0, r0_ = 0;                                          \
+  __syncthreads();                                                    \
+  if (threadIdx.x == 0) { t0_ = clk(); r0_ = rclk(); }
+#define STAMP_END                                                     \
+  __syncthreads();                                                    \
+  if (threadIdx.x == 0) {                                             \
+    uint64_t t1_ = clk(), r1_ = rclk();                               \
+    st[blockIdx.x] = Stamp{t0_, t1_, r0_, r1_};                       \
+  }
+
+// 32-bit accumulators, two-operand forms "INSN acc, acc, b"
+#define K_U32(NAME, BODY, BCONS)                                                       \
+  __global__ void __launch_bounds__(256) NAME(uint64_t* out, Stamp* st, uint32_t seed, int iters) { \
+    uint32_t a = threadIdx.x * 2654435761u + seed, b = seed ^ 0x9e3779b9u;            \
+    uint32_t acc[NACC];                                                               \
+    for (int j = 0; j < NACC; ++j) acc[j] = a + j;                                    \
+    STAMP_BEGIN                                                                       \
+    for (int i = 0; i < iters; ++i) {                                                 \
+      _Pragma("unroll") for (int u = 0; u < INNER; ++u)                               \
+      _Pragma("unroll") for (int j = 0; j < NACC; ++j)                                \
+        asm volatile(BODY : "+v"(acc[j]) : BCONS(b), "v"(a));                         \
+    }                                                                                 \
+    STAMP_END                                                                         \
+    uint64_t s = 0; for (int j = 0; j < NACC; ++j) s ^= acc[j];                       \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                   \
+  }
+#define VCONS(x) "v"(x)
+#define SCONS(x) "s"(x)
+
+K_U32(k_add_u32_vv, "v_add_u32 %0, %0, %1", VCONS)
+K_U32(k_mul_lo_vv, "v_mul_lo_u32 %0, %0, %1", VCONS)
+K_U32(k_mul_hi_vv, "v_mul_hi_u32 %0, %0, %1", VCONS)
+K_U32(k_mul_lo_vs, "v_mul_lo_u32 %0, %0, %1", SCONS)
+K_U32(k_mul_hi_vs, "v_mul_hi_u32 %0, %0, %1", SCONS)
+K_U32(k_mad_u24_vv, "v_mad_u32_u24 %0, %2, %1, %0", VCONS)
+
+// v_mad_u64_u32 acc64 = a * b + acc64 (the Fq product's instruction); carry-out to an SGPR pair
+#define K_MAD64(NAME, BCONS)                                                           \
+  __global__ void __launch_bounds__(256) NAME(uint64_t* out, Stamp* st, uint32_t seed, int iters) { \
+    uint32_t a = threadIdx.x * 2654435761u + seed, b = seed ^ 0x9e3779b9u;            \
+    uint64_t acc[NACC];                                                               \
+    for (int j = 0; j < NACC; ++j) acc[j] = a + j;                                    \
+    STAMP_BEGIN                                                                       \
+    for (int i = 0; i < iters; ++i) {                                                 \
+      _Pragma("unroll") for (int u = 0; u < INNER; ++u)                               \
+      _Pragma("unroll") for (int j = 0; j < NACC; ++j) {                              \
+        uint64_t sc;                                                                  \
+        asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0"                               \
+                     : "+v"(acc[j]), "=&s"(sc) : "v"(a), BCONS(b));                    \
+      }                                                                               \
+    }                                                                                 \
+    STAMP_END                                                                         \
+    uint64_t s = 0; for (int j = 0; j < NACC; ++j) s ^= acc[j];                       \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                   \
+  }
+K_MAD64(k_mad64_vv, VCONS)
+K_MAD64(k_mad64_vs, SCONS)
+
+// v_mad_u64_u32 with the a operand varying per chain (a product column: every MAD reads a
+// different limb of a, the same limb of b)
+__global__ void __launch_bounds__(256) k_mad64_col(uint64_t* out, Stamp* st, uint32_t seed, int iters) {
+  uint32_t b = seed ^ 0x9e3779b9u;
+  uint32_t a[NACC];
   uint64_t acc[NACC];
-  for (int j = 0; j < NACC; ++j) acc[j] = a + j;
+  for (int j = 0; j < NACC; ++j) { a[j] = threadIdx.x * 2654435761u + seed + 77u * j; acc[j] = a[j] + j; }
+  STAMP_BEGIN
   for (int i = 0; i < iters; ++i) {
 #pragma unroll
     for (int u = 0; u < INNER; ++u)
 #pragma unroll
       for (int j = 0; j < NACC; ++j) {
         uint64_t sc;
-        asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc[j]), "=s"(sc) : "v"(a), "v"(b));
+        asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc[j]), "=&s"(sc) : "v"(a[(j + u) % NACC]), "v"(b));
       }
   }
+  STAMP_END
   uint64_t s = 0; for (int j = 0; j < NACC; ++j) s ^= acc[j];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
-#define K_U32(NAME, INSN)                                                              \
-  __global__ void __launch_bounds__(256) NAME(uint64_t* out, uint32_t seed, int iters) { \
-    uint32_t a = threadIdx.x * 2654435761u + seed, b = seed ^ 0x9e3779b9u;            \
-    uint32_t acc[NACC];                                                               \
+// add-with-carry pair (the carry chains of the field additions)
+__global__ void __launch_bounds__(256) k_addc_pair(uint64_t* out, Stamp* st, uint32_t seed, int iters) {
+  uint32_t b = seed ^ 0x9e3779b9u;
+  uint32_t lo[NACC], hi[NACC];
+  for (int j = 0; j < NACC; ++j) { lo[j] = threadIdx.x + j; hi[j] = seed + j; }
+  STAMP_BEGIN
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int u = 0; u < INNER / 2; ++u)
+#pragma unroll
+      for (int j = 0; j < NACC; ++j)
+        asm volatile("v_add_co_u32 %0, vcc, %0, %2\n\tv_addc_co_u32 %1, vcc, %1, %2, vcc"
+                     : "+v"(lo[j]), "+v"(hi[j]) : "v"(b) : "vcc");
+  }
+  STAMP_END
+  uint64_t s = 0; for (int j = 0; j < NACC; ++j) s ^= lo[j] ^ ((uint64_t)hi[j] << 32);
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+#define K_F32(NAME, BODY, CCONS)                                                       \
+  __global__ void __launch_bounds__(256) NAME(uint64_t* out, Stamp* st, uint32_t seed, int iters) { \
+    float a = 1.0000001f + threadIdx.x * 1e-9f, c = 0.9999999f + seed * 1e-12f;       \
+    float acc[NACC];                                                                  \
     for (int j = 0; j < NACC; ++j) acc[j] = a + j;                                    \
+    STAMP_BEGIN                                                                       \
     for (int i = 0; i < iters; ++i) {                                                 \
       _Pragma("unroll") for (int u = 0; u < INNER; ++u)                               \
       _Pragma("unroll") for (int j = 0; j < NACC; ++j)                                \
-        asm volatile(INSN " %0, %0, %1" : "+v"(acc[j]) : "v"(b));                     \
+        asm volatile(BODY : "+v"(acc[j]) : "v"(a), CCONS(c));                         \
     }                                                                                 \
-    uint64_t s = 0; for (int j = 0; j < NACC; ++j) s ^= acc[j];                       \
-    out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                   \
+    STAMP_END                                                                         \
+    float s = 0; for (int j = 0; j < NACC; ++j) s += acc[j];                          \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)s;                         \
   }
+K_F32(k_fma_f32_vv, "v_fma_f32 %0, %0, %1, %2", VCONS)
+K_F32(k_fma_f32_vs, "v_fma_f32 %0, %0, %1, %2", SCONS)
+K_F32(k_fmac_f32, "v_fmac_f32 %0, %1, %2", VCONS)
 
-K_U32(k_mul_lo, "v_mul_lo_u32")
-K_U32(k_mul_hi, "v_mul_hi_u32")
-K_U32(k_mul_u24, "v_mul_u32_u24")
-K_U32(k_mul_hi_u24, "v_mul_hi_u32_u24")
-K_U32(k_add_u32, "v_add_u32")
-
-__global__ void __launch_bounds__(256) k_mad_u24(uint64_t* out, uint32_t seed, int iters) {
-  uint32_t a = threadIdx.x * 2654435761u + seed, b = seed ^ 0x9e3779b9u;
-  uint32_t acc[NACC];
-  for (int j = 0; j < NACC; ++j) acc[j] = a + j;
+// packed f32: two FMAs per lane per instruction
+__global__ void __launch_bounds__(256) k_pk_fma_f32(uint64_t* out, Stamp* st, uint32_t seed, int iters) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 a = {1.0000001f + threadIdx.x * 1e-9f, 1.0000002f}, c = {0.9999999f + seed * 1e-12f, 0.9999998f};
+  f2 acc[NACC];
+  for (int j = 0; j < NACC; ++j) acc[j] = a + (float)j;
+  STAMP_BEGIN
   for (int i = 0; i < iters; ++i) {
 #pragma unroll
     for (int u = 0; u < INNER; ++u)
 #pragma unroll
       for (int j = 0; j < NACC; ++j)
-        asm volatile("v_mad_u32_u24 %0, %1, %2, %0" : "+v"(acc[j]) : "v"(a), "v"(b));
+        asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(acc[j]) : "v"(a), "v"(c));
   }
-  uint64_t s = 0; for (int j = 0; j < NACC; ++j) s ^= acc[j];
-  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
-}
-
-// add-with-carry chain: v_add_co_u32 + v_addc_co_u32 pairs (what a 64-bit add costs)
-__global__ void __launch_bounds__(256) k_addc(uint64_t* out, uint32_t seed, int iters) {
-  uint32_t a = threadIdx.x * 2654435761u + seed, b = seed ^ 0x9e3779b9u;
-  uint64_t acc[NACC];
-  for (int j = 0; j < NACC; ++j) acc[j] = a + j;
-  uint64_t bb = ((uint64_t)b << 32) | a;
-  for (int i = 0; i < iters; ++i) {
-#pragma unroll
-    for (int u = 0; u < INNER; ++u)
-#pragma unroll
-      for (int j = 0; j < NACC; ++j) {
-        asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(acc[j]) : "v"(bb));
-      }
-  }
-  uint64_t s = 0; for (int j = 0; j < NACC; ++j) s ^= acc[j];
-  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
-}
-
-__global__ void __launch_bounds__(256) k_fma_f64(uint64_t* out, uint32_t seed, int iters) {
-  double a = 1.0000001 + threadIdx.x * 1e-9, b = 0.9999999;
-  double acc[NACC];
-  for (int j = 0; j < NACC; ++j) acc[j] = a + j;
-  for (int i = 0; i < iters; ++i) {
-#pragma unroll
-    for (int u = 0; u < INNER; ++u)
-#pragma unroll
-      for (int j = 0; j < NACC; ++j)
-        asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(acc[j]) : "v"(a), "v"(b));
-  }
-  double s = 0; for (int j = 0; j < NACC; ++j) s += acc[j];
+  STAMP_END
+  float s = 0; for (int j = 0; j < NACC; ++j) s += acc[j].x + acc[j].y;
   out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)s;
 }
 
-__global__ void __launch_bounds__(256) k_fma_f32(uint64_t* out, uint32_t seed, int iters) {
-  float a = 1.0000001f + threadIdx.x * 1e-9f, b = 0.9999999f;
-  float acc[NACC];
-  for (int j = 0; j < NACC; ++j) acc[j] = a + j;
-  for (int i = 0; i < iters; ++i) {
-#pragma unroll
-    for (int u = 0; u < INNER; ++u)
-#pragma unroll
-      for (int j = 0; j < NACC; ++j)
-        asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(acc[j]) : "v"(a), "v"(b));
-  }
-  float s = 0; for (int j = 0; j < NACC; ++j) s += acc[j];
-  out[blockIdx.x * blockDim.x + threadIdx.x] = (uint64_t)s;
-}
+typedef void (*kfn)(uint64_t*, Stamp*, uint32_t, int);
 
-typedef void (*kfn)(uint64_t*, uint32_t, int);
+struct Variant { const char* name; kfn f; int lane_ops_per_insn; int insn_per_group; };
 
-int main() {
+int main(int argc, char** argv) {
   hipDeviceProp_t prop; CHK(hipGetDeviceProperties(&prop, 0));
-  printf("device %s CUs=%d clock=%d kHz\n", prop.gcnArchName, prop.multiProcessorCount, prop.clockRate);
-  const int blocks = prop.multiProcessorCount * 8, threads = 256, iters = 200;
-  uint64_t* d; CHK(hipMalloc(&d, sizeof(uint64_t) * blocks * threads));
-  struct { const char* name; kfn f; } ks[] = {
-    {"v_mad_u64_u32", k_mad_u64}, {"v_mul_lo_u32", k_mul_lo}, {"v_mul_hi_u32", k_mul_hi},
-    {"v_mul_u32_u24", k_mul_u24}, {"v_mul_hi_u32_u24", k_mul_hi_u24}, {"v_mad_u32_u24", k_mad_u24},
-    {"v_add_u32", k_add_u32}, {"v_lshl_add_u64", k_addc}, {"v_fma_f64", k_fma_f64}, {"v_fma_f32", k_fma_f32}};
+  const int cus = prop.multiProcessorCount;
+  const double spec_ghz = 2.4;
+  printf("device %s CUs=%d clockRate=%d kHz (spec clock for the peak column: %.1f GHz)\n",
+         prop.gcnArchName, cus, prop.clockRate, spec_ghz);
+  printf("%-16s %4s %9s %9s %7s %9s %10s\n", "instruction", "w/S", "ms", "Tlane/s", "GHz", "cyc/insn",
+         "peak@2.4");
+  Variant vs[] = {
+      {"v_fma_f32 vv", k_fma_f32_vv, 1, 1},   {"v_fma_f32 vs", k_fma_f32_vs, 1, 1},
+      {"v_fmac_f32", k_fmac_f32, 1, 1},       {"v_pk_fma_f32", k_pk_fma_f32, 2, 1},
+      {"v_add_u32", k_add_u32_vv, 1, 1},      {"v_mul_lo_u32 vv", k_mul_lo_vv, 1, 1},
+      {"v_mul_lo_u32 vs", k_mul_lo_vs, 1, 1}, {"v_mul_hi_u32 vv", k_mul_hi_vv, 1, 1},
+      {"v_mul_hi_u32 vs", k_mul_hi_vs, 1, 1}, {"v_mad_u32_u24", k_mad_u24_vv, 1, 1},
+      {"v_mad_u64_u32 vv", k_mad64_vv, 1, 1}, {"v_mad_u64_u32 vs", k_mad64_vs, 1, 1},
+      {"v_mad_u64 column", k_mad64_col, 1, 1}, {"v_add_co+addc", k_addc_pair, 1, 1}};
+  const int wps_list[] = {1, 2, 4, 8};
+  const int max_blocks = cus * 8;
+  uint64_t* d; CHK(hipMalloc(&d, sizeof(uint64_t) * max_blocks * 256));
+  Stamp* dst; CHK(hipMalloc(&dst, sizeof(Stamp) * max_blocks));
+  std::vector<Stamp> hst(max_blocks);
   hipEvent_t e0, e1; CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
-  for (auto& k : ks) {
-    hipLaunchKernelGGL(k.f, dim3(blocks), dim3(threads), 0, 0, d, 7u, iters);
-    CHK(hipDeviceSynchronize());
-    CHK(hipEventRecord(e0));
-    for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(k.f, dim3(blocks), dim3(threads), 0, 0, d, 7u + r, iters);
-    CHK(hipEventRecord(e1)); CHK(hipEventSynchronize(e1));
-    float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
-    double ops = 5.0 * blocks * threads * (double)iters * INNER * NACC;
-    printf("%-18s %8.3f ms  %8.2f Tops/s (lane-ops)\n", k.name, ms, ops / (ms * 1e-3) / 1e12);
+  for (auto& v : vs) {
+    for (int wps : wps_list) {
+      const int blocks = cus * wps;               // 256-thread blocks: one wave per SIMD each
+      const int iters = 6400 / wps;               // about the same wall time at every occupancy
+      hipLaunchKernelGGL(v.f, dim3(blocks), dim3(256), 0, 0, d, dst, 7u, iters / 8);
+      CHK(hipDeviceSynchronize());
+      const int reps = 3;
+      CHK(hipEventRecord(e0));
+      for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(v.f, dim3(blocks), dim3(256), 0, 0, d, dst, 7u + r, iters);
+      CHK(hipEventRecord(e1)); CHK(hipEventSynchronize(e1));
+      float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
+      CHK(hipMemcpy(hst.data(), dst, sizeof(Stamp) * blocks, hipMemcpyDeviceToHost));
+      std::vector<double> ghz(blocks);
+      for (int b = 0; b < blocks; ++b) {
+        const double ticks = (double)(hst[b].t1 - hst[b].t0), real_s = (double)(hst[b].r1 - hst[b].r0) / 100e6;
+        ghz[b] = real_s > 0 ? ticks / real_s / 1e9 : 0.0;
+      }
+      std::nth_element(ghz.begin(), ghz.begin() + blocks / 2, ghz.end());
+      const double clock = ghz[blocks / 2];
+      const double insns = (double)reps * blocks * 4 /*waves*/ * (double)iters * INNER * NACC;  // wave-instructions
+      const double lane_ops = insns * 64 * v.lane_ops_per_insn;
+      const double t = ms * 1e-3;
+      const double simds = cus * 4.0;
+      const double cyc = clock * 1e9 * t * simds / insns;   // cycles per wave-instruction per SIMD
+      const double peak = simds * 64.0 * v.lane_ops_per_insn / cyc * spec_ghz * 1e9;
+      printf("%-16s %4d %9.3f %9.2f %7.3f %9.3f %10.2f\n", v.name, wps, ms / reps, lane_ops / t / 1e12, clock, cyc,
+             peak / 1e12);
+    }
   }
   return 0;
 }
