@@ -218,6 +218,59 @@ HD void jac_add(Jac<F>& r, const Jac<F>& p, const Jac<F>& q) {
   r.z = z3;
 }
 
+// add-2007-bl in place, a += q, ordered so that at most four temporaries are live beside a and q
+// (the same formulas and special cases as jac_add; for register-tight kernels: the lane-pair G2
+// trees, pair.h)
+template <class F>
+HD void jac_add_lean(Jac<F>& a, const Jac<F>& q) {
+  if (jac_is_inf(q)) return;
+  if (jac_is_inf(a)) {
+    a = q;
+    return;
+  }
+  F z1z1, z2z2, h, rr;
+  fsqr(z1z1, a.z);
+  fsqr(z2z2, q.z);
+  fmul(a.x, a.x, z2z2);  // U1
+  fmul(h, q.x, z1z1);
+  fsub(h, h, a.x);       // H = U2 - U1
+  fmul(a.y, a.y, q.z);
+  fmul(a.y, a.y, z2z2);  // S1
+  fmul(rr, q.y, a.z);
+  fmul(rr, rr, z1z1);
+  fsub(rr, rr, a.y);     // S2 - S1
+  if (fis_zero(h)) {
+    if (fis_zero(rr)) {
+      jac_dbl(a, q);
+    } else {
+      jac_set_inf(a);
+    }
+    return;
+  }
+  fadd(a.z, a.z, q.z);
+  fsqr(a.z, a.z);
+  fsub(a.z, a.z, z1z1);
+  fsub(a.z, a.z, z2z2);
+  fmul(a.z, a.z, h);     // Z3
+  F i, j;
+  fdbl(i, h);
+  fsqr(i, i);            // I = (2H)^2
+  fmul(j, h, i);         // J = H I
+  fmul(i, a.x, i);       // V = U1 I
+  fdbl(rr, rr);          // r
+  F x3;
+  fsqr(x3, rr);
+  fsub(x3, x3, j);
+  fsub(x3, x3, i);
+  fsub(x3, x3, i);       // X3 = r^2 - J - 2 V
+  fsub(i, i, x3);
+  fmul(i, rr, i);        // r (V - X3)
+  fmul(j, a.y, j);
+  fdbl(j, j);            // 2 S1 J
+  fsub(a.y, i, j);
+  a.x = x3;
+}
+
 template <class F>
 HD void jac_neg(Jac<F>& r, const Jac<F>& p) {
   r.x = p.x;

@@ -132,8 +132,8 @@ struct hbtc_ctx {
   hipEvent_t ev_main = nullptr, ev_prep = nullptr, ev_comb = nullptr;
   hipEvent_t ev_ext = nullptr, ev_ext2 = nullptr, ev_ext3 = nullptr;  // external-stream ordering
   // speculative coin combines (hbtc_coin_decide), created on first use, high priority
-  hipStream_t s_spec = nullptr;
-  hipEvent_t ev_spec_in = nullptr, ev_spec_out = nullptr;
+  hipStream_t s_spec = nullptr, s_spec2 = nullptr;  // G2 combines / G1 master checks
+  hipEvent_t ev_spec_in = nullptr, ev_spec_out = nullptr, ev_spec_out2 = nullptr;
   std::map<std::string, Stage> stages;
   std::map<std::string, unsigned> stage_next;
   std::mutex mu;
@@ -267,6 +267,7 @@ int retire_fence(hbtc_ctx* c) {
     streams.push_back(l.s_prep);
   }
   if (c->s_spec) streams.push_back(c->s_spec);
+  if (c->s_spec2) streams.push_back(c->s_spec2);
   hipError_t e = hipSuccess;
   for (hipStream_t st : streams) {
     hipEvent_t ev = nullptr;
@@ -374,6 +375,7 @@ int sync(hbtc_ctx* c) {
     HB_CHECK(c, hipStreamSynchronize(l.s_prep));
   }
   if (c->s_spec) HB_CHECK(c, hipStreamSynchronize(c->s_spec));
+  if (c->s_spec2) HB_CHECK(c, hipStreamSynchronize(c->s_spec2));
   return reap_retired(c, true);
 }
 
@@ -1598,7 +1600,9 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
   ev_free(c->ev_ext3);
   ev_free(c->ev_spec_in);
   ev_free(c->ev_spec_out);
+  ev_free(c->ev_spec_out2);
   if (c->s_spec) (void)hipStreamDestroy(c->s_spec);
+  if (c->s_spec2) (void)hipStreamDestroy(c->s_spec2);
   delete c;
 }
 
@@ -1750,8 +1754,10 @@ int hbtc_coin_decide(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uin
       int lo = 0, hi = 0;
       if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
       HB_CHECK(c, hipStreamCreateWithPriority(&c->s_spec, hipStreamNonBlocking, hi));
+      HB_CHECK(c, hipStreamCreateWithPriority(&c->s_spec2, hipStreamNonBlocking, hi));
       HB_CHECK(c, hipEventCreateWithFlags(&c->ev_spec_in, hipEventDisableTiming));
       HB_CHECK(c, hipEventCreateWithFlags(&c->ev_spec_out, hipEventDisableTiming));
+      HB_CHECK(c, hipEventCreateWithFlags(&c->ev_spec_out2, hipEventDisableTiming));
     }
     const size_t slots = (size_t)n_inst * n_sub;
     HB_TRY(wst(c, "coin.s_cst", slots, &s_cst));
@@ -1768,6 +1774,7 @@ int hbtc_coin_decide(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uin
     a.inst_status = s_cst;
     a.out = s_sig;
     a.parity = s_par;
+    a.nocheck = 1;  // a subset is committed only when all its items passed the full decode
     CombSmallArgs m{};
     m.t = t;
     m.offsets = d_off;
@@ -1777,11 +1784,15 @@ int hbtc_coin_decide(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uin
     m.n_nodes = ks->n;
     m.inst_status = s_master;
     m.cmp = ks->master;
-    HB_TRY(timed_on(c, c->s_spec, "coin_spec", [&] {
-      hipError_t e = launch_comb_small(c->s_spec, 2, n_inst, n_sub, a);
-      if (e != hipSuccess) return e;
-      return launch_comb_small(c->s_spec, 1, n_inst, n_sub, m);
+    m.xtab = ks->tab;
+    // the G2 combines and the G1 master checks of the subsets are independent: two streams
+    HB_CHECK(c, hipStreamWaitEvent(c->s_spec2, c->ev_spec_in, 0));
+    HB_TRY(timed_on(c, c->s_spec, "coin_spec", [&] { return launch_comb_small(c->s_spec, 2, n_inst, n_sub, a); }));
+    HB_TRY(timed_on(c, c->s_spec2, "coin_spec_master", [&] {
+      return launch_comb_small(c->s_spec2, 1, n_inst, n_sub, m);
     }));
+    HB_CHECK(c, hipEventRecord(c->ev_spec_out2, c->s_spec2));
+    HB_CHECK(c, hipStreamWaitEvent(c->s_spec, c->ev_spec_out2, 0));
     HB_CHECK(c, hipEventRecord(c->ev_spec_out, c->s_spec));
   }
   HB_TRY(sig_shares_dev(c, keyset_id, n_inst, (const uint8_t*)d_H, offsets, (const uint32_t*)d_idx,
@@ -1818,6 +1829,7 @@ int hbtc_coin_decide(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uin
     m.n_nodes = ks->n;
     m.inst_status = d_master;
     m.cmp = ks->master;
+    m.xtab = ks->tab;
     m.only = spec ? d_redo : nullptr;
     HB_TRY(timed(c, "combine", [&] {
       hipError_t e = launch_comb_small(c->stream, 2, n_inst, 1, a);

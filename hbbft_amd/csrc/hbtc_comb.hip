@@ -21,6 +21,7 @@
 // decoded are gathered, never decoded again (as k_msm_decode); others are decoded with the
 // subgroup check unless their status says the verifier accepted them.
 #include "hbtc_kernels.h"
+#include "pair.h"
 
 namespace hbtc {
 
@@ -40,6 +41,14 @@ __device__ __forceinline__ void comb_upoint(G2J& r, const G2A& p) {
   q.inf = 0;
   jac_from_aff(r, q);
 }
+// [u] pk from the key set's fixed-base table: -([x] pk) (G1 only; G2 has no table)
+__device__ __forceinline__ void comb_upoint_tab(G1J& r, const PtXY* tab, uint32_t node) {
+  const PtXY e = tab[((size_t)node * PK_TAB_WIN + 4) * 256 + 1];
+  r.x = e.x;
+  fq_neg(r.y, e.y);
+  fq_one(r.z);
+}
+__device__ __forceinline__ void comb_upoint_tab(G2J&, const PtXY*, uint32_t) {}
 // r <- [u^2] r (Jacobian): G1 -phi(X, Y, Z) = (beta X, -Y, Z); G2 psi^2 = -(-psi^2) = (zeta X, -Y, Z)
 __device__ __forceinline__ void comb_u2(G1J& r) {
   Fq c;
@@ -157,7 +166,7 @@ __global__ void __launch_bounds__(COMB_SMALL_BS, 1) k_comb_small(CombSmallArgs A
       } else {
         uint32_t w[NW];
         comb_load(w, A.pts, pos, NW);
-        if (!comb_decode(P, w, !accepted)) {
+        if (!comb_decode(P, w, !accepted && !A.nocheck)) {
           atomicOr(&s_bad, 1u);
           P.inf = 1;
         }
@@ -165,7 +174,10 @@ __global__ void __launch_bounds__(COMB_SMALL_BS, 1) k_comb_small(CombSmallArgs A
     }
     if (!P.inf) {
       Jac<F> XP;
-      comb_upoint(XP, P);
+      if (A.xtab && A.by_node)
+        comb_upoint_tab(XP, A.xtab, A.idx[pos]);
+      else
+        comb_upoint(XP, P);
       sac2_mul(R, P, XP, h ? d[2] : d[0], h ? d[3] : d[1], 64);
       if (h) comb_u2(R);
     }
@@ -209,6 +221,190 @@ __global__ void __launch_bounds__(COMB_SMALL_BS, 1) k_comb_small(CombSmallArgs A
   }
 }
 
+#ifndef HBTC_COMB_G2_PAIR
+#define HBTC_COMB_G2_PAIR 1  // G2 combines in lane-pair form (pair.h): four lanes per share
+#endif
+#if HBTC_COMB_G2_PAIR
+// The G2 form of k_comb_small on lane pairs (round 6): share i on lanes 4i .. 4i + 3, lane
+// (4i + 2h + e) holding component e of the digit-half h chain [d_2h] P + [d_2h+1] [u] P, so every
+// Fq2 product of the 64-doubling chain is one fused two-product per lane (pair.h) instead of three
+// products on one lane: half the chain's latency.  Selection, Lagrange coefficients and statuses
+// as k_comb_small (every lane of a share computes its coefficient); the tree sums the 128 pair
+// units in LDS; the final point is assembled on lane 0 for the encoding and the parity.
+constexpr uint32_t COMB_G2P_BS = 4 * COMB_SMALL_T;
+__global__ void __launch_bounds__(COMB_G2P_BS, 1) k_comb_small_g2p(CombSmallArgs A) {
+  HBTC_LATENCY_PRIO();
+  __shared__ uint32_t s_pos[COMB_SMALL_T];
+  __shared__ Fr s_x[COMB_SMALL_T];
+  __shared__ uint32_t s_cnt, s_bad, s_dup;
+  __shared__ uint32_t s_red[36 * COMB_G2P_BS];  // [word][lane]
+  const uint32_t k = blockIdx.x, tid = threadIdx.x;
+  if (A.only && !A.only[k]) return;  // block-uniform
+  const uint32_t t = A.t;
+  const uint32_t skip = gridDim.y > 1 ? blockIdx.y : 0xffffffffu;
+  const size_t o = (size_t)k * gridDim.y + blockIdx.y;
+  if (tid < 64) {  // wave 0: the first t items whose status is ACCEPT (all items without status)
+    const uint32_t a = A.offsets[k], b = A.offsets[k + 1];
+    uint32_t found = 0;
+    for (uint32_t base = a; base < b && found < t; base += 64) {
+      const uint32_t i = base + tid;
+      const bool ok = i < b && i - a != skip && (!A.item_status || A.item_status[i] == HBTC_ACCEPT);
+      const uint64_t mask = __ballot(ok);
+      const uint32_t slot = found + (uint32_t)__popcll(mask & ((1ull << tid) - 1ull));
+      if (ok && slot < t) s_pos[slot] = i;
+      found += (uint32_t)__popcll(mask);
+    }
+    if (tid == 0) {
+      s_cnt = found < t ? found : t;
+      s_bad = 0;
+      s_dup = 0;
+    }
+  }
+  __syncthreads();
+  const uint32_t cnt = s_cnt;
+  const uint32_t pi = tid >> 2, h = (tid >> 1) & 1u;
+  const bool live = cnt == t && pi < cnt;
+  if (live && (tid & 3u) == 0) {
+    Fr x;
+    fr_from_u64(x, (uint64_t)A.idx[s_pos[pi]] + 1);
+    s_x[pi] = x;
+  }
+  __syncthreads();
+  G2Jp R;
+  jac_set_inf(R);
+  if (live) {
+    const Fr xi = s_x[pi];
+    Fr num, den;
+    limbs_set_const<8>(num, FR_ONE);
+    limbs_set_const<8>(den, FR_ONE);
+    bool dup = false;
+    for (uint32_t j = 0; j < cnt; ++j) {
+      if (j == pi) continue;
+      const Fr xj = s_x[j];
+      dup |= limbs_eq<8>(xj, xi);
+      Fr d;
+      fr_sub(d, xj, xi);
+      fr_mul(den, den, d);
+      fr_mul(num, num, xj);
+    }
+    if (dup) atomicOr(&s_dup, 1u);
+    Fr inv, l, lc;
+    fr_inv(inv, den);
+    fr_mul(l, num, inv);
+    fr_from_mont(lc, l);
+    uint64_t d[4];
+    gls_u_digits(lc.v, d);
+    const uint32_t pos = s_pos[pi];
+    const G2A* dec = static_cast<const G2A*>(A.dec);
+    G2Ap P;
+    P.inf = 1;
+    if (A.by_node) {
+      const uint32_t id = A.idx[pos];
+      if (id < A.n_nodes)
+        g2p_load_aff(P, dec + id);
+      else
+        atomicOr(&s_bad, 1u);  // an unknown sender (only speculative subsets get here)
+    } else {
+      const bool accepted = A.item_status && A.item_status[pos] == HBTC_ACCEPT;
+      if (accepted && dec) {
+        g2p_load_aff(P, dec + pos);
+      } else {  // decoded on every lane of the pair (one-lane code), then split
+        uint32_t w[24];
+        comb_load(w, A.pts, pos, 24);
+        G2A f;
+        if (!comb_decode(f, w, !accepted && !A.nocheck)) {
+          atomicOr(&s_bad, 1u);
+        } else {
+          const bool odd = pair_odd();
+          P.x.v = odd ? f.x.c1 : f.x.c0;
+          P.y.v = odd ? f.y.c1 : f.y.c0;
+          P.inf = f.inf;
+        }
+      }
+    }
+    if (!P.inf) {
+      G2Ap xp;  // [u] P = -psi(P)
+      g2p_psi(xp.x, xp.y, P);
+      fneg(xp.y, xp.y);
+      xp.inf = 0;
+      G2Jp XP;
+      jac_from_aff(XP, xp);
+      sac2_mul(R, P, XP, h ? d[2] : d[0], h ? d[3] : d[1], 64);
+      if (h) {  // [u^2] = psi^2 = (zeta X, -Y)
+        Fq c;
+        fq_set(c, G2_ZETA);
+        fmul_by_fq(R.x, R.x, c);
+        fneg(R.y, R.y);
+      }
+    }
+  }
+  auto put = [&](uint32_t unit, const G2Jp& x) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&x);
+    const uint32_t l = 2 * unit + (tid & 1u);
+#pragma unroll
+    for (int w = 0; w < 36; ++w) s_red[w * COMB_G2P_BS + l] = src[w];
+  };
+  auto get = [&](G2Jp& x, uint32_t unit) {
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&x);
+    const uint32_t l = 2 * unit + (tid & 1u);
+#pragma unroll
+    for (int w = 0; w < 36; ++w) dst[w] = s_red[w * COMB_G2P_BS + l];
+  };
+  const uint32_t unit = tid >> 1;
+  put(unit, R);
+  __syncthreads();
+  for (uint32_t s = COMB_G2P_BS / 4; s >= 1; s >>= 1) {
+    if (unit < s) {
+      G2Jp a, b;
+      get(a, unit);
+      get(b, unit + s);
+      jac_add_lean(a, b);
+      put(unit, a);
+    }
+    __syncthreads();
+  }
+  if (tid < 2) {
+    int32_t st = HBTC_ACCEPT;
+    if (cnt < t)
+      st = HBTC_NOT_ENOUGH_SHARES;
+    else if (s_bad)
+      st = HBTC_DECODE_ERR;
+    else if (s_dup)
+      st = HBTC_DUPLICATE_ENTRY;
+    G2Jp sum;
+    get(sum, 0);
+    const bool si = jac_is_inf(sum);
+    if (A.cmp) {  // compare with a point instead of encoding the sum
+      G2Ap q;
+      g2p_load_aff(q, static_cast<const G2A*>(A.cmp));
+      const bool eq = (si || q.inf) ? (si && q.inf) : jac_eq_aff(sum, q.x, q.y);
+      if (tid == 0) A.inst_status[o] = st != HBTC_ACCEPT ? st : (eq ? HBTC_ACCEPT : HBTC_REJECT);
+      return;
+    }
+    G2Ap ap;
+    jac_to_aff(ap, sum);
+    Fq px, py;  // the partner's components: lane 0 assembles the Fq2 point
+    fq_xchg(px, ap.x.v);
+    fq_xchg(py, ap.y.v);
+    if (tid == 0) {
+      A.inst_status[o] = st;
+      G2A a;
+      a.x.c0 = ap.x.v;
+      a.x.c1 = px;
+      a.y.c0 = ap.y.v;
+      a.y.c1 = py;
+      a.inf = si ? 1u : 0u;
+      uint32_t w[24];
+      comb_compress(w, a);
+      if (st != HBTC_ACCEPT)
+        for (int j = 0; j < 24; ++j) w[j] = 0;
+      comb_store(A.out, o, w, 24);
+      if (A.parity) A.parity[o] = (st == HBTC_ACCEPT) ? (uint8_t)comb_parity(a) : 0;
+    }
+  }
+}
+#endif
+
 hipError_t launch_comb_small(hipStream_t s, int group, uint32_t n_inst, uint32_t n_sub,
                              const CombSmallArgs& a) {
   if (n_inst == 0) return hipSuccess;
@@ -216,7 +412,11 @@ hipError_t launch_comb_small(hipStream_t s, int group, uint32_t n_inst, uint32_t
   if (group == 1)
     hipLaunchKernelGGL((k_comb_small<Fq, 12>), dim3(n_inst, n_sub), dim3(COMB_SMALL_BS), 0, s, a);
   else
+#if HBTC_COMB_G2_PAIR
+    hipLaunchKernelGGL(k_comb_small_g2p, dim3(n_inst, n_sub), dim3(COMB_G2P_BS), 0, s, a);
+#else
     hipLaunchKernelGGL((k_comb_small<Fq2, 24>), dim3(n_inst, n_sub), dim3(COMB_SMALL_BS), 0, s, a);
+#endif
   return hipGetLastError();
 }
 

@@ -307,6 +307,12 @@ struct CombSmallArgs {
   uint8_t* parity;             // G2 Signature::parity per slot, or null
   const void* cmp;             // Aff<F>*: compare the sum with it (status ACCEPT / REJECT) instead of encoding
   const uint32_t* only;        // per instance: run only where only[k] != 0 (null: all)
+  const PtXY* xtab;            // by_node, G1: the key set's fixed-base table, whose entry
+                               // (node * PK_TAB_WIN + 4) * 256 + 1 is [x] pk (so [u] pk = -it is
+                               // free instead of 64 doublings); null: computed
+  uint32_t nocheck;            // decode without the subgroup test: speculative subsets, whose
+                               // sums are kept only when every item passed the verification's
+                               // full decode (k_coin_commit)
 };
 // group 1: G1 (DecryptionShares, key-set pk), 2: G2 (SignatureShares).  n_sub > 1: speculative
 // subsets, block (k, j) leaves out instance k's j-th item

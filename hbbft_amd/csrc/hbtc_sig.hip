@@ -15,6 +15,7 @@
 // per group (k_plines: one lane walks the 68 steps of the affine sum, projective (A, B, C) per
 // step) and evaluated at the fixed point -G1 by the cooperative check (gt6.h miller2_t<true>).
 #include "gt6.h"
+#include "pair.h"
 #include "rlc_common.h"
 
 namespace hbtc {
@@ -104,10 +105,9 @@ hipError_t launch_sig_decode(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
                              int32_t* status);
 // One wave per tile: decode every SignatureShare (zcash compressed G2 + subgroup check), r_i,
 // r_i sigma_i, r_i pk_i, then the plain and weighted tile / sub-tile sums in both groups.  One
-// wave per SIMD (256 VGPRs + 256 AGPRs: 736 B/lane of scratch).  Round 5 dropped the two-wave
-// form (2.7 KB/lane) and its 15-entry G2 table (8.2 KB/lane), which had to run on one
-// process-wide stream: the runtime reserves a kernel's scratch per hardware queue, and with 16
-// queues those private segments aborted queues (HSA_STATUS_ERROR_OUT_OF_RESOURCES).
+// wave per SIMD (256 VGPRs + 256 AGPRs).  No kernel keeps a multi-KB private segment any more:
+// the runtime reserves a kernel's scratch per hardware queue, and with 16 queues such segments
+// aborted queues in round 3 (HSA_STATUS_ERROR_OUT_OF_RESOURCES).
 __global__ void __launch_bounds__(64, 1) k_sig_items(
     const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
     const uint8_t* __restrict__ sigs, const G1A* __restrict__ pk,
@@ -188,6 +188,276 @@ __global__ void __launch_bounds__(64, 1) k_sig_items(
   rlc_reduce<Fq>(red1, red1 + 64, P, lane, ts->P, ts->PW);
 }
 
+#ifndef HBTC_SIG_PAIR
+#define HBTC_SIG_PAIR 1  // k_sig_items in lane-pair form (pair.h; 0: the one-lane kernel above)
+#endif
+#if HBTC_SIG_PAIR
+#ifndef HBTC_SIGP_WAVES
+#define HBTC_SIGP_WAVES 2  // k_sig_items_pair: minimum waves per SIMD of the register allocation
+#endif
+// The wave-local form of a __syncthreads between LDS writes and reads of ONE wave: a wave's LDS
+// operations execute in order, so only the compiler's reordering and the outstanding counters
+// need fencing.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// r pk_i of the x-adic scalar on a lane pair: lane e takes digits e and e + 2 (the pk window of
+// digit e, then the phi window of digit e + 2: the beta product is on the same iteration for
+// both lanes), 8 of the 16 mixed additions; the pair's halves are then added (both lanes hold
+// the sum).
+__device__ __forceinline__ void rlc_pk_mul_x_pair(G1J& r, const PtXY* __restrict__ tab, const XDigits& x) {
+  const uint32_t e = pair_odd() ? 1u : 0u;
+  jac_set_inf(r);
+  const int nwin = x.nbits / 8;
+#pragma unroll 1
+  for (int i = 0; i < 2; ++i) {
+    const uint32_t j = e + 2u * (uint32_t)i;
+    const uint32_t dj = x.d[0] * (j == 0) + x.d[1] * (j == 1) + x.d[2] * (j == 2) + x.d[3] * (j == 3);
+    const int tw = (j & 1u) ? 4 : 0;  // d1, d3: the [x] pk windows
+#pragma unroll 1
+    for (int w = 0; w < nwin; ++w) {
+      const uint32_t v = (dj >> (8 * w)) & 0xffu;
+      if (!v) continue;
+      const PtXY en = tab[(tw + w) * 256 + v];
+      G1A q;
+      q.y = en.y;
+      q.inf = 0;
+      if (i == 1) {  // digits 2, 3: phi
+        Fq beta;
+        fq_set(beta, G1_BETA);
+        fq_mul(q.x, en.x, beta);
+      } else {
+        q.x = en.x;
+      }
+      jac_add_aff(r, r, q);
+    }
+  }
+  G1J o;
+  fq_xchg(o.x, r.x);
+  fq_xchg(o.y, r.y);
+  fq_xchg(o.z, r.z);
+  jac_add(r, r, o);
+}
+
+// LDS layouts of the two reductions: word w of item m's G2 point component e at
+// w * 128 + 2 m + e (36 words), of its G1 point at w * 64 + m -- a wave's stores are conflict-free.
+__device__ __forceinline__ void g2p_lds_put(uint32_t* lds, uint32_t m, const G2Jp& a) {
+  const uint32_t o = 2 * m + (pair_odd() ? 1u : 0u);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&a);
+#pragma unroll
+  for (int w = 0; w < 36; ++w) lds[w * 128 + o] = src[w];
+}
+__device__ __forceinline__ void g2p_lds_get(G2Jp& a, const uint32_t* lds, uint32_t m) {
+  const uint32_t o = 2 * m + (pair_odd() ? 1u : 0u);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&a);
+#pragma unroll
+  for (int w = 0; w < 36; ++w) dst[w] = lds[w * 128 + o];
+}
+__device__ __forceinline__ void g1_lds_put(uint32_t* lds, uint32_t m, const G1J& a) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&a);
+#pragma unroll
+  for (int w = 0; w < 36; ++w) lds[w * 64 + m] = src[w];
+}
+__device__ __forceinline__ void g1_lds_get(G1J& a, const uint32_t* lds, uint32_t m) {
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&a);
+#pragma unroll
+  for (int w = 0; w < 36; ++w) dst[w] = lds[w * 64 + m];
+}
+template <class J>
+__device__ __forceinline__ void shfl_words(J& r, const J& x, uint32_t src) {
+  const uint32_t* xs = reinterpret_cast<const uint32_t*>(&x);
+  uint32_t* rs = reinterpret_cast<uint32_t*>(&r);
+  const int addr = (int)((src & 63u) << 2);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(J) / 4); ++i) rs[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)xs[i]);
+}
+
+// 36 words of one lane at w * 64 + l (the B area of the G2 tree)
+template <class J>
+__device__ __forceinline__ void g1w_put36(uint32_t* lds, uint32_t l, const J& x) {
+  static_assert(sizeof(J) == 144, "36 words");
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&x);
+#pragma unroll
+  for (int w = 0; w < 36; ++w) lds[w * 64 + l] = src[w];
+}
+template <class J>
+__device__ __forceinline__ void g1w_get36(J& x, const uint32_t* lds, uint32_t l) {
+  static_assert(sizeof(J) == 144, "36 words");
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&x);
+#pragma unroll
+  for (int w = 0; w < 36; ++w) dst[w] = lds[w * 64 + l];
+}
+
+// The tile's G2 tree (rlc_reduce's merges: A = A_l + A_r, B = 2 (B_l + B_r) + A_r) on ONE wave of
+// 32 lane pairs: pair j owns node m = 2 j.  A and B both in LDS (B at w * 64 + lane: the right
+// node's B is the one of pair j + s / 2, i.e. lane + s), so at most two points are live beside the
+// product's fixed registers (B in registers left a 848 B/lane frame).
+__device__ __forceinline__ void rlc_reduce_g2p(uint32_t* lds, uint32_t* ldsB, uint32_t lane, G2J* outA, G2J* outB) {
+  const uint32_t j = lane >> 1, m = 2 * j;
+  {  // level 1: the leaves' B are infinity, so B = A_r
+    G2Jp a, ar;
+    g2p_lds_get(ar, lds, m + 1);
+    g1w_put36(ldsB, lane, ar);
+    g2p_lds_get(a, lds, m);
+    jac_add_lean(a, ar);
+    g2p_lds_put(lds, m, a);
+    wave_lds_sync();
+  }
+#pragma unroll 1
+  for (uint32_t s = 2; s < 64; s <<= 1) {
+    if ((j & (s - 1)) == 0) {  // active pairs read only inactive pairs' entries besides their own
+      G2Jp b, x;
+      g1w_get36(b, ldsB, lane);
+      g1w_get36(x, ldsB, lane + s);
+      jac_add_lean(b, x);
+      jac_dbl(b, b);
+      g2p_lds_get(x, lds, m + s);  // A_r
+      jac_add_lean(b, x);
+      g1w_put36(ldsB, lane, b);
+      g2p_lds_get(b, lds, m);
+      jac_add_lean(b, x);
+      g2p_lds_put(lds, m, b);
+    }
+    wave_lds_sync();
+    if (s == 4 && (j & 3u) == 0) {
+      G2Jp x;
+      g2p_lds_get(x, lds, m);
+      g2p_store_jac(outA + (m >> 3), x);
+      g1w_get36(x, ldsB, lane);
+      g2p_store_jac(outB + (m >> 3), x);
+    }
+  }
+  if (j == 0) {
+    G2Jp x;
+    g2p_lds_get(x, lds, 0);
+    g2p_store_jac(outA + 8, x);
+    g1w_get36(x, ldsB, lane);
+    g2p_store_jac(outB + 8, x);
+  }
+}
+
+// The tile's G1 tree, one lane per item on ONE wave (rlc_reduce1 without workgroup barriers).
+__device__ __forceinline__ void rlc_reduce_g1w(uint32_t* lds, uint32_t lane, G1J* outA, G1J* outB) {
+  G1J b;
+  jac_set_inf(b);
+  for (uint32_t s = 1; s < 64; s <<= 1) {
+    const bool active = (lane & (2 * s - 1)) == 0;
+    {
+      G1J br;
+      shfl_words(br, b, lane + s);
+      if (active) jac_add(b, b, br);
+    }
+    if (active) {
+      G1J ar, a;
+      g1_lds_get(ar, lds, lane + s);
+      jac_dbl(b, b);
+      jac_add(b, b, ar);
+      g1_lds_get(a, lds, lane);
+      jac_add(a, a, ar);
+      g1_lds_put(lds, lane, a);
+    }
+    wave_lds_sync();
+    if (s == 4 && (lane & 7u) == 0) {
+      G1J a;
+      g1_lds_get(a, lds, lane);
+      outA[lane >> 3] = a;
+      outB[lane >> 3] = b;
+    }
+  }
+  if (lane == 0) {
+    G1J a;
+    g1_lds_get(a, lds, 0);
+    outA[8] = a;
+    outB[8] = b;
+  }
+}
+
+// k_sig_items in lane-pair form: one workgroup of two waves per 64-share tile, share i on lanes
+// (2i, 2i + 1).  r_i sigma_i by the x-adic two-addition loop in pair arithmetic (table in
+// registers: 72 per lane), r_i pk_i split over the pair (rlc_pk_mul_x_pair), then the two trees
+// side by side: the G2 tree on wave 0 (pair form), the G1 tree on wave 1 (one lane per share).
+__global__ void __launch_bounds__(128, HBTC_SIGP_WAVES) k_sig_items_pair(
+    const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx,
+    const uint8_t* __restrict__ sigs, const G1A* __restrict__ pk,
+    const int32_t* __restrict__ pk_status, const PtXY* __restrict__ pk_tab, uint32_t n_pk,
+    RlcKey key, Suspects sus, SigTileSums* __restrict__ sums, G2A* __restrict__ dec,
+    int32_t* __restrict__ status) {
+#ifndef HBTC_SIGP_TAB_LDS
+#define HBTC_SIGP_TAB_LDS 1  // the x-adic table's three points in LDS (72 words per lane)
+#endif
+  // the table ([entry][word][lane], 36 KB) while the scalars run, then the two trees' arrays
+  // (G2 A 18 KB, G1 A 9 KB, G2 B 9 KB)
+  __shared__ uint32_t lds[72 * 128];
+  uint32_t* lds2 = lds;
+  uint32_t* lds1 = lds + 36 * 128;
+  uint32_t* ldsB = lds + 36 * 128 + 36 * 64;  // the G2 tree's B: 36 words x 64 lanes of wave 0
+  const Tile tile = tiles[blockIdx.x];
+  const uint32_t m = threadIdx.x >> 1;  // the share's position in the tile
+  const bool even = (threadIdx.x & 1u) == 0;
+  const size_t item = (size_t)tile.first + m;
+  G2Jp S;
+  G1J P;
+  jac_set_inf(S);
+  jac_set_inf(P);
+  bool leaf = false;
+  if (m < tile.count) {
+    int32_t st = HBTC_RLC_PENDING;
+    const uint32_t id = idx[item];
+    if (id >= n_pk) {
+      st = HBTC_UNKNOWN_SENDER;
+    } else if (pk_status[id] != HBTC_ACCEPT) {
+      st = HBTC_DECODE_ERR;
+    } else if (status[item] == HBTC_DECODE_ERR) {  // k_sig_decode ran first
+      st = HBTC_DECODE_ERR;
+    } else if (is_suspect(sus, id)) {
+      st = HBTC_RLC_LEAF;  // straight to an exact check, outside the group sums
+    } else {
+      const XDigits xd = rlc_digits(key, item);
+      G2Ap sg;
+      g2p_load_aff(sg, dec + item);
+      if (!sg.inf) {
+        // [x] sigma = psi(sigma), m = -psi^2 = (zeta x, y)
+        G2Ap xp, pxp;
+        g2p_psi(xp.x, xp.y, sg);
+        xp.inf = 0;
+        G2Jp xj;
+        jac_from_aff(xj, xp);
+        xadic_table(xp, pxp, sg, xj);
+        Fq zeta;
+        fq_set(zeta, G2_ZETA);
+#if HBTC_SIGP_TAB_LDS
+        xy_lds_put_aff<Fq2p, 128>(lds, threadIdx.x, 0, sg);
+        xy_lds_put_aff<Fq2p, 128>(lds, threadIdx.x, 1, xp);
+        xy_lds_put_aff<Fq2p, 128>(lds, threadIdx.x, 2, pxp);
+        xadic_mul_uniform_lds<Fq2p, 128>(S, lds, threadIdx.x, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3],
+                                         xd.nbits);
+#else
+        xadic_mul_uniform(S, sg, xp, pxp, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
+#endif
+      }
+      if (!pk[id].inf) rlc_pk_mul_x_pair(P, pk_tab + (size_t)id * PK_TAB_WIN * 256, xd);
+    }
+    if (even) status[item] = st;
+    leaf = even && st == HBTC_RLC_LEAF;
+  }
+  rlc_list_leaf(sus, leaf, (uint32_t)item, tile.inst, threadIdx.x & 63u);
+#if HBTC_SIGP_TAB_LDS
+  __syncthreads();  // every lane's table reads are over before the trees' arrays are written
+#endif
+  g2p_lds_put(lds2, m, S);
+  if (even) g1_lds_put(lds1, m, P);
+  __syncthreads();
+  SigTileSums* ts = sums + blockIdx.x;
+  if (threadIdx.x < 64)
+    rlc_reduce_g2p(lds2, ldsB, threadIdx.x, ts->S, ts->SW);
+  else
+    rlc_reduce_g1w(lds1, threadIdx.x - 64, ts->P, ts->PW);
+}
+#endif
+
 // Projective line table of one G2 sum: affine (one Fq2 inversion) then the 68 steps.
 __device__ __forceinline__ void g2j_plines(Fq2* out, uint32_t* inf, const G2J& S) {
   if (jac_is_inf(S)) {
@@ -264,8 +534,13 @@ hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, 
   const hipError_t e = launch_sig_decode(s, n_tiles, tiles, idx, sigs, pk_status, n_pk, dec, status);
   if (e != hipSuccess) return e;
 #endif
+#if HBTC_SIG_PAIR && HBTC_SIG_SPLIT
+  hipLaunchKernelGGL(k_sig_items_pair, dim3(n_tiles), dim3(128), 0, s, tiles, idx, sigs, pk, pk_status,
+                     pk_tab, n_pk, key, sus, sums, dec, status);
+#else
   hipLaunchKernelGGL(k_sig_items, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk, pk_status,
                      pk_tab, n_pk, key, sus, sums, dec, status);
+#endif
   return hipGetLastError();
 }
 

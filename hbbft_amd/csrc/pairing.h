@@ -62,41 +62,43 @@ HD void g2_dbl_step(G2J& T, Fq2& A, Fq2& B, Fq2& C) {
 
 // The doubling step with the line fused into the point doubling (the same line as g2_dbl_step up
 // to nothing: A = 3X^3 - 2Y^2 = X E - 2 YY, B = -E Z^2, C = Z3 Z^2 with E = 3 X^2, Z3 = 2 Y Z):
-// 6 squarings + 5 multiplications in Fq2 instead of 8 + 6.
-HD void g2_dbl_line(G2J& T, Fq2& A, Fq2& B, Fq2& C) {
-  Fq2 XX, YY, YYYY, ZZ, D, E, F, t;
-  fq2_sqr(XX, T.x);
-  fq2_sqr(YY, T.y);
-  fq2_sqr(YYYY, YY);
-  fq2_sqr(ZZ, T.z);
-  fq2_add(t, T.x, YY);
-  fq2_sqr(t, t);
-  fq2_sub(t, t, XX);
-  fq2_sub(t, t, YYYY);
-  fq2_dbl(D, t);
-  fq2_dbl(E, XX);
-  fq2_add(E, E, XX);
+// 6 squarings + 5 multiplications in Fq2 instead of 8 + 6.  Templated over the Fq2 type so the
+// lane-pair form (pair.h Fq2p) runs the same steps.
+template <class F>
+HD void g2_dbl_line(Jac<F>& T, F& A, F& B, F& C) {
+  F XX, YY, YYYY, ZZ, D, E, Fv, t;
+  fsqr(XX, T.x);
+  fsqr(YY, T.y);
+  fsqr(YYYY, YY);
+  fsqr(ZZ, T.z);
+  fadd(t, T.x, YY);
+  fsqr(t, t);
+  fsub(t, t, XX);
+  fsub(t, t, YYYY);
+  fdbl(D, t);
+  fdbl(E, XX);
+  fadd(E, E, XX);
   // line
-  fq2_mul(A, T.x, E);
-  fq2_dbl(t, YY);
-  fq2_sub(A, A, t);
-  fq2_mul(B, E, ZZ);
-  fq2_neg(B, B);
-  Fq2 z3;
-  fq2_mul(z3, T.y, T.z);
-  fq2_dbl(z3, z3);
-  fq2_mul(C, z3, ZZ);
+  fmul(A, T.x, E);
+  fdbl(t, YY);
+  fsub(A, A, t);
+  fmul(B, E, ZZ);
+  fneg(B, B);
+  F z3;
+  fmul(z3, T.y, T.z);
+  fdbl(z3, z3);
+  fmul(C, z3, ZZ);
   // point
-  fq2_sqr(F, E);
-  Fq2 x3, y3;
-  fq2_dbl(t, D);
-  fq2_sub(x3, F, t);
-  fq2_sub(t, D, x3);
-  fq2_mul(y3, E, t);
-  fq2_dbl(YYYY, YYYY);
-  fq2_dbl(YYYY, YYYY);
-  fq2_dbl(YYYY, YYYY);
-  fq2_sub(y3, y3, YYYY);
+  fsqr(Fv, E);
+  F x3, y3;
+  fdbl(t, D);
+  fsub(x3, Fv, t);
+  fsub(t, D, x3);
+  fmul(y3, E, t);
+  fdbl(YYYY, YYYY);
+  fdbl(YYYY, YYYY);
+  fdbl(YYYY, YYYY);
+  fsub(y3, y3, YYYY);
   T.x = x3;
   T.y = y3;
   T.z = z3;
@@ -104,19 +106,20 @@ HD void g2_dbl_line(G2J& T, Fq2& A, Fq2& B, Fq2& C) {
 
 // Addition step T <- T + Q (Q affine):  r = yQ Z^3 - Y, H = xQ Z^2 - X,
 //   A = r xQ - yQ Z H,  B = -r,  C = Z H
-HD void g2_add_step(G2J& T, const G2A& Q, Fq2& A, Fq2& B, Fq2& C) {
-  Fq2 z2, z3, r, H, t;
-  fq2_sqr(z2, T.z);
-  fq2_mul(z3, z2, T.z);
-  fq2_mul(r, Q.y, z3);
-  fq2_sub(r, r, T.y);
-  fq2_mul(H, Q.x, z2);
-  fq2_sub(H, H, T.x);
-  fq2_mul(C, T.z, H);
-  fq2_mul(A, r, Q.x);
-  fq2_mul(t, Q.y, C);
-  fq2_sub(A, A, t);
-  fq2_neg(B, r);
+template <class F>
+HD void g2_add_step(Jac<F>& T, const Aff<F>& Q, F& A, F& B, F& C) {
+  F z2, z3, r, H, t;
+  fsqr(z2, T.z);
+  fmul(z3, z2, T.z);
+  fmul(r, Q.y, z3);
+  fsub(r, r, T.y);
+  fmul(H, Q.x, z2);
+  fsub(H, H, T.x);
+  fmul(C, T.z, H);
+  fmul(A, r, Q.x);
+  fmul(t, Q.y, C);
+  fsub(A, A, t);
+  fneg(B, r);
   jac_add_aff(T, T, Q);
 }
 

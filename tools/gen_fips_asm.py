@@ -438,6 +438,93 @@ KARA_BODIES = (("hbtc_fqmacsub_sr", ((SR_MACC, "+"), (SR_MACC2, "-"))),
                ("hbtc_fqsubsub_sr", ((SR_MACC, "-"), (SR_MACC2, "-"))))
 
 
+# ------------------------------------------------------------------ lane-pair Fq2 product (pair.h)
+# hbtc_fqmul2_sr: r = (a b + c d) 2^-384 mod p in ONE product scanning, for operands < 2p (a b +
+# c d < 8p^2, so r < 2p): the component of a lane-pair Fq2 product (lane 0: a0 b0 + (-a1) b1,
+# lane 1: a0 b1 + a1 b0).  144 + 144 + 144 MACs + 12 digits against 2 x 144 + 168 for two lazy MACs
+# and a reduction, and no 25-word accumulator.  Registers: a / r v8..v19, b v20..v31, c v32..v43,
+# d v44..v55, q v56..v67, column accumulators v68..v71 (r_j is written at column 12 + j, after the
+# last reads of a_j, b_j, c_j, d_j at column j + 11).
+M2_A, M2_B, M2_C, M2_D, M2_Q, M2_ACC = 8, 20, 32, 44, 56, 68
+
+
+def mul2_body():
+    A = lambda i: "v%d" % (M2_A + i)
+    B = lambda i: "v%d" % (M2_B + i)
+    C = lambda i: "v%d" % (M2_C + i)
+    D = lambda i: "v%d" % (M2_D + i)
+    Q = lambda i: "v%d" % (M2_Q + i)
+    P = lambda i: "s%d" % (SR_P + i)
+    reg = lambda n: "v%d" % (M2_ACC + n)
+    pair = lambda p: "v[%d:%d]" % (M2_ACC + 2 * p, M2_ACC + 2 * p + 1)
+    out = ["v_mov_b32 %s, 0" % reg(0), "v_mov_b32 %s, 0" % reg(1)]
+    for k in range(23):
+        p = k % 2
+        acc, lo, hi, c2, nlo = pair(p), reg(2 * p), reg(2 * p + 1), reg(2 * (1 - p) + 1), reg(2 * (1 - p))
+        lo_i, hi_i = (0, k) if k < 12 else (k - 11, 11)
+        terms = [(A(i), B(k - i)) for i in range(lo_i, hi_i + 1)]
+        terms += [(C(i), D(k - i)) for i in range(lo_i, hi_i + 1)]
+        terms += [(Q(i), P(k - i)) for i in range(lo_i, (k - 1 if k < 12 else 11) + 1)]
+        for n, (x, y) in enumerate(terms):
+            out.append("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (acc, x, y, acc))
+            out.append("v_addc_co_u32_e64 %s, vcc, %s, 0, vcc" % (c2, "0" if n == 0 else c2))
+        if k < 12:
+            out.append("v_mul_lo_u32 %s, %s, s%d" % (Q(k), lo, SR_NP))
+            out.append("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (acc, Q(k), P(0), acc))
+            out.append("v_addc_co_u32_e64 %s, vcc, %s, 0, vcc" % (c2, c2))
+        else:
+            out.append("v_mov_b32 %s, %s" % (A(k - 12), lo))
+        if k < 22:
+            out.append("v_mov_b32 %s, %s" % (nlo, hi))
+    out.append("v_mov_b32 %s, %s" % (A(11), reg(1)))  # column 22's high word; its overflow is 0
+    return out
+
+
+def mul2_call():
+    call = ('      "s_getpc_b64 s[%d:%d]\\n\\t"\n' % (SR_TGT, SR_TGT + 1) +
+            '      "s_add_u32 s%d, s%d, hbtc_fqmul2_sr@rel32@lo+4\\n\\t"\n' % (SR_TGT, SR_TGT) +
+            '      "s_addc_u32 s%d, s%d, hbtc_fqmul2_sr@rel32@hi+12\\n\\t"\n' % (SR_TGT + 1, SR_TGT + 1) +
+            '      "s_swappc_b64 s[%d:%d], s[%d:%d]"' % (SR_RET, SR_RET + 1, SR_TGT, SR_TGT + 1))
+    outs = ", ".join('"={v%d}"(r[%d])' % (M2_A + i, i) for i in range(12))
+    ins = []
+    for base, nm in ((M2_A, "a"), (M2_B, "b"), (M2_C, "c"), (M2_D, "d")):
+        ins.append(", ".join('"{v%d}"(%s[%d])' % (base + i, nm, i) for i in range(12)))
+    clob = ['"v%d"' % v for v in range(M2_Q, M2_ACC + 4)]
+    clob += ['"s%d"' % s for s in range(SR_P, SR_RET + 2)]
+    clob += ['"vcc"', '"scc"']
+    return """__device__ __forceinline__ void mont_mul2_sr(uint32_t* r, const uint32_t* a, const uint32_t* b,
+                                             const uint32_t* c, const uint32_t* d) {
+  asm volatile(
+%s
+      : %s
+      : %s
+      : %s);
+}
+""" % (call, outs, ",\n        ".join(ins), ", ".join(clob))
+
+
+def selftest_mul2(trials=300):
+    """hbtc_fqmul2_sr on the register-file simulator: r < 2p and r = (a b + c d) 2^-384 mod p,
+    with the extreme operands 2p - 1 first."""
+    import random
+    M32 = (1 << 32) - 1
+    rng = random.Random(11)
+    prog = lazy_text("x", mul2_body())[2:-1]
+    for t in range(trials):
+        ops = [2 * P_MOD - 1] * 4 if t == 0 else [rng.randrange(2 * P_MOD) for _ in range(4)]
+        regs = {}
+        for base, v in zip((M2_A, M2_B, M2_C, M2_D), ops):
+            for i in range(12):
+                regs["v%d" % (base + i)] = (v >> (32 * i)) & M32
+        run_prog(prog, regs)
+        r = sum(regs["v%d" % (M2_A + i)] << (32 * i) for i in range(12))
+        a, b, c, d = ops
+        assert r < 2 * P_MOD and r % P_MOD == (a * b + c * d) * pow(2, -384, P_MOD) % P_MOD, t
+        for base, v in zip((M2_B, M2_C, M2_D), ops[1:]):
+            assert sum(regs["v%d" % (base + i)] << (32 * i) for i in range(12)) == v
+    print("selftest_mul2 ok (%d instructions)" % len(prog))
+
+
 def main_sr():
     print("""// GENERATED by tools/gen_fips_asm.py --sr -- do not edit.
 // The Fq Montgomery product and squaring of fq_fips_asm.h as ONE shared subroutine each, called
@@ -458,7 +545,8 @@ def main_sr():
             print('    "%s\\n"' % l)
     for label, body in (("hbtc_fqmac_sr", mac_body()), ("hbtc_fqredc_sr", redc_body()),
                         ("hbtc_fqmac2_sr", mac_body(SR_MACC2)), ("hbtc_fqredc2_sr", redc_body(SR_MACC2))) + tuple(
-                            (label, mac_body(targets=list(t))) for label, t in KARA_BODIES):
+                            (label, mac_body(targets=list(t))) for label, t in KARA_BODIES) + (
+                                ("hbtc_fqmul2_sr", mul2_body()),):
         for l in lazy_text(label, body):
             print('    "%s\\n"' % l)
     print('    ::: "memory");')
@@ -469,6 +557,7 @@ namespace fips {
     print(sr_call("mont_mul_sr", "hbtc_fqmul_sr", False))
     print(sr_call("mont_sqr_sr", "hbtc_fqsqr_sr", True))
     print(lazy_calls())
+    print(mul2_call())
     print("""}  // namespace fips
 }  // namespace hbtc
 #endif""")
@@ -716,3 +805,4 @@ def selftest_lazy(trials=200):
 
 if __name__ == "__main__" and len(__import__("sys").argv) > 1 and __import__("sys").argv[1] == "--selftest-lazy":
     selftest_lazy()
+    selftest_mul2()
