@@ -53,6 +53,9 @@ SIGNATURES = {
     "hbtc_keyset_free": (_I32, [_P, _U32]),
     "hbtc_verify_sig_shares": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _P]),
     "hbtc_keyset_set_master": (_I32, [_P, _U32, _P]),
+    "hbtc_prepare_g2": (_I32, [_P, _U32, _P, _P]),
+    "hbtc_unprepare_g2": (_I32, [_P, _U32, _P]),
+    "hbtc_prepared_g2_count": (_I32, [_P, _P]),
     "hbtc_coin_decide": (_I32, [_P, _U32, _U32, _P, _P, _P, _P, _U32, _P, _P, _P, _P]),
     "hbtc_verify_sigs": (_I32, [_P, _U32, _P, _P, _P, _P]),
     "hbtc_combine_sigs": (_I32, [_P, _U32, _P, _P, _P, _U32, _P, _P, _P]),
@@ -390,6 +393,23 @@ class Context:
     def keyset_set_master(self, kid, master_pk):
         mp = _join([master_pk], 48)
         self._check(self.lib.hbtc_keyset_set_master(self.h, kid, _ptr(mp)), "hbtc_keyset_set_master")
+
+    def prepare_g2(self, points):
+        """hbtc.h hbtc_prepare_g2: the G2 tables of these compressed points (a coin's H, a
+        ciphertext's H and w) built ahead of the shares; per-point ACCEPT / DECODE_ERR."""
+        pb = _join(points, 96)
+        st = np.zeros(max(len(points), 1), np.int32)
+        self._check(self.lib.hbtc_prepare_g2(self.h, len(points), _ptr(pb), _ptr(st)), "hbtc_prepare_g2")
+        return st[:len(points)]
+
+    def unprepare_g2(self, points):
+        pb = _join(points, 96)
+        self._check(self.lib.hbtc_unprepare_g2(self.h, len(points), _ptr(pb)), "hbtc_unprepare_g2")
+
+    def prepared_g2_count(self):
+        n = np.zeros(1, np.uint32)
+        self._check(self.lib.hbtc_prepared_g2_count(self.h, _ptr(n)), "hbtc_prepared_g2_count")
+        return int(n[0])
 
     # ---- verification
     def coin_decide(self, keyset, H, counts, idx, sigs, t, offsets=None):

@@ -9,6 +9,7 @@
 #include <mutex>
 #include <random>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "hbtc_kernels.h"
@@ -121,6 +122,24 @@ struct hbtc_ctx {
   bool comb_small = true;
   // hbtc_coin_decide's speculative combines (HBTC_COIN_SPEC=0: combine after the checks only)
   bool coin_spec = true;
+  // hbtc_prepare_g2: per-instance G2 tables built ahead of the shares, resident, keyed by the
+  // point's 96 bytes (a slot: decoded point, status, 68 affine lines)
+  struct Prep {
+    std::unordered_map<std::string, uint32_t> slot;
+    std::vector<uint32_t> free;
+    uint32_t cap = 0, top = 0;
+    G2A* aff = nullptr;
+    int32_t* st = nullptr;
+    Line* lines = nullptr;
+  } prep;
+  // the host copies of the per-instance G2 arguments of the call in progress (set by the entry
+  // points that take host bytes, for the prepared-table lookup of prepare_g2)
+  struct HostG2 {
+    const uint8_t *d0 = nullptr, *h0 = nullptr, *d1 = nullptr, *h1 = nullptr;
+  } host_g2;
+  // the exact small-call path of SignatureShares / pair checks as one fused launch (k_sig_exact;
+  // HBTC_SIG_FUSED=0: decode, listing and line tables as three launches)
+  bool sig_fused = true;
   // factorial tables of the Lagrange coefficients (k_lagrange_fact): 0..FACT_N, built at the first
   // Pippenger combine (HBTC_LAGRANGE_FACT=0: the O(t) per term kernels)
   bool lagrange_fact = true;
@@ -647,6 +666,17 @@ int get_keyset(hbtc_ctx* c, uint32_t id, Keyset** ks) {
 
 // Decode + line tables for the per-instance G2 arguments: d0 (n items) and, when d1 is given,
 // d1 (n more) in one launch pair; outputs for d1 start at index n.
+// The host bytes of a call's per-instance G2 arguments, for prepare_g2's lookup of prepared
+// tables, for the duration of one entry point.
+struct HostG2Args {
+  hbtc_ctx* c;
+  HostG2Args(hbtc_ctx* cx, const void* d0, const uint8_t* h0, const void* d1 = nullptr, const uint8_t* h1 = nullptr)
+      : c(cx) {
+    c->host_g2 = {static_cast<const uint8_t*>(d0), h0, static_cast<const uint8_t*>(d1), h1};
+  }
+  ~HostG2Args() { c->host_g2 = {}; }
+};
+
 int prepare_g2(hbtc_ctx* c, const uint8_t* d0, const uint8_t* d1, uint32_t n, G2A** aff,
                int32_t** st, Line** lines, hipStream_t on = nullptr) {
   hipStream_t strm = on ? on : c->stream;
@@ -655,6 +685,28 @@ int prepare_g2(hbtc_ctx* c, const uint8_t* d0, const uint8_t* d1, uint32_t n, G2
   HB_TRY(wst(c, "g2.aff", m, aff));
   HB_TRY(wst(c, "g2.st", m, st));
   HB_TRY(wst(c, "g2.lines", (size_t)m * MILLER_STEPS, lines));
+  // every argument prepared (hbtc_prepare_g2): gather the resident tables instead of building them
+  const auto& hg = c->host_g2;
+  if (!c->prep.slot.empty() && hg.d0 == d0 && hg.h0 && hg.d1 == d1 && (!d1 || hg.h1)) {
+    std::vector<uint32_t> slots(m);
+    bool all = true;
+    for (uint32_t i = 0; i < m && all; ++i) {
+      const uint8_t* key = i < n ? hg.h0 + (size_t)96 * i : hg.h1 + (size_t)96 * (i - n);
+      auto it = c->prep.slot.find(std::string(reinterpret_cast<const char*>(key), 96));
+      if (it == c->prep.slot.end()) all = false; else slots[i] = it->second;
+    }
+    if (all) {
+      void* p;
+      HB_TRY(stage_upload(c, "g2.slots", slots.data(), (size_t)4 * m, strm, &p));
+      const uint32_t* d_slots = static_cast<const uint32_t*>(p);
+      G2A* a = *aff;
+      int32_t* s = *st;
+      Line* l = *lines;
+      return timed_on(c, strm, "prepare_cached", [&] {
+        return launch_g2_tab_copy(strm, m, d_slots, nullptr, c->prep.aff, c->prep.st, c->prep.lines, a, s, l);
+      });
+    }
+  }
   HB_TRY(wst(c, "g2.ws", (size_t)m * 3 * MILLER_STEPS, &wsp));
   G2A* a = *aff;
   int32_t* s = *st;
@@ -994,8 +1046,14 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   const bool exact = c->verify_mode == HBTC_MODE_PER_SHARE || n_items < c->exact_below;
   const Suspects sus =
       exact ? Suspects{nullptr, 0, leaf_count, leaves, 1} : suspects_of(c, ks, leaf_count, leaves);
+  // the exact path in one launch when every share's line table fits the buffer (k_sig_exact:
+  // decode, listing, line tables with the subgroup test at the end of their walk)
+  const bool fused = exact && c->sig_fused && n_items <= n_tables;
   HB_TRY(items_gate(c, n_tiles));
   HB_TRY(timed(c, "sig_items", [&] {
+    if (fused)
+      return launch_sig_exact(c->stream, n_items, d_idx, d_sig, ks->st, ks->n, tiles, n_tiles, leaf_count,
+                              leaves, dec, tables, inf, d_status);
     return launch_sig_items(c->stream, n_tiles, tiles, d_idx, d_sig, ks->pk, ks->st, ks->tab, ks->n,
                             key, sus, sums, dec, d_status);
   }));
@@ -1039,10 +1097,11 @@ int sig_shares_dev(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uint8
   const uint32_t leaf_chunk = (uint32_t)n_tables;
   for (uint32_t base = 0; base < n_items; base += leaf_chunk) {
     const uint32_t chunk = std::min(leaf_chunk, n_items - base);
-    HB_TRY(timed(c, "sig_lines", [&] {
-      return launch_plines(c->stream, 2, chunk, base, leaf_count, leaves, tiles, sums, dec, tables,
-                           inf);
-    }));
+    if (!fused)
+      HB_TRY(timed(c, "sig_lines", [&] {
+        return launch_plines(c->stream, 2, chunk, base, leaf_count, leaves, tiles, sums, dec, tables,
+                             inf);
+      }));
     HB_TRY(timed(c, "chk_leaves", [&] {
       // a short list (<= 2 leaves per SIMD, all in the first chunk) in the latency form
       const uint32_t lim = (rep3 && base == 0) ? std::min(chunk, 8u * (uint32_t)c->n_cu) : 0u;
@@ -1408,6 +1467,7 @@ int epoch_submit(hbtc_ctx* c, int group, uint32_t keyset_id, uint32_t n_inst, co
   const bool comb = t > 0 && n_inst > 0;
   {
     PinLane pin(c);  // the uploads above went to lane l: verification and combine stay there
+    HostG2Args hg(c, d_H, sH ? hi : nullptr, d_w, sW ? hi + oW : nullptr);
     if (group == 1)
       HB_TRY(dec_shares_dev(c, keyset_id, n_inst, (const uint8_t*)d_H, (const uint8_t*)d_w, offsets,
                             (const uint32_t*)d_idx, (const uint8_t*)d_items, (int32_t*)d_st));
@@ -1479,6 +1539,8 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (const char* e = getenv("HBTC_G1_GLV")) c->g1_glv = atoi(e) != 0;
   if (const char* e = getenv("HBTC_COMB_SMALL")) c->comb_small = atoi(e) != 0;
   if (const char* e = getenv("HBTC_COIN_SPEC")) c->coin_spec = atoi(e) != 0;
+  c->sig_fused = sig_exact_built();
+  if (const char* e = getenv("HBTC_SIG_FUSED")) c->sig_fused = c->sig_fused && atoi(e) != 0;
   if (const char* e = getenv("HBTC_TRACK")) c->track_senders = atoi(e) != 0;
   if (const char* e = getenv("HBTC_LAGRANGE_FACT")) c->lagrange_fact = atoi(e) != 0;
   if (const char* e = getenv("HBTC_PROBE")) c->probe_cold = atoi(e) != 0;
@@ -1554,6 +1616,9 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
   (void)retire_fence(c);
   (void)reap_retired(c, true);
   if (c->fact) (void)hipFree(c->fact);  // inv_fact lives in the same allocation
+  if (c->prep.aff) (void)hipFree(c->prep.aff);
+  if (c->prep.st) (void)hipFree(c->prep.st);
+  if (c->prep.lines) (void)hipFree(c->prep.lines);
   for (auto& kv : c->keysets) {
     (void)hipFree(kv.second.pk);
     (void)hipFree(kv.second.st);
@@ -1673,10 +1738,118 @@ int hbtc_verify_sig_shares(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, con
   HB_TRY(upload(c, "in2", sig, (size_t)96 * n, &d_sig));
   HB_TRY(ws(c, "out0", (size_t)4 * n, &d_st));
   PinLane pin(c);  // the uploads above went to the current lane
+  HostG2Args hg(c, d_H, H);
   HB_TRY(sig_shares_dev(c, keyset_id, n_inst, (const uint8_t*)d_H, offsets,
                         (const uint32_t*)d_idx, (const uint8_t*)d_sig, (int32_t*)d_st));
   HB_TRY(download(c, status, d_st, (size_t)4 * n));
   return sync(c);
+}
+
+// hbtc.h hbtc_prepare_g2: the new points' tables built by the usual preparation (k_g2_steps +
+// k_g2_norm) into a scratch batch, then copied into their resident slots.
+int hbtc_prepare_g2(hbtc_ctx* c, uint32_t n, const uint8_t* pts, int32_t* out_status) {
+  if (!c || (n && !pts)) return HBTC_ERR_ARG;
+  Guard g(c);
+  if (n == 0) return HBTC_OK;
+  HB_TRY(sync(c));  // no call in flight reads a slot this one fills
+  auto& P = c->prep;
+  std::vector<uint32_t> fresh;  // positions of points not prepared yet (first occurrence)
+  {
+    std::unordered_map<std::string, uint32_t> seen;
+    for (uint32_t i = 0; i < n; ++i) {
+      std::string key(reinterpret_cast<const char*>(pts + (size_t)96 * i), 96);
+      if (P.slot.count(key) || seen.count(key)) continue;
+      seen.emplace(std::move(key), i);
+      fresh.push_back(i);
+    }
+  }
+  const uint32_t m = (uint32_t)fresh.size();
+  if (m) {
+    const uint32_t reuse = std::min<uint32_t>(m, (uint32_t)P.free.size());
+    const uint32_t need = P.top + (m - reuse);
+    if (need > P.cap) {  // grow: new arrays, the resident slots copied over
+      const uint32_t cap = std::max<uint32_t>(std::max<uint32_t>(2 * P.cap, need), 64);
+      G2A* aff = nullptr;
+      int32_t* st = nullptr;
+      Line* lines = nullptr;
+      hipError_t e = hipMalloc(&aff, sizeof(G2A) * cap);
+      if (e == hipSuccess) e = hipMalloc(&st, sizeof(int32_t) * cap);
+      if (e == hipSuccess) e = hipMalloc(&lines, sizeof(Line) * (size_t)cap * MILLER_STEPS);
+      if (e == hipSuccess && P.top) e = launch_g2_tab_copy(c->stream, P.top, nullptr, nullptr, P.aff, P.st, P.lines,
+                                                          aff, st, lines);
+      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+      if (e != hipSuccess) {
+        if (aff) (void)hipFree(aff);
+        if (st) (void)hipFree(st);
+        if (lines) (void)hipFree(lines);
+        HB_CHECK(c, e);
+      }
+      if (P.aff) (void)hipFree(P.aff);
+      if (P.st) (void)hipFree(P.st);
+      if (P.lines) (void)hipFree(P.lines);
+      P.aff = aff;
+      P.st = st;
+      P.lines = lines;
+      P.cap = cap;
+    }
+    std::vector<uint32_t> slots(m);
+    std::vector<uint8_t> in((size_t)96 * m);
+    for (uint32_t j = 0; j < m; ++j) {
+      if (!P.free.empty()) {
+        slots[j] = P.free.back();
+        P.free.pop_back();
+      } else {
+        slots[j] = P.top++;
+      }
+      memcpy(in.data() + (size_t)96 * j, pts + (size_t)96 * fresh[j], 96);
+    }
+    void *d_in, *d_slots;
+    G2A* taff;
+    int32_t* tst;
+    Line* tl;
+    Fq2* tws;
+    HB_TRY(upload(c, "prep.in", in.data(), in.size(), &d_in));
+    HB_TRY(upload(c, "prep.slots", slots.data(), (size_t)4 * m, &d_slots));
+    HB_TRY(wst(c, "prep.aff", m, &taff));
+    HB_TRY(wst(c, "prep.st", m, &tst));
+    HB_TRY(wst(c, "prep.lines", (size_t)m * MILLER_STEPS, &tl));
+    HB_TRY(wst(c, "prep.ws", (size_t)m * 3 * MILLER_STEPS, &tws));
+    HB_TRY(timed(c, "prepare", [&] {
+      return launch_g2_prepare(c->stream, (const uint8_t*)d_in, m, nullptr, 0, taff, tl, tws, tst);
+    }));
+    HB_CHECK(c, launch_g2_tab_copy(c->stream, m, nullptr, (const uint32_t*)d_slots, taff, tst, tl, P.aff, P.st,
+                                   P.lines));
+    HB_TRY(sync(c));
+    for (uint32_t j = 0; j < m; ++j)
+      P.slot.emplace(std::string(reinterpret_cast<const char*>(pts + (size_t)96 * fresh[j]), 96), slots[j]);
+  }
+  if (out_status) {
+    std::vector<int32_t> st(P.top);
+    HB_CHECK(c, hipMemcpy(st.data(), P.st, sizeof(int32_t) * P.top, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < n; ++i)
+      out_status[i] = st[P.slot.at(std::string(reinterpret_cast<const char*>(pts + (size_t)96 * i), 96))];
+  }
+  return HBTC_OK;
+}
+
+int hbtc_unprepare_g2(hbtc_ctx* c, uint32_t n, const uint8_t* pts) {
+  if (!c || (n && !pts)) return HBTC_ERR_ARG;
+  Guard g(c);
+  HB_TRY(sync(c));  // calls in flight may still read the slots
+  for (uint32_t i = 0; i < n; ++i) {
+    auto it = c->prep.slot.find(std::string(reinterpret_cast<const char*>(pts + (size_t)96 * i), 96));
+    if (it == c->prep.slot.end()) continue;
+    c->prep.free.push_back(it->second);
+    c->prep.slot.erase(it);
+  }
+  return HBTC_OK;
+}
+
+int hbtc_prepared_g2_count(hbtc_ctx* c, uint32_t* count) {
+  if (!c || !count) return HBTC_ERR_ARG;
+  Guard g(c);
+  *count = (uint32_t)c->prep.slot.size();
+  return HBTC_OK;
 }
 
 int hbtc_keyset_set_master(hbtc_ctx* c, uint32_t keyset_id, const uint8_t* mpk) {
@@ -1795,8 +1968,11 @@ int hbtc_coin_decide(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_inst, const uin
     HB_CHECK(c, hipStreamWaitEvent(c->s_spec, c->ev_spec_out2, 0));
     HB_CHECK(c, hipEventRecord(c->ev_spec_out, c->s_spec));
   }
-  HB_TRY(sig_shares_dev(c, keyset_id, n_inst, (const uint8_t*)d_H, offsets, (const uint32_t*)d_idx,
-                        (const uint8_t*)d_sig, (int32_t*)d_st));
+  {
+    HostG2Args hg(c, d_H, H);
+    HB_TRY(sig_shares_dev(c, keyset_id, n_inst, (const uint8_t*)d_H, offsets, (const uint32_t*)d_idx,
+                          (const uint8_t*)d_sig, (int32_t*)d_st));
+  }
   const int32_t* d_item = (const int32_t*)d_st;
   if (spec) {
     HB_CHECK(c, hipStreamWaitEvent(c->stream, c->ev_spec_out, 0));
@@ -1891,13 +2067,17 @@ int pb_small_exact_chunk(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint
   key.bits = c->rlc_bits;
   const Suspects sus{nullptr, 0, counters, leaves, 1};
   HB_TRY(timed(c, "sig_items", [&] {
+    if (c->sig_fused)  // W decoded, listed and its line table built in one launch (k_sig_exact)
+      return launch_sig_exact(c->stream, n, d_idx, d_w, a_st, n, tiles, n_tiles, counters, leaves, dec,
+                              tables, inf, d_status);
     return launch_sig_items(c->stream, n_tiles, tiles, d_idx, d_w, A, a_st, nullptr, n, key, sus, sums,
                             dec, d_status);
   }));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
-  HB_TRY(timed(c, "sig_lines", [&] {
-    return launch_plines(c->stream, 2, n, 0, counters, leaves, tiles, sums, dec, tables, inf);
-  }));
+  if (!c->sig_fused)
+    HB_TRY(timed(c, "sig_lines", [&] {
+      return launch_plines(c->stream, 2, n, 0, counters, leaves, tiles, sums, dec, tables, inf);
+    }));
   HB_TRY(timed(c, "chk_leaves", [&] {
     const uint32_t lim = c->small_rep == 3 ? std::min(n, 8u * (uint32_t)c->n_cu) : 0u;
     const hipError_t e = launch_sigchk_leaves_rep3(c->stream, n, lim, counters, leaves, d_idx, A,
@@ -2086,6 +2266,7 @@ int hbtc_verify_dec_shares(hbtc_ctx* c, uint32_t keyset_id, uint32_t n_ct, const
   HB_TRY(upload(c, "in3", share, (size_t)48 * n, &d_sh));
   HB_TRY(ws(c, "out0", (size_t)4 * n, &d_st));
   PinLane pin(c);  // the uploads above went to the current lane
+  HostG2Args hg(c, d_H, H, d_w, w);
   HB_TRY(dec_shares_dev(c, keyset_id, n_ct, (const uint8_t*)d_H, (const uint8_t*)d_w, offsets,
                         (const uint32_t*)d_idx, (const uint8_t*)d_sh, (int32_t*)d_st));
   HB_TRY(download(c, status, d_st, (size_t)4 * n));

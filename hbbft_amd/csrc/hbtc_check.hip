@@ -861,7 +861,9 @@ __global__ void __launch_bounds__(64, REP == 1 ? HBTC_GT_WAVES : HBTC_GT_WAVES_S
   sig_pair_value(e, P, use1, h_lines + (size_t)k * MILLER_STEPS,
                  tables + (size_t)(active ? g : 0) * PLINES_FQ2, use2, ul.ps);
   const bool ok = gt::is_one(e, ul.ps);
-  if (active && ul.ps.k == 0 && ul.ps.sub == 0) status[item] = ok ? HBTC_ACCEPT : HBTC_REJECT;
+  // a share the fused exact pass (k_sig_exact) listed before its psi test failed keeps DECODE_ERR
+  if (active && ul.ps.k == 0 && ul.ps.sub == 0 && status[item] != HBTC_DECODE_ERR)
+    status[item] = ok ? HBTC_ACCEPT : HBTC_REJECT;
 }
 
 // ------------------------------------------------------------------------------ launchers

@@ -168,6 +168,15 @@ hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, 
 // (2 per tile: plain, weighted), mode 1 the 8 sub-tiles of the listed tiles (16 per listed
 // tile), mode 2 the listed leaf shares (decoded sigma).  inf[g] = 1: the sum is infinity.
 // (mode 2 handles leaves [base, base + max_groups) of the list: chunks bound the tables)
+// The exact small-call path of SignatureShares (and pair checks) in one launch (hbtc_sig.hip
+// k_sig_exact): decode, leaf listing of every decodable share of a known sender, its projective
+// line table at its leaf position, the psi subgroup test at the end of the line walk.  Tables
+// must hold n items.  hipErrorNotSupported when built without the lane-pair kernels.
+bool sig_exact_built();
+hipError_t launch_sig_exact(hipStream_t s, uint32_t n, const uint32_t* idx, const uint8_t* sigs,
+                            const int32_t* pk_status, uint32_t n_pk, const Tile* tiles, uint32_t n_tiles,
+                            uint32_t* leaf_count, uint32_t* leaves, G2A* dec, Fq2* tables, uint32_t* inf,
+                            int32_t* status);
 hipError_t launch_plines(hipStream_t s, int mode, uint32_t max_groups, uint32_t base,
                          const uint32_t* count, const uint32_t* list, const Tile* tiles,
                          const SigTileSums* sums, const G2A* dec, Fq2* tables, uint32_t* inf);
@@ -202,6 +211,9 @@ hipError_t launch_g1_decode(hipStream_t s, const uint8_t* in, uint32_t n, G1A* o
                             int32_t* status);
 // Decode + affine-normalised line tables of n0 + n1 G2 arguments (two input arrays, outputs
 // contiguous); ws holds 3 * MILLER_STEPS Fq2 per argument.
+// Copy prepared G2 tables entry by entry between slot arrays (ss / ds null: identity).
+hipError_t launch_g2_tab_copy(hipStream_t s, uint32_t n, const uint32_t* ss, const uint32_t* ds, const G2A* saff,
+                              const int32_t* sst, const Line* sl, G2A* daff, int32_t* dst, Line* dl);
 hipError_t launch_g2_prepare(hipStream_t s, const uint8_t* in0, uint32_t n0, const uint8_t* in1,
                              uint32_t n1, G2A* aff, Line* lines, Fq2* ws, int32_t* status);
 // ---- pair batches e(A_i, Q_i) == e(G1, W_i) by RLC (hbtc_pb.hip, checks in hbtc_check.hip)

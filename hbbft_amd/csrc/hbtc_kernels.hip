@@ -17,6 +17,7 @@
 //     reads the same line: the loads are wave-uniform and go through the scalar cache into
 //     SGPRs, which the multiplies consume directly as operands.
 #include "hbtc_kernels.h"
+#include "pair.h"
 
 // Kernel groups are selected by -DHBTC_PART (one group left since round 5: the per-item exact
 // kernels k_dec_verify / k_sig_verify / k_pair_verify, a whole Fq12 tower per lane and ~6 KB of
@@ -132,6 +133,54 @@ __global__ void __launch_bounds__(64) k_g2_steps(const uint8_t* __restrict__ in0
   fq2_neg(npy, py);
   ok = !jac_is_inf(T) && jac_eq_aff(T, px, npy);
   status[g] = ok ? HBTC_ACCEPT : HBTC_DECODE_ERR;
+}
+
+#ifndef HBTC_G2STEPS_PAIR
+#define HBTC_G2STEPS_PAIR 1  // k_g2_steps on lane pairs (pair.h): the 68 steps at half the latency
+#endif
+#if HBTC_G2STEPS_PAIR
+// k_g2_steps on lane pairs: argument g on lanes (2g, 2g + 1).  The decode (square roots) runs on
+// both lanes in one-lane form, the 68 line steps and the psi test in pair form.
+__global__ void __launch_bounds__(64) k_g2_steps_pair(const uint8_t* __restrict__ in0, uint32_t n0,
+                                                      const uint8_t* __restrict__ in1, uint32_t n1,
+                                                      G2A* __restrict__ aff, Fq2* __restrict__ ws,
+                                                      int32_t* __restrict__ status) {
+  HBTC_LATENCY_PRIO();
+  const uint32_t g = (blockIdx.x * 64 + threadIdx.x) >> 1;
+  const bool even = (threadIdx.x & 1u) == 0;
+  if (g >= n0 + n1) return;  // pair-uniform
+  uint32_t w[24];
+  load_words(w, g < n0 ? in0 : in1, g < n0 ? g : g - n0, 24);
+  G2A q;
+  bool ok = g2_decompress(q, w, false);
+  if (even) aff[g] = q;
+  if (ok && !q.inf) {
+    G2Ap Q;
+    g2p_from_full(Q, q);
+    G2Jp T;
+    g2p_walk_lines(ws + (size_t)g * 3 * MILLER_STEPS, T, Q);
+    ok = g2p_psi_test(T, Q);
+  }
+  if (even) status[g] = ok ? HBTC_ACCEPT : HBTC_DECODE_ERR;
+}
+#endif
+
+// Prepared G2 tables (hbtc.h hbtc_prepare_g2): entry i copied from slot ss[i] to slot ds[i]
+// (null: i) -- the decoded point, its status and its 68 affine lines, one lane per (entry, line).
+__global__ void __launch_bounds__(64) k_g2_tab_copy(uint32_t n, const uint32_t* __restrict__ ss,
+                                                    const uint32_t* __restrict__ ds,
+                                                    const G2A* __restrict__ saff, const int32_t* __restrict__ sst,
+                                                    const Line* __restrict__ sl, G2A* __restrict__ daff,
+                                                    int32_t* __restrict__ dst, Line* __restrict__ dl) {
+  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+  if (g >= n * MILLER_STEPS) return;
+  const uint32_t i = g / MILLER_STEPS, j = g % MILLER_STEPS;
+  const uint32_t s = ss ? ss[i] : i, d = ds ? ds[i] : i;
+  dl[(size_t)d * MILLER_STEPS + j] = sl[(size_t)s * MILLER_STEPS + j];
+  if (j == 0) {
+    daff[d] = saff[s];
+    dst[d] = sst[s];
+  }
 }
 
 // One lane per (argument, step): the affine-normalised line (A / C, B / C) (pairing.h Line).
@@ -283,12 +332,25 @@ hipError_t launch_pk_table(hipStream_t s, const G1A* pk, const int32_t* pk_statu
   return hipGetLastError();
 }
 
+hipError_t launch_g2_tab_copy(hipStream_t s, uint32_t n, const uint32_t* ss, const uint32_t* ds, const G2A* saff,
+                              const int32_t* sst, const Line* sl, G2A* daff, int32_t* dst, Line* dl) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_g2_tab_copy, dim3(blocks_for((uint64_t)n * MILLER_STEPS, 64)), dim3(64), 0, s, n, ss, ds,
+                     saff, sst, sl, daff, dst, dl);
+  return hipGetLastError();
+}
+
 hipError_t launch_g2_prepare(hipStream_t s, const uint8_t* in0, uint32_t n0, const uint8_t* in1,
                              uint32_t n1, G2A* aff, Line* lines, Fq2* ws, int32_t* status) {
   const uint32_t n = n0 + n1;
   if (n == 0) return hipSuccess;
+#if HBTC_G2STEPS_PAIR
+  hipLaunchKernelGGL(k_g2_steps_pair, dim3(blocks_for(2 * (uint64_t)n, 64)), dim3(64), 0, s, in0, n0, in1,
+                     n1, aff, ws, status);
+#else
   hipLaunchKernelGGL(k_g2_steps, dim3(blocks_for(n, 64)), dim3(64), 0, s, in0, n0, in1, n1, aff, ws,
                      status);
+#endif
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_g2_norm, dim3(blocks_for((uint64_t)n * MILLER_STEPS, 64)), dim3(64), 0, s, n,

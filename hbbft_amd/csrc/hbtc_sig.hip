@@ -103,6 +103,81 @@ hipError_t launch_sig_decode(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
 hipError_t launch_sig_decode(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                              const uint8_t* sigs, const int32_t* pk_status, uint32_t n_pk, G2A* dec,
                              int32_t* status);
+#ifndef HBTC_SIGDEC_PAIR
+#define HBTC_SIGDEC_PAIR 1  // k_sig_decode with its psi chains on lane pairs (k_sig_decode_pair)
+#endif
+#ifndef HBTC_SIGDEC_WAVES
+#define HBTC_SIGDEC_WAVES 2
+#endif
+#if HBTC_SIGDEC_PAIR
+// The decode half of the SignatureShare item pass with the subgroup test's chain on lane pairs:
+// every lane decodes one share (the square roots, one-lane form: no redundant work), then each lane
+// pair runs the psi test of its two shares one after the other in pair form ([|x|] P: 63 doublings
+// and 5 additions, the point exchanged from its lane by DPP), so the chain's state is 36 + 24
+// registers per lane instead of 72 + 48 and the kernel runs more waves per SIMD.
+__global__ void __launch_bounds__(64, HBTC_SIGDEC_WAVES) k_sig_decode_pair(
+    const Tile* __restrict__ tiles, const uint32_t* __restrict__ idx, const uint8_t* __restrict__ sigs,
+    const int32_t* __restrict__ pk_status, uint32_t n_pk, G2A* __restrict__ dec,
+    int32_t* __restrict__ status) {
+  const Tile tile = tiles[blockIdx.x];
+  const uint32_t lane = threadIdx.x;
+  const size_t item = (size_t)tile.first + lane;
+  const bool in = lane < tile.count;
+  int32_t st = HBTC_RLC_PENDING;
+  bool test = false;  // decoded, not infinity: needs the subgroup test
+  G2A sg;
+  fq2_zero(sg.x);
+  fq2_zero(sg.y);
+  sg.inf = 1;
+  if (in) {
+    const uint32_t id = idx[item];
+    if (id < n_pk && pk_status[id] == HBTC_ACCEPT) {
+      uint32_t w[24];
+      rlc_load_words(w, sigs, item, 24);
+      if (!g2_decompress(sg, w, false)) {
+        st = HBTC_DECODE_ERR;
+      } else {
+        dec[item] = sg;
+        test = !sg.inf;
+      }
+    }
+  }
+  const bool odd = (lane & 1u) != 0;
+#pragma unroll 1
+  for (uint32_t k = 0; k < 2; ++k) {
+    // the pair's share k (held by lane 2j + k): each lane takes its component of it
+    const bool holder = (odd ? 1u : 0u) == k;
+    G2Ap P;
+    {
+      Fq sx, sy, rx, ry;
+      fq_sel(sx, odd, sg.x.c0, sg.x.c1);  // what the partner needs: the other component
+      fq_sel(sy, odd, sg.y.c0, sg.y.c1);
+      fq_xchg(rx, sx);
+      fq_xchg(ry, sy);
+      Fq ox, oy;
+      fq_sel(ox, odd, sg.x.c1, sg.x.c0);  // the own component of the own share
+      fq_sel(oy, odd, sg.y.c1, sg.y.c0);
+      fq_sel(P.x.v, holder, ox, rx);
+      fq_sel(P.y.v, holder, oy, ry);
+      P.inf = 0;
+    }
+    const uint32_t t_other = pair_xchg(test ? 1u : 0u);
+    const bool run = holder ? test : t_other != 0u;  // pair-uniform
+    if (run) {
+      G2Jp t;
+      jac_from_aff(t, P);  // bit 63 of |x|
+#pragma unroll 1
+      for (int b = 62; b >= 0; --b) {
+        jac_dbl(t, t);
+        if ((BLS_X_ABS >> b) & 1ull) jac_add_aff(t, t, P);
+      }
+      const bool ok = g2p_psi_test(t, P);
+      if (holder && !ok) st = HBTC_DECODE_ERR;
+    }
+  }
+  if (in) status[item] = st;
+}
+#endif
 // One wave per tile: decode every SignatureShare (zcash compressed G2 + subgroup check), r_i,
 // r_i sigma_i, r_i pk_i, then the plain and weighted tile / sub-tile sums in both groups.  One
 // wave per SIMD (256 VGPRs + 256 AGPRs).  No kernel keeps a multi-KB private segment any more:
@@ -458,6 +533,76 @@ __global__ void __launch_bounds__(128, HBTC_SIGP_WAVES) k_sig_items_pair(
 }
 #endif
 
+#if HBTC_SIG_PAIR
+// The exact small-call path in ONE kernel (round 6): per SignatureShare on a lane pair, the zcash
+// decode (square roots, one-lane form on both lanes), the leaf listing (every decodable share of a
+// known sender), then its 68 projective Miller lines straight into the leaf's table (pair form,
+// g2p_walk_lines), whose double-and-add ends at [|x|] sigma: the psi subgroup test needs no chain
+// of its own.  A share failing that test is DECODE_ERR (k_sigchk_leaves skips it).  Replaces
+// k_sig_decode (decode + a separate psi chain), k_sig_items (the listing) and k_plines (an
+// inversion and the 68 steps on one lane): three dependent launches of c1's chain.
+__global__ void __launch_bounds__(64) k_sig_exact(uint32_t n, const uint32_t* __restrict__ idx,
+                                                  const uint8_t* __restrict__ sigs,
+                                                  const int32_t* __restrict__ pk_status, uint32_t n_pk,
+                                                  const Tile* __restrict__ tiles, uint32_t n_tiles,
+                                                  uint32_t* __restrict__ leaf_count, uint32_t* __restrict__ leaves,
+                                                  G2A* __restrict__ dec, Fq2* __restrict__ tables,
+                                                  uint32_t* __restrict__ inf, int32_t* __restrict__ status) {
+  HBTC_LATENCY_PRIO();
+  const uint32_t item = (blockIdx.x * 64 + threadIdx.x) >> 1;
+  const bool even = (threadIdx.x & 1u) == 0;
+  const bool in = item < n;
+  int32_t st = HBTC_DECODE_ERR;
+  bool leaf = false;
+  G2A sg;
+  sg.inf = 1;
+  uint32_t inst = 0;
+  if (in) {
+    const uint32_t id = idx[item];
+    uint32_t lo = 0, hi = n_tiles;  // the last tile starting at or before the item
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (tiles[mid].first <= item) lo = mid; else hi = mid;
+    }
+    inst = tiles[lo].inst;
+    if (id >= n_pk) {
+      st = HBTC_UNKNOWN_SENDER;
+    } else if (pk_status[id] == HBTC_ACCEPT) {
+      uint32_t w[24];
+      rlc_load_words(w, sigs, item, 24);
+      if (g2_decompress(sg, w, false)) {
+        st = HBTC_RLC_LEAF;
+        leaf = true;
+        if (even) dec[item] = sg;
+      }
+    }
+  }
+  // the leaf position: one atomic per wave over the even lanes, then to the odd lane
+  const uint64_t m = __ballot(leaf && even);
+  uint32_t base = 0;
+  if (m && (threadIdx.x & 63u) == 0) base = atomicAdd(leaf_count, (uint32_t)__popcll(m));
+  base = __shfl(base, 0);
+  const uint32_t mine = base + (uint32_t)__popcll(m & ((1ull << (threadIdx.x & 63u)) - 1ull));
+  const uint32_t other = pair_xchg(mine);  // odd lanes hold no bit of m: the even lane's slot
+  const uint32_t pos = even ? mine : other;
+  if (leaf) {
+    if (even) {
+      leaves[2 * pos] = item;
+      leaves[2 * pos + 1] = inst;
+      inf[pos] = sg.inf;
+    }
+    if (!sg.inf) {
+      G2Ap Q;
+      g2p_from_full(Q, sg);
+      G2Jp T;
+      g2p_walk_lines(tables + (size_t)pos * PLINES_FQ2, T, Q);
+      if (!g2p_psi_test(T, Q)) st = HBTC_DECODE_ERR;
+    }
+  }
+  if (in && even) status[item] = st;
+}
+#endif
+
 // Projective line table of one G2 sum: affine (one Fq2 inversion) then the 68 steps.
 __device__ __forceinline__ void g2j_plines(Fq2* out, uint32_t* inf, const G2J& S) {
   if (jac_is_inf(S)) {
@@ -523,6 +668,72 @@ __global__ void __launch_bounds__(64) k_plines(int mode, uint32_t max_groups, ui
   g2j_plines(tables + (size_t)g * PLINES_FQ2, inf + g, S);
 }
 
+#ifndef HBTC_PLINES_PAIR
+#define HBTC_PLINES_PAIR HBTC_SIG_PAIR
+#endif
+#if HBTC_PLINES_PAIR
+// k_plines on lane pairs: group g on lanes (2g, 2g + 1); the affine normalisation (one binary-GCD
+// inversion of the norm) and the 68 projective steps in pair form (g2p_walk_lines).
+#ifndef HBTC_PLINES_WAVES
+#define HBTC_PLINES_WAVES 2
+#endif
+__global__ void __launch_bounds__(64, HBTC_PLINES_WAVES) k_plines_pair(int mode, uint32_t max_groups, uint32_t base,
+                                                    const uint32_t* __restrict__ count,
+                                                    const uint32_t* __restrict__ list,
+                                                    const Tile* __restrict__ tiles,
+                                                    const SigTileSums* __restrict__ sums,
+                                                    const G2A* __restrict__ dec,
+                                                    Fq2* __restrict__ tables,
+                                                    uint32_t* __restrict__ inf) {
+  HBTC_LATENCY_PRIO();
+  const uint32_t g = (blockIdx.x * 64 + threadIdx.x) >> 1;
+  const bool even = (threadIdx.x & 1u) == 0;
+  const uint32_t c = (mode == 0 || mode == 3) ? 0u : *count;
+  const uint32_t n = (mode == 0 || mode == 3) ? max_groups
+                   : mode == 1 ? c * 16u
+                   : mode == 4 ? c * 8u
+                               : (c > base ? min(c - base, max_groups) : 0u);
+  if (g >= n) return;  // pair-uniform
+  G2Jp S;
+  if (mode == 3) {
+    g2p_load_jac(S, &sums[g].S[8]);
+  } else if (mode == 4) {
+    g2p_load_jac(S, &sums[list[g >> 3]].S[g & 7u]);
+  } else if (mode == 0) {
+    const uint32_t t = g >> 1;
+    g2p_load_jac(S, (g & 1u) ? &sums[t].SW[8] : &sums[t].S[8]);
+  } else if (mode == 1) {
+    const uint32_t t = list[g >> 4], sub = (g >> 1) & 7u;
+    const Tile tile = tiles[t];
+    if (sub * 8u >= tile.count)
+      jac_set_inf(S);
+    else
+      g2p_load_jac(S, (g & 1u) ? &sums[t].SW[sub] : &sums[t].S[sub]);
+  } else {
+    G2Ap a;
+    g2p_load_aff(a, dec + list[2 * (base + g)]);
+    jac_from_aff(S, a);
+  }
+  if (jac_is_inf(S)) {
+    if (even) inf[g] = 1;
+    return;
+  }
+  if (even) inf[g] = 0;
+  G2Ap Q;
+  {
+    Fq2p zi, zi2, zi3;
+    finv_fast(zi, S.z);
+    fsqr(zi2, zi);
+    fmul(zi3, zi2, zi);
+    fmul(Q.x, S.x, zi2);
+    fmul(Q.y, S.y, zi3);
+    Q.inf = 0;
+  }
+  G2Jp T;
+  g2p_walk_lines(tables + (size_t)g * PLINES_FQ2, T, Q);
+}
+#endif
+
 static inline uint32_t sig_blocks(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
 
 hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
@@ -531,7 +742,13 @@ hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, 
                             SigTileSums* sums, G2A* dec, int32_t* status) {
   if (n_tiles == 0) return hipSuccess;
 #if HBTC_SIG_SPLIT
+#if HBTC_SIGDEC_PAIR
+  hipLaunchKernelGGL(k_sig_decode_pair, dim3(n_tiles), dim3(64), 0, s, tiles, idx, sigs, pk_status, n_pk, dec,
+                     status);
+  const hipError_t e = hipGetLastError();
+#else
   const hipError_t e = launch_sig_decode(s, n_tiles, tiles, idx, sigs, pk_status, n_pk, dec, status);
+#endif
   if (e != hipSuccess) return e;
 #endif
 #if HBTC_SIG_PAIR && HBTC_SIG_SPLIT
@@ -544,12 +761,33 @@ hipError_t launch_sig_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, 
   return hipGetLastError();
 }
 
+bool sig_exact_built() { return HBTC_SIG_PAIR != 0; }
+
+hipError_t launch_sig_exact(hipStream_t s, uint32_t n, const uint32_t* idx, const uint8_t* sigs,
+                            const int32_t* pk_status, uint32_t n_pk, const Tile* tiles, uint32_t n_tiles,
+                            uint32_t* leaf_count, uint32_t* leaves, G2A* dec, Fq2* tables, uint32_t* inf,
+                            int32_t* status) {
+#if HBTC_SIG_PAIR
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sig_exact, dim3(sig_blocks(2 * (uint64_t)n, 64)), dim3(64), 0, s, n, idx, sigs, pk_status,
+                     n_pk, tiles, n_tiles, leaf_count, leaves, dec, tables, inf, status);
+  return hipGetLastError();
+#else
+  return hipErrorNotSupported;
+#endif
+}
+
 hipError_t launch_plines(hipStream_t s, int mode, uint32_t max_groups, uint32_t base,
                          const uint32_t* count, const uint32_t* list, const Tile* tiles,
                          const SigTileSums* sums, const G2A* dec, Fq2* tables, uint32_t* inf) {
   if (max_groups == 0) return hipSuccess;
+#if HBTC_PLINES_PAIR
+  hipLaunchKernelGGL(k_plines_pair, dim3(sig_blocks(2 * (uint64_t)max_groups, 64)), dim3(64), 0, s, mode,
+                     max_groups, base, count, list, tiles, sums, dec, tables, inf);
+#else
   hipLaunchKernelGGL(k_plines, dim3(sig_blocks(max_groups, 64)), dim3(64), 0, s, mode, max_groups,
                      base, count, list, tiles, sums, dec, tables, inf);
+#endif
   return hipGetLastError();
 }
 #endif  // part 2

@@ -47,7 +47,15 @@ HD void fq_xchg(Fq& r, const Fq& a) {
 #pragma unroll
   for (int i = 0; i < 12; ++i) r.v[i] = pair_xchg(a.v[i]);
 }
-HD bool pair_all(bool b) { return b && pair_xchg(b ? 1u : 0u) != 0u; }
+// both lanes' b.  The exchange runs on both lanes unconditionally: a short-circuit `b && xchg(b)`
+// would leave the lane with b = false out of the DPP, and its partner would read a disabled lane
+// (this broke every pair test of a point with one zero component, e.g. Z = (1, 0) after
+// jac_from_aff).
+HD bool pair_all(bool b) {
+  const uint32_t mine = b ? 1u : 0u;
+  const uint32_t other = pair_xchg(mine);
+  return (mine & other) != 0u;
+}
 
 // MONT(a b + c d) for operands < 2p: < 8p^2 before the reduction, < 2p after (one product
 // scanning of both products: fq_fips_sr.h hbtc_fqmul2_sr, 432 MACs)

@@ -107,6 +107,21 @@ int hbtc_verify_sigs(hbtc_ctx* ctx, uint32_t n, const uint8_t* pk_c48, const uin
  * HBTC_OK, or HBTC_ERR_ARG when it fails to decode (the key set keeps no master key then). */
 int hbtc_keyset_set_master(hbtc_ctx* ctx, uint32_t keyset_id, const uint8_t* master_pk_c48);
 
+/* Per-instance G2 preparation ahead of the shares.  hbbft knows a coin's nonce when it creates
+ * the Coin (src/binary_agreement/binary_agreement.rs:320; H = hash_g2(nonce)) and a ciphertext
+ * at set_ciphertext (src/threshold_decryption.rs:94-113; H = hash_g1_g2(u, v) and w), before most
+ * shares arrive.  hbtc_prepare_g2 decodes n compressed G2 points (subgroup-checked) and builds
+ * their Miller-line tables, kept resident and keyed by the 96 bytes.  A later
+ * hbtc_verify_sig_shares / hbtc_coin_decide / hbtc_verify_dec_shares / *_epoch_submit call whose
+ * per-instance G2 arguments are ALL prepared copies their tables instead of building them; the
+ * outputs are identical either way.  out_status[i] (optional): HBTC_ACCEPT, or HBTC_DECODE_ERR
+ * for a point that fails to decode (a call with it reports the instance error as usual).  Points
+ * already prepared are not rebuilt.  Entries stay until hbtc_unprepare_g2 (unknown points are
+ * ignored) or hbtc_ctx_destroy.  Both calls wait for the context's calls in flight. */
+int hbtc_prepare_g2(hbtc_ctx* ctx, uint32_t n, const uint8_t* g2_c96, int32_t* out_status);
+int hbtc_unprepare_g2(hbtc_ctx* ctx, uint32_t n, const uint8_t* g2_c96);
+int hbtc_prepared_g2_count(hbtc_ctx* ctx, uint32_t* count);
+
 /* A Threshold Coin round of n_inst coin instances in ONE call (the batch queue of src/coin.rs:
  * 149-207): every SignatureShare verified as hbtc_verify_sig_shares (status[i], coin.rs:151),
  * the first t ACCEPTed shares of each instance combined (combine_signatures, coin.rs:185-191:
