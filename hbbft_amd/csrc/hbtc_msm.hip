@@ -33,6 +33,7 @@
 //   roff   [m][w][r]      u32 start of bucket rank r (rank 0 = bucket 2^(c-1)), r = 0..B
 //   part   [m][w][s]      Jac<F> segment partial sums;  wsum [m][w] Jac<F>
 #include "hbtc_kernels.h"
+#include "pair.h"
 
 #ifndef HBTC_PART
 #define HBTC_PART 0
@@ -692,6 +693,130 @@ template __global__ void k_msm_final<Fq2, 24>(uint32_t, uint32_t, uint32_t, cons
                                               const uint32_t*, int32_t*, uint8_t*, uint8_t*);
 #endif
 
+#ifndef HBTC_MSM_G2_PAIR
+#define HBTC_MSM_G2_PAIR 1  // the G2 bucket / window / final passes on lane pairs (pair.h)
+#endif
+#ifndef HBTC_MSM_G2P_WAVES
+#define HBTC_MSM_G2P_WAVES 2
+#endif
+#ifndef HBTC_MSM_G2P_BUCKET_WAVES
+#define HBTC_MSM_G2P_BUCKET_WAVES HBTC_MSM_G2P_WAVES
+#endif
+#if HBTC_IN_PART(9) && HBTC_MSM_G2_PAIR
+// The three G2 reduction passes above on lane pairs (round 6): unit g (one (msm, window,
+// segment) slice, one window sum, one MSM) on lanes 2g, 2g + 1, lane 2g + e holding component e
+// of every Fq2 (pair.h): each Fq2 product is one fused two-product per lane, half the one-lane
+// chain's latency, and the state fits two waves per SIMD where the one-lane form runs one.  All
+// control flow depends on g only (pair-uniform).  Same outputs as k_msm_buckets / k_msm_wsum /
+// k_msm_final<Fq2, 24>.
+__global__ void __launch_bounds__(64, HBTC_MSM_G2P_BUCKET_WAVES)
+    k_msm_buckets_g2p(uint64_t n_lanes, uint32_t n, uint32_t c, uint32_t W,
+                      const G2A* __restrict__ pts, const uint32_t* __restrict__ list,
+                      const uint32_t* __restrict__ roff, const uint32_t* __restrict__ pts_map,
+                      G2J* __restrict__ part) {
+  HBTC_LATENCY_PRIO();
+  const uint64_t g = ((uint64_t)blockIdx.x * 64 + threadIdx.x) >> 1;
+  if (g >= n_lanes) return;  // pair-uniform
+  const uint32_t B = 1u << (c - 1), S = B / 8;
+  const uint32_t s = (uint32_t)(g % S);
+  const uint64_t mw = g / S;
+  const uint32_t* ro = roff + mw * (B + 1);
+  const uint32_t* L = list + mw * n;
+  const uint64_t blk = pts_map ? (uint64_t)pts_map[mw / W] : mw / W;
+  const G2A* P = pts + blk * n;
+  G2Jp run, tot;
+  jac_set_inf(run);
+  jac_set_inf(tot);
+  const uint32_t total = ro[B];
+  const uint32_t p0 = (uint32_t)((uint64_t)total * s / S);
+  const uint32_t p1 = (uint32_t)((uint64_t)total * (s + 1) / S);
+  if (p0 < p1) {
+    const uint32_t r_last = msm_rank(ro, B, p1 - 1);
+    uint32_t e = p0;
+    for (uint32_t r = msm_rank(ro, B, p0); r <= r_last; ++r) {
+      const uint32_t end = min(ro[r + 1], p1);
+      for (; e < end; ++e) {
+        const uint32_t v = L[e];
+        G2Ap q;
+        g2p_load_aff(q, P + (v & 0x7fffffffu));
+        if (v >> 31) fneg(q.y, q.y);
+        jac_add_aff(run, run, q);
+      }
+      jac_add(tot, tot, run);
+    }
+    const uint32_t base = B - r_last - 1;
+    if (base) {
+      G2Jp m;
+      jac_mul_small(m, run, base);
+      jac_add(tot, tot, m);
+    }
+  }
+  g2p_store_jac(part + g, tot);
+}
+
+__global__ void __launch_bounds__(64, HBTC_MSM_G2P_WAVES)
+    k_msm_wsum_g2p(uint64_t n_mw, uint32_t S, const G2J* __restrict__ part,
+                   G2J* __restrict__ wsum) {
+  HBTC_LATENCY_PRIO();
+  const uint64_t g = ((uint64_t)blockIdx.x * 64 + threadIdx.x) >> 1;
+  if (g >= n_mw) return;
+  const G2J* p = part + g * S;
+  G2Jp acc, x;
+  g2p_load_jac(acc, p);
+  for (uint32_t s = 1; s < S; ++s) {
+    g2p_load_jac(x, p + s);
+    jac_add(acc, acc, x);
+  }
+  g2p_store_jac(wsum + g, acc);
+}
+
+__global__ void __launch_bounds__(64, HBTC_MSM_G2P_WAVES)
+    k_msm_final_g2p(uint32_t n_msm, uint32_t c, uint32_t W, const G2J* __restrict__ wsum,
+                    const uint32_t* __restrict__ sel_cnt, uint32_t t,
+                    const uint32_t* __restrict__ bad, const uint32_t* __restrict__ dup,
+                    int32_t* __restrict__ status, uint8_t* __restrict__ out,
+                    uint8_t* __restrict__ parity) {
+  HBTC_LATENCY_PRIO();
+  const uint32_t m = (blockIdx.x * 64 + threadIdx.x) >> 1;
+  if (m >= n_msm) return;
+  const G2J* ws = wsum + (size_t)m * W;
+  G2Jp acc, x;
+  g2p_load_jac(acc, ws + (W - 1));
+  for (int w = (int)W - 2; w >= 0; --w) {
+    for (uint32_t j = 0; j < c; ++j) jac_dbl(acc, acc);
+    g2p_load_jac(x, ws + w);
+    jac_add(acc, acc, x);
+  }
+  int32_t st = HBTC_ACCEPT;
+  if (sel_cnt && sel_cnt[m] < t)
+    st = HBTC_NOT_ENOUGH_SHARES;
+  else if (bad[m])
+    st = HBTC_DECODE_ERR;
+  else if (dup && dup[m])
+    st = HBTC_DUPLICATE_ENTRY;
+  const bool si = jac_is_inf(acc);
+  G2Ap ap;
+  jac_to_aff(ap, acc);
+  Fq px, py;  // the partner's components: the even lane assembles the Fq2 point
+  fq_xchg(px, ap.x.v);
+  fq_xchg(py, ap.y.v);
+  if (pair_odd()) return;
+  status[m] = st;
+  G2A a;
+  a.x.c0 = ap.x.v;
+  a.x.c1 = px;
+  a.y.c0 = ap.y.v;
+  a.y.c1 = py;
+  a.inf = si ? 1u : 0u;
+  uint32_t w[24];
+  msm_compress(w, a);
+  if (st != HBTC_ACCEPT)
+    for (int j = 0; j < 24; ++j) w[j] = 0;
+  msm_store_words(out, m, w, 24);
+  if (parity) parity[m] = (st == HBTC_ACCEPT) ? (uint8_t)msm_parity(a) : 0;
+}
+#endif
+
 // ------------------------------------------------------------------ launchers
 static inline uint32_t msm_blocks(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
 
@@ -929,8 +1054,24 @@ hipError_t launch_msm_reduce_g2(hipStream_t s, const MsmPlan& p, const G2A* pts,
                                 const uint32_t* dup, int32_t* status, uint8_t* out,
                                 uint8_t* parity) {
   if (p.n_msm == 0) return hipSuccess;
+#if HBTC_MSM_G2_PAIR
+  const uint32_t S = (1u << (p.c - 1)) / 8;
+  const uint64_t lanes = (uint64_t)p.n_msm * p.W * S;
+  hipLaunchKernelGGL(k_msm_buckets_g2p, dim3(msm_blocks(2 * lanes, 64)), dim3(64), 0, s, lanes, p.n,
+                     p.c, p.W, pts, list, roff, pts_map, part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint64_t n_mw = (uint64_t)p.n_msm * p.W;
+  hipLaunchKernelGGL(k_msm_wsum_g2p, dim3(msm_blocks(2 * n_mw, 64)), dim3(64), 0, s, n_mw, S,
+                     (const G2J*)part, wsum);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_msm_final_g2p, dim3(msm_blocks(2 * (uint64_t)p.n_msm, 64)), dim3(64), 0, s,
+                     p.n_msm, p.c, p.W, (const G2J*)wsum, sel_cnt, t, bad, dup, status, out, parity);
+  return hipGetLastError();
+#else
   return launch_msm_reduce<Fq2, 24>(s, p, pts, pts_map, list, roff, part, wsum, sel_cnt, t, bad, dup, status,
                                     out, parity);
+#endif
 }
 #endif
 
