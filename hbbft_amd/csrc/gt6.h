@@ -116,8 +116,10 @@ HD void mul2_one(Fq2& r, const Fq2& a, const Fq2& b) {
 #pragma unroll 1
   for (uint32_t t = 0; t < 3; ++t) {
     Fq x, y, q;
-    fq_sel(x, t == 0, a.c0, t == 1 ? a.c1 : sa);
-    fq_sel(y, t == 0, b.c0, t == 1 ? b.c1 : sb);
+    fq_sel(x, t == 1, a.c1, sa);
+    fq_sel(x, t == 0, a.c0, x);
+    fq_sel(y, t == 1, b.c1, sb);
+    fq_sel(y, t == 0, b.c0, y);
     fq_mul(q, x, y);
     fq_sel(t0, t == 0, q, t0);
     fq_sel(t1, t == 1, q, t1);
@@ -133,7 +135,9 @@ HD void mul2_fq_one(Fq2& r, const Fq2& a, const Fq& y) {
 #pragma unroll 1
   for (uint32_t t = 0; t < 2; ++t) {
     Fq q;
-    fq_mul(q, t == 0 ? a.c0 : a.c1, y);
+    Fq x;
+    fq_sel(x, t == 0, a.c0, a.c1);
+    fq_mul(q, x, y);
     fq_sel(t0, t == 0, q, t0);
     r.c1 = q;
   }
@@ -155,8 +159,10 @@ HD void mul2(Fq2& r, const Fq2& a, const Fq2& b, const Pos& ps) {
     Fq sa, sb;
     fq_add(sa, a.c0, a.c1);
     fq_add(sb, b.c0, b.c1);
-    fq_sel(x, ps.sub == 0, a.c0, ps.sub == 1 ? a.c1 : sa);
-    fq_sel(y, ps.sub == 0, b.c0, ps.sub == 1 ? b.c1 : sb);
+    fq_sel(x, ps.sub == 1, a.c1, sa);
+    fq_sel(x, ps.sub == 0, a.c0, x);
+    fq_sel(y, ps.sub == 1, b.c1, sb);
+    fq_sel(y, ps.sub == 0, b.c0, y);
   }
   fq_mul(t, x, y);
   const uint32_t l0 = ps.base + ps.rep * ps.k;  // sub-lane 0 of this coefficient
@@ -286,6 +292,68 @@ HD void redc_pass(Fq2& r, const FqAcc& a0, const FqAcc& a1, uint32_t h) {
   }
 }
 
+// LDS staging of the operands of mul / sqr (device, rep = 1): each lane stores its coefficient
+// once and every term reads the one it needs from the group's lanes, so the operands are not
+// live in VGPRs across the term loop.  With them live (48 VGPRs) beside the accumulators and the
+// shared subroutines' fixed registers, the three-wave check kernels reloaded a and b from
+// scratch in every iteration (k_chk_plain: 576 B/lane, 618 spill instructions).  The stage is one
+// [word][lane] array per wave (12 KB; every kernel using these runs one wave per block), read
+// in program order by the same wave (LDS operations of a wave complete in order).
+#ifndef HBTC_GT_LDS
+#define HBTC_GT_LDS 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && HBTC_GT_LDS
+constexpr uint32_t GT_STAGE_WORDS = 24u * 64u;
+__device__ __forceinline__ uint32_t* gt_stage() {
+  __shared__ uint32_t s_gt_stage[2 * GT_STAGE_WORDS];
+  return s_gt_stage;
+}
+__device__ __forceinline__ void stage_put(uint32_t* s, const Fq2& x) {
+  const uint32_t l = lane_id();
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&x);
+#pragma unroll
+  for (int i = 0; i < 24; ++i) s[i * 64 + l] = w[i];
+}
+__device__ __forceinline__ void stage_get(Fq2& x, const uint32_t* s, uint32_t from) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(&x);
+#pragma unroll
+  for (int i = 0; i < 24; ++i) w[i] = s[i * 64 + from];
+}
+#define HBTC_GT_STAGED 1
+#else
+#define HBTC_GT_STAGED 0
+#endif
+
+#if HBTC_GT_STAGED
+// f = a * b with both operands staged (sa, sb)
+GTN void mul_staged(Fq2& f, const uint32_t* sa, const uint32_t* sb, const Pos& ps) {
+  Fq2 r;
+#pragma unroll
+  for (uint32_t h = 0; h < GT_LAZY_PASSES; ++h) {
+    FqAcc a0, a1;
+    acc_init(a0, a1);
+#pragma unroll 1
+    for (uint32_t i = 0; i < 6; ++i) {
+      const bool wrap = i > ps.k;
+      const uint32_t j = wrap ? ps.k + 6 - i : ps.k - i;
+      Fq2 ai, bj;
+      stage_get(ai, sa, src(ps, i));
+      stage_get(bj, sb, src(ps, j));
+      fq2_xi_if(bj, wrap, bj);
+      mac2_pass(a0, a1, ai, bj, h);
+    }
+    redc_pass(r, a0, a1, h);
+  }
+  f = r;
+}
+GTN void mul_lazy(Fq2& f, const Fq2& a, const Fq2& b, const Pos& ps) {
+  uint32_t* sa = gt_stage();
+  uint32_t* sb = sa + GT_STAGE_WORDS;
+  stage_put(sa, a);
+  stage_put(sb, b);
+  mul_staged(f, sa, sb, ps);
+}
+#else
 GTN void mul_lazy(Fq2& f, const Fq2& a, const Fq2& b, const Pos& ps) {
   Fq2 r;
 #pragma unroll
@@ -306,6 +374,7 @@ GTN void mul_lazy(Fq2& f, const Fq2& a, const Fq2& b, const Pos& ps) {
   }
   f = r;
 }
+#endif
 #endif
 
 // f = a * b
@@ -366,6 +435,10 @@ HD void sqr(Fq2& f, const Fq2& a, const Pos& ps) {
   if (ps.rep == 1) {
     // the doubling and xi go on the second operand (reduced: < 2p), a missing term multiplies 0
     Fq2 r;
+#if HBTC_GT_STAGED
+    uint32_t* sa = gt_stage();
+    stage_put(sa, a);
+#endif
 #pragma unroll
     for (uint32_t h = 0; h < GT_LAZY_PASSES; ++h) {
       FqAcc lacc, lacc1;
@@ -375,8 +448,13 @@ HD void sqr(Fq2& f, const Fq2& a, const Pos& ps) {
         const uint32_t e = (terms >> (8 * t)) & 0xffu;
         const bool none = e == 0xffu;
         Fq2 ai, aj, d, z;
+#if HBTC_GT_STAGED
+        stage_get(ai, sa, src(ps, e & 7u));
+        stage_get(aj, sa, src(ps, (e >> 3) & 7u));
+#else
         fetch2(ai, a, src(ps, e & 7u));
         fetch2(aj, a, src(ps, (e >> 3) & 7u));
+#endif
         fq2_xi_if(aj, ((e >> 6) & 1u) && !none, aj);
         fq2_dbl(d, aj);
         fq2_sel(aj, ((e >> 7) & 1u) && !none, d, aj);
@@ -425,6 +503,10 @@ HD void mul_line_t(Fq2& f, const Fq& pa, uint32_t a, const Fq2& Ad, const Fq& pb
   if (ps.rep == 1) {
     // xi on the f coefficient (the operand every term has), so an Fq Y stays one product a half
     Fq2 r;
+#if HBTC_GT_STAGED
+    uint32_t* sa = gt_stage();  // f staged: not live across the terms
+    stage_put(sa, f);
+#endif
 #pragma unroll
     for (uint32_t h = 0; h < GT_LAZY_PASSES; ++h) {
       FqAcc lacc, lacc1;
@@ -433,10 +515,15 @@ HBTC_GT_SMALL_LOOP
       for (uint32_t t = 0; t < 3; ++t) {
         const uint32_t fk = t == 0 ? k : (t == 1 ? (k >= 2 ? k - 2 : k + 4) : (k >= 3 ? k - 3 : k + 3));
         Fq2 x, q;
+#if HBTC_GT_STAGED
+        stage_get(x, sa, src(ps, fk));
+#else
         fetch2(x, f, src(ps, fk));
-        Fq o0, o1;
-        fq_sel(o0, t == 0, pa, t == 1 ? pb : py);
-        fq_sel(o1, t == 0, pa, t == 1 ? pb : py);
+#endif
+        Fq o0, o1;  // element-wise selects (no conditional between two referenced objects)
+        fq_sel(o0, t == 1, pb, py);
+        fq_sel(o0, t == 0, pa, o0);
+        o1 = o0;
         const uint32_t l0 = t == 0 ? a : (t == 1 ? b : y);
         fetch(q.c0, o0, src(ps, l0));
         fetch(q.c1, o1, src(ps, l0 + 1));  // unused for an Fq Y
@@ -466,8 +553,9 @@ HBTC_GT_SMALL_LOOP
     Fq2 x, q, z;
     fetch2(x, f, src(ps, fk));
     Fq o0, o1;
-    fq_sel(o0, t == 0, pa, t == 1 ? pb : py);
-    fq_sel(o1, t == 0, pa, t == 1 ? pb : py);
+    fq_sel(o0, t == 1, pb, py);
+    fq_sel(o0, t == 0, pa, o0);
+    o1 = o0;
     const uint32_t l0 = t == 0 ? a : (t == 1 ? b : y);
     fetch(q.c0, o0, src(ps, l0));
     fetch(q.c1, o1, src(ps, l0 + 1));  // unused for an Fq Y
@@ -534,7 +622,9 @@ HD void cyc_sqr(Fq2& f, const Pos& ps) {
   fetch2(partner, f, src(ps, pk));
   Fq2 x, y, r;
   {
-    Fq2 b = lo ? partner : f, a = lo ? f : partner, xb, apb, apxb;
+    Fq2 b, a, xb, apb, apxb;
+    fq2_sel(b, lo, partner, f);
+    fq2_sel(a, lo, f, partner);
     fq2_mul_xi(xb, b);
     fq2_add(apb, a, b);
     fq2_add(apxb, a, xb);
@@ -593,10 +683,27 @@ HD void set_one(Fq2& f, const Pos& ps) {
 // y^x for cyclotomic y (x < 0: y^|x| then conjugate)
 GTN void exp_by_x(Fq2& r, const Fq2& y, const Pos& ps) {
   Fq2 acc = y;
+#if HBTC_GT_STAGED
+  // y stays in the second stage for the whole chain (cyc_sqr does not use the stages): not live
+  // in VGPRs across the 63 squarings, and not re-staged by each of the five products
+  uint32_t* sa = gt_stage();
+  uint32_t* sb = sa + GT_STAGE_WORDS;
+  const bool staged = ps.rep == 1;
+  if (staged) stage_put(sb, y);
+#endif
 #pragma unroll 1
   for (int bit = 62; bit >= 0; --bit) {
     cyc_sqr(acc, ps);
-    if ((BLS_X_ABS >> bit) & 1ull) mul(acc, acc, y, ps);
+    if ((BLS_X_ABS >> bit) & 1ull) {
+#if HBTC_GT_STAGED
+      if (staged) {
+        stage_put(sa, acc);
+        mul_staged(acc, sa, sb, ps);
+        continue;
+      }
+#endif
+      mul(acc, acc, y, ps);
+    }
   }
   conj(acc, ps);
   r = acc;
@@ -731,7 +838,12 @@ HD void miller2_t(Fq2& f, const MillerArg& m1, const MillerArg& m2, const Pos& p
   fq_zero(zero);
   {
     const bool second = k >= 4;
-    const G1J& P = second ? m2.P : m1.P;
+    // element-wise selects, not a reference chosen between m1.P and m2.P: a select of two
+    // objects' addresses keeps both in private memory (scratch) for the whole kernel
+    G1J P;
+    fq_sel(P.x, second, m2.P.x, m1.P.x);
+    fq_sel(P.y, second, m2.P.y, m1.P.y);
+    fq_sel(P.z, second, m2.P.z, m1.P.z);
     Fq z2, z3, xz;
     fq_sqr(z2, P.z);
     fq_mul(z3, z2, P.z);
@@ -750,6 +862,18 @@ HD void miller2_t(Fq2& f, const MillerArg& m1, const MillerArg& m2, const Pos& p
   const uint32_t c1 = k < 4 ? k : (PROJ2 ? k - 2 : k - 4);  // Fq component: a.c0 a.c1 b.c0 b.c1 / A B C
   const uint32_t c2 = (PROJ2 ? 4 : 2) + (k & 1u);            // round-2 component (b2 / C2)
   set_one(f, ps);
+#if HBTC_GT_STAGED
+  // s1 | s2 in the second stage for the whole loop (sqr and the line products use only the
+  // first): two Fq off the loop's live set
+  uint32_t* ss = gt_stage() + GT_STAGE_WORDS;
+  const bool s_staged = ps.rep == 1;
+  if (s_staged) {
+    Fq2 s12;
+    s12.c0 = s1;
+    s12.c1 = s2;
+    stage_put(ss, s12);
+  }
+#endif
   int j = 0;
   bool first = true;
 #pragma unroll 1
@@ -767,7 +891,19 @@ HD void miller2_t(Fq2& f, const MillerArg& m1, const MillerArg& m2, const Pos& p
 HBTC_GT_SMALL_LOOP
       for (uint32_t t = 0; t < 2; ++t) {
         Fq q;
-        fq_mul(q, t == 0 ? Lr1[c1] : L2[c2], t == 0 ? s1 : s2);
+        Fq sv;
+#if HBTC_GT_STAGED
+        if (s_staged) {
+          const uint32_t l = lane_id();
+#pragma unroll
+          for (int i = 0; i < 12; ++i) sv.v[i] = ss[(12 * t + i) * 64 + l];
+        } else {
+          fq_sel(sv, t == 0, s1, s2);
+        }
+#else
+        fq_sel(sv, t == 0, s1, s2);
+#endif
+        fq_mul(q, t == 0 ? Lr1[c1] : L2[c2], sv);
         fq_sel(p1, t == 0, q, p1);
         p2 = q;
       }

@@ -636,8 +636,12 @@ __global__ void __launch_bounds__(64, HBTC_GT_WAVES_SMALL) k_chk_split(
   const bool unresolved = need && !located;
   if (LVL < 3) {
     const uint32_t ab_child = ul.side ? (kaR | (betaR << 8)) : 0u;
-    split_list(split, unresolved, (t << 3) | (2u * j + ul.side), ul.side ? TR : TL,
-               ul.side ? UR : WL, ab_child, ul.ps);
+    // values selected element-wise: `side ? TR : TL` as a reference argument would select
+    // between two addresses and keep all four values in scratch (388 B/lane)
+    Fq2 To, Uo;
+    gt::fq2_sel(To, ul.side != 0, TR, TL);
+    gt::fq2_sel(Uo, ul.side != 0, UR, WL);
+    split_list(split, unresolved, (t << 3) | (2u * j + ul.side), To, Uo, ab_child, ul.ps);
   }
   if (ul.ps.k != 0 || ul.ps.sub != 0) return;
   if (located) status[lo + loc] = HBTC_REJECT;
@@ -1121,7 +1125,9 @@ __device__ __forceinline__ void pb_line_values(const Fq2* L, const Fq& x, const 
     A = L[0];
     const Fq2& BC = k < 2 ? L[2] : L[1];
     const Fq& m = (k & 1u) ? BC.c1 : BC.c0;
-    fq_mul(prod, m, k < 2 ? y : x);
+    Fq s;  // element-wise: a reference select would keep x and y in scratch
+    fq_sel(s, k < 2, y, x);
+    fq_mul(prod, m, s);
     if (k >= 4) fq_zero(prod);
   }
 }
