@@ -2147,12 +2147,13 @@ int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_
     const uint32_t m = std::min(PB_CHUNK, n - base);
     const uint32_t T = (m + 63) / 64;
     G1A* rA;
-    G2A* qdec;
+    G2A *qdec, *wdec;
     SigTileSums* sums;
     Fq2 *qtab, *wtab, *fbuf;
     uint32_t *winf, *counters, *tlist, *leaves;
     HB_TRY(wst(c, "pb.ra", m, &rA));
     HB_TRY(wst(c, "pb.qdec", m, &qdec));
+    HB_TRY(wst(c, "pb.wdec", m, &wdec));
     HB_TRY(wst(c, "pb.sums", T, &sums));
     HB_TRY(wst(c, "pb.qtab", (size_t)m * PLINES_FQ2, &qtab));
     HB_TRY(wst(c, "pb.wtab", (size_t)8 * T * PLINES_FQ2, &wtab));
@@ -2170,7 +2171,7 @@ int pb_verify_dev(hbtc_ctx* c, uint32_t n, const uint8_t* d_a, const uint8_t* d_
     key.bits = c->rlc_bits;
     HB_CHECK(c, launch_zero_u32(c->stream, counters, 2));
     HB_TRY(timed(c, "pb_items", [&] {
-      return launch_pb_items(c->stream, m, a, q, q_trusted, w, key, rA, qdec, sums, st,
+      return launch_pb_items(c->stream, m, a, q, q_trusted, w, key, rA, qdec, wdec, sums, st,
                              d_adec ? d_adec + base : nullptr);
     }));
     HB_TRY(timed(c, "pb_lines", [&] { return launch_pb_lines(c->stream, m, qdec, st, qtab); }));

@@ -23,6 +23,7 @@
 
 #include "hbtc.h"
 #include "hbtc_kernels.h"
+#include "pair.h"
 
 namespace hbtc {
 namespace {
@@ -393,21 +394,35 @@ hipError_t launch_zero_u32(hipStream_t s, uint32_t* p, size_t n) {
   return hipGetLastError();
 }
 
-// [h2] P for candidates P (one lane each) -> compressed G2 words; st = 1 if [h2] P = O (the
-// host then continues G2::rand's loop itself).
-__global__ void __launch_bounds__(64) k_g2_clear_cofactor(uint32_t n, const G2A* __restrict__ in,
-                                                          uint32_t* __restrict__ out_w,
-                                                          int32_t* __restrict__ st) {
-  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= n) return;
-  G2J q;
-  g2_clear_cofactor(q, in[i]);
+// [h2] P for candidates P -> compressed G2 words; st = 1 if [h2] P = O (the host then continues
+// G2::rand's loop itself).  Lane pairs (pair.h g2p_clear_cofactor): candidate i on lanes 2i,
+// 2i + 1; the even lane assembles the affine point for the encoding.  One wave per SIMD: no
+// scratch (two: 500 B/lane; the one-lane form kept 760 B at one); hash batches are small.
+__global__ void __launch_bounds__(64, 1) k_g2_clear_cofactor(uint32_t n, const G2A* __restrict__ in,
+                                                             uint32_t* __restrict__ out_w,
+                                                             int32_t* __restrict__ st) {
+  const uint32_t i = (blockIdx.x * 64 + threadIdx.x) >> 1;
+  if (i >= n) return;  // pair-uniform
+  G2Ap p;
+  g2p_load_aff(p, in + i);
+  G2Jp q;
+  g2p_clear_cofactor(q, p);
   if (jac_is_inf(q)) {
-    st[i] = 1;
+    if (!pair_odd()) st[i] = 1;
     return;
   }
+  G2Ap ap;
+  jac_to_aff(ap, q);
+  Fq px, py;
+  fq_xchg(px, ap.x.v);
+  fq_xchg(py, ap.y.v);
+  if (pair_odd()) return;
   G2A a;
-  jac_to_aff(a, q);
+  a.x.c0 = ap.x.v;
+  a.x.c1 = px;
+  a.y.c0 = ap.y.v;
+  a.y.c1 = py;
+  a.inf = 0;
   uint32_t w[24];
   g2_compress(w, a);
   uint4* o = reinterpret_cast<uint4*>(out_w + 24 * (size_t)i);
@@ -418,7 +433,7 @@ __global__ void __launch_bounds__(64) k_g2_clear_cofactor(uint32_t n, const G2A*
 hipError_t launch_g2_clear_cofactor(hipStream_t s, uint32_t n, const G2A* in, uint8_t* out_c96,
                                     int32_t* st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_g2_clear_cofactor, dim3((n + 63) / 64), dim3(64), 0, s, n, in,
+  hipLaunchKernelGGL(k_g2_clear_cofactor, dim3((2 * n + 63) / 64), dim3(64), 0, s, n, in,
                      reinterpret_cast<uint32_t*>(out_c96), st);
   return hipGetLastError();
 }

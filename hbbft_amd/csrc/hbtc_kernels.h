@@ -226,7 +226,11 @@ hipError_t launch_pb_scatter(hipStream_t s, uint32_t n, const uint32_t* list, co
                              int32_t* st);
 hipError_t launch_pb_items(hipStream_t s, uint32_t n, const uint8_t* a_c48, const uint8_t* q_c96,
                            bool q_trusted, const uint8_t* w_c96, RlcKey key, G1A* rA, G2A* Qdec,
-                           SigTileSums* sums, int32_t* status, G1A* adec = nullptr);
+                           G2A* Wdec, SigTileSums* sums, int32_t* status, G1A* adec = nullptr);
+// r_i W_i of the PENDING items and the tile / sub-tile sums S, on lane pairs (hbtc_sig.hip; the
+// second launch of launch_pb_items)
+hipError_t launch_pb_wsum(hipStream_t s, uint32_t n, RlcKey key, const G2A* wdec, const int32_t* status,
+                          SigTileSums* sums);
 // g_i = [k0 + k1 x^2] A_i (compressed) for the ACCEPTed items, zero bytes for the others
 hipError_t launch_pb_mul_glv(hipStream_t s, uint32_t n, const G1A* adec, const int32_t* status,
                              const uint32_t* k0, const uint32_t* k1, uint8_t* out_c48);

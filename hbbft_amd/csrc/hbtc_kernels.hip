@@ -87,6 +87,10 @@ __global__ void __launch_bounds__(64) k_g1_decode(const uint8_t* __restrict__ in
   status[i] = ok ? HBTC_ACCEPT : HBTC_DECODE_ERR;
 }
 
+#ifndef HBTC_G2STEPS_PAIR
+#define HBTC_G2STEPS_PAIR 1  // k_g2_steps on lane pairs (pair.h): the 68 steps at half the latency
+#endif
+#if !HBTC_G2STEPS_PAIR  // the one-lane form (variant builds only)
 // Decode the fixed per-instance G2 arguments (H = hash_g2(nonce), and w for ciphertexts) and
 // walk their Miller-loop steps: one lane per argument, both argument sets in ONE launch
 // (in0: n0 items, in1: n1 items; outputs [0, n0) then [n0, n0 + n1)).  The 68 projective
@@ -134,10 +138,8 @@ __global__ void __launch_bounds__(64) k_g2_steps(const uint8_t* __restrict__ in0
   ok = !jac_is_inf(T) && jac_eq_aff(T, px, npy);
   status[g] = ok ? HBTC_ACCEPT : HBTC_DECODE_ERR;
 }
-
-#ifndef HBTC_G2STEPS_PAIR
-#define HBTC_G2STEPS_PAIR 1  // k_g2_steps on lane pairs (pair.h): the 68 steps at half the latency
 #endif
+
 #if HBTC_G2STEPS_PAIR
 // k_g2_steps on lane pairs: argument g on lanes (2g, 2g + 1).  The decode (square roots) runs on
 // both lanes in one-lane form, the 68 line steps and the psi test in pair form.

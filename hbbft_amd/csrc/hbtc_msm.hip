@@ -680,10 +680,14 @@ template __global__ void k_msm_final<Fq, 12>(uint32_t, uint32_t, uint32_t, const
                                              const uint32_t*, uint32_t, const uint32_t*,
                                              const uint32_t*, int32_t*, uint8_t*, uint8_t*);
 #endif
+#ifndef HBTC_MSM_G2_PAIR
+#define HBTC_MSM_G2_PAIR 1  // the G2 bucket / window / final passes on lane pairs (pair.h)
+#endif
 #if HBTC_IN_PART(9)
 template __global__ void k_msm_decode<Fq2, 24>(uint32_t, uint32_t, uint32_t, const uint8_t*,
                                                const uint32_t*, const uint32_t*, const int32_t*,
                                                const G2A*, G2A*, uint32_t*);
+#if !HBTC_MSM_G2_PAIR  // the one-lane G2 passes (variant builds only)
 template __global__ void k_msm_buckets<Fq2>(uint64_t, uint32_t, uint32_t, uint32_t, const G2A*,
                                             const uint32_t*, const uint32_t*, const uint32_t*,
                                             G2J*);
@@ -692,15 +696,15 @@ template __global__ void k_msm_final<Fq2, 24>(uint32_t, uint32_t, uint32_t, cons
                                               const uint32_t*, uint32_t, const uint32_t*,
                                               const uint32_t*, int32_t*, uint8_t*, uint8_t*);
 #endif
-
-#ifndef HBTC_MSM_G2_PAIR
-#define HBTC_MSM_G2_PAIR 1  // the G2 bucket / window / final passes on lane pairs (pair.h)
 #endif
+
 #ifndef HBTC_MSM_G2P_WAVES
 #define HBTC_MSM_G2P_WAVES 2
 #endif
 #ifndef HBTC_MSM_G2P_BUCKET_WAVES
-#define HBTC_MSM_G2P_BUCKET_WAVES HBTC_MSM_G2P_WAVES
+// one wave: no scratch (two: 324 B/lane); C4 6.069 / 6.062 M shares/s and C2 1.111 / 1.091 M at
+// one / two waves (profiles/r06/run12/)
+#define HBTC_MSM_G2P_BUCKET_WAVES 1
 #endif
 #if HBTC_IN_PART(9) && HBTC_MSM_G2_PAIR
 // The three G2 reduction passes above on lane pairs (round 6): unit g (one (msm, window,

@@ -22,26 +22,23 @@
 namespace hbtc {
 
 #ifndef HBTC_PB_ITEMS_WAVES
-#define HBTC_PB_ITEMS_WAVES 1  // one wave per SIMD: 740 B/lane of scratch (two: 1.5 KB)
+#define HBTC_PB_ITEMS_WAVES 1  // the G1 half and the decodes (the G2 half: k_pb_wsum_pair)
 #endif
 
-// One wave per tile of 64 consecutive items: decode A (G1, subgroup check; null = the G1
-// generator), W and Q (G2, subgroup checks; Q trusted = our own hash output, in the subgroup by
-// construction: on-curve decode only), draw r_i, store r_i A_i (affine) and the decoded Q_i, and
-// sum r_i W_i over the tile and its 8 sub-tiles.  An item that fails to decode gets DECODE_ERR
-// and contributes nothing.
+// One lane per item: decode A (G1, subgroup check; null = the G1 generator), W and Q (G2,
+// subgroup checks; Q trusted = our own hash output, in the subgroup by construction: on-curve
+// decode only), draw r_i, store r_i A_i (affine), the decoded Q_i and W_i.  An item that fails to
+// decode gets DECODE_ERR and contributes nothing.  r_i W_i and its tile / sub-tile sums follow on
+// lane pairs (k_pb_wsum_pair, hbtc_sig.hip).
 __global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n, const uint8_t* __restrict__ a_c48,
                                                     const uint8_t* __restrict__ q_c96, bool q_trusted,
                                                     const uint8_t* __restrict__ w_c96, RlcKey key,
                                                     G1A* __restrict__ rA, G2A* __restrict__ Qdec,
-                                                    SigTileSums* __restrict__ sums,
+                                                    G2A* __restrict__ Wdec,
                                                     int32_t* __restrict__ status,
                                                     G1A* __restrict__ adec) {
-  __shared__ G2J red[64];
   const uint32_t lane = threadIdx.x;
   const uint32_t i = blockIdx.x * 64u + lane;
-  G2J S;
-  jac_set_inf(S);
   if (i < n) {
     uint32_t w[24];
     G1A A;
@@ -90,25 +87,13 @@ __global__ void __launch_bounds__(64, HBTC_PB_ITEMS_WAVES) k_pb_items(uint32_t n
           ra.inf = 0;
         }
       }
-      if (!W.inf) {  // r W, m = -psi^2: (x, y) -> (zeta x, y)
-        G2A xp;
-        g2_psi(xp.x, xp.y, W);
-        xp.inf = 0;
-        G2J xj;
-        jac_from_aff(xj, xp);
-        Fq zeta;
-        fq_set(zeta, G2_ZETA);
-        G2A pxp;  // the two-addition loop (the 8-entry table is 384 dwords per lane on G2)
-        xadic_table(xp, pxp, W, xj);
-        xadic_mul_uniform(S, W, xp, pxp, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3], xd.nbits);
-      }
     }
     rA[i] = ra;
     Qdec[i] = Q;
+    Wdec[i] = W;  // r W and the tile sums: k_pb_wsum_pair (hbtc_sig.hip), on lane pairs
     if (adec) adec[i] = A;  // the decoded A for the caller (hbtc_decrypt's g = sk u)
     status[i] = ok ? HBTC_RLC_PENDING : HBTC_DECODE_ERR;
   }
-  rlc_reduce_plain<Fq2>(red, S, lane, sums[blockIdx.x].S);
 }
 
 // The projective line table of every pending item's Q_i (one lane per item).
@@ -162,11 +147,13 @@ hipError_t launch_pb_scatter(hipStream_t s, uint32_t n, const uint32_t* list, co
 
 hipError_t launch_pb_items(hipStream_t s, uint32_t n, const uint8_t* a_c48, const uint8_t* q_c96,
                            bool q_trusted, const uint8_t* w_c96, RlcKey key, G1A* rA, G2A* Qdec,
-                           SigTileSums* sums, int32_t* status, G1A* adec) {
+                           G2A* Wdec, SigTileSums* sums, int32_t* status, G1A* adec) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_pb_items, dim3((n + 63) / 64), dim3(64), 0, s, n, a_c48, q_c96, q_trusted, w_c96,
-                     key, rA, Qdec, sums, status, adec);
-  return hipGetLastError();
+                     key, rA, Qdec, Wdec, status, adec);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_pb_wsum(s, n, key, Wdec, status, sums);
 }
 
 // g_i = [k] A_i for the ACCEPTed items of a pair batch (hbtc_decrypt: g = sk u), from the decoded

@@ -29,6 +29,15 @@ namespace hbtc {
 #ifndef HBTC_SIG_DEC_WAVES
 #define HBTC_SIG_DEC_WAVES 2
 #endif
+// Round 6 defaults: the lane-pair kernels.  The one-lane kernels they replace are compiled only
+// into variant builds that switch them back (tools/build_variant.sh), so the library holds no
+// unused one-lane G2 kernel.
+#ifndef HBTC_SIG_PAIR
+#define HBTC_SIG_PAIR 1  // k_sig_items in lane-pair form (pair.h; 0: the one-lane kernel)
+#endif
+#ifndef HBTC_SIGDEC_PAIR
+#define HBTC_SIGDEC_PAIR 1  // k_sig_decode with its psi chains on lane pairs (k_sig_decode_pair)
+#endif
 // The file is compiled twice (Makefile): part 1 = the decode half with the Fq product inlined
 // (its loops then run without scratch: the shared subroutine's 102 fixed VGPRs left the G2
 // doubling loop re-reading ~150 spilled dwords per bit at two waves), part 2 = the rest with the
@@ -37,7 +46,7 @@ namespace hbtc {
 #define HBTC_SIG_PART 0
 #endif
 #define HBTC_SIG_IN(n) (HBTC_SIG_PART == 0 || HBTC_SIG_PART == (n))
-#if HBTC_SIG_SPLIT && HBTC_SIG_IN(1)
+#if HBTC_SIG_SPLIT && HBTC_SIG_IN(1) && !HBTC_SIGDEC_PAIR
 // The decode half of the SignatureShare item pass, a kernel of its own so it runs at two waves per
 // SIMD (432 B/lane of scratch; in one kernel with the scalar half the G2 state needs one wave per
 // SIMD): zcash G2 decode with the psi subgroup test into dec, DECODE_ERR into status (every other
@@ -103,9 +112,6 @@ hipError_t launch_sig_decode(hipStream_t s, uint32_t n_tiles, const Tile* tiles,
 hipError_t launch_sig_decode(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                              const uint8_t* sigs, const int32_t* pk_status, uint32_t n_pk, G2A* dec,
                              int32_t* status);
-#ifndef HBTC_SIGDEC_PAIR
-#define HBTC_SIGDEC_PAIR 1  // k_sig_decode with its psi chains on lane pairs (k_sig_decode_pair)
-#endif
 #ifndef HBTC_SIGDEC_WAVES
 #define HBTC_SIGDEC_WAVES 2
 #endif
@@ -178,6 +184,7 @@ __global__ void __launch_bounds__(64, HBTC_SIGDEC_WAVES) k_sig_decode_pair(
   if (in) status[item] = st;
 }
 #endif
+#if !(HBTC_SIG_PAIR && HBTC_SIG_SPLIT)
 // One wave per tile: decode every SignatureShare (zcash compressed G2 + subgroup check), r_i,
 // r_i sigma_i, r_i pk_i, then the plain and weighted tile / sub-tile sums in both groups.  One
 // wave per SIMD (256 VGPRs + 256 AGPRs).  No kernel keeps a multi-KB private segment any more:
@@ -263,10 +270,8 @@ __global__ void __launch_bounds__(64, 1) k_sig_items(
   rlc_reduce<Fq>(red1, red1 + 64, P, lane, ts->P, ts->PW);
 }
 
-#ifndef HBTC_SIG_PAIR
-#define HBTC_SIG_PAIR 1  // k_sig_items in lane-pair form (pair.h; 0: the one-lane kernel above)
-#endif
-#if HBTC_SIG_PAIR
+#endif  // one-lane k_sig_items
+
 #ifndef HBTC_SIGP_WAVES
 #define HBTC_SIGP_WAVES 2  // k_sig_items_pair: minimum waves per SIMD of the register allocation
 #endif
@@ -450,6 +455,7 @@ __device__ __forceinline__ void rlc_reduce_g1w(uint32_t* lds, uint32_t lane, G1J
   }
 }
 
+#if HBTC_SIG_PAIR
 // k_sig_items in lane-pair form: one workgroup of two waves per 64-share tile, share i on lanes
 // (2i, 2i + 1).  r_i sigma_i by the x-adic two-addition loop in pair arithmetic (table in
 // registers: 72 per lane), r_i pk_i split over the pair (rlc_pk_mul_x_pair), then the two trees
@@ -532,6 +538,56 @@ __global__ void __launch_bounds__(128, HBTC_SIGP_WAVES) k_sig_items_pair(
     rlc_reduce_g1w(lds1, threadIdx.x - 64, ts->P, ts->PW);
 }
 #endif
+
+// The G2 half of the pair-batch item pass (hbtc_pb.hip: PublicKey::verify's sigma /
+// Ciphertext::verify's w, DESIGN.md §4 "Pair batches") in lane-pair form: item i of the chunk on
+// lanes (2i, 2i + 1) of its tile's workgroup, r_i W_i by the same x-adic loop as
+// k_sig_items_pair (r_i from the same key and index as k_pb_items' G1 half), then the tile's G2
+// tree on wave 0.  The pair batches use the plain sums S only (the weighted SW are written
+// too, unused).  k_pb_items decoded W_i (wdec) and set the status: PENDING items count.
+__global__ void __launch_bounds__(128, HBTC_SIGP_WAVES) k_pb_wsum_pair(
+    uint32_t n, RlcKey key, const G2A* __restrict__ wdec, const int32_t* __restrict__ status,
+    SigTileSums* __restrict__ sums) {
+  __shared__ uint32_t lds[72 * 128];
+  uint32_t* ldsB = lds + 36 * 128 + 36 * 64;
+  const uint32_t m = threadIdx.x >> 1;
+  const uint32_t i = blockIdx.x * 64u + m;
+  G2Jp S;
+  jac_set_inf(S);
+  if (i < n && status[i] == HBTC_RLC_PENDING) {  // pair-uniform
+    G2Ap W;
+    g2p_load_aff(W, wdec + i);
+    if (!W.inf) {  // r W, m = -psi^2: (x, y) -> (zeta x, y)
+      const XDigits xd = rlc_digits(key, i);
+      G2Ap xp, pxp;
+      g2p_psi(xp.x, xp.y, W);
+      xp.inf = 0;
+      G2Jp xj;
+      jac_from_aff(xj, xp);
+      xadic_table(xp, pxp, W, xj);
+      Fq zeta;
+      fq_set(zeta, G2_ZETA);
+      xy_lds_put_aff<Fq2p, 128>(lds, threadIdx.x, 0, W);
+      xy_lds_put_aff<Fq2p, 128>(lds, threadIdx.x, 1, xp);
+      xy_lds_put_aff<Fq2p, 128>(lds, threadIdx.x, 2, pxp);
+      xadic_mul_uniform_lds<Fq2p, 128>(S, lds, threadIdx.x, zeta, xd.d[0], xd.d[1], xd.d[2], xd.d[3],
+                                       xd.nbits);
+    }
+  }
+  __syncthreads();  // every lane's table reads are over before the tree's arrays are written
+  g2p_lds_put(lds, m, S);
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    SigTileSums* ts = sums + blockIdx.x;
+    rlc_reduce_g2p(lds, ldsB, threadIdx.x, ts->S, ts->SW);
+  }
+}
+hipError_t launch_pb_wsum(hipStream_t s, uint32_t n, RlcKey key, const G2A* wdec, const int32_t* status,
+                          SigTileSums* sums) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pb_wsum_pair, dim3((n + 63) / 64), dim3(128), 0, s, n, key, wdec, status, sums);
+  return hipGetLastError();
+}
 
 #if HBTC_SIG_PAIR
 // The exact small-call path in ONE kernel (round 6): per SignatureShare on a lane pair, the zcash

@@ -200,6 +200,87 @@ HD bool g2p_psi_test(const G2Jp& T, const G2Ap& Q) {
   fneg(py, py);
   return jac_eq_aff(T, px, py);
 }
+// psi on Jacobian coordinates (curve.h g2j_psi) in pair form: X and Y as in g2p_psi, Z conjugated
+HD void g2p_psi_jac(G2Jp& r, const G2Jp& p) {
+  Fq px, c;
+  fq_xchg(px, p.x.v);
+  fq_set(c, G2_PSI_CX + 12);
+  Fq2p cy, yc;
+  fq2p_set(cy, G2_PSI_CY);
+  fconj(yc, p.y);
+  fq_mul(r.x.v, px, c);
+  fmul(r.y, yc, cy);
+  fconj(r.z, p.z);
+}
+
+// [h2] P (curve.h g2_clear_cofactor: Budroni-Pintore g(P), then [s] g(P) by the m-split) in pair
+// form; the same chain of group operations, so the same point
+HD void g2p_clear_cofactor(G2Jp& out, const G2Ap& p) {
+  if (p.inf) {  // pair-uniform
+    jac_set_inf(out);
+    return;
+  }
+  G2Jp pj, t1, t2, t3;
+  jac_from_aff(pj, p);
+  jac_mul_u64(t1, p, BLS_X_ABS);
+  jac_neg(t1, t1);  // [x] P
+  G2Ap ps;
+  g2p_psi(ps.x, ps.y, p);
+  ps.inf = 0;
+  jac_dbl(t3, pj);
+  g2p_psi_jac(t3, t3);
+  g2p_psi_jac(t3, t3);  // psi^2(2P)
+  {
+    G2Ap nps;
+    aff_neg(nps, ps);
+    jac_add_aff(t3, t3, nps);
+  }
+  jac_add_aff(t2, t1, ps);
+  jac_mul_u64_jac(t2, t2, BLS_X_ABS);
+  jac_neg(t2, t2);
+  jac_add(t3, t3, t2);
+  {
+    G2Jp nt1;
+    jac_neg(nt1, t1);
+    jac_add(t3, t3, nt1);
+  }
+  {
+    G2Ap np;
+    aff_neg(np, p);
+    jac_add_aff(t3, t3, np);  // Q = g(P)
+  }
+  if (jac_is_inf(t3)) {
+    out = t3;
+    return;
+  }
+  G2Jp mq = t3;  // m(Q) = (zeta X, Y, Z)
+  {
+    Fq zeta;
+    fq_set(zeta, G2_ZETA);
+    fmul_by_fq(mq.x, t3.x, zeta);
+  }
+  G2Jp bj;
+  jac_add(bj, t3, mq);
+  G2Ap b;
+  {
+    Fq2p zi, zi2, zi3;
+    finv_fast(zi, bj.z);
+    fsqr(zi2, zi);
+    fmul(zi3, zi2, zi);
+    fmul(b.x, bj.x, zi2);
+    fmul(b.y, bj.y, zi3);
+    b.inf = 0;
+  }
+  G2Jp acc;
+  jac_from_aff(acc, b);
+#pragma unroll 1
+  for (int bit = 125; bit >= 0; --bit) {
+    jac_dbl(acc, acc);
+    if ((cofactor_c0_word(bit >> 5) >> (bit & 31)) & 1u) jac_add_aff(acc, acc, b);
+  }
+  jac_add(out, acc, mq);
+}
+
 // An Fq2 point decoded on both lanes of the pair (one-lane code) -> pair form
 HD void g2p_from_full(G2Ap& r, const G2A& f) {
   const bool odd = pair_odd();
