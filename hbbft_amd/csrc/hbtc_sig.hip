@@ -31,7 +31,8 @@ namespace hbtc {
 #endif
 // Round 6 defaults: the lane-pair kernels.  The one-lane kernels they replace are compiled only
 // into variant builds that switch them back (tools/build_variant.sh), so the library holds no
-// unused one-lane G2 kernel.
+// unused one-lane G2 kernel.  HBTC_SIGDEC_PAIR=0 goes on both objects (hbtc_sig.s1 defines the
+// one-lane decode that s2 launches).
 #ifndef HBTC_SIG_PAIR
 #define HBTC_SIG_PAIR 1  // k_sig_items in lane-pair form (pair.h; 0: the one-lane kernel)
 #endif
