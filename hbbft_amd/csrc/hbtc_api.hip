@@ -83,6 +83,8 @@ struct Lane {
   hipEvent_t ev_main = nullptr, ev_prep = nullptr, done = nullptr;
   hipEvent_t items_done = nullptr;  // recorded after the lane's last item pass
   bool items_rec = false;
+  hipEvent_t dec_done = nullptr;  // recorded after the decode half of the lane's last G1 item pass
+  bool dec_rec = false;
   int dec_flip = 0;  // alternates the lane's decoded-item buffers (a combine may still read one)
   std::vector<std::pair<uintptr_t, uintptr_t>> rd, wr;
   bool busy = false;
@@ -109,10 +111,10 @@ struct hbtc_ctx {
   int lane = 0;
   int last_items_lane = -1;  // the lane of the most recent item pass (items_gate)
   bool pin_lane = false;  // host entry points: stay on the lane their uploads went to
-  // item passes of the lanes run one after the other (HBTC_ITEMS_SERIAL, default on): epoch
+  // item passes of the lanes run one after the other (HBTC_ITEMS_SERIAL, default 1): epoch
   // k+1's item pass then overlaps epoch k's check levels instead of sharing the chip with epoch
-  // k's item pass
-  bool items_serial = true;
+  // k's item pass; 2 also staggers the small passes, each decode after the previous one
+  int items_serial = 1;
   int n_cu = 256;               // compute units of the device (check schedule, check_mode)
   int check_mode_forced = -1;  // HBTC_CHECK_MODE
   bool g2_gls = true;          // G2 combines through the ψ split (HBTC_G2_GLS=0: 255-bit terms)
@@ -467,11 +469,17 @@ int end_verify(hbtc_ctx* c) {
 // beside the other lanes' check levels.  A pass that fits the chip in one round (at most two
 // waves per SIMD: 8 n_cu) is not chained -- the 125-ciphertext slice (2,000 tiles) runs 16.3
 // instead of 17.4 ms per epoch unchained, the 250 one (4,000) 29.3-29.9 chained against 30.6-31.4,
-// C3 (16,000) 84.2-84.5 against 85.1 (profiles/r04/run22/, run23/).
+// C3 (16,000) 84.2-84.5 against 85.1 (profiles/r04/run22/, run23/).  HBTC_ITEMS_SERIAL=2 also
+// staggers the small passes (each decode after the previous lane's decode, to break the lanes'
+// lockstep in the slice's trace): 125-ciphertext slice 14.0-14.2 against 13.6-13.8 ms, 250 and
+// C3 unchanged (profiles/r06/run22/), so not the default.
 int items_gate(hbtc_ctx* c, uint32_t n_tiles) {
   const int o = c->last_items_lane;
-  if (c->items_serial && n_tiles > 8u * (uint32_t)c->n_cu && o >= 0 && o != c->lane)
+  if (!c->items_serial || o < 0 || o == c->lane) return HBTC_OK;
+  if (n_tiles > 8u * (uint32_t)c->n_cu)
     HB_CHECK(c, hipStreamWaitEvent(c->stream, c->lanes[o].items_done, 0));
+  else if (c->items_serial == 2 && c->lanes[o].dec_rec)  // a small pass: after the previous decode
+    HB_CHECK(c, hipStreamWaitEvent(c->stream, c->lanes[o].dec_done, 0));
   return HBTC_OK;
 }
 int items_mark(hbtc_ctx* c) {
@@ -908,8 +916,9 @@ int rlc_dec_pass(hbtc_ctx* c, Keyset* ks, uint32_t n_ct, const uint32_t* offsets
   if (rlc_items_split()) HB_TRY(wst(c, "rlc.t1", n_items, &t1s));
   HB_TRY(timed(c, "rlc_items", [&] {
     return launch_rlc_items(c->stream, n_tiles, tiles, d_idx, d_share, ks->pk, ks->st, ks->tab,
-                            ks->n, key, sus, sums, dec, d_status, t1s);
+                            ks->n, key, sus, sums, dec, d_status, t1s, c->lanes[c->lane].dec_done);
   }));
+  c->lanes[c->lane].dec_rec = rlc_items_split();
   HB_TRY(items_mark(c));
   HB_TRY(stream_after(c, c->stream, c->s_prep, c->ev_prep));
   if (exact) {
@@ -1534,7 +1543,7 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return HBTC_ERR_DEVICE;
   hbtc_ctx* c = new hbtc_ctx();
   c->device = device;
-  if (const char* e = getenv("HBTC_ITEMS_SERIAL")) c->items_serial = atoi(e) != 0;
+  if (const char* e = getenv("HBTC_ITEMS_SERIAL")) c->items_serial = atoi(e);
   if (const char* e = getenv("HBTC_G2_GLS")) c->g2_gls = atoi(e) != 0;
   if (const char* e = getenv("HBTC_G1_GLV")) c->g1_glv = atoi(e) != 0;
   if (const char* e = getenv("HBTC_COMB_SMALL")) c->comb_small = atoi(e) != 0;
@@ -1581,7 +1590,8 @@ int hbtc_ctx_create(int device, hbtc_ctx** out) {
         !created(hipEventCreateWithFlags(&l.ev_main, hipEventDisableTiming), "hipEventCreateWithFlags") ||
         !created(hipEventCreateWithFlags(&l.ev_prep, hipEventDisableTiming), "hipEventCreateWithFlags") ||
         !created(hipEventCreateWithFlags(&l.done, hipEventDisableTiming), "hipEventCreateWithFlags") ||
-        !created(hipEventCreateWithFlags(&l.items_done, hipEventDisableTiming), "hipEventCreateWithFlags")) {
+        !created(hipEventCreateWithFlags(&l.items_done, hipEventDisableTiming), "hipEventCreateWithFlags") ||
+        !created(hipEventCreateWithFlags(&l.dec_done, hipEventDisableTiming), "hipEventCreateWithFlags")) {
       hbtc_ctx_destroy(c);
       return HBTC_ERR_DEVICE;
     }
@@ -1656,6 +1666,7 @@ void hbtc_ctx_destroy(hbtc_ctx* c) {
     ev_free(l.ev_prep);
     ev_free(l.done);
     ev_free(l.items_done);
+    ev_free(l.dec_done);
     if (l.stream) (void)hipStreamDestroy(l.stream);
   }
   if (c->lanes[0].s_prep) (void)hipStreamDestroy(c->lanes[0].s_prep);

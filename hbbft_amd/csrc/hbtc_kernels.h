@@ -87,7 +87,8 @@ bool rlc_items_split();
 hipError_t launch_rlc_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* shares, const G1A* pk, const int32_t* pk_status,
                             const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,
-                            TileSums* sums, G1A* dec, int32_t* status, G1J* t1s);
+                            TileSums* sums, G1A* dec, int32_t* status, G1J* t1s,
+                            hipEvent_t after_decode = nullptr);
 // Final decisions; with last_bad != null, counts every sender's REJECTs in `rejects` and stamps
 // last_bad[i] = now for the senders with >= thresh of them (clearing the counts).
 hipError_t launch_status_remap(hipStream_t s, uint32_t n, int32_t* status, int32_t from, int32_t to);

@@ -261,13 +261,15 @@ bool rlc_items_split() { return HBTC_RLC_SPLIT != 0; }
 hipError_t launch_rlc_items(hipStream_t s, uint32_t n_tiles, const Tile* tiles, const uint32_t* idx,
                             const uint8_t* shares, const G1A* pk, const int32_t* pk_status,
                             const PtXY* pk_tab, uint32_t n_pk, RlcKey key, Suspects sus,
-                            TileSums* sums, G1A* dec, int32_t* status, G1J* t1s) {
+                            TileSums* sums, G1A* dec, int32_t* status, G1J* t1s,
+                            hipEvent_t after_decode) {
   if (n_tiles == 0) return hipSuccess;
 #if HBTC_RLC_SPLIT
   hipLaunchKernelGGL(k_rlc_decode, dim3(n_tiles), dim3(64), 0, s, tiles, idx, shares, pk_status, n_pk,
                      dec, t1s, status);
-  const hipError_t e = hipGetLastError();
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (after_decode && (e = hipEventRecord(after_decode, s)) != hipSuccess) return e;
 #endif
   hipLaunchKernelGGL(k_rlc_items, dim3(n_tiles), dim3(64), 0, s, tiles, idx, shares, pk, pk_status,
                      pk_tab, n_pk, key, sus, sums, dec, status, t1s);
