@@ -339,10 +339,21 @@ def bench_coins(ctx, name, n, n_inst, steps, warmup, corrupt=0.01, corrupt_mode=
     items0 = (run.slots[0]["hi"] - run.slots[0]["lo"]) if node is not None else total
     bits = tctx.rlc_bits()
     key = "sig_rlc_item" if bits == 64 or "sig_rlc_item_128" not in consts else "sig_rlc_item_128"
-    # (one form since round 5: r_i sigma_i by the two-addition x-adic loop at one wave per SIMD)
-    roof = roofline_line(tctx, "sig_items", "k_sig_items", consts[key] * items0,
+    # (round 6: k_sig_decode_pair + k_sig_items_pair, the G2 arithmetic on lane pairs)
+    roof = roofline_line(tctx, "sig_items", "k_sig_decode_pair + k_sig_items_pair", consts[key] * items0,
                          "%s Fqm (G2 decode + subgroup test, [a]s + [b](-psi^2 s), r pk from "
                          "the fixed-base table, tile-tree share) x %d SignatureShares per launch" % (key, items0))
+    if roof and node is None:
+        # the same step once more with nothing else in flight: the item pass on an idle chip,
+        # beside its pipelined span above (where the other lanes' checks and combines share the CUs)
+        tctx.timing_reset()
+        run.step()
+        run.sync()
+        iso = roofline_line(tctx, "sig_items", roof["kernel"], roof["fqm_per_launch"], roof["work_unit"])
+        if iso:
+            roof["kernel_ms_per_launch_isolated"] = iso["kernel_ms_per_launch"]
+            roof["frac_isolated"] = iso["frac"]
+            roof["isolated_note"] = "one extra step after the timed region with no other step in flight"
     stv, out, par, cst = run.results()
     lat = None
     if node is None and latency_steps:
